@@ -1,0 +1,258 @@
+#!/usr/bin/env python
+"""MM-PDE rollout benchmark (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cy-mmpde]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
+
+A *step* is one full MM-PDE forward step over the rank's trajectories (DMM
+moved mesh, moved-mesh kNN-35 graph, model_b, kNN-30 + ItpNet interpolation +
+res_cut, model on the fixed-grid graph, sum), fed back autoregressively.
+Default workload = BASELINE config 4: cylinder MM-PDE, 16 trajectories of the
+2521-node mesh per GPU (weak scaling: trajectories shard across ranks, no
+data-path collective).  value = node-updates/s of the whole job
+= trajectories_total * 2521 * K / max-over-ranks(time of the K timed steps).
+
+Also reported (rank 0):
+* roofline: the dominant kernel (GNN edge stage, 12 launches per step) timed
+  live with hipEvents recorded on its own stream around every launch inside
+  the timed region; achieved = algorithmic FLOP per launch / mean launch time.
+* cpu_baseline (N = 1 only): the CPU oracle (op-for-op restatement of the
+  reference, oracle/refcpu.py) timed on a bounded sample on this host.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "mm-pde_amd"))
+
+import torch  # noqa: E402
+
+METRIC = "MM-PDE rollout node-updates/sec, cylinder 2521-node mesh, 1/2/4/8 GPUs"
+F32_MFMA_PEAK_TFLOPS = 157.3          # MI355X_MICROARCH.md: dense fp32 matrix peak
+HBM_PEAK_GBS = 8000.0
+CONFIGS = {
+    # name: (kind, moving_mesh, default trajectories per GPU, BASELINE.json config)
+    "cy-mmpde": ("cy", True, 16, "configs[3]: Cylinder MM-PDE, batch=16"),
+    "cy-gnn": ("cy", False, 8, "configs[2]: Cylinder GNN, batch=8"),
+    "burgers-mmpde": ("burgers", True, 32, "configs[1]: Burgers' MM-PDE, batch=32"),
+    "burgers-gnn": ("burgers", False, 1, "configs[0]: Burgers' GNN, batch=1"),
+}
+
+
+class HipEvents:
+    """hipEvent pool through libamdhip64 (the events are recorded by the C-ABI on
+    the stream the edge kernel is launched on)."""
+
+    def __init__(self, count):
+        self.h = ctypes.CDLL("libamdhip64.so")
+        self.h.hipEventCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+        self.h.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p,
+                                               ctypes.c_void_p]
+        self.h.hipEventDestroy.argtypes = [ctypes.c_void_p]
+        self.ev = []
+        for _ in range(count):
+            e = ctypes.c_void_p()
+            if self.h.hipEventCreate(ctypes.byref(e)) != 0:
+                raise RuntimeError("hipEventCreate failed")
+            self.ev.append(e.value)
+
+    def elapsed_ms(self, a, b):
+        ms = ctypes.c_float()
+        if self.h.hipEventElapsedTime(ctypes.byref(ms), a, b) != 0:
+            raise RuntimeError("hipEventElapsedTime failed")
+        return ms.value
+
+    def close(self):
+        for e in self.ev:
+            self.h.hipEventDestroy(e)
+
+
+class EdgeTracer:
+    """Hands out one GnnTrace (n_layers begin/end events) per GNN forward."""
+
+    def __init__(self, n_forwards, n_layers=6):
+        from mmpde_amd import _lib
+
+        self.L = n_layers
+        self.pool = HipEvents(2 * n_forwards * n_layers)
+        self.used = 0
+        self.traces = []
+        self._lib = _lib
+        self.active = False
+
+    def __call__(self):
+        if not self.active:
+            return None
+        i = self.used
+        self.used += 1
+        base = 2 * self.L * i
+        beg = (ctypes.c_void_p * self.L)(*self.pool.ev[base:base + self.L])
+        end = (ctypes.c_void_p * self.L)(*self.pool.ev[base + self.L:base + 2 * self.L])
+        t = self._lib.GnnTrace(ctypes.cast(beg, ctypes.POINTER(ctypes.c_void_p)),
+                               ctypes.cast(end, ctypes.POINTER(ctypes.c_void_p)))
+        self.traces.append((t, beg, end))
+        return t
+
+    def launch_times_ms(self):
+        out = []
+        for _, beg, end in self.traces:
+            for a, b in zip(beg, end):
+                out.append(self.pool.elapsed_ms(a, b))
+        return out
+
+
+def cpu_baseline(kind, moving_mesh, seconds):
+    """The CPU oracle (op-for-op restatement of the reference forward, unfused,
+    brute-force kNN) on a bounded sample: 2 trajectories, repeated one-step
+    forwards until `seconds` of work (>= 1 step)."""
+    sys.path.insert(0, ROOT)
+    from mmpde_amd.synth import build_models, burgers_grid_points, fields
+    from oracle import refcpu
+
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    torch.set_num_threads(cores)
+    B = 2
+    pde, model, model_b, itp, dmm, gc = build_models(kind, moving_mesh=moving_mesh)
+    if kind == "cy":
+        grid = pde.ori_grid
+        u = fields(grid, B, 30)
+        opde = refcpu.PDEConst("cy", [30, grid.shape[0]], ori_grid=grid)
+        n_nodes = grid.shape[0]
+    else:
+        u = fields(burgers_grid_points(), B, 31).reshape(B, 31, 48, 48)
+        opde = refcpu.PDEConst("burgers", [31, 48, 48])
+        n_nodes = 48 * 48
+    sds = {k: {n: t.detach() for n, t in m.state_dict().items()}
+           for k, m in (("model", model), ("model_b", model_b), ("itp", itp), ("dmm", dmm))
+           if m is not None}
+    steps, t0 = 0, time.perf_counter()
+    data = u[:, 0:1]
+    while True:
+        s = 1 + steps % 29
+        pred, _ = refcpu.mmpde_step(opde, sds, data, data, [s] * B, moving_mesh=moving_mesh)
+        data = pred.reshape(data.shape)
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": B * n_nodes * steps / el, "unit": "node-updates/s", "cores": cores,
+            "kind": "port",
+            "sample": f"oracle/refcpu.py, {B} trajectories x {steps} autoregressive steps "
+                      f"({el:.1f} s, torch CPU fp32, {cores} threads)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="cy-mmpde", choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=None, help="trajectories per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    from mmpde_amd import dist as D
+    from mmpde_amd.rollout import MMPDERollout
+    from mmpde_amd.synth import build_models, burgers_grid_points, fields
+
+    rank, local, world = D.init()
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    device = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(device)
+    kind, moving, b_default, cfg_name = CONFIGS[args.config]
+    B = args.batch or b_default
+    total = B * world
+    lo, hi = D.shard_range(total, rank, world)
+
+    pde, model, model_b, itp, dmm, gc = build_models(kind, moving_mesh=moving)
+    for m in (model, model_b, itp, dmm):
+        if m is not None:
+            m.to(device)
+    if kind == "cy":
+        pts, t_len = pde.ori_grid, 30
+        u_all = fields(pts, total, t_len)[lo:hi]
+    else:
+        pts, t_len = burgers_grid_points(), 31
+        u_all = fields(pts, total, t_len).reshape(total, t_len, 48, 48)[lo:hi]
+    n_nodes = pts.shape[0]
+    eng = MMPDERollout(kind, model, model_b, itp, dmm, gc, hi - lo, device, moving_mesh=moving)
+    n_gnn = 2 if moving else 1
+    tracer = EdgeTracer(n_forwards=n_gnn * args.steps)
+    eng.trace_hook = tracer
+    u = u_all[:, 0].to(device).contiguous()
+    n_t = t_len - 1
+
+    with torch.no_grad():
+        for i in range(args.warmup):
+            u = eng.step(u, 1 + i % n_t)
+        torch.cuda.synchronize(device)
+        D.barrier(device)
+        tracer.active = True
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            u = eng.step(u, 1 + (args.warmup + i) % n_t)
+        torch.cuda.synchronize(device)
+        D.barrier(device)
+        t1 = time.perf_counter()
+        tracer.active = False
+    local_s = t1 - t0
+    elapsed = D.max_over_ranks(local_s, device)
+    finite = bool(torch.isfinite(u).all())
+    launches = tracer.launch_times_ms()
+    edge_ms = sum(launches) / max(len(launches), 1)
+    tracer.pool.close()
+
+    if rank != 0:
+        return
+    n_local = (hi - lo) * n_nodes
+    flop_per_launch = n_local * gc.n * 2 * 128 * 128      # per target: k edges x 128x128 GEMV
+    achieved = flop_per_launch / (edge_ms * 1e-3) / 1e12
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "edge_pmc_r01.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            rec = json.load(f)
+        if rec.get("workload") == args.config and rec.get("nodes") == n_local:
+            traffic = rec.get("hbm_bytes_per_launch")
+    line = {
+        "metric": METRIC if kind == "cy" else METRIC.replace("cylinder 2521-node mesh",
+                                                             "Burgers 48x48 grid"),
+        "value": total * n_nodes * args.steps / elapsed,
+        "unit": "node-updates/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: seeded cy-synth 2521-node mesh / 48x48 grid, seeded sin-cos+noise "
+                "fields, seeded default-init weights (no dataset or checkpoint offline)",
+        "config": {"workload": args.config, "baseline_config": cfg_name,
+                   "trajectories_per_gpu": B, "global_trajectories": total,
+                   "nodes_per_trajectory": n_nodes, "neighbors": gc.n, "time_window": 1,
+                   "parallelism": f"trajectory-shard x{world} (no data-path collective)",
+                   "rollout": "autoregressive (pred -> next input)"},
+        "roofline": {"kernel": "edge_mean_kernel (GNN message_net_2 + mean, 12 launches/step)",
+                     "bound": "mfma", "achieved": achieved, "peak": F32_MFMA_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": achieved / F32_MFMA_PEAK_TFLOPS,
+                     "traffic": traffic, "launch_ms": edge_ms, "launches": len(launches),
+                     "flop_per_launch": flop_per_launch},
+        "finite": finite,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(kind, moving, args.cpu_seconds)
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,265 @@
+/*
+ * mmpde_hip.h -- C-ABI of libmmpde_hip.so, the MI355X (gfx950) kernels behind
+ * the MM-PDE forward step.
+ *
+ * The reference (Peiyannn/MM-PDE) is pure Python and has no FFI: its hot path
+ * calls PyG / torch_scatter / torch_cluster / scikit-learn / cuBLAS from
+ * Python.  Each entry point below replaces one of those call sites (cited
+ * per function as reference file:line); the Python host mirror in
+ * mm-pde_amd/mmpde_amd binds them with ctypes.
+ *
+ * Conventions (all entry points):
+ *  - every tensor is a caller-owned, contiguous, row-major DEVICE buffer;
+ *    fp32 for features / coordinates, int32 for neighbour tables;
+ *  - node rows are trajectory-major: row = b * n_per + p;
+ *  - `stream` is a hipStream_t; every call is asynchronous and stream-ordered,
+ *    never allocates, never synchronises (safe inside hipGraph capture);
+ *  - the return value is a status: 0 ok, < 0 error (see MMPDE_ERR_*);
+ *    hipError_t e from a launch is returned as MMPDE_ERR_HIP_BASE - e;
+ *  - calls are stateless and re-entrant (no global mutable state).
+ */
+#ifndef MMPDE_HIP_H
+#define MMPDE_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MMPDE_OK 0
+#define MMPDE_ERR_INVALID_ARG (-1)
+#define MMPDE_ERR_UNSUPPORTED (-2)
+#define MMPDE_ERR_HIP_BASE (-1000)
+
+#define MMPDE_ACT_NONE 0
+#define MMPDE_ACT_TANH 1
+#define MMPDE_ACT_RELU 2
+
+typedef void *mmpde_stream_t; /* hipStream_t */
+
+/* ABI version: major*10000 + minor*100 + patch */
+int mmpde_version(void);
+/* Static description of a status code (never NULL). */
+const char *mmpde_status_string(int status);
+
+/* ------------------------------------------------------------------------
+ * Neighbour search
+ * ---------------------------------------------------------------------- */
+
+/* torch_cluster.knn_graph(x, k, batch, loop=False) for `batches` equal,
+ * contiguous segments of n_per points.  Replaces reference
+ * data_creator_2d.py:260 and mesh/dmm_model.py:228.
+ * pos      [batches*n_per, 2] fp32
+ * nbr_out  [batches*n_per, k] int32: GLOBAL source index of the e-th nearest
+ *          neighbour of each query, e ordered by (d2, index), d2 =
+ *          fmaf(dy, dy, dx*dx); self excluded.  PyG edge_index is
+ *          [nbr_out.flatten(), repeat_interleave(arange(n), k)].
+ * degenerate (nullable, device int32[1], accumulated): queries whose degree
+ *          would be ragged in the reference (self not among the k+1 nearest).
+ * Requires k+1 <= n_per <= 4096, k <= 63. */
+int mmpde_knn_graph(const float *pos, int64_t batches, int64_t n_per, int k,
+                    int32_t *nbr_out, int32_t *degenerate, mmpde_stream_t stream);
+
+/* sklearn NearestNeighbors(n_neighbors=k).fit(src_b).kneighbors(qry_b) per
+ * trajectory b (reference data_creator_2d.py:66-78).  Distances in fp64
+ * (dx*dx + dy*dy), ascending, ties by index.
+ * src [batches*n_src, 2], qry [batches*n_qry, 2] fp32
+ * idx_out [batches*n_qry, k] int32 LOCAL source index (0..n_src-1).
+ * Requires k <= n_src <= 4096, k <= 63. */
+int mmpde_knn_query(const float *src, const float *qry, int64_t batches, int64_t n_src,
+                    int64_t n_qry, int k, int32_t *idx_out, mmpde_stream_t stream);
+
+/* PyG edge_index (int64 [2, n*k]) from a target-major neighbour table.
+ * Row 0 = source (nbr), row 1 = target. (data_creator_2d.py:260-262) */
+int mmpde_edge_index_from_nbr(const int32_t *nbr, int64_t n, int k, int64_t *edge_index,
+                              mmpde_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * Dense helpers
+ * ---------------------------------------------------------------------- */
+
+/* y[m, n] = act(x[m, k] . w[n, k]^T + b[n]) for skinny m (<= 4096 rows, tuned
+ * for m <= 32): res_cut MLP (interpolate.py:74-82), DMM output_mlp / fc
+ * layers (mesh/dmm_model.py:59-60, 175-181).  ldx / ldw / ldy are row strides
+ * in elements; b nullable. */
+int mmpde_linear_skinny(const float *x, int64_t ldx, int64_t m, int64_t k, const float *w,
+                        int64_t ldw, const float *b, int64_t n, int act, float *y,
+                        int64_t ldy, mmpde_stream_t stream);
+
+/* Direct 2-D convolution, NCHW fp32, square kernel ks, zero padding pad,
+ * stride 1 or 2, fused act(conv + bias [+ residual]).  residual nullable,
+ * same shape as the output.  ConvNet branch (mesh/dmm_model.py:53-57,65-81)
+ * and burgers res_cut (interpolate.py:63-72). */
+int mmpde_conv2d(const float *x, int64_t batches, int cin, int h, int w, const float *weight,
+                 const float *bias, int cout, int ks, int stride, int pad,
+                 const float *residual, int act, float *y, mmpde_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * MP_PDE_Solver_2D (reference gnn_2d.py:19-141), hidden width 128, tw = 1.
+ * Node inputs: u [n] fp32 (data.x), pos [n, 3] fp32 = (t, x, y) (data.pos).
+ * ---------------------------------------------------------------------- */
+typedef struct {
+    float inv_lx, inv_ly, inv_tmax; /* 1/pde.Lx, 1/pde.Ly, 1/pde.tmax (gnn_2d.py:122-124) */
+} mmpde_gnn_scales;
+
+typedef struct {
+    /* embedding_mlp: Linear(4,128) BN ReLU Linear(128,128) BN (gnn_2d.py:99-106) */
+    const float *w0, *b0;                 /* [128,4], [128]   */
+    const float *bn1_w, *bn1_b, *bn1_rm, *bn1_rv;
+    const float *w3, *b3;                 /* [128,128], [128] */
+    const float *bn4_w, *bn4_b, *bn4_rm, *bn4_rv;
+    float eps;
+} mmpde_gnn_embed_params;
+
+typedef struct {
+    /* GNN_Layer_FS_2D (gnn_2d.py:30-69).  msg1_w is the reference
+     * message_net_1.0.weight [128, 260] (columns: h_i | h_j | du | dx | dy | t_i);
+     * upd1_w is update_net_1.0.weight [128, 257] (h | mean | t). */
+    const float *msg1_w, *msg1_b, *msg2_w, *msg2_b;
+    const float *upd1_w, *upd1_b, *upd2_w, *upd2_b;
+    const float *bn_w, *bn_b, *bn_rm, *bn_rv; /* norm.module.* */
+    float eps;
+    /* Row strides (elements) of msg1_w / upd1_w: multiples of 4 and >= 260 /
+     * 257.  The reference message_net_1 weight is usable as-is (ld 260);
+     * update_net_1's [128, 257] needs a copy padded to ld 260 so rows stay
+     * 16-B aligned for dwordx4 loads (the host mirror keeps one). */
+    int64_t msg1_ld, upd1_ld;
+} mmpde_gnn_layer_params;
+
+typedef struct {
+    /* output_mlp Conv1d(1,4,16,s3) ReLU Conv1d(4,8,12,s3) ReLU Conv1d(8,1,8,s2)
+     * (gnn_2d.py:108-114) */
+    const float *c0_w, *c0_b, *c2_w, *c2_b, *c4_w, *c4_b;
+    float out_scale; /* cumsum(ones(1,tw) * pde.dt * 0.1) for tw = 1 (gnn_2d.py:137-139) */
+} mmpde_gnn_head_params;
+
+/* Bytes of device workspace mmpde_gnn_forward needs for n nodes. */
+int64_t mmpde_gnn_workspace_bytes(int64_t n);
+
+/* h_out[n,128] = embedding_mlp(cat(u, x/Lx, y/Ly, t/tmax)) */
+int mmpde_gnn_embed(const float *u, const float *pos, int64_t n, mmpde_gnn_scales sc,
+                    const mmpde_gnn_embed_params *p, float *workspace, float *h_out,
+                    mmpde_stream_t stream);
+
+/* One message-passing layer: h_out = BN(h + upd(h, mean_j msg(h_i, h_j, ...))).
+ * nbr [n, k] int32 target-major (global source indices), fixed degree k
+ * (PyG aggr='mean' over the k in-edges).  workspace >= 4*n*128 floats.
+ * h_out must not alias h_in. */
+int mmpde_gnn_layer(const float *h_in, const float *u, const float *pos, int64_t n, int k,
+                    const int32_t *nbr, mmpde_gnn_scales sc, const mmpde_gnn_layer_params *p,
+                    float *workspace, float *h_out, mmpde_stream_t stream);
+
+/* Only the edge stage: mean[i] = (1/k) sum_e relu(W2 relu(a[i] + b[nbr[i,e]]) + b2)
+ * with a, b the per-node halves of message_net_1 ([n,128] each). */
+int mmpde_gnn_edge_mean(const float *a, const float *b, const int32_t *nbr, int64_t n, int k,
+                        const float *msg2_w, const float *msg2_b, float *mean_out,
+                        mmpde_stream_t stream);
+
+/* out[n] = out_scale * output_mlp(h[:, None]) */
+int mmpde_gnn_head(const float *h, int64_t n, const mmpde_gnn_head_params *p, float *out,
+                   mmpde_stream_t stream);
+
+/* Whole MP_PDE_Solver_2D.forward (gnn_2d.py:119-141): embed, n_layers layers,
+ * head.  layers: array of n_layers parameter blocks.  workspace >=
+ * mmpde_gnn_workspace_bytes(n). */
+int mmpde_gnn_forward(const float *u, const float *pos, int64_t n, int k, const int32_t *nbr,
+                      mmpde_gnn_scales sc, const mmpde_gnn_embed_params *emb,
+                      const mmpde_gnn_layer_params *layers, int n_layers,
+                      const mmpde_gnn_head_params *head, void *workspace, float *out,
+                      mmpde_stream_t stream);
+
+/* Same as mmpde_gnn_forward, plus optional instrumentation: when `trace` is
+ * non-NULL, hipEventRecord(trace->edge_begin[l]) / (trace->edge_end[l]) are
+ * issued on `stream` immediately before / after layer l's edge-stage kernel
+ * (the dominant kernel), so a caller can time exactly that launch. */
+typedef struct {
+    void *const *edge_begin; /* n_layers hipEvent_t */
+    void *const *edge_end;   /* n_layers hipEvent_t */
+} mmpde_gnn_trace;
+
+int mmpde_gnn_forward_ex(const float *u, const float *pos, int64_t n, int k, const int32_t *nbr,
+                         mmpde_gnn_scales sc, const mmpde_gnn_embed_params *emb,
+                         const mmpde_gnn_layer_params *layers, int n_layers,
+                         const mmpde_gnn_head_params *head, void *workspace, float *out,
+                         const mmpde_gnn_trace *trace, mmpde_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * DMM mesh mover (reference mesh/dmm_model.py, data_creator_2d.py:88-137)
+ * ---------------------------------------------------------------------- */
+typedef struct {
+    /* tiny GNN branch, hidden h = 4, 3 layers (dmm_model.py:154-173) */
+    const float *emb0_w, *emb0_b, *emb1_w, *emb1_b, *emb1_rm, *emb1_rv;
+    const float *emb3_w, *emb3_b, *emb4_w, *emb4_b, *emb4_rm, *emb4_rv;
+    const float *g_msg1_w[3], *g_msg1_b[3], *g_msg2_w[3], *g_msg2_b[3];
+    const float *g_upd1_w[3], *g_upd1_b[3], *g_upd2_w[3], *g_upd2_b[3];
+    const float *g_bn_w[3], *g_bn_b[3], *g_bn_rm[3], *g_bn_rv[3];
+    int n_gnn_layers;
+    const float *dec0_w, *dec0_b, *dec1_w, *dec1_b; /* decoding_mlp DenseNet[4,128,1] */
+    const float *om0_w, *om0_b, *om2_w, *om2_b, *om4_w, *om4_b; /* output_mlp N->512->256->512 */
+    float eps;
+} mmpde_dmm_graph_branch;
+
+typedef struct {
+    /* ConvNet(s, 7) branch (dmm_model.py:48-81) */
+    const float *c0_w, *c0_b, *c1_w, *c1_b, *c2_w, *c2_b, *c3_w, *c3_b;
+    const float *fc2_w, *fc2_b, *fc3_w, *fc3_b;
+    int s;
+} mmpde_dmm_array_branch;
+
+typedef struct {
+    /* trunk DenseNet [2, th, L] and out_nn DenseNet [2L, L', 1] */
+    const float *t0_w, *t0_b; /* [th, 2] */
+    const float *t1_w, *t1_b; /* [L, th] */
+    int th, latent;           /* th <= 64, latent = L (branch width) */
+    const float *o0_w, *o0_b; /* [L', 2L] */
+    const float *o1_w;        /* [1, L']  (its bias does not reach d(phi)/d(xi)) */
+    int hidden;               /* L' */
+} mmpde_dmm_head;
+
+/* Workspace bytes for mmpde_dmm_mesh_* with B trajectories of N points. */
+int64_t mmpde_dmm_workspace_bytes(int64_t batches, int64_t n_per, int latent, int hidden);
+
+/* x = xi + d(phi)/d(xi), phi = DMM(u, xi), graph mode (cylinder).
+ * Replaces moving_mesh_tri (data_creator_2d.py:115-137) incl. the two
+ * autograd.grad calls, by an analytic VJP.
+ * u [B, N]; grid [N, 2] = pde.ori_grid (= xi for every trajectory);
+ * grid_nbr [N, 35] int32 LOCAL kNN-35 table of the fixed grid
+ * (dmm_model.py:222-234, built once with mmpde_knn_graph(batches=1));
+ * mesh_out [B*N, 2]. */
+int mmpde_dmm_mesh_graph(const float *u, const float *grid, int64_t batches, int64_t n_per,
+                         const int32_t *grid_nbr, int k, const mmpde_dmm_graph_branch *br,
+                         const mmpde_dmm_head *hd, void *workspace, float *mesh_out,
+                         mmpde_stream_t stream);
+
+/* Array mode (Burgers): u [B, s, s]; xi [N, 2] (np.meshgrid xy order,
+ * data_creator_2d.py:94-100), N = s*s. */
+int mmpde_dmm_mesh_array(const float *u, const float *xi, int64_t batches, int64_t n_per,
+                         const mmpde_dmm_array_branch *br, const mmpde_dmm_head *hd,
+                         void *workspace, float *mesh_out, mmpde_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * ItpNet interpolation (reference interpolate.py:77-93 + data_creator_2d.py:80-83)
+ * ---------------------------------------------------------------------- */
+typedef struct {
+    /* Linear(62,128) tanh Linear(128,64) tanh Linear(64,30): ItpNet.layers
+     * (mode '1') or ItpNet.layers2 (mode '2') */
+    const float *w0, *b0, *w1, *b1, *w2, *b2;
+} mmpde_itp_mlp;
+
+/* Bytes of the packed weight image mmpde_itp_pack writes. */
+int64_t mmpde_itp_pack_bytes(void);
+/* Re-lay the MLP weights into the MFMA operand image used by mmpde_itp_interp. */
+int mmpde_itp_pack(const mmpde_itp_mlp *mlp, void *packed, mmpde_stream_t stream);
+
+/* out[b*Nq+q] = sum_e ItpNet(nbrs, q)[e] * vals[b*Ns + idx[q,e]] (+ addend).
+ * src [B*Ns,2], vals [B*Ns], qry [B*Nq,2], idx [B*Nq,30] LOCAL (from
+ * mmpde_knn_query with k = 30); addend nullable [B*Nq]. */
+int mmpde_itp_interp(const float *src, const float *vals, const float *qry, const int32_t *idx,
+                     int64_t batches, int64_t n_src, int64_t n_qry, const void *packed,
+                     const float *addend, float *out, mmpde_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MMPDE_HIP_H */

@@ -1,0 +1,52 @@
+// Shared device helpers for libmmpde_hip.so (gfx950 / CDNA4, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mmpde_hip.h"
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define MMPDE_RET_LAUNCH()                                   \
+    do {                                                     \
+        hipError_t e_ = hipGetLastError();                   \
+        if (e_ != hipSuccess) return MMPDE_ERR_HIP_BASE - (int)e_; \
+    } while (0)
+
+#define MMPDE_REQUIRE(cond)                          \
+    do {                                             \
+        if (!(cond)) return MMPDE_ERR_INVALID_ARG;   \
+    } while (0)
+
+static inline hipStream_t as_stream(mmpde_stream_t s) { return (hipStream_t)s; }
+
+// v_mfma_f32_32x32x2_f32: lane l supplies A[l&31][l>>5] and B[l>>5][l&31];
+// D[row][col] with col = l&31, row = (r&3) + 8*(r>>2) + 4*(l>>5) for register r.
+__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ int acc_row(int reg, int lane) {
+    return (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ float act_apply(float v, int act) {
+    if (act == MMPDE_ACT_TANH) return tanhf(v);
+    if (act == MMPDE_ACT_RELU) return fmaxf(v, 0.0f);
+    return v;
+}
+
+// Eval-mode BatchNorm1d on one channel value (torch: (x - rm) / sqrt(rv + eps) * w + b)
+__device__ __forceinline__ float bn_eval(float v, float rm, float rv, float w, float b,
+                                         float eps) {
+    return (v - rm) / sqrtf(rv + eps) * w + b;
+}
+
+static inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }

@@ -1,0 +1,442 @@
+// DMM mesh mover on gfx950: x = xi + d(phi)/d(xi) (reference
+// data_creator_2d.py:88-137, mesh/dmm_model.py:145-234).
+//
+// phi(b, n) = w_o . tanh(Wb . branch_b + Wt . trunk(xi_n) + b_o1) + b_o2, where
+// out_nn's first Linear(2L, L') acts on cat(branch, trunk) (dmm_model.py:190,213).
+// The branch depends only on the trajectory b, the trunk only on the grid point
+// n (xi is the same fixed grid for every trajectory), so
+//     z(b, n) = P[b] + Q[n],   P = Wb . branch + b_o1  [B, L'],  Q = Wt . trunk  [N, L']
+// and the two autograd.grad calls of the reference reduce to the analytic VJP
+//     d(phi)/d(xi)(b, n) = sum_k w_o[k] (1 - tanh^2 z_k) J[n, k, :],
+//     J[n] = (Wt T1) diag(1 - s_n^2) T0,  s_n = tanh(T0 xi_n + t0b)   [L', 2]
+// (trunk = DenseNet[2, th, L]: T0 [th, 2], T1 [L, th]).  Q and J are recomputed
+// every call from the weights (no cross-call caching).
+#include "common.hpp"
+#include "gemm.hpp"
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// Graph-mode branch (cylinder): embedding, 3 tiny GNN layers (h = 4, tanh),
+// decoding DenseNet[4,128,1].  One thread per node; the trajectory's nodes use
+// the fixed grid's LOCAL neighbour table (same for every trajectory,
+// dmm_model.py:222-234).
+// ---------------------------------------------------------------------------
+struct DmmEmbW {
+    float w0[12], b0[4], bn1[16], w3[16], b3[4], bn4[16];  // bn: w, b, rm, rv
+};
+
+__global__ __launch_bounds__(256) void dmm_embed_kernel(const float *__restrict__ u,
+                                                        const float2 *__restrict__ grid,
+                                                        int64_t n_tot, int64_t n_per,
+                                                        mmpde_dmm_graph_branch p,
+                                                        float4 *__restrict__ h) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n_tot) return;
+    const float2 g = grid[i % n_per];
+    const float in[3] = {u[i], g.x, g.y};  // cat(x, pos_x, pos_y), dmm_model.py:205
+    float z[4], o[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        float v = p.emb0_b[c];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) v += p.emb0_w[c * 3 + j] * in[j];
+        z[c] = tanhf(bn_eval(v, p.emb1_rm[c], p.emb1_rv[c], p.emb1_w[c], p.emb1_b[c], p.eps));
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        float v = p.emb3_b[c];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v += p.emb3_w[c * 4 + j] * z[j];
+        o[c] = bn_eval(v, p.emb4_rm[c], p.emb4_rv[c], p.emb4_w[c], p.emb4_b[c], p.eps);
+    }
+    h[i] = make_float4(o[0], o[1], o[2], o[3]);
+}
+
+// DMM GNN_Layer_FS_2D (dmm_model.py:94-142): message cat(x_i, x_j, u_i-u_j,
+// px_i-px_j, py_i-py_j) (11) -> 4 tanh -> 4 tanh; mean; update cat(x, m) (8) ->
+// 4 tanh -> 4 tanh; x + upd; BN.
+__global__ __launch_bounds__(256) void dmm_gnn_kernel(const float4 *__restrict__ h,
+                                                      const float *__restrict__ u,
+                                                      const float2 *__restrict__ grid,
+                                                      const int32_t *__restrict__ nbr, int k,
+                                                      int64_t n_tot, int64_t n_per,
+                                                      const float *__restrict__ w1,
+                                                      const float *__restrict__ b1,
+                                                      const float *__restrict__ w2,
+                                                      const float *__restrict__ b2,
+                                                      const float *__restrict__ v1,
+                                                      const float *__restrict__ c1,
+                                                      const float *__restrict__ v2,
+                                                      const float *__restrict__ c2,
+                                                      const float *__restrict__ bnw,
+                                                      const float *__restrict__ bnb,
+                                                      const float *__restrict__ bnrm,
+                                                      const float *__restrict__ bnrv, float eps,
+                                                      float4 *__restrict__ h_out) {
+    __shared__ float sW1[44], sB1[4], sW2[16], sB2[4], sV1[32], sC1[4], sV2[16], sC2[4];
+    if (threadIdx.x < 44) sW1[threadIdx.x] = w1[threadIdx.x];
+    if (threadIdx.x < 16) {
+        sW2[threadIdx.x] = w2[threadIdx.x];
+        sV2[threadIdx.x] = v2[threadIdx.x];
+    }
+    if (threadIdx.x < 32) sV1[threadIdx.x] = v1[threadIdx.x];
+    if (threadIdx.x < 4) {
+        sB1[threadIdx.x] = b1[threadIdx.x];
+        sB2[threadIdx.x] = b2[threadIdx.x];
+        sC1[threadIdx.x] = c1[threadIdx.x];
+        sC2[threadIdx.x] = c2[threadIdx.x];
+    }
+    __syncthreads();
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n_tot) return;
+    const int64_t b = i / n_per;
+    const int64_t p = i - b * n_per;
+    const float4 hi4 = h[i];
+    const float hi[4] = {hi4.x, hi4.y, hi4.z, hi4.w};
+    const float ui = u[i];
+    const float2 gi = grid[p];
+    float sum[4] = {0.f, 0.f, 0.f, 0.f};
+    const int32_t *nr = nbr + p * k;
+    for (int e = 0; e < k; ++e) {
+        const int64_t jl = min((uint32_t)nr[e], (uint32_t)(n_per - 1));
+        const int64_t j = b * n_per + jl;
+        const float4 hj4 = h[j];
+        const float2 gj = grid[jl];
+        const float in[11] = {hi[0], hi[1], hi[2], hi[3], hj4.x, hj4.y, hj4.z, hj4.w,
+                              ui - u[j], gi.x - gj.x, gi.y - gj.y};
+        float m1[4];
+#pragma unroll
+        for (int o = 0; o < 4; ++o) {
+            float v = sB1[o];
+#pragma unroll
+            for (int t = 0; t < 11; ++t) v += sW1[o * 11 + t] * in[t];
+            m1[o] = tanhf(v);
+        }
+#pragma unroll
+        for (int o = 0; o < 4; ++o) {
+            float v = sB2[o];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) v += sW2[o * 4 + t] * m1[t];
+            sum[o] += tanhf(v);
+        }
+    }
+    float cat[8];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+        cat[o] = hi[o];
+        cat[4 + o] = sum[o] / (float)k;
+    }
+    float up1[4], res[4];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+        float v = sC1[o];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v += sV1[o * 8 + t] * cat[t];
+        up1[o] = tanhf(v);
+    }
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+        float v = sC2[o];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) v += sV2[o * 4 + t] * up1[t];
+        res[o] = bn_eval(hi[o] + tanhf(v), bnrm[o], bnrv[o], bnw[o], bnb[o], eps);
+    }
+    h_out[i] = make_float4(res[0], res[1], res[2], res[3]);
+}
+
+// decoding_mlp DenseNet([4, 128, 1]) (dmm_model.py:173,209): d = W1 tanh(W0 h + b0) + b1
+__global__ __launch_bounds__(256) void dmm_decode_kernel(const float4 *__restrict__ h,
+                                                         int64_t n_tot,
+                                                         const float *__restrict__ w0,
+                                                         const float *__restrict__ b0,
+                                                         const float *__restrict__ w1,
+                                                         const float *__restrict__ b1,
+                                                         float *__restrict__ out) {
+    __shared__ float sW0[512], sB0[128], sW1[128];
+    for (int t = threadIdx.x; t < 512; t += 256) sW0[t] = w0[t];
+    if (threadIdx.x < 128) {
+        sB0[threadIdx.x] = b0[threadIdx.x];
+        sW1[threadIdx.x] = w1[threadIdx.x];
+    }
+    __syncthreads();
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n_tot) return;
+    const float4 hv = h[i];
+    float acc = 0.0f;
+    for (int j = 0; j < 128; ++j) {
+        const float z = tanhf(sB0[j] + sW0[4 * j] * hv.x + sW0[4 * j + 1] * hv.y +
+                              sW0[4 * j + 2] * hv.z + sW0[4 * j + 3] * hv.w);
+        acc += sW1[j] * z;
+    }
+    out[i] = acc + b1[0];
+}
+
+// ---------------------------------------------------------------------------
+// Shared head: trunk, Q, J and the mesh VJP.
+// ---------------------------------------------------------------------------
+// trunk hidden s = tanh(T0 xi + t0b) ([N, th]) and trunk = T1 s + t1b ([N, L]); one
+// block per grid point.
+__global__ __launch_bounds__(256) void trunk_kernel(const float2 *__restrict__ xi, int th,
+                                                    int latent, const float *__restrict__ t0w,
+                                                    const float *__restrict__ t0b,
+                                                    const float *__restrict__ t1w,
+                                                    const float *__restrict__ t1b,
+                                                    float *__restrict__ s_out,
+                                                    float *__restrict__ trunk) {
+    __shared__ float s[64];
+    const int64_t nidx = blockIdx.x;
+    const float2 x = xi[nidx];
+    if (threadIdx.x < th) {
+        const float v = tanhf(t0w[threadIdx.x * 2] * x.x + t0w[threadIdx.x * 2 + 1] * x.y +
+                              t0b[threadIdx.x]);
+        s[threadIdx.x] = v;
+        s_out[nidx * th + threadIdx.x] = v;
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < latent; j += 256) {
+        float v = t1b[j];
+        for (int m = 0; m < th; ++m) v += t1w[(int64_t)j * th + m] * s[m];
+        trunk[nidx * latent + j] = v;
+    }
+}
+
+// out[c][r] = in[r][c] (rows x cols -> cols x rows)
+__global__ void transpose_kernel(const float *__restrict__ in, int rows, int cols,
+                                 float *__restrict__ out) {
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= rows * cols) return;
+    const int r = e / cols, c = e - r * cols;
+    out[(int64_t)c * rows + r] = in[e];
+}
+
+// J[n][k][d] = sum_m Gt[m][k] (1 - s[n][m]^2) T0[m][d]; one block per grid point.
+__global__ __launch_bounds__(256) void jac_kernel(const float *__restrict__ s, int th,
+                                                  const float *__restrict__ gt, int hidden,
+                                                  const float *__restrict__ t0w,
+                                                  float2 *__restrict__ jac) {
+    __shared__ float a0[64], a1[64];
+    const int64_t nidx = blockIdx.x;
+    if (threadIdx.x < th) {
+        const float sv = s[nidx * th + threadIdx.x];
+        const float ds = 1.0f - sv * sv;
+        a0[threadIdx.x] = ds * t0w[threadIdx.x * 2];
+        a1[threadIdx.x] = ds * t0w[threadIdx.x * 2 + 1];
+    }
+    __syncthreads();
+    for (int kk = threadIdx.x; kk < hidden; kk += 256) {
+        float j0 = 0.0f, j1 = 0.0f;
+        for (int m = 0; m < th; ++m) {
+            const float g = gt[(int64_t)m * hidden + kk];
+            j0 += g * a0[m];
+            j1 += g * a1[m];
+        }
+        jac[nidx * hidden + kk] = make_float2(j0, j1);
+    }
+}
+
+// mesh[b*N + n] = xi[n] + sum_k w_o[k] (1 - tanh^2(P[b,k] + Q[n,k])) J[n,k]; one wave
+// per grid point, looping over trajectories.
+__global__ __launch_bounds__(256) void mesh_vjp_kernel(const float *__restrict__ P,
+                                                       const float *__restrict__ Q,
+                                                       const float2 *__restrict__ jac,
+                                                       const float *__restrict__ wo,
+                                                       const float2 *__restrict__ xi,
+                                                       int64_t batches, int64_t n_per,
+                                                       int hidden, float2 *__restrict__ mesh) {
+    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int64_t nidx = (int64_t)blockIdx.x * 4 + wave;
+    if (nidx >= n_per) return;
+    const float *q = Q + nidx * hidden;
+    const float2 *jr = jac + nidx * hidden;
+    const float2 x = xi[nidx];
+    for (int64_t b = 0; b < batches; ++b) {
+        const float *pb = P + b * hidden;
+        float gx = 0.0f, gy = 0.0f;
+        for (int kk = lane; kk < hidden; kk += 64) {
+            const float t = tanhf(pb[kk] + q[kk]);
+            const float g = wo[kk] * (1.0f - t * t);
+            const float2 jj = jr[kk];
+            gx += g * jj.x;
+            gy += g * jj.y;
+        }
+        gx = wave_sum(gx);
+        gy = wave_sum(gy);
+        if (lane == 0) mesh[b * n_per + nidx] = make_float2(gx + x.x, gy + x.y);
+    }
+}
+
+struct HeadWs {
+    float *trunk, *s, *q, *t1t, *gt, *p;
+    float2 *jac;
+};
+
+int64_t head_floats(int64_t batches, int64_t n_per, int latent, int hidden, int th) {
+    return n_per * latent + n_per * th + n_per * hidden + (int64_t)th * latent +
+           (int64_t)th * hidden + batches * hidden + 2 * n_per * hidden + 64;
+}
+
+HeadWs carve_head(float *ws, int64_t batches, int64_t n_per, int latent, int hidden, int th) {
+    HeadWs h;
+    auto take = [&](int64_t nf) {
+        float *p = ws;
+        ws += (nf + 3) & ~int64_t(3);  // keep 16-B alignment
+        return p;
+    };
+    h.trunk = take(n_per * latent);
+    h.s = take(n_per * th);
+    h.q = take(n_per * hidden);
+    h.t1t = take((int64_t)th * latent);
+    h.gt = take((int64_t)th * hidden);
+    h.p = take(batches * hidden);
+    h.jac = (float2 *)take(2 * n_per * hidden);
+    return h;
+}
+
+// branch [B, L] -> mesh [B*N, 2]
+int dmm_head(const float *branch, const float *xi, int64_t batches, int64_t n_per,
+             const mmpde_dmm_head *hd, float *ws, float *mesh_out, hipStream_t st) {
+    const int L = hd->latent, Lp = hd->hidden, th = hd->th;
+    if (th < 1 || th > 64 || L % 8 != 0 || Lp % 128 != 0) return MMPDE_ERR_UNSUPPORTED;
+    HeadWs w = carve_head(ws, batches, n_per, L, Lp, th);
+    int rc;
+    // P = Wb . branch + b_o1 (Wb = out_nn.layers.0.weight[:, :L], row stride 2L)
+    rc = mmpde_linear_skinny(branch, L, batches, L, hd->o0_w, 2 * L, hd->o0_b, Lp,
+                             MMPDE_ACT_NONE, w.p, Lp, st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(trunk_kernel, dim3((unsigned)n_per), dim3(256), 0, st,
+                       (const float2 *)xi, th, L, hd->t0_w, hd->t0_b, hd->t1_w, hd->t1_b, w.s,
+                       w.trunk);
+    MMPDE_RET_LAUNCH();
+    // Q = Wt . trunk (Wt = out_nn.layers.0.weight[:, L:2L]) on MFMA
+    {
+        const int kh = L / 2;
+        GemmArgs g{n_per, w.trunk, w.trunk + kh, L, hd->o0_w + L, hd->o0_w + L + kh, 2 * L, kh};
+        EpiStore epi{w.q, Lp};
+        rc = launch_gemm(g, Lp / 128, epi, st);
+        if (rc) return rc;
+    }
+    // Gt = (Wt . T1)^T = T1^T . Wt^T  ([th, L'])
+    hipLaunchKernelGGL(transpose_kernel, dim3(ceil_div((int64_t)L * th, 256)), dim3(256), 0, st,
+                       hd->t1_w, L, th, w.t1t);
+    MMPDE_RET_LAUNCH();
+    rc = mmpde_linear_skinny(w.t1t, L, th, L, hd->o0_w + L, 2 * L, nullptr, Lp, MMPDE_ACT_NONE,
+                             w.gt, Lp, st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(jac_kernel, dim3((unsigned)n_per), dim3(256), 0, st, w.s, th, w.gt, Lp,
+                       hd->t0_w, w.jac);
+    MMPDE_RET_LAUNCH();
+    hipLaunchKernelGGL(mesh_vjp_kernel, dim3(ceil_div(n_per, 4)), dim3(256), 0, st, w.p, w.q,
+                       w.jac, hd->o1_w, (const float2 *)xi, batches, n_per, Lp,
+                       (float2 *)mesh_out);
+    MMPDE_RET_LAUNCH();
+    return MMPDE_OK;
+}
+
+inline bool al16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
+
+}  // namespace
+
+extern "C" int64_t mmpde_dmm_workspace_bytes(int64_t batches, int64_t n_per, int latent,
+                                             int hidden) {
+    // branch-side scratch (graph: 2 h buffers + decode + MLP activations; array:
+    // conv activations), then the shared head region.
+    const int64_t branch_side = 2 * 4 * batches * n_per + batches * n_per + batches * 2048 +
+                                8 * batches * n_per + 256;
+    return (branch_side + head_floats(batches, n_per, latent, hidden, 64) + 256) *
+           (int64_t)sizeof(float);
+}
+
+extern "C" int mmpde_dmm_mesh_graph(const float *u, const float *grid, int64_t batches,
+                                    int64_t n_per, const int32_t *grid_nbr, int k,
+                                    const mmpde_dmm_graph_branch *br, const mmpde_dmm_head *hd,
+                                    void *workspace, float *mesh_out, mmpde_stream_t stream) {
+    MMPDE_REQUIRE(u && grid && grid_nbr && br && hd && workspace && mesh_out);
+    MMPDE_REQUIRE(batches > 0 && n_per > k && k > 0 && br->n_gnn_layers >= 0 &&
+                  br->n_gnn_layers <= 3 && al16(workspace));
+    hipStream_t st = as_stream(stream);
+    const int64_t nt = batches * n_per;
+    float *ws = (float *)workspace;
+    float4 *h0 = (float4 *)ws;
+    float4 *h1 = h0 + nt;
+    float *dec = (float *)(h1 + nt);
+    float *om1 = dec + ((nt + 3) & ~int64_t(3));
+    float *om2 = om1 + batches * 512;
+    float *branch = om2 + batches * 256;
+    float *head_ws = branch + ((batches * hd->latent + 3) & ~int64_t(3));
+    const dim3 g1(ceil_div(nt, 256));
+    hipLaunchKernelGGL(dmm_embed_kernel, g1, dim3(256), 0, st, u, (const float2 *)grid, nt, n_per,
+                       *br, h0);
+    MMPDE_RET_LAUNCH();
+    for (int l = 0; l < br->n_gnn_layers; ++l) {
+        hipLaunchKernelGGL(dmm_gnn_kernel, g1, dim3(256), 0, st, h0, u, (const float2 *)grid,
+                           grid_nbr, k, nt, n_per, br->g_msg1_w[l], br->g_msg1_b[l],
+                           br->g_msg2_w[l], br->g_msg2_b[l], br->g_upd1_w[l], br->g_upd1_b[l],
+                           br->g_upd2_w[l], br->g_upd2_b[l], br->g_bn_w[l], br->g_bn_b[l],
+                           br->g_bn_rm[l], br->g_bn_rv[l], br->eps, h1);
+        MMPDE_RET_LAUNCH();
+        float4 *t = h0;
+        h0 = h1;
+        h1 = t;
+    }
+    hipLaunchKernelGGL(dmm_decode_kernel, g1, dim3(256), 0, st, h0, nt, br->dec0_w, br->dec0_b,
+                       br->dec1_w, br->dec1_b, dec);
+    MMPDE_RET_LAUNCH();
+    // output_mlp: Linear(N,512) tanh Linear(512,256) tanh Linear(256,L) on [B, N]
+    int rc = mmpde_linear_skinny(dec, n_per, batches, n_per, br->om0_w, n_per, br->om0_b, 512,
+                                 MMPDE_ACT_TANH, om1, 512, stream);
+    if (rc) return rc;
+    rc = mmpde_linear_skinny(om1, 512, batches, 512, br->om2_w, 512, br->om2_b, 256,
+                             MMPDE_ACT_TANH, om2, 256, stream);
+    if (rc) return rc;
+    rc = mmpde_linear_skinny(om2, 256, batches, 256, br->om4_w, 256, br->om4_b, hd->latent,
+                             MMPDE_ACT_NONE, branch, hd->latent, stream);
+    if (rc) return rc;
+    return dmm_head(branch, grid, batches, n_per, hd, head_ws, mesh_out, st);
+}
+
+extern "C" int mmpde_dmm_mesh_array(const float *u, const float *xi, int64_t batches,
+                                    int64_t n_per, const mmpde_dmm_array_branch *br,
+                                    const mmpde_dmm_head *hd, void *workspace, float *mesh_out,
+                                    mmpde_stream_t stream) {
+    MMPDE_REQUIRE(u && xi && br && hd && workspace && mesh_out && batches > 0);
+    MMPDE_REQUIRE((int64_t)br->s * br->s == n_per && al16(workspace));
+    hipStream_t st = as_stream(stream);
+    const int s = br->s;
+    const int s1 = (s + 4 - 5) / 2 + 1;   // conv0, stride 2, pad 2
+    const int s3 = (s1 + 4 - 5) / 2 + 1;  // conv3, stride 2, pad 2
+    float *ws = (float *)workspace;
+    auto take = [&](int64_t nf) {
+        float *p = ws;
+        ws += (nf + 3) & ~int64_t(3);
+        return p;
+    };
+    float *x1 = take(batches * 8 * s1 * s1);
+    float *x2 = take(batches * 16 * s1 * s1);
+    float *x3 = take(batches * 8 * s1 * s1);
+    float *x4 = take(batches * s3 * s3);
+    float *f2 = take(batches * 1024);
+    float *branch = take(batches * hd->latent);
+    int rc;
+    // ConvNet.forward, dmm_model.py:65-81
+    rc = mmpde_conv2d(u, batches, 1, s, s, br->c0_w, br->c0_b, 8, 5, 2, 2, nullptr, MMPDE_ACT_TANH,
+                      x1, stream);
+    if (rc) return rc;
+    rc = mmpde_conv2d(x1, batches, 8, s1, s1, br->c1_w, br->c1_b, 16, 5, 1, 2, nullptr,
+                      MMPDE_ACT_TANH, x2, stream);
+    if (rc) return rc;
+    rc = mmpde_conv2d(x2, batches, 16, s1, s1, br->c2_w, br->c2_b, 8, 5, 1, 2, x1, MMPDE_ACT_TANH,
+                      x3, stream);
+    if (rc) return rc;
+    rc = mmpde_conv2d(x3, batches, 8, s1, s1, br->c3_w, br->c3_b, 1, 5, 2, 2, nullptr,
+                      MMPDE_ACT_TANH, x4, stream);
+    if (rc) return rc;
+    rc = mmpde_linear_skinny(x4, s3 * s3, batches, s3 * s3, br->fc2_w, s3 * s3, br->fc2_b, 1024,
+                             MMPDE_ACT_TANH, f2, 1024, stream);
+    if (rc) return rc;
+    rc = mmpde_linear_skinny(f2, 1024, batches, 1024, br->fc3_w, 1024, br->fc3_b, hd->latent,
+                             MMPDE_ACT_NONE, branch, hd->latent, stream);
+    if (rc) return rc;
+    return dmm_head(branch, xi, batches, n_per, hd, ws, mesh_out, st);
+}

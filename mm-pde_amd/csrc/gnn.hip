@@ -1,0 +1,424 @@
+// MP_PDE_Solver_2D forward on gfx950 (reference gnn_2d.py:19-141).
+//
+// Layout: node features are [n, 128] fp32 rows (512 B), trajectory-major.
+// Per message-passing layer (gnn_2d.py:53-69) we run
+//   1. node_gemm<EpiProj>  : a = W1[:, :128] h + (w_du u + w_dx x + w_dy y + w_t t + b1)
+//                            b = W1[:,128:256] h - (w_du u + w_dx x + w_dy y)
+//      -- message_net_1 factored exactly into a target half and a source half
+//         (its 260-wide input is cat(h_i, h_j, u_i-u_j, x_i-x_j, y_i-y_j, t_i));
+//   2. edge_mean_kernel    : mean_i = (1/k) sum_e relu(W2 relu(a_i + b_{nbr(i,e)}) + b2)
+//      -- the only per-edge work left: one 128x128 fp32 MFMA GEMM per edge,
+//         never materialised in HBM (PyG gather + scatter-mean replaced);
+//   3. node_gemm<EpiUpd1>  : v = relu(U1[:, :128] h + U1[:,128:256] mean + u1_t t + c1)
+//   4. node_gemm<EpiUpd2>  : h' = BN(h + relu(U2 v + c2))
+// All GEMMs use v_mfma_f32_32x32x2_f32 (exact fp32 products, fp32 accumulate).
+#include <vector>
+
+#include "common.hpp"
+#include "gemm.hpp"
+
+namespace {
+
+constexpr int H = 128;  // hidden width (gnn_2d.py:77)
+
+// ---------------------------------------------------------------------------
+// Embedding first half: z = relu(BN1(W0 [u, x/Lx, y/Ly, t/tmax] + b0)), one thread
+// per (node, channel).  gnn_2d.py:99-102,122-131.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void embed0_kernel(const float *__restrict__ u,
+                                                     const float *__restrict__ pos, int64_t n,
+                                                     mmpde_gnn_scales sc,
+                                                     mmpde_gnn_embed_params p,
+                                                     float *__restrict__ z) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= n * H) return;
+    const int64_t i = e >> 7;
+    const int c = (int)(e & (H - 1));
+    const float in0 = u[i];
+    const float in1 = pos[i * 3 + 1] * sc.inv_lx;
+    const float in2 = pos[i * 3 + 2] * sc.inv_ly;
+    const float in3 = pos[i * 3 + 0] * sc.inv_tmax;
+    const float *w = p.w0 + c * 4;
+    float v = p.b0[c] + w[0] * in0 + w[1] * in1 + w[2] * in2 + w[3] * in3;
+    v = bn_eval(v, p.bn1_rm[c], p.bn1_rv[c], p.bn1_w[c], p.bn1_b[c], p.eps);
+    z[e] = fmaxf(v, 0.0f);
+}
+
+struct EpiProj {  // message_net_1 split (see header comment)
+    float *out_a, *out_b;
+    const float *b1, *w_du, *w_dx, *w_dy, *w_t;  // bias and columns 256..259 of W1
+    int64_t ldw1;
+    const float *u, *pos;
+    mmpde_gnn_scales sc;
+    __device__ void operator()(const f32x16 &acc, int64_t row0, int col0, int lane, int64_t m,
+                               int part) const {
+        const int c = col0 + (lane & 31);
+        const float wdu = w_du[c * ldw1], wdx = w_dx[c * ldw1], wdy = w_dy[c * ldw1];
+        const float wt = w_t[c * ldw1], bb = b1[c];
+        float *dst = part == 0 ? out_a : out_b;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int64_t row = row0 + acc_row(r, lane);
+            if (row < m) {
+                const float uu = u[row];
+                const float px = pos[row * 3 + 1] * sc.inv_lx;
+                const float py = pos[row * 3 + 2] * sc.inv_ly;
+                const float node = wdu * uu + wdx * px + wdy * py;
+                float v;
+                if (part == 0) {
+                    const float pt = pos[row * 3 + 0] * sc.inv_tmax;
+                    v = acc[r] + node + wt * pt + bb;
+                } else {
+                    v = acc[r] - node;
+                }
+                dst[row * H + c] = v;
+            }
+        }
+    }
+};
+
+struct EpiUpd1 {  // relu(U1 [h | mean | t] + c1), gnn_2d.py:67
+    float *out;
+    const float *c1, *w_t;  // w_t: column 256 of U1 (stride ldw1)
+    int64_t ldw1;
+    const float *pos;
+    float inv_tmax;
+    __device__ void operator()(const f32x16 &acc, int64_t row0, int col0, int lane, int64_t m,
+                               int) const {
+        const int c = col0 + (lane & 31);
+        const float wt = w_t[c * ldw1], bb = c1[c];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int64_t row = row0 + acc_row(r, lane);
+            if (row < m) {
+                const float pt = pos[row * 3 + 0] * inv_tmax;
+                out[row * H + c] = fmaxf(acc[r] + wt * pt + bb, 0.0f);
+            }
+        }
+    }
+};
+
+struct EpiUpd2 {  // BN(h + relu(U2 v + c2)), gnn_2d.py:68-69,56
+    float *out;
+    const float *c2, *h;
+    const float *bn_w, *bn_b, *bn_rm, *bn_rv;
+    float eps;
+    __device__ void operator()(const f32x16 &acc, int64_t row0, int col0, int lane, int64_t m,
+                               int) const {
+        const int c = col0 + (lane & 31);
+        const float bb = c2[c], rm = bn_rm[c], rv = bn_rv[c], g = bn_w[c], be = bn_b[c];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int64_t row = row0 + acc_row(r, lane);
+            if (row < m) {
+                const float x = h[row * H + c] + fmaxf(acc[r] + bb, 0.0f);
+                out[row * H + c] = bn_eval(x, rm, rv, g, be, eps);
+            }
+        }
+    }
+};
+
+struct EpiBiasBn {  // BN(W x + b): embedding_mlp.3/.4
+    float *out;
+    const float *b;
+    const float *bn_w, *bn_b, *bn_rm, *bn_rv;
+    float eps;
+    __device__ void operator()(const f32x16 &acc, int64_t row0, int col0, int lane, int64_t m,
+                               int) const {
+        const int c = col0 + (lane & 31);
+        const float bb = b[c], rm = bn_rm[c], rv = bn_rv[c], g = bn_w[c], be = bn_b[c];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int64_t row = row0 + acc_row(r, lane);
+            if (row < m) out[row * H + c] = bn_eval(acc[r] + bb, rm, rv, g, be, eps);
+        }
+    }
+};
+
+// ---------------------------------------------------------------------------
+// Edge stage: the hot loop.  One workgroup = 32 target nodes, 4 waves; wave w
+// takes neighbour slots e = w, w+4, ...  For slot e the 32x128 tile
+// M1[r, :] = relu(a[tgt r] + b[nbr(tgt r, e)]) is built in registers (lane
+// (r, half) owns hidden units 64*half .. 64*half+63 of row r), multiplied by
+// W2^T (64 KB, staged once in LDS as the exact per-lane MFMA operand image) into
+// four 32x32 accumulators initialised with b2, then relu'd and summed into
+// per-wave running sums S.  Because slot e of all 32 targets shares one
+// accumulator row, the per-target sum needs no cross-lane traffic.  The 4
+// waves' S are reduced through the (then free) LDS image; / k gives the mean.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256, 2) void edge_mean_kernel(const float *__restrict__ a,
+                                                           const float *__restrict__ b,
+                                                           const int32_t *__restrict__ nbr,
+                                                           int64_t n, int k,
+                                                           const float *__restrict__ w2,
+                                                           const float *__restrict__ b2,
+                                                           float *__restrict__ out) {
+    __shared__ float4 ws[4 * 16 * 64];  // [ctile][s4][lane] : 64 KB
+    for (int e = threadIdx.x; e < 4 * 16 * 64; e += 256) {
+        const int l = e & 63, s4 = (e >> 6) & 15, c = e >> 10;
+        ws[e] = *(const float4 *)(w2 + (32 * c + (l & 31)) * H + 64 * (l >> 5) + 4 * s4);
+    }
+    __syncthreads();
+
+    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int half = lane >> 5;
+    const int64_t tile0 = (int64_t)blockIdx.x * 32;
+    int64_t tgt = tile0 + (lane & 31);
+    if (tgt >= n) tgt = n - 1;
+    const float *arow = a + tgt * H + 64 * half;
+    const int32_t *nrow = nbr + tgt * k;
+
+    float bias[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) bias[c] = b2[32 * c + (lane & 31)];
+
+    f32x16 S[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) S[c] = (f32x16){0};
+
+    for (int e = wave; e < k; e += 4) {
+        // clamp: a malformed caller table must not fault the GPU (knn output is always valid)
+        const int64_t src = min((uint32_t)nrow[e], (uint32_t)(n - 1));
+        const float *brow = b + src * H + 64 * half;
+        f32x16 acc[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[c][r] = bias[c];
+        }
+#pragma unroll 2
+        for (int s4 = 0; s4 < 16; ++s4) {
+            const float4 av = *(const float4 *)(arow + 4 * s4);
+            const float4 bv = *(const float4 *)(brow + 4 * s4);
+            const float m0 = fmaxf(av.x + bv.x, 0.0f);
+            const float m1 = fmaxf(av.y + bv.y, 0.0f);
+            const float m2 = fmaxf(av.z + bv.z, 0.0f);
+            const float m3 = fmaxf(av.w + bv.w, 0.0f);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const float4 w = ws[(c * 16 + s4) * 64 + lane];
+                acc[c] = mfma32(m0, w.x, acc[c]);
+                acc[c] = mfma32(m1, w.y, acc[c]);
+                acc[c] = mfma32(m2, w.z, acc[c]);
+                acc[c] = mfma32(m3, w.w, acc[c]);
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) S[c][r] += fmaxf(acc[c][r], 0.0f);
+        }
+    }
+
+    // cross-wave reduction through the LDS image (now free): red[wave][c][r][lane]
+    __syncthreads();
+    float *red = (float *)ws;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) red[((wave * 4 + c) * 16 + r) * 64 + lane] = S[c][r];
+    }
+    __syncthreads();
+    const int c = wave;  // each wave finalises one 32-column tile
+    const float inv_cnt_div = (float)k;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        float v = 0.0f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) v += red[((w * 4 + c) * 16 + r) * 64 + lane];
+        const int64_t row = tile0 + acc_row(r, lane);
+        if (row < n) out[row * H + 32 * c + (lane & 31)] = v / inv_cnt_div;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Conv1d head (gnn_2d.py:108-114,136-139): one wave per node.
+// 128 -> conv(1->4, k16, s3) 38 -> relu -> conv(4->8, k12, s3) 9 -> relu ->
+// conv(8->1, k8, s2) 1, times out_scale.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void head_kernel(const float *__restrict__ h, int64_t n,
+                                                   mmpde_gnn_head_params p,
+                                                   float *__restrict__ out) {
+    __shared__ float sw0[64 + 4], sw2[384 + 8], sw4[64 + 1];
+    __shared__ float y1[4][4 * 38];
+    __shared__ float y2[4][8 * 9];
+    for (int i = threadIdx.x; i < 64; i += 256) sw0[i] = p.c0_w[i];
+    for (int i = threadIdx.x; i < 4; i += 256) sw0[64 + i] = p.c0_b[i];
+    for (int i = threadIdx.x; i < 384; i += 256) sw2[i] = p.c2_w[i];
+    for (int i = threadIdx.x; i < 8; i += 256) sw2[384 + i] = p.c2_b[i];
+    for (int i = threadIdx.x; i < 64; i += 256) sw4[i] = p.c4_w[i];
+    if (threadIdx.x == 0) sw4[64] = p.c4_b[0];
+    __syncthreads();
+    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    for (int64_t i = (int64_t)blockIdx.x * 4 + wave; i < n; i += (int64_t)gridDim.x * 4) {
+        const float *hr = h + i * H;
+        for (int e = lane; e < 4 * 38; e += 64) {
+            const int c = e / 38, q = e - c * 38;
+            float v = sw0[64 + c];
+#pragma unroll
+            for (int t = 0; t < 16; ++t) v += sw0[c * 16 + t] * hr[3 * q + t];
+            y1[wave][e] = fmaxf(v, 0.0f);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (lane < 72) {
+            const int c = lane / 9, q = lane - c * 9;
+            float v = sw2[384 + c];
+            for (int ci = 0; ci < 4; ++ci) {
+#pragma unroll
+                for (int t = 0; t < 12; ++t) v += sw2[(c * 4 + ci) * 12 + t] * y1[wave][ci * 38 + 3 * q + t];
+            }
+            y2[wave][lane] = fmaxf(v, 0.0f);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        {
+            const int ci = lane >> 3, t = lane & 7;
+            float v = sw4[ci * 8 + t] * y2[wave][ci * 9 + t];
+            v = wave_sum(v);
+            if (lane == 0) out[i] = p.out_scale * (v + sw4[64]);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+inline bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
+
+}  // namespace
+
+// ===========================================================================
+// C-ABI
+// ===========================================================================
+extern "C" int64_t mmpde_gnn_workspace_bytes(int64_t n) {
+    // h ping-pong (2) + a + b + mean + v  = 6 x [n,128] fp32
+    return 6 * n * H * (int64_t)sizeof(float);
+}
+
+extern "C" int mmpde_gnn_embed(const float *u, const float *pos, int64_t n,
+                               mmpde_gnn_scales sc, const mmpde_gnn_embed_params *p,
+                               float *workspace, float *h_out, mmpde_stream_t stream) {
+    MMPDE_REQUIRE(u && pos && p && workspace && h_out && n > 0);
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(embed0_kernel, dim3(ceil_div(n * H, 256)), dim3(256), 0, st, u, pos, n,
+                       sc, *p, workspace);
+    MMPDE_RET_LAUNCH();
+    GemmArgs g{n, workspace, workspace + 64, H, p->w3, p->w3 + 64, H, 64};
+    EpiBiasBn epi{h_out, p->b3, p->bn4_w, p->bn4_b, p->bn4_rm, p->bn4_rv, p->eps};
+    return launch_gemm(g, 1, epi, st);
+}
+
+extern "C" int mmpde_gnn_edge_mean(const float *a, const float *b, const int32_t *nbr,
+                                   int64_t n, int k, const float *msg2_w, const float *msg2_b,
+                                   float *mean_out, mmpde_stream_t stream) {
+    MMPDE_REQUIRE(a && b && nbr && msg2_w && msg2_b && mean_out && n > 0 && k > 0);
+    MMPDE_REQUIRE(aligned16(a) && aligned16(b) && aligned16(msg2_w));
+    hipLaunchKernelGGL(edge_mean_kernel, dim3(ceil_div(n, 32)), dim3(256), 0, as_stream(stream),
+                       a, b, nbr, n, k, msg2_w, msg2_b, mean_out);
+    MMPDE_RET_LAUNCH();
+    return MMPDE_OK;
+}
+
+static int gnn_layer_impl(const float *h_in, const float *u, const float *pos, int64_t n, int k,
+                          const int32_t *nbr, mmpde_gnn_scales sc,
+                          const mmpde_gnn_layer_params *p, float *workspace, float *h_out,
+                          hipEvent_t ev_begin, hipEvent_t ev_end, mmpde_stream_t stream) {
+    MMPDE_REQUIRE(h_in && u && pos && nbr && p && workspace && h_out && n > 0 && k > 0);
+    MMPDE_REQUIRE(h_in != h_out && aligned16(h_in) && aligned16(workspace));
+    MMPDE_REQUIRE(p->msg1_ld >= 260 && (p->msg1_ld & 3) == 0 && aligned16(p->msg1_w));
+    MMPDE_REQUIRE(p->upd1_ld >= 257 && (p->upd1_ld & 3) == 0 && aligned16(p->upd1_w));
+    MMPDE_REQUIRE(aligned16(p->upd2_w));
+    hipStream_t st = as_stream(stream);
+    float *wa = workspace;
+    float *wb = wa + n * H;
+    float *wm = wb + n * H;
+    float *wv = wm + n * H;
+    int rc;
+    // 1. message_net_1 split into per-node target / source halves (W1 row stride 260)
+    {
+        const int64_t ld = p->msg1_ld;
+        GemmArgs g{n, h_in, h_in + 64, H, p->msg1_w, p->msg1_w + 64, ld, 64};
+        EpiProj epi{wa, wb, p->msg1_b, p->msg1_w + 256, p->msg1_w + 257, p->msg1_w + 258,
+                    p->msg1_w + 259, ld, u, pos, sc};
+        rc = launch_gemm<EpiProj, true>(g, 2, epi, st);
+        if (rc) return rc;
+    }
+    // 2. per-edge message_net_2 + mean aggregation
+    if (ev_begin && hipEventRecord(ev_begin, st) != hipSuccess) return MMPDE_ERR_INVALID_ARG;
+    rc = mmpde_gnn_edge_mean(wa, wb, nbr, n, k, p->msg2_w, p->msg2_b, wm, stream);
+    if (rc) return rc;
+    if (ev_end && hipEventRecord(ev_end, st) != hipSuccess) return MMPDE_ERR_INVALID_ARG;
+    // 3. update_net_1 over cat(h, mean, t) (row stride upd1_ld, 16-B aligned rows)
+    {
+        const int64_t ld = p->upd1_ld;
+        GemmArgs g{n, h_in, wm, H, p->upd1_w, p->upd1_w + 128, ld, 128};
+        EpiUpd1 epi{wv, p->upd1_b, p->upd1_w + 256, ld, pos, sc.inv_tmax};
+        rc = launch_gemm(g, 1, epi, st);
+        if (rc) return rc;
+    }
+    // 4. update_net_2 + residual + BatchNorm(eval)
+    {
+        GemmArgs g{n, wv, wv + 64, H, p->upd2_w, p->upd2_w + 64, H, 64};
+        EpiUpd2 epi{h_out, p->upd2_b, h_in, p->bn_w, p->bn_b, p->bn_rm, p->bn_rv, p->eps};
+        rc = launch_gemm(g, 1, epi, st);
+    }
+    return rc;
+}
+
+extern "C" int mmpde_gnn_layer(const float *h_in, const float *u, const float *pos, int64_t n,
+                               int k, const int32_t *nbr, mmpde_gnn_scales sc,
+                               const mmpde_gnn_layer_params *p, float *workspace,
+                               float *h_out, mmpde_stream_t stream) {
+    return gnn_layer_impl(h_in, u, pos, n, k, nbr, sc, p, workspace, h_out, nullptr, nullptr,
+                          stream);
+}
+
+extern "C" int mmpde_gnn_head(const float *h, int64_t n, const mmpde_gnn_head_params *p,
+                              float *out, mmpde_stream_t stream) {
+    MMPDE_REQUIRE(h && p && out && n > 0);
+    int blocks = ceil_div(n, 4);
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(head_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), h, n, *p,
+                       out);
+    MMPDE_RET_LAUNCH();
+    return MMPDE_OK;
+}
+
+extern "C" int mmpde_gnn_forward_ex(const float *u, const float *pos, int64_t n, int k,
+                                    const int32_t *nbr, mmpde_gnn_scales sc,
+                                    const mmpde_gnn_embed_params *emb,
+                                    const mmpde_gnn_layer_params *layers, int n_layers,
+                                    const mmpde_gnn_head_params *head, void *workspace,
+                                    float *out, const mmpde_gnn_trace *trace,
+                                    mmpde_stream_t stream) {
+    MMPDE_REQUIRE(u && pos && nbr && emb && layers && head && workspace && out);
+    MMPDE_REQUIRE(n > 0 && k > 0 && n_layers >= 0);
+    float *ws = (float *)workspace;
+    float *h0 = ws;
+    float *h1 = h0 + n * H;
+    float *lw = h1 + n * H;  // 4 x [n,128] layer scratch
+    int rc = mmpde_gnn_embed(u, pos, n, sc, emb, lw, h0, stream);
+    if (rc) return rc;
+    for (int l = 0; l < n_layers; ++l) {
+        hipEvent_t eb = trace ? (hipEvent_t)trace->edge_begin[l] : nullptr;
+        hipEvent_t ee = trace ? (hipEvent_t)trace->edge_end[l] : nullptr;
+        rc = gnn_layer_impl(h0, u, pos, n, k, nbr, sc, &layers[l], lw, h1, eb, ee, stream);
+        if (rc) return rc;
+        float *t = h0;
+        h0 = h1;
+        h1 = t;
+    }
+    return mmpde_gnn_head(h0, n, head, out, stream);
+}
+
+extern "C" int mmpde_gnn_forward(const float *u, const float *pos, int64_t n, int k,
+                                 const int32_t *nbr, mmpde_gnn_scales sc,
+                                 const mmpde_gnn_embed_params *emb,
+                                 const mmpde_gnn_layer_params *layers, int n_layers,
+                                 const mmpde_gnn_head_params *head, void *workspace, float *out,
+                                 mmpde_stream_t stream) {
+    return mmpde_gnn_forward_ex(u, pos, n, k, nbr, sc, emb, layers, n_layers, head, workspace, out,
+                                nullptr, stream);
+}

@@ -1,0 +1,218 @@
+// Batched exact k-nearest-neighbour search for gfx950.
+//
+// Replaces torch_cluster.knn_graph (reference data_creator_2d.py:260,
+// mesh/dmm_model.py:228) and sklearn NearestNeighbors.kneighbors
+// (data_creator_2d.py:66-78).  One wave per query; the trajectory's point set
+// (<= 4096 points, <= 32 KB) is staged once per workgroup in LDS; every lane
+// keeps CPL candidate keys in registers.  The k-th smallest key is found by a
+// bitwise radix select (ballot + popcount per candidate, no data movement),
+// ties at the threshold are resolved in index order, the k winners are
+// compacted into a per-wave LDS list and ranked by (key, index).  The result
+// is exactly the (distance, index)-ordered list of the reference's insertion
+// sort, independent of scheduling.
+//
+// Distance keys (must match oracle/knn_oracle.c bit for bit):
+//   graph: d2 = fmaf(dy, dy, dx*dx) in fp32  (torch_cluster under nvcc fmad)
+//   query: d2 = dx*dx + dy*dy in fp64        (sklearn float64 rdist)
+// Non-negative IEEE values order like their bit patterns, so keys are the
+// raw bits.
+#include <type_traits>
+
+#include "common.hpp"
+
+namespace {
+
+constexpr int kQueriesPerBlock = 16;  // 4 per wave
+
+template <bool QUERY>
+struct KeyTraits;
+
+template <>
+struct KeyTraits<false> {
+    typedef uint32_t key_t;
+    static constexpr int kTopBit = 30;  // valid keys are < 2^31
+    __device__ static key_t key(float2 p, float2 q) {
+#pragma clang fp contract(off)
+        float dx = p.x - q.x;
+        float dy = p.y - q.y;
+        float a = dx * dx;
+        return __float_as_uint(fmaf(dy, dy, a));
+    }
+};
+
+template <>
+struct KeyTraits<true> {
+    typedef uint64_t key_t;
+    static constexpr int kTopBit = 62;  // valid keys are < 2^63
+    __device__ static key_t key(float2 p, float2 q) {
+#pragma clang fp contract(off)
+        double dx = (double)p.x - (double)q.x;
+        double dy = (double)p.y - (double)q.y;
+        double a = dx * dx;
+        double c = dy * dy;
+        return (key_t)__double_as_longlong(a + c);
+    }
+};
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <int CPL, bool QUERY>
+__global__ __launch_bounds__(256) void knn_kernel(const float2 *__restrict__ pts,
+                                                  const float2 *__restrict__ qry, int n_src,
+                                                  int n_q, int k, int32_t *__restrict__ out,
+                                                  int32_t *__restrict__ degenerate) {
+    typedef KeyTraits<QUERY> KT;
+    typedef typename KT::key_t key_t;
+    __shared__ float2 sP[CPL * 64];
+    __shared__ key_t sKey[4][64];
+    __shared__ int sIdx[4][64];
+
+    const int b = blockIdx.y;
+    const float2 *P = pts + (int64_t)b * n_src;
+    for (int i = threadIdx.x; i < n_src; i += 256) sP[i] = P[i];
+    __syncthreads();
+
+    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int kk = QUERY ? k : k + 1;
+    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const int q_end = min((int)(blockIdx.x + 1) * kQueriesPerBlock, n_q);
+
+    for (int qi = blockIdx.x * kQueriesPerBlock + wave; qi < q_end; qi += 4) {
+        const float2 q = QUERY ? qry[(int64_t)b * n_q + qi] : sP[qi];
+        key_t key[CPL];
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            const int j = lane + 64 * c;
+            key[c] = (j < n_src) ? KT::key(sP[j], q) : ~key_t(0);
+        }
+        // Radix select: largest T with #(key < T) <= kk-1, i.e. the kk-th smallest key.
+        key_t T = 0;
+        for (int bit = KT::kTopBit; bit >= 0; --bit) {
+            const key_t Tc = T | (key_t(1) << bit);
+            int cnt = 0;
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) cnt += __popcll(__ballot(key[c] < Tc));
+            if (cnt <= kk - 1) T = Tc;
+        }
+        int m = 0;
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) m += __popcll(__ballot(key[c] < T));
+        const int need = kk - m;  // >= 1 candidates equal to T, taken in index order
+        int base = 0, eq_taken = 0;
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            const bool lt = key[c] < T;
+            const bool eq = key[c] == T;
+            const uint64_t em = __ballot(eq);
+            const int eqrank = eq_taken + __popcll(em & below);
+            const bool sel = lt || (eq && eqrank < need);
+            eq_taken += __popcll(em);
+            const uint64_t sm = __ballot(sel);
+            if (sel) {
+                const int p = base + __popcll(sm & below);
+                sKey[wave][p] = key[c];
+                sIdx[wave][p] = lane + 64 * c;
+            }
+            base += __popcll(sm);
+        }
+        wave_lds_sync();
+        key_t mk = ~key_t(0);
+        int mi = 0x7fffffff;
+        if (lane < kk) {
+            mk = sKey[wave][lane];
+            mi = sIdx[wave][lane];
+        }
+        int rank = 0;
+        for (int f = 0; f < kk; ++f) {
+            const key_t fk = sKey[wave][f];
+            const int fi = sIdx[wave][f];
+            rank += (fk < mk) || (fk == mk && fi < mi);
+        }
+        wave_lds_sync();  // the next query overwrites sKey / sIdx
+        const int64_t row = ((int64_t)b * n_q + qi) * k;
+        if (QUERY) {
+            if (lane < kk) out[row + rank] = mi;
+        } else {
+            const uint64_t smask = __ballot(lane < kk && mi == qi);
+            const bool has_self = smask != 0ull;
+            const int self_rank = has_self ? __shfl(rank, __ffsll((unsigned long long)smask) - 1, 64) : kk;
+            const int pos = rank - ((has_self && rank > self_rank) ? 1 : 0);
+            if (lane < kk && !(has_self && mi == qi) && pos < k)
+                out[row + pos] = b * n_src + mi;
+            if (!has_self && lane == 0 && degenerate) atomicAdd(degenerate, 1);
+        }
+    }
+}
+
+template <bool QUERY>
+int launch_knn(const float *pts, const float *qry, int64_t batches, int64_t n_src, int64_t n_q,
+               int k, int32_t *out, int32_t *degenerate, hipStream_t st) {
+    const int kk = QUERY ? k : k + 1;
+    if (k < 1 || kk > 64 || n_src < kk || n_src > 4096 || n_q < 1 || batches < 1 ||
+        batches > 65535)
+        return MMPDE_ERR_INVALID_ARG;
+    dim3 grid(ceil_div(n_q, kQueriesPerBlock), (unsigned)batches);
+    const int cpl = ceil_div(n_src, 64);
+    const float2 *p = (const float2 *)pts;
+    const float2 *q = (const float2 *)qry;
+    const int ns = (int)n_src, nq = (int)n_q;
+#define MMPDE_KNN_CASE(C)                                                                     \
+    if (cpl <= C) {                                                                           \
+        hipLaunchKernelGGL((knn_kernel<C, QUERY>), grid, dim3(256), 0, st, p, q, ns, nq, k, out, \
+                           degenerate);                                                       \
+        MMPDE_RET_LAUNCH();                                                                   \
+        return MMPDE_OK;                                                                      \
+    }
+    MMPDE_KNN_CASE(4)
+    MMPDE_KNN_CASE(8)
+    MMPDE_KNN_CASE(16)
+    MMPDE_KNN_CASE(24)
+    MMPDE_KNN_CASE(32)
+    MMPDE_KNN_CASE(40)
+    MMPDE_KNN_CASE(48)
+    MMPDE_KNN_CASE(56)
+    MMPDE_KNN_CASE(64)
+#undef MMPDE_KNN_CASE
+    return MMPDE_ERR_UNSUPPORTED;
+}
+
+__global__ void edge_index_kernel(const int32_t *__restrict__ nbr, int64_t n, int k,
+                                  int64_t *__restrict__ ei) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t ne = n * k;
+    if (e < ne) {
+        ei[e] = nbr[e];
+        ei[ne + e] = e / k;
+    }
+}
+
+}  // namespace
+
+extern "C" int mmpde_knn_graph(const float *pos, int64_t batches, int64_t n_per, int k,
+                               int32_t *nbr_out, int32_t *degenerate, mmpde_stream_t stream) {
+    MMPDE_REQUIRE(pos && nbr_out);
+    return launch_knn<false>(pos, nullptr, batches, n_per, n_per, k, nbr_out, degenerate,
+                             as_stream(stream));
+}
+
+extern "C" int mmpde_knn_query(const float *src, const float *qry, int64_t batches,
+                               int64_t n_src, int64_t n_qry, int k, int32_t *idx_out,
+                               mmpde_stream_t stream) {
+    MMPDE_REQUIRE(src && qry && idx_out);
+    return launch_knn<true>(src, qry, batches, n_src, n_qry, k, idx_out, nullptr,
+                            as_stream(stream));
+}
+
+extern "C" int mmpde_edge_index_from_nbr(const int32_t *nbr, int64_t n, int k,
+                                         int64_t *edge_index, mmpde_stream_t stream) {
+    MMPDE_REQUIRE(nbr && edge_index && n > 0 && k > 0);
+    const int64_t ne = n * k;
+    hipLaunchKernelGGL(edge_index_kernel, dim3(ceil_div(ne, 256)), dim3(256), 0,
+                       as_stream(stream), nbr, n, k, edge_index);
+    MMPDE_RET_LAUNCH();
+    return MMPDE_OK;
+}

@@ -1,0 +1,200 @@
+"""GraphCreator_FS_2D on the HIP kernels (drop-in for reference
+data_creator_2d.py:18-305).
+
+Same constructor and method signatures as the reference; every method that
+the MM-PDE step calls (create_graph, interpolate, interpolate_pred,
+moving_mesh, moving_mesh_tri) runs on device kernels:
+
+* kNN graphs: mmpde_knn_graph (torch_cluster.knn_graph replacement).  The graph
+  of the *fixed* grid is a pure function of the grid and B, so it is built once
+  and cached (the reference rebuilds it every call, train_helper_2d.py:177);
+  the moved-mesh graph is rebuilt every call, as in the reference.
+* interpolation: mmpde_knn_query (sklearn replacement, no host round trip) +
+  mmpde_itp_interp (ItpNet weights and weighted sum in one kernel).
+* moving mesh: DMM.mesh (analytic d(phi)/d(xi), no autograd graph).
+
+Only the torch plumbing (reshapes, the (t, x, y) position tensor) uses torch
+ops; there is no CPU or eager compute fallback.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+from torch import nn
+
+from . import ops
+from .graph import Data
+
+
+class GraphCreator_FS_2D(nn.Module):  # noqa: N801 - reference name
+    def __init__(self, pde, neighbors: int = 2, connect_edge: str = "knn",
+                 time_window: int = 10, t_resolution: int = 100):
+        super().__init__()
+        self.pde = pde
+        self.n = neighbors
+        self.e = connect_edge
+        self.tw = time_window
+        self.t_res = t_resolution
+        assert isinstance(self.n, int)
+        assert isinstance(self.tw, int)
+        self._fixed_graph_cache = {}
+
+    # ------------------------------------------------------------------ grids
+    def _is_array(self):
+        return len(self.pde.grid_size) == 3
+
+    def time_grid(self):
+        """t = linspace(tmin, tmax, nt) computed on the host in fp32 exactly as
+        data_creator_2d.py:185,220."""
+        return torch.linspace(self.pde.tmin, self.pde.tmax, self.pde.grid_size[0])
+
+    def uniform_grid(self, device, nx=None, ny=None):
+        """Array mode: meshgrid(linspace, linspace) 'ij' flattened (data_creator_2d.py:187-194);
+        cylinder: pde.ori_grid.  Returns [N, 2] fp32 on `device`."""
+        if self._is_array():
+            nx = self.pde.grid_size[1] if nx is None else nx
+            ny = self.pde.grid_size[2] if ny is None else ny
+            x = torch.linspace(0, self.pde.Lx, nx)
+            y = torch.linspace(0, self.pde.Ly, ny)
+            gx, gy = torch.meshgrid(x, y, indexing="ij")
+            return torch.stack((gx, gy), 2).float().reshape(-1, 2).to(device)
+        return self.pde.ori_grid.float().reshape(-1, 2).to(device)
+
+    def xi_grid_xy(self, n_grid_x, n_grid_y, device):
+        """The DMM xi grid of moving_mesh (data_creator_2d.py:94-96): numpy
+        linspace in float64, np.meshgrid 'xy' order, then cast to fp32."""
+        gx = np.linspace(0, self.pde.Lx, n_grid_x)
+        gy = np.linspace(0, self.pde.Ly, n_grid_y)
+        g = torch.tensor(np.array(np.meshgrid(gx, gy)), dtype=torch.float)
+        return g.reshape(2, -1).permute(1, 0).contiguous().to(device)
+
+    def fixed_graph_nbr(self, grid: torch.Tensor, batches: int) -> torch.Tensor:
+        """kNN-k table of `batches` copies of the fixed grid (cached)."""
+        key = (grid.data_ptr(), grid._version, str(grid.device), batches, self.n)
+        nbr = self._fixed_graph_cache.get(key)
+        if nbr is None:
+            nbr = ops.knn_graph_nbr(grid.repeat(batches, 1), batches, self.n)
+            self._fixed_graph_cache = {key: nbr}
+        return nbr
+
+    # ------------------------------------------------------------------ data
+    def create_data(self, datapoints, steps):
+        """data_creator_2d.py:139-154: input window u[step-tw:step] and target
+        u[step:step+tw] of every trajectory (stacked once, not cat'ed in a loop)."""
+        data = torch.stack([dp[s - self.tw:s] for dp, s in zip(datapoints, steps)])
+        labels = torch.stack([dp[s:s + self.tw] for dp, s in zip(datapoints, steps)])
+        return data, labels
+
+    # ------------------------------------------------------------------ mesh
+    def moving_mesh(self, u, mesh_model, n_grid_x, n_grid_y):
+        """data_creator_2d.py:88-113 (Burgers, DMM array mode).  u [B, nx, ny].
+        Returns (x1, x2), each [B*nx*ny, 1]."""
+        if (self.pde.movingmesh_grid_size[-2] != n_grid_x
+                or self.pde.movingmesh_grid_size[-1] != n_grid_y):
+            raise NotImplementedError("bilinear pre-resampling of u (data_creator_2d.py:102-103) "
+                                      "is not on the benchmarked path")
+        xi = self.xi_grid_xy(n_grid_x, n_grid_y, u.device)
+        mesh = mesh_model.mesh(u, xi)
+        return mesh[:, 0:1], mesh[:, 1:2]
+
+    def moving_mesh_tri(self, u, mesh_model, grid_x, grid_y):
+        """data_creator_2d.py:115-137 (cylinder, DMM graph mode).  grid_x/grid_y are
+        the fixed grid repeated per trajectory ([B, N]); all trajectories share it."""
+        xi = torch.stack((grid_x[0], grid_y[0]), -1)
+        mesh = mesh_model.mesh(u, xi)
+        return mesh[:, 0:1], mesh[:, 1:2]
+
+    # ------------------------------------------------------------------ interpolation
+    def interpolate(self, itp_model, u, init_x, init_y, x, y, mode):
+        """data_creator_2d.py:46-85: per trajectory, the 30 nearest source points
+        (fp64 distance order) of every query, ItpNet weights, weighted sum of
+        the source values.  Returns [nu * n_query]."""
+        nu = u.shape[0]
+        src = torch.cat((init_x, init_y), -1).reshape(-1, 2)
+        qry = torch.cat((x, y), -1).reshape(-1, 2)
+        idx = ops.knn_query(src, qry, nu, 30)
+        return ops.itp_interp(src, u.reshape(-1), qry, idx, nu, itp_model.packed(mode))
+
+    # ------------------------------------------------------------------ graph
+    def _graph(self, u_nodes, mesh, t_nodes, labels_nodes, nbr, B, n):
+        pos = torch.cat((t_nodes[:, None], mesh), 1).contiguous()
+        batch = torch.arange(B, device=mesh.device).repeat_interleave(n)
+        g = Data(x=u_nodes, edge_index=None)
+        g.y = labels_nodes
+        g.pos = pos
+        g.batch = batch
+        g.nbr = nbr
+        return g
+
+    def create_graph(self, itp_model, data, labels, steps, device, mesh_model=None):
+        """data_creator_2d.py:157-267 (connect_edge 'knn')."""
+        if self.e != "knn":
+            raise NotImplementedError("connect_edge='radius' is a §8(f) 'next' row")
+        data = data.to(device)
+        labels = labels.to(device)
+        B = data.shape[0]
+        t = self.time_grid()
+        if self._is_array():
+            nt, nx, ny = self.pde.grid_size
+            n = nx * ny
+            grid = self.uniform_grid(device, nx, ny)
+            if mesh_model is not None:
+                ori_nx, ori_ny = data.shape[-2], data.shape[-1]
+                mm_nx, mm_ny = self.pde.movingmesh_grid_size[-2:]
+                u_mm = data.reshape(-1, ori_nx, ori_ny)[:, ::int(ori_nx / mm_nx),
+                                                        ::int(ori_ny / mm_ny)]
+                mx, my = self.moving_mesh(u_mm.contiguous(), mesh_model, nx, ny)
+                mesh = torch.cat((mx, my), -1)
+                ori = self.uniform_grid(device, ori_nx, ori_ny).repeat(B, 1)
+                data = self.interpolate(itp_model, data.reshape(-1, ori_nx, ori_ny),
+                                        ori[:, 0:1], ori[:, 1:2], mx, my, "1"
+                                        ).reshape(-1, self.tw, nx, ny)
+                labels = self.interpolate(itp_model, labels.reshape(-1, ori_nx, ori_ny),
+                                          ori[:, 0:1], ori[:, 1:2], mx, my, "1"
+                                          ).reshape(-1, self.tw, nx, ny)
+            else:
+                mesh = grid.repeat(B, 1)
+        else:
+            n = self.pde.ori_grid_size[1]
+            grid = self.uniform_grid(device)
+            if mesh_model is not None:
+                gx = grid[:, 0][None].expand(B, n)
+                gy = grid[:, 1][None].expand(B, n)
+                mx, my = self.moving_mesh_tri(data.reshape(-1, n), mesh_model, gx, gy)
+                mesh = torch.cat((mx, my), -1)
+            else:
+                mesh = grid.repeat(B, 1)
+        # node tensors (data_creator_2d.py:242-254): u [B*n, tw], labels, t[step]
+        u_nodes = data.reshape(B, self.tw, n).permute(0, 2, 1).reshape(B * n, self.tw)
+        y_nodes = labels.reshape(B, self.tw, n).permute(0, 2, 1).reshape(B * n, self.tw)
+        t_nodes = t[list(steps)].to(device).repeat_interleave(n)
+        if mesh_model is None:
+            nbr = self.fixed_graph_nbr(grid, B)
+        else:
+            nbr = ops.knn_graph_nbr(mesh, B, self.n)
+        return self._graph(u_nodes.contiguous(), mesh.contiguous(), t_nodes, y_nodes, nbr, B, n)
+
+    def interpolate_pred(self, itp_model, pred, graph, data, device):
+        """data_creator_2d.py:270-305: moved-mesh prediction -> fixed grid (kNN-30 of
+        each fixed point among the moved points + ItpNet mode '2') plus
+        res_cut(data)."""
+        data = data.to(device)
+        if self._is_array():
+            ori_nx, ori_ny = self.pde.ori_grid_size[1], self.pde.ori_grid_size[2]
+            nx, ny = self.pde.grid_size[1], self.pde.grid_size[2]
+            nu = pred.shape[0] // (nx * ny)
+            qry = self.uniform_grid(device, ori_nx, ori_ny).repeat(nu, 1)
+            res = itp_model.res_cut(data.reshape(-1, 1, ori_nx, ori_ny)).reshape(-1)
+            n_src = nx * ny
+        else:
+            n = self.pde.ori_grid_size[1]
+            nu = pred.shape[0] // n
+            qry = self.uniform_grid(device).repeat(nu, 1)
+            res = itp_model.res_cut(data.reshape(-1, n)).reshape(-1)
+            n_src = n
+        src = graph.pos[:, 1:3].contiguous()
+        idx = ops.knn_query(src, qry, nu, 30)
+        out = ops.itp_interp(src, pred.reshape(-1), qry, idx, nu, itp_model.packed("2"),
+                             addend=res)
+        assert src.shape[0] == nu * n_src
+        return out.reshape(-1, 1)

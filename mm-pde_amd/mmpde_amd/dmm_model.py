@@ -1,0 +1,228 @@
+"""DMM mesh mover on the HIP kernels (drop-in for reference mesh/dmm_model.py).
+
+Module tree and ``state_dict`` keys match the reference (including the unused
+``DenseNet.fc0``, which also keeps the default-init RNG stream aligned), so
+the reference checkpoints ``cy_checkpoint`` / ``burgers_checkpoint``
+(``model_state_dict``) load unchanged.  Unlike the reference, nothing is
+hard-wired to ``device="cuda"`` at construction (dmm_model.py:27-28).
+
+The MM-PDE step never needs phi itself, only the moved mesh
+x = xi + d(phi)/d(xi) that GraphCreator_FS_2D.moving_mesh[_tri] obtains with
+two autograd.grad calls (data_creator_2d.py:106-107,130-131).  ``DMM.mesh``
+returns exactly that through an analytic vector-Jacobian product
+(mmpde_dmm_mesh_graph / mmpde_dmm_mesh_array; derivation in dmm.hip).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+from torch import nn
+
+from . import _lib as L
+from .gnn_2d import BatchNorm
+from .ops import knn_graph_nbr
+
+
+class DenseNet(nn.Module):
+    """Reference dmm_model.py:9-45 (normalize=False): Linear layers with tanh on
+    all but the last.  ``fc0`` is unused by the reference forward but is a
+    parameter there, so it is kept for state_dict / RNG parity."""
+
+    def __init__(self, layers, width=32, normalize=False):
+        super().__init__()
+        if normalize:
+            raise NotImplementedError("DenseNet(normalize=True) is not used by MM-PDE")
+        self.n_layers = len(layers) - 1
+        assert self.n_layers >= 1
+        self.layers = nn.ModuleList(nn.Linear(a, b) for a, b in zip(layers[:-1], layers[1:]))
+        self.normalize = normalize
+        self.width = width
+        self.fc0 = nn.Linear(4, width)
+
+    def forward(self, x):
+        raise NotImplementedError("DenseNet runs inside the fused DMM mesh kernels")
+
+
+class ConvNet(nn.Module):
+    """Reference dmm_model.py:48-81 (layers == 7, the only configuration it builds)."""
+
+    def __init__(self, s, layers):
+        super().__init__()
+        if layers != 7:
+            raise NotImplementedError("ConvNet is only defined for layers == 7")
+        self.layers = nn.ModuleList([
+            nn.Conv2d(1, 8, 5, stride=2, padding=2), nn.Conv2d(8, 16, 5, padding=2),
+            nn.Conv2d(16, 8, 5, padding=2), nn.Conv2d(8, 1, 5, stride=2, padding=2)])
+        self.fc1 = None
+        self.fc2 = nn.Linear(int(((s + 1) / 2 + 1) / 2) ** 2, 1024)
+        self.fc3 = nn.Linear(1024, 512)
+        self.s = s
+
+    def forward(self, x):
+        raise NotImplementedError("ConvNet runs inside mmpde_dmm_mesh_array")
+
+
+class GNN_Layer_FS_2D(nn.Module):  # noqa: N801 - reference name
+    """The DMM branch's tanh GNN layer (reference dmm_model.py:94-142)."""
+
+    def __init__(self, in_features, out_features, hidden_features):
+        super().__init__()
+        self.message_net_1 = nn.Sequential(nn.Linear(2 * in_features + 3, hidden_features),
+                                           nn.Tanh())
+        self.message_net_2 = nn.Sequential(nn.Linear(hidden_features, out_features), nn.Tanh())
+        self.update_net_1 = nn.Sequential(nn.Linear(in_features + hidden_features,
+                                                    hidden_features), nn.Tanh())
+        self.update_net_2 = nn.Sequential(nn.Linear(hidden_features, out_features), nn.Tanh())
+        self.norm = BatchNorm(hidden_features)
+
+    def forward(self, *args, **kwargs):
+        raise NotImplementedError("runs inside mmpde_dmm_mesh_graph")
+
+
+class DMM(nn.Module):
+    """Reference dmm_model.py:145-219."""
+
+    def __init__(self, branch_layer, trunk_layer, grid=None, out_layer=None, s=None,
+                 mode="array"):
+        super().__init__()
+        self.mode = mode
+        self.ori_grid = grid
+        if mode == "array":
+            self.branch = ConvNet(s, branch_layer)
+            self.trunk = DenseNet(trunk_layer)
+            self.out_nn = DenseNet(out_layer)
+        elif mode == "graph":
+            self.hidden_features = branch_layer[0]
+            self.hidden_layer = branch_layer[1]
+            self.gnn_layers = nn.ModuleList(
+                GNN_Layer_FS_2D(in_features=self.hidden_features,
+                                hidden_features=self.hidden_features,
+                                out_features=self.hidden_features)
+                for _ in range(self.hidden_layer))
+            self.embedding_mlp = nn.Sequential(
+                nn.Linear(3, self.hidden_features), nn.BatchNorm1d(self.hidden_features),
+                nn.Tanh(), nn.Linear(self.hidden_features, self.hidden_features),
+                nn.BatchNorm1d(self.hidden_features))
+            self.decoding_mlp = DenseNet([self.hidden_features, 128, 1])
+            self.output_mlp = nn.Sequential(
+                nn.Linear(grid.shape[0], 512), nn.Tanh(), nn.Linear(512, 256), nn.Tanh(),
+                nn.Linear(256, trunk_layer[-1]))
+            self.trunk = DenseNet(trunk_layer)
+            self.out_nn = DenseNet(out_layer)
+        else:
+            raise ValueError(mode)
+        self._pack_key = None
+        self._pack = None
+        self._grid_cache = {}
+
+    def forward(self, u, grid, rf=False):
+        raise NotImplementedError(
+            "the MM-PDE step only needs the moved mesh: use DMM.mesh(u, xi) (analytic "
+            "d(phi)/d(xi)); phi values are used by DMM training, which is out of scope")
+
+    # ----------------------------------------------------------------- packing
+    def _check(self):
+        if self.training:
+            raise NotImplementedError("training-mode forward is out of scope; call .eval()")
+        tl = self.trunk.layers
+        ol = self.out_nn.layers
+        if len(tl) != 2 or len(ol) != 2 or ol[1].out_features != 1:
+            raise NotImplementedError("trunk DenseNet[2, th, L] / out_nn DenseNet[2L, L', 1] only")
+        if self.mode == "graph" and (self.hidden_features != 4 or self.hidden_layer > 3):
+            raise NotImplementedError("graph branch: hidden 4, <= 3 layers (cy checkpoint)")
+
+    def _tensors(self):
+        tl, ol = self.trunk.layers, self.out_nn.layers
+        head = [tl[0].weight, tl[0].bias, tl[1].weight, tl[1].bias, ol[0].weight, ol[0].bias,
+                ol[1].weight]
+        if self.mode == "graph":
+            e = self.embedding_mlp
+            br = [e[0].weight, e[0].bias, e[1].weight, e[1].bias, e[1].running_mean,
+                  e[1].running_var, e[3].weight, e[3].bias, e[4].weight, e[4].bias,
+                  e[4].running_mean, e[4].running_var]
+            for g in self.gnn_layers:
+                br += [g.message_net_1[0].weight, g.message_net_1[0].bias,
+                       g.message_net_2[0].weight, g.message_net_2[0].bias,
+                       g.update_net_1[0].weight, g.update_net_1[0].bias,
+                       g.update_net_2[0].weight, g.update_net_2[0].bias,
+                       g.norm.module.weight, g.norm.module.bias, g.norm.module.running_mean,
+                       g.norm.module.running_var]
+            d, o = self.decoding_mlp.layers, self.output_mlp
+            br += [d[0].weight, d[0].bias, d[1].weight, d[1].bias, o[0].weight, o[0].bias,
+                   o[2].weight, o[2].bias, o[4].weight, o[4].bias]
+        else:
+            b = self.branch
+            br = [b.layers[0].weight, b.layers[0].bias, b.layers[1].weight, b.layers[1].bias,
+                  b.layers[2].weight, b.layers[2].bias, b.layers[3].weight, b.layers[3].bias,
+                  b.fc2.weight, b.fc2.bias, b.fc3.weight, b.fc3.bias]
+        return head, br
+
+    def device_params(self):
+        self._check()
+        head, br = self._tensors()
+        key = tuple((t.data_ptr(), t._version) for t in head + br)
+        if key == self._pack_key:
+            return self._pack[0]
+        fh = [L.f32c(t) for t in head]
+        fb = [L.f32c(t) for t in br]
+        tl, ol = self.trunk.layers, self.out_nn.layers
+        hd = L.DmmHead(fh[0].data_ptr(), fh[1].data_ptr(), fh[2].data_ptr(), fh[3].data_ptr(),
+                       tl[0].out_features, tl[1].out_features, fh[4].data_ptr(),
+                       fh[5].data_ptr(), fh[6].data_ptr(), ol[0].out_features)
+        if self.mode == "graph":
+            p = [t.data_ptr() for t in fb]
+            nl = self.hidden_layer
+            per = [p[12 + 12 * i: 24 + 12 * i] for i in range(nl)]
+            arrs = []
+            for fld in range(12):
+                vals = [per[i][fld] if i < nl else None for i in range(3)]
+                arrs.append(L._P3(*vals))
+            tail = p[12 + 12 * nl:]
+            bn_eps = float(self.embedding_mlp[1].eps)
+            bp = L.DmmGraphBranch(*p[:12], *arrs, nl, *tail, bn_eps)
+        else:
+            bp = L.DmmArrayBranch(*[t.data_ptr() for t in fb], self.branch.s)
+        self._pack = ((bp, hd), fh + fb)
+        self._pack_key = key
+        return self._pack[0]
+
+    def grid_nbr(self, grid: torch.Tensor, k: int = 35) -> torch.Tensor:
+        """kNN-35 table of the fixed grid (reference dmm_model.py:222-234 builds it
+        every call on B identical copies; it depends only on the grid, so it is
+        built once per grid here).  LOCAL indices [N, k] int32."""
+        key = (grid.data_ptr(), grid._version, str(grid.device), k)
+        if key not in self._grid_cache:
+            self._grid_cache = {key: knn_graph_nbr(grid, 1, k)}
+        return self._grid_cache[key]
+
+    # ----------------------------------------------------------------- the API
+    def mesh(self, u: torch.Tensor, xi: torch.Tensor, out: torch.Tensor | None = None,
+             workspace: torch.Tensor | None = None) -> torch.Tensor:
+        """Moved mesh x = xi + d(phi)/d(xi) for every trajectory.
+        u: graph mode [B, N] (values on the fixed grid), array mode [B, s, s];
+        xi: [N, 2] grid shared by all trajectories (graph: self.ori_grid;
+        array: the np.meshgrid 'xy' grid of data_creator_2d.py:94-100).
+        Returns [B*N, 2] fp32."""
+        L.require_device(u, xi)
+        bp, hd = self.device_params()
+        u = L.f32c(u)
+        xi = L.f32c(xi).reshape(-1, 2)
+        B, N = u.shape[0], xi.shape[0]
+        if workspace is None:
+            nb = L.lib().mmpde_dmm_workspace_bytes(B, N, hd.latent, hd.hidden)
+            workspace = torch.empty((nb // 4,), dtype=torch.float32, device=u.device)
+        if out is None:
+            out = torch.empty((B * N, 2), dtype=torch.float32, device=u.device)
+        st = L.stream(u.device)
+        if self.mode == "graph":
+            nbr = self.grid_nbr(xi)
+            L.check(L.lib().mmpde_dmm_mesh_graph(L.ptr(u), L.ptr(xi), B, N, L.ptr(nbr),
+                                                 nbr.shape[1], ctypes.byref(bp), ctypes.byref(hd),
+                                                 L.ptr(workspace), L.ptr(out), st),
+                    "mmpde_dmm_mesh_graph")
+        else:
+            L.check(L.lib().mmpde_dmm_mesh_array(L.ptr(u), L.ptr(xi), B, N, ctypes.byref(bp),
+                                                 ctypes.byref(hd), L.ptr(workspace), L.ptr(out),
+                                                 st), "mmpde_dmm_mesh_array")
+        return out

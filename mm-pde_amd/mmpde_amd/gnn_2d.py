@@ -1,0 +1,193 @@
+"""MP_PDE_Solver_2D on the HIP kernels (drop-in for reference gnn_2d.py:19-141).
+
+Module tree, parameter names, ``state_dict`` keys, constructor arguments and
+``__repr__() == 'GNN'`` (the type switch of train_helper_2d.py:107,174) match the
+reference, so reference checkpoints load unchanged.  ``forward(data)`` runs the
+whole solver in one C-ABI call (mmpde_gnn_forward): embedding, 6 fused
+message-passing layers, Conv1d head -- eval-mode semantics (BatchNorm with
+running statistics), fp32 throughout.  There is no CPU / eager fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+from torch import nn
+
+from . import _lib as L
+from .ops import nbr_from_edge_index
+
+
+class BatchNorm(nn.Module):
+    """Key-compatible stand-in for torch_geometric.nn.BatchNorm (PyG 2.0.3 wraps
+    nn.BatchNorm1d as ``.module``; reference gnn_2d.py:51)."""
+
+    def __init__(self, in_channels, eps=1e-5, momentum=0.1, affine=True,
+                 track_running_stats=True):
+        super().__init__()
+        self.module = nn.BatchNorm1d(in_channels, eps, momentum, affine, track_running_stats)
+
+    def forward(self, x):
+        raise NotImplementedError("BatchNorm is fused into the HIP GNN layer kernels")
+
+
+class GNN_Layer_FS_2D(nn.Module):  # noqa: N801 - reference name
+    """Message-passing layer (reference gnn_2d.py:19-69): message
+    relu(W2 relu(W1 cat(h_i, h_j, u_i-u_j, dx, dy, t_i))), mean over the
+    in-edges, update h + relu(U2 relu(U1 cat(h, m, t))), BatchNorm."""
+
+    def __init__(self, in_features, out_features, hidden_features, time_window, n_variables):
+        super().__init__()
+        self.in_features, self.out_features = in_features, out_features
+        self.hidden_features, self.time_window, self.n_variables = \
+            hidden_features, time_window, n_variables
+        msg_in = 2 * in_features + time_window + 2 + n_variables
+        self.message_net_1 = nn.Sequential(nn.Linear(msg_in, hidden_features), nn.ReLU())
+        self.message_net_2 = nn.Sequential(nn.Linear(hidden_features, out_features), nn.ReLU())
+        self.update_net_1 = nn.Sequential(
+            nn.Linear(in_features + hidden_features + n_variables, hidden_features), nn.ReLU())
+        self.update_net_2 = nn.Sequential(nn.Linear(hidden_features, out_features), nn.ReLU())
+        self.norm = BatchNorm(hidden_features)
+        self._pack_key = None
+        self._pack = None
+
+    def supported(self):
+        return (self.in_features == self.out_features == self.hidden_features == 128
+                and self.time_window == 1 and self.n_variables == 1)
+
+    def _params(self):
+        """ctypes parameter block (cached until a parameter changes)."""
+        ts = [self.message_net_1[0].weight, self.message_net_1[0].bias,
+              self.message_net_2[0].weight, self.message_net_2[0].bias,
+              self.update_net_1[0].weight, self.update_net_1[0].bias,
+              self.update_net_2[0].weight, self.update_net_2[0].bias,
+              self.norm.module.weight, self.norm.module.bias,
+              self.norm.module.running_mean, self.norm.module.running_var]
+        key = tuple((t.data_ptr(), t._version) for t in ts)
+        if key != self._pack_key:
+            f = [L.f32c(t) for t in ts]
+            u1 = f[4]
+            u1p = torch.zeros((u1.shape[0], 260), dtype=torch.float32, device=u1.device)
+            u1p[:, :u1.shape[1]] = u1          # row stride 260 keeps rows 16-B aligned
+            keep = f[:4] + [u1p] + f[5:]
+            p = L.GnnLayerParams(*[t.data_ptr() for t in keep], float(self.norm.module.eps),
+                                 f[0].shape[1], 260)
+            self._pack, self._pack_key = (p, keep), key
+        return self._pack[0]
+
+    def forward(self, x, u, pos_x, pos_y, variables, edge_index, batch):
+        """Layer-level API of the reference (gnn_2d.py:53-57)."""
+        if self.training:
+            raise NotImplementedError("training-mode forward is out of scope; call .eval()")
+        if not self.supported():
+            raise NotImplementedError("HIP layer supports hidden 128, time_window 1, 1 variable")
+        L.require_device(x, u, pos_x, pos_y, variables)
+        n = x.shape[0]
+        nbr = nbr_from_edge_index(edge_index, n)
+        pos = torch.cat((variables, pos_x, pos_y), dim=-1).float().contiguous()
+        ws = torch.empty((4 * n * 128,), dtype=torch.float32, device=x.device)
+        out = torch.empty((n, 128), dtype=torch.float32, device=x.device)
+        p = self._params()
+        L.check(L.lib().mmpde_gnn_layer(L.ptr(L.f32c(x)), L.ptr(L.f32c(u).reshape(-1)), L.ptr(pos),
+                                        n, nbr.shape[1], L.ptr(nbr), L.GnnScales(1.0, 1.0, 1.0),
+                                        ctypes.byref(p), L.ptr(ws), L.ptr(out),
+                                        L.stream(x.device)), "mmpde_gnn_layer")
+        return out
+
+
+class MP_PDE_Solver_2D(nn.Module):  # noqa: N801 - reference name
+    """Reference gnn_2d.py:72-141.  forward(data) -> [n, time_window]."""
+
+    def __init__(self, pde, time_window=1, hidden_features=128, hidden_layer=6,
+                 eq_variables={}):  # noqa: B006 - reference signature
+        super().__init__()
+        self.pde = pde
+        self.out_features = time_window
+        self.hidden_features = hidden_features
+        self.hidden_layer = hidden_layer
+        self.time_window = time_window
+        self.eq_variables = eq_variables
+        self.gnn_layers = nn.ModuleList(
+            GNN_Layer_FS_2D(in_features=hidden_features, hidden_features=hidden_features,
+                            out_features=hidden_features, time_window=time_window,
+                            n_variables=len(eq_variables) + 1)
+            for _ in range(hidden_layer))
+        self.embedding_mlp = nn.Sequential(
+            nn.Linear(time_window + 3 + len(eq_variables), hidden_features),
+            nn.BatchNorm1d(hidden_features), nn.ReLU(),
+            nn.Linear(hidden_features, hidden_features), nn.BatchNorm1d(hidden_features))
+        self.output_mlp = nn.Sequential(
+            nn.Conv1d(1, 4, 16, stride=3), nn.ReLU(),
+            nn.Conv1d(4, 8, 12, stride=3), nn.ReLU(),
+            nn.Conv1d(8, 1, 8, stride=2))
+        self._pack_key = None
+        self._pack = None
+
+    def __repr__(self):
+        return "GNN"
+
+    # ----------------------------------------------------------------- packing
+    def out_scale(self) -> float:
+        """cumsum(ones(1, tw) * pde.dt * 0.1) evaluated exactly as gnn_2d.py:137-138
+        (fp32, on the host); tw = 1 -> one scalar."""
+        dt = torch.ones(1, self.time_window) * self.pde.dt * 0.1
+        return float(torch.cumsum(dt, dim=1)[0, -1])
+
+    def scales(self) -> L.GnnScales:
+        one = torch.ones((), dtype=torch.float32)
+        return L.GnnScales(float(one / self.pde.Lx), float(one / self.pde.Ly),
+                           float(one / self.pde.tmax))
+
+    def device_params(self):
+        """(scales, embed, layer array, head) ctypes blocks, cached by parameter
+        identity/version."""
+        e, o = self.embedding_mlp, self.output_mlp
+        ts = [e[0].weight, e[0].bias, e[1].weight, e[1].bias, e[1].running_mean,
+              e[1].running_var, e[3].weight, e[3].bias, e[4].weight, e[4].bias,
+              e[4].running_mean, e[4].running_var,
+              o[0].weight, o[0].bias, o[2].weight, o[2].bias, o[4].weight, o[4].bias]
+        layer_params = [g._params() for g in self.gnn_layers]
+        key = (tuple((t.data_ptr(), t._version) for t in ts),
+               tuple(ctypes.addressof(p) for p in layer_params), self.pde.dt, self.pde.tmax)
+        if key != self._pack_key:
+            f = [L.f32c(t) for t in ts]
+            emb = L.GnnEmbedParams(*[t.data_ptr() for t in f[:12]], float(e[1].eps))
+            head = L.GnnHeadParams(*[t.data_ptr() for t in f[12:]], self.out_scale())
+            arr = (L.GnnLayerParams * len(layer_params))(*layer_params)
+            self._pack = ((self.scales(), emb, arr, head), f, [g._pack for g in self.gnn_layers])
+            self._pack_key = key
+        return self._pack[0]
+
+    def check_supported(self):
+        if self.training:
+            raise NotImplementedError("training-mode forward is out of scope; call .eval()")
+        if self.hidden_features != 128 or self.time_window != 1 or len(self.eq_variables):
+            raise NotImplementedError("HIP solver supports hidden 128, time_window 1, no "
+                                      "extra equation variables (reference defaults)")
+
+    # ----------------------------------------------------------------- forward
+    def forward(self, data, out: torch.Tensor | None = None, workspace=None, trace=None):
+        """gnn_2d.py:119-141 on one C-ABI call.  `data` needs .x [n,1], .pos [n,3]
+        and either .nbr (int32 [n,k]) or a knn-style .edge_index.  `trace`: optional
+        _lib.GnnTrace of hipEvents recorded around each layer's edge kernel."""
+        self.check_supported()
+        u, pos = data.x, data.pos
+        L.require_device(u, pos)
+        n = u.shape[0]
+        nbr = getattr(data, "nbr", None)
+        if nbr is None:
+            nbr = nbr_from_edge_index(data.edge_index, n)
+        u = L.f32c(u).reshape(-1)
+        pos = L.f32c(pos)
+        sc, emb, arr, head = self.device_params()
+        if workspace is None:
+            workspace = torch.empty((L.lib().mmpde_gnn_workspace_bytes(n) // 4,),
+                                    dtype=torch.float32, device=u.device)
+        if out is None:
+            out = torch.empty((n, 1), dtype=torch.float32, device=u.device)
+        L.check(L.lib().mmpde_gnn_forward_ex(
+            L.ptr(u), L.ptr(pos), n, nbr.shape[1], L.ptr(nbr), sc, ctypes.byref(emb), arr,
+            len(arr), ctypes.byref(head), L.ptr(workspace), L.ptr(out),
+            ctypes.byref(trace) if trace is not None else None, L.stream(u.device)),
+            "mmpde_gnn_forward")
+        return out

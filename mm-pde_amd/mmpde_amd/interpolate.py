@@ -1,0 +1,101 @@
+"""ItpNet on the HIP kernels (drop-in for reference interpolate.py:5-99).
+
+Parameters and state_dict keys match the reference: ``layers`` (mode '1'),
+``layers2`` (mode '2'), the never-used ``layers3`` (kept for key parity) and the
+``down`` residual-cut network (Linear MLP for the cylinder mesh, Conv2d stack
+for Burgers).  Modes '1'/'2' run inside the fused kNN-30 + MLP + weighted-sum
+kernel driven by GraphCreator_FS_2D.interpolate; ``forward(..., 'res_cut')``
+runs the ``down`` network on the skinny-GEMM / conv kernels.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+from torch import nn
+
+from . import _lib as L
+from . import ops
+
+
+def _mlp(widths):
+    return nn.ModuleList(nn.Linear(a, b) for a, b in zip(widths[:-1], widths[1:]))
+
+
+class ItpNet(nn.Module):
+    def __init__(self, ori_nx, ori_ny, layers1, layers2, layers3, normalize=False):
+        super().__init__()
+        if normalize:
+            raise NotImplementedError("ItpNet(normalize=True) is not used by MM-PDE")
+        self.n = 30
+        self.layers1_node = [self.n * 2 + 2] + list(layers1) + [self.n]
+        self.n_layers1 = len(self.layers1_node) - 1
+        assert self.n_layers1 >= 1
+        self.layers = _mlp(self.layers1_node)
+        self.layers2_node = [self.n * 2 + 2] + list(layers2) + [self.n]
+        self.n_layers2 = len(self.layers2_node) - 1
+        self.layers2 = _mlp(self.layers2_node)
+        npts = ori_nx * ori_ny if ori_ny is not None else ori_nx
+        self.layers3_node = [npts] + list(layers3) + [npts]
+        self.n_layers3 = len(self.layers3_node) - 1
+        self.layers3 = _mlp(self.layers3_node)   # built but never used (interpolate.py:48-60)
+        self.conv = ori_ny is not None
+        if self.conv:
+            c = layers3
+            self.down = nn.Sequential(
+                nn.Conv2d(c[0], c[1], 5, padding=2), nn.Tanh(),
+                nn.Conv2d(c[1], c[2], 5, padding=2), nn.Tanh(),
+                nn.Conv2d(c[2], c[3], 5, padding=2), nn.Tanh(),
+                nn.Conv2d(c[3], c[4], 5, padding=2), nn.Tanh())
+        else:
+            self.down = nn.Sequential(
+                nn.Linear(ori_nx, 2048), nn.Tanh(), nn.Linear(2048, 512), nn.Tanh(),
+                nn.Linear(512, 2048), nn.Tanh(), nn.Linear(2048, ori_nx))
+        self._packs = {}
+
+    # ----------------------------------------------------------------- packing
+    def packed(self, mode: str) -> torch.Tensor:
+        """Weights of mode '1' / '2' re-laid as the MFMA operand image of
+        mmpde_itp_interp (cached until a parameter changes)."""
+        mods = self.layers if mode == "1" else self.layers2
+        if [m.out_features for m in mods] != [128, 64, 30] or mods[0].in_features != 62:
+            raise NotImplementedError("fused ItpNet kernel needs layers [62, 128, 64, 30] "
+                                      "(the reference defaults --itpnet_node1/2 = 128,64)")
+        ts = [t for m in mods for t in (m.weight, m.bias)]
+        key = tuple((t.data_ptr(), t._version) for t in ts)
+        hit = self._packs.get(mode)
+        if hit is not None and hit[0] == key:
+            return hit[1]
+        L.require_device(*ts)
+        f = [L.f32c(t) for t in ts]
+        mlp = L.ItpMlp(*[t.data_ptr() for t in f])
+        buf = torch.empty((L.lib().mmpde_itp_pack_bytes() // 4,), dtype=torch.float32,
+                          device=f[0].device)
+        L.check(L.lib().mmpde_itp_pack(ctypes.byref(mlp), L.ptr(buf), L.stream(buf.device)),
+                "mmpde_itp_pack")
+        self._packs[mode] = (key, buf, f)
+        return buf
+
+    def res_cut(self, data: torch.Tensor) -> torch.Tensor:
+        """``down`` network (interpolate.py:95-97): data [B, N] (cylinder) or
+        [B, 1, s, s] (Burgers)."""
+        L.require_device(data)
+        d = self.down
+        if self.conv:
+            x = data
+            for i in (0, 2, 4, 6):
+                x = ops.conv2d(x, d[i].weight, d[i].bias, 1, 2, L.ACT_TANH)
+            return x
+        x = data.reshape(data.shape[0], -1)
+        for i, act in ((0, L.ACT_TANH), (2, L.ACT_TANH), (4, L.ACT_TANH), (6, L.ACT_NONE)):
+            x = ops.linear_skinny(x, d[i].weight, d[i].bias, act)
+        return x
+
+    def forward(self, neighbors, query_points, mode, data=None):
+        if self.training:
+            raise NotImplementedError("training-mode forward is out of scope; call .eval()")
+        if mode == "res_cut":
+            return self.res_cut(data)
+        raise NotImplementedError(
+            "modes '1'/'2' are fused with the kNN-30 search and the weighted sum: call "
+            "GraphCreator_FS_2D.interpolate (mmpde_itp_interp)")

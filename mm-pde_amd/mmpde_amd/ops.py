@@ -1,0 +1,113 @@
+"""Tensor-level wrappers over the C-ABI (one function per entry point).
+
+Every function launches on the current torch stream of the input's device and
+returns new device tensors; nothing here synchronises or falls back to CPU.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib as L
+
+
+def knn_graph_nbr(pos: torch.Tensor, batches: int, k: int, count_degenerate: bool = False):
+    """torch_cluster.knn_graph(pos, k, batch, loop=False) for `batches` equal
+    contiguous segments (reference data_creator_2d.py:260, dmm_model.py:228).
+    Returns nbr [n, k] int32 (global source indices, (d2, index) order)
+    [, degenerate count tensor]."""
+    L.require_device(pos)
+    pos = L.f32c(pos).reshape(-1, 2)
+    n = pos.shape[0]
+    if n % batches:
+        raise ValueError("pos rows must split into equal batch segments")
+    nbr = torch.empty((n, k), dtype=torch.int32, device=pos.device)
+    deg = torch.zeros((1,), dtype=torch.int32, device=pos.device) if count_degenerate else None
+    L.check(L.lib().mmpde_knn_graph(L.ptr(pos), batches, n // batches, k, L.ptr(nbr),
+                                    L.ptr(deg), L.stream(pos.device)), "mmpde_knn_graph")
+    return (nbr, deg) if count_degenerate else nbr
+
+
+def edge_index_from_nbr(nbr: torch.Tensor) -> torch.Tensor:
+    """PyG edge_index int64 [2, n*k] (row 0 source, row 1 target)."""
+    L.require_device(nbr)
+    n, k = nbr.shape
+    ei = torch.empty((2, n * k), dtype=torch.int64, device=nbr.device)
+    L.check(L.lib().mmpde_edge_index_from_nbr(L.ptr(nbr.contiguous()), n, k, L.ptr(ei),
+                                              L.stream(nbr.device)), "mmpde_edge_index_from_nbr")
+    return ei
+
+
+def nbr_from_edge_index(edge_index: torch.Tensor, n: int) -> torch.Tensor:
+    """Recover the fixed-degree target-major table from a PyG edge_index whose
+    targets are grouped (the layout knn_graph produces).  Raises on ragged
+    degree (only possible for degenerate point sets)."""
+    e = edge_index.shape[1]
+    if e % n:
+        raise ValueError("edge_index has ragged in-degree; fixed-degree kernels need k*n edges")
+    k = e // n
+    tgt = torch.arange(n, device=edge_index.device).repeat_interleave(k)
+    if not bool(torch.equal(edge_index[1], tgt)):
+        raise ValueError("edge_index targets are not grouped as knn_graph emits them")
+    return edge_index[0].reshape(n, k).to(torch.int32).contiguous()
+
+
+def knn_query(src: torch.Tensor, qry: torch.Tensor, batches: int, k: int) -> torch.Tensor:
+    """Per-trajectory sklearn NearestNeighbors(k).fit(src_b).kneighbors(qry_b):
+    LOCAL indices int32 [batches * n_qry, k], fp64-distance order
+    (reference data_creator_2d.py:66-78)."""
+    L.require_device(src, qry)
+    src = L.f32c(src).reshape(-1, 2)
+    qry = L.f32c(qry).reshape(-1, 2)
+    ns, nq = src.shape[0] // batches, qry.shape[0] // batches
+    idx = torch.empty((batches * nq, k), dtype=torch.int32, device=src.device)
+    L.check(L.lib().mmpde_knn_query(L.ptr(src), L.ptr(qry), batches, ns, nq, k, L.ptr(idx),
+                                    L.stream(src.device)), "mmpde_knn_query")
+    return idx
+
+
+def linear_skinny(x: torch.Tensor, w: torch.Tensor, b=None, act: int = L.ACT_NONE,
+                  out: torch.Tensor | None = None) -> torch.Tensor:
+    """act(x @ w.T + b) for a few rows (M = trajectories)."""
+    L.require_device(x, w)
+    x = L.f32c(x)
+    w = L.f32c(w)
+    m, k = x.shape
+    n = w.shape[0]
+    y = out if out is not None else torch.empty((m, n), dtype=torch.float32, device=x.device)
+    L.check(L.lib().mmpde_linear_skinny(L.ptr(x), k, m, k, L.ptr(w), k,
+                                        L.ptr(L.f32c(b)) if b is not None else None, n, act,
+                                        L.ptr(y), n, L.stream(x.device)), "mmpde_linear_skinny")
+    return y
+
+
+def conv2d(x: torch.Tensor, w: torch.Tensor, b, stride: int, pad: int, act: int,
+           residual=None) -> torch.Tensor:
+    """act(conv2d(x, w, b, stride, pad) [+ residual]), NCHW fp32."""
+    L.require_device(x, w)
+    x = L.f32c(x)
+    bt, cin, h, wd = x.shape
+    cout, _, ks, _ = w.shape
+    oh = (h + 2 * pad - ks) // stride + 1
+    ow = (wd + 2 * pad - ks) // stride + 1
+    y = torch.empty((bt, cout, oh, ow), dtype=torch.float32, device=x.device)
+    L.check(L.lib().mmpde_conv2d(L.ptr(x), bt, cin, h, wd, L.ptr(L.f32c(w)),
+                                 L.ptr(L.f32c(b)) if b is not None else None, cout, ks, stride,
+                                 pad, L.ptr(residual), act, L.ptr(y), L.stream(x.device)),
+            "mmpde_conv2d")
+    return y
+
+
+def itp_interp(src, vals, qry, idx, batches: int, packed: torch.Tensor, addend=None):
+    """ItpNet weights + weighted neighbour sum (interpolate.py:77-93,
+    data_creator_2d.py:80-83).  Returns [batches * n_qry] fp32."""
+    L.require_device(src, vals, qry, idx, packed)
+    src = L.f32c(src).reshape(-1, 2)
+    qry = L.f32c(qry).reshape(-1, 2)
+    vals = L.f32c(vals).reshape(-1)
+    ns, nq = src.shape[0] // batches, qry.shape[0] // batches
+    out = torch.empty((batches * nq,), dtype=torch.float32, device=src.device)
+    add = L.f32c(addend).reshape(-1) if addend is not None else None
+    L.check(L.lib().mmpde_itp_interp(L.ptr(src), L.ptr(vals), L.ptr(qry), L.ptr(idx.contiguous()),
+                                     batches, ns, nq, L.ptr(packed), L.ptr(add), L.ptr(out),
+                                     L.stream(src.device)), "mmpde_itp_interp")
+    return out

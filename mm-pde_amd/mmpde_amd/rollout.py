@@ -1,0 +1,121 @@
+"""Autoregressive MM-PDE rollout engine (the benchmarked hot path).
+
+One step is the forward of train_helper_2d.py:479-488 (test_timestep_losses),
+composed directly on the C-ABI with every buffer preallocated:
+
+    pred = interpolate_pred(itp, model_b(graph_moved), graph_moved, data) + model(graph_uni)
+
+cylinder (DMM graph mode):
+    mesh   = DMM.mesh(u, grid)                      # x = xi + d(phi)/d(xi)
+    nbr_m  = knn_graph(mesh, k=35)                  # moved-mesh graph (every step)
+    out_b  = model_b(u, (t, mesh), nbr_m)
+    idx    = knn_query(src=mesh, qry=grid, k=30)    # sklearn replacement
+    pred   = itp_interp(mesh, out_b, grid, idx, '2') + res_cut(u) + model(u, (t, grid), nbr_u)
+Burgers (DMM array mode) additionally interpolates u onto the moved mesh first
+(ItpNet mode '1'); the reference's interpolation of the *labels* onto the
+moved mesh (data_creator_2d.py:208-209) feeds only graph.y, which no step
+reads, so the rollout (which has no labels) does not compute it.
+
+Rollout: the prediction becomes the next step's input (u <- pred, t index + 1),
+which the reference itself never does (it only evaluates one-step losses,
+SURVEY.md §3); ``step`` is that one-step forward.  The fixed-grid graph
+(``nbr_u``) is built once at construction (it depends only on the grid).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib as L
+from . import ops
+
+
+class MMPDERollout:
+    def __init__(self, kind, model, model_b, itp, dmm, graph_creator, batches: int, device,
+                 moving_mesh: bool = True):
+        self.kind = kind
+        self.model, self.model_b, self.itp, self.dmm = model, model_b, itp, dmm
+        self.gc = graph_creator
+        self.B = batches
+        self.device = torch.device(device)
+        self.moving_mesh = moving_mesh
+        self.trace_hook = None   # callable() -> _lib.GnnTrace | None, one per GNN forward
+        gc = graph_creator
+        self.grid = gc.uniform_grid(self.device).contiguous()           # [N, 2]
+        self.N = N = self.grid.shape[0]
+        self.n = n = batches * N
+        self.grid_rep = self.grid.repeat(batches, 1).contiguous()        # [B*N, 2]
+        self.nbr_u = gc.fixed_graph_nbr(self.grid, batches)
+        self.t = gc.time_grid()
+        f32 = dict(dtype=torch.float32, device=self.device)
+        self.pos_u = torch.empty((n, 3), **f32)
+        self.pos_u[:, 1:3] = self.grid_rep
+        self.pos_m = torch.empty((n, 3), **f32)
+        self.out_u = torch.empty((n, 1), **f32)
+        self.out_b = torch.empty((n, 1), **f32)
+        self.ws_gnn = torch.empty((L.lib().mmpde_gnn_workspace_bytes(n) // 4,), **f32)
+        if moving_mesh:
+            hd = dmm.device_params()[1]
+            self.ws_dmm = torch.empty(
+                (L.lib().mmpde_dmm_workspace_bytes(batches, N, hd.latent, hd.hidden) // 4,), **f32)
+            self.mesh = torch.empty((n, 2), **f32)
+            if kind == "burgers":
+                s = int(round(N ** 0.5))
+                self.s = s
+                self.xi = gc.xi_grid_xy(s, s, self.device)
+            else:
+                self.xi = self.grid
+            for mode in ("1", "2") if kind == "burgers" else ("2",):
+                itp.packed(mode)
+
+    def _trace(self):
+        return self.trace_hook() if self.trace_hook is not None else None
+
+    def _set_t(self, pos, step_idx):
+        pos[:, 0].fill_(float(self.t[step_idx]))
+
+    def step(self, u: torch.Tensor, step_idx: int) -> torch.Tensor:
+        """u: [B, N] (cylinder) or [B, s, s] (Burgers) on the device -> pred, same shape."""
+        B, N = self.B, self.N
+        u = u.contiguous()
+        u_flat = u.reshape(-1)
+        self._set_t(self.pos_u, step_idx)
+        if not self.moving_mesh:
+            return self.model(_Nodes(u_flat, self.pos_u, self.nbr_u), out=self.out_u,
+                              workspace=self.ws_gnn, trace=self._trace()).reshape(u.shape)
+        mesh = self.dmm.mesh(u, self.xi, out=self.mesh, workspace=self.ws_dmm)
+        self.pos_m[:, 1:3] = mesh
+        self._set_t(self.pos_m, step_idx)
+        nbr_m = ops.knn_graph_nbr(mesh, B, self.gc.n)
+        if self.kind == "burgers":
+            idx1 = ops.knn_query(self.grid_rep, mesh, B, 30)
+            u_m = ops.itp_interp(self.grid_rep, u_flat, mesh, idx1, B, self.itp.packed("1"))
+            res = self.itp.res_cut(u.reshape(B, 1, self.s, self.s)).reshape(-1)
+        else:
+            u_m = u_flat
+            res = self.itp.res_cut(u.reshape(B, N)).reshape(-1)
+        out_b = self.model_b(_Nodes(u_m, self.pos_m, nbr_m), out=self.out_b,
+                             workspace=self.ws_gnn, trace=self._trace())
+        idx2 = ops.knn_query(mesh, self.grid_rep, B, 30)
+        interp = ops.itp_interp(mesh, out_b, self.grid_rep, idx2, B, self.itp.packed("2"),
+                                addend=res)
+        out_u = self.model(_Nodes(u_flat, self.pos_u, self.nbr_u), out=self.out_u,
+                           workspace=self.ws_gnn, trace=self._trace())
+        return torch.add(interp, out_u.reshape(-1)).reshape(u.shape)
+
+    def rollout(self, u0: torch.Tensor, start_step: int, n_steps: int):
+        """Feed each prediction back as the next input; returns the final state."""
+        u = u0
+        for s in range(start_step, start_step + n_steps):
+            u = self.step(u, s)
+        return u
+
+
+class _Nodes:
+    """The three graph fields the solver reads (x, pos, nbr)."""
+    __slots__ = ("x", "pos", "nbr", "edge_index")
+
+    def __init__(self, x, pos, nbr):
+        self.x = x.reshape(-1, 1)
+        self.pos = pos
+        self.nbr = nbr
+        self.edge_index = None

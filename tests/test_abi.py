@@ -1,0 +1,53 @@
+"""The C-ABI library loads without a GPU and exports exactly what include/*.h declares."""
+import ctypes
+import os
+import re
+
+from conftest import ROOT
+
+
+def _declared():
+    names = set()
+    for f in os.listdir(os.path.join(ROOT, "include")):
+        if f.endswith(".h"):
+            src = open(os.path.join(ROOT, "include", f)).read()
+            src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+            names |= set(re.findall(r"\b(mmpde_[a-z0-9_]+)\s*\(", src))
+    return names
+
+
+def test_header_declares_entry_points():
+    names = _declared()
+    for must in ("mmpde_knn_graph", "mmpde_knn_query", "mmpde_gnn_forward", "mmpde_gnn_edge_mean",
+                 "mmpde_dmm_mesh_graph", "mmpde_dmm_mesh_array", "mmpde_itp_interp"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    from mmpde_amd import _lib
+
+    h = ctypes.CDLL(_lib.LIB_PATH)
+    for name in _declared():
+        assert hasattr(h, name), name
+    assert set(_lib.EXPORTS) == _declared()
+
+
+def test_version_and_status_strings_without_gpu():
+    from mmpde_amd import _lib
+
+    lib = _lib.lib()
+    assert lib.mmpde_version() == _lib.ABI_VERSION
+    assert lib.mmpde_status_string(0) == b"ok"
+    assert lib.mmpde_status_string(-1) == b"invalid argument"
+    # sizing helpers are pure host arithmetic
+    assert lib.mmpde_gnn_workspace_bytes(1000) == 6 * 1000 * 128 * 4
+    assert lib.mmpde_itp_pack_bytes() > 0
+
+
+def test_null_arguments_are_rejected_before_launch():
+    from mmpde_amd import _lib
+
+    lib = _lib.lib()
+    assert lib.mmpde_knn_graph(None, 1, 100, 35, None, None, None) == -1
+    assert lib.mmpde_gnn_edge_mean(None, None, None, 10, 35, None, None, None, None) == -1
+    assert lib.mmpde_linear_skinny(None, 1, 1, 1, None, 1, None, 1, 0, None, 1, None) == -1

@@ -1,0 +1,331 @@
+"""GPU parity: every HIP stage against the CPU oracle on identical inputs.
+
+Bars (stated per test):
+* neighbour index maps (knn_graph, knn_query): bit-exact;
+* fp32 floating point: max|hip - oracle| <= RTOL * max|oracle| + ATOL with the
+  tolerance written in each test (fp32 MFMA products are exact; differences
+  come from summation order and the factored message_net_1).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle import refcpu
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(got, ref, rtol, atol=0.0, what=""):
+    got = got.detach().float().cpu().reshape(-1)
+    ref = ref.detach().float().cpu().reshape(-1)
+    err = (got - ref).abs().max().item()
+    bound = rtol * ref.abs().max().item() + atol
+    print(f"{what}: max|err| {err:.3e} bound {bound:.3e} max|ref| {ref.abs().max().item():.3e}")
+    assert err <= bound, (what, err, bound)
+
+
+def _sds(**mods):
+    return {k: {n: t.detach().cpu() for n, t in m.state_dict().items()} for k, m in mods.items()}
+
+
+# ============================================================================ kNN graph
+def _graph_case(pos, B, dev, k=35):
+    from mmpde_amd import ops
+
+    nbr, deg = ops.knn_graph_nbr(pos.to(dev), B, k, count_degenerate=True)
+    _, ref, rdeg = refcpu.knn_graph(pos, k, B)
+    assert int(deg.item()) == rdeg
+    assert torch.equal(nbr.cpu().long(), ref)
+
+
+def test_knn_graph_cy_mesh_bit_exact(dev):
+    from mmpde_amd.synth import cy_synth_mesh
+
+    g = cy_synth_mesh()
+    moved = g + 0.01 * torch.sin(7 * g.flip(1))            # a moved-mesh-like input
+    _graph_case(torch.cat((g, moved)), 2, dev)
+
+
+def test_knn_graph_burgers_grid_ties_bit_exact(dev):
+    from mmpde_amd.synth import burgers_grid_points
+
+    _graph_case(burgers_grid_points().repeat(2, 1), 2, dev)   # linspace grid: ties at the cut
+
+
+def test_knn_graph_integer_lattice_golden(dev):
+    from mmpde_amd import ops
+
+    g = np.load(f"{GOLDEN}/knn35_lattice.npz")
+    nbr = ops.knn_graph_nbr(torch.from_numpy(g["pos"]).to(dev), 1, 35)
+    assert np.array_equal(nbr.cpu().numpy(), g["nbr"])
+
+
+@pytest.mark.parametrize("n,B", [(36, 3), (100, 5), (640, 2), (4096, 1), (3000, 2)])
+def test_knn_graph_sizes(dev, n, B):
+    torch.manual_seed(n)
+    _graph_case(torch.rand(n * B, 2), B, dev)
+
+
+def test_knn_graph_duplicates(dev):
+    pos = torch.rand(200, 2)
+    pos[50:100] = pos[3]                                       # 51 coincident points
+    pos[120:125] = pos[7]
+    _graph_case(pos, 1, dev)
+
+
+# ============================================================================ kNN-30 query
+def test_knn_query_sklearn_golden(dev):
+    from mmpde_amd import ops
+
+    g = np.load(f"{GOLDEN}/sklearn_knn30.npz")
+    B = g["src"].shape[0]
+    idx = ops.knn_query(torch.from_numpy(g["src"]).to(dev), torch.from_numpy(g["qry"]).to(dev),
+                        B, 30)
+    assert np.array_equal(idx.cpu().numpy().reshape(g["idx"].shape), g["idx"])
+
+
+@pytest.mark.parametrize("ns,nq,B", [(2521, 2521, 2), (30, 7, 2), (2304, 2304, 1), (4096, 50, 1)])
+def test_knn_query_bit_exact(dev, ns, nq, B):
+    from mmpde_amd import ops
+
+    torch.manual_seed(ns + nq)
+    src, qry = torch.rand(B * ns, 2), torch.rand(B * nq, 2)
+    qry[:3] = src[:3]                                          # zero-distance hits
+    idx = ops.knn_query(src.to(dev), qry.to(dev), B, 30)
+    ref = refcpu.knn_query(src, qry, B, 30)
+    assert torch.equal(idx.cpu().long().reshape(ref.shape), ref)
+
+
+def test_knn_query_lattice_ties(dev):
+    from mmpde_amd import ops
+
+    src = torch.tensor([[float(i), float(j)] for i in range(10) for j in range(10)])
+    qry = src[torch.randperm(100)[:20]] + 0.5 * (torch.rand(20, 2) > 0.5)
+    idx = ops.knn_query(src.to(dev), qry.to(dev), 1, 30)
+    assert torch.equal(idx.cpu().long(), refcpu.knn_query(src, qry, 1, 30)[0])
+
+
+# ============================================================================ GNN
+def _gnn_inputs(kind, B, seed=0):
+    from mmpde_amd.synth import build_models, burgers_grid_points
+
+    pde, model, _, _, _, gc = build_models(kind, moving_mesh=False, seed=seed)
+    pts = pde.ori_grid if kind == "cy" else burgers_grid_points()
+    torch.manual_seed(seed + 7)
+    n = B * pts.shape[0]
+    pos = torch.cat((torch.full((n, 1), float(gc.time_grid()[5])), pts.repeat(B, 1)), 1)
+    u = torch.randn(n, 1)
+    ei, nbr, _ = refcpu.knn_graph(pts.repeat(B, 1), 35, B)
+    return pde, model, u, pos, ei, nbr
+
+
+@pytest.mark.parametrize("kind", ["cy", "burgers"])
+def test_gnn_forward_matches_oracle(dev, kind):
+    from mmpde_amd.rollout import _Nodes
+
+    pde, model, u, pos, ei, nbr = _gnn_inputs(kind, 2)
+    opde = refcpu.PDEConst(kind, pde.grid_size, ori_grid=getattr(pde, "ori_grid", None))
+    ref, hs = refcpu.mp_pde_solver(_sds(m=model)["m"], opde, u, pos, ei, return_hidden=True)
+    model.to(dev)
+    out = model(_Nodes(u.to(dev), pos.to(dev), nbr.int().to(dev)))
+    # fp32 tolerance for 6 BN'd layers + head: 2e-4 of the output range
+    _close(out, ref, 2e-4, 1e-7, f"gnn {kind}")
+
+
+def test_gnn_layer_api_and_edge_index_input(dev):
+    """Layer-level reference API (x, u, pos_x, pos_y, variables, edge_index, batch)
+    and a PyG-style edge_index input both run the HIP path."""
+    pde, model, u, pos, ei, nbr = _gnn_inputs("cy", 1)
+    sd = _sds(m=model)["m"]
+    h = torch.randn(u.shape[0], 128)
+    px, py, pt = pos[:, 1:2], pos[:, 2:3], pos[:, 0:1] / 2.9
+    ref = refcpu.gnn_layer(sd, "gnn_layers.0", h, u, px, py, pt, ei)
+    model.to(dev)
+    got = model.gnn_layers[0](h.to(dev), u.to(dev), px.to(dev), py.to(dev), pt.to(dev),
+                              ei.to(dev), None)
+    _close(got, ref, 5e-5, 1e-6, "gnn layer")
+
+    class G:
+        x, pos, edge_index, nbr = u.to(dev), pos.to(dev), ei.to(dev), None
+    ref2 = refcpu.mp_pde_solver(sd, refcpu.PDEConst("cy", pde.grid_size), u, pos, ei)
+    _close(model(G()), ref2, 2e-4, 1e-7, "gnn edge_index input")
+
+
+def test_edge_mean_vs_torch_fp32(dev):
+    """The hot kernel alone against a plain torch fp32 evaluation of
+    mean_e relu(W2 relu(a_i + b_nbr) + b2)."""
+    from mmpde_amd import _lib as L
+
+    torch.manual_seed(1)
+    n, k = 3000, 35
+    a, b = torch.randn(n, 128), torch.randn(n, 128)
+    nbr = torch.randint(0, n, (n, k), dtype=torch.int32)
+    w2, b2 = torch.randn(128, 128) / 11, torch.randn(128) / 10
+    m1 = torch.relu(a[:, None, :] + b[nbr.long()])
+    ref = torch.relu(m1 @ w2.T + b2).mean(1)
+    d = [t.to(dev) for t in (a, b, nbr, w2, b2)]
+    out = torch.empty(n, 128, device=dev)
+    L.check(L.lib().mmpde_gnn_edge_mean(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), n, k,
+                                        d[3].data_ptr(), d[4].data_ptr(), out.data_ptr(),
+                                        L.stream(dev)), "edge_mean")
+    _close(out, ref, 1e-5, 1e-6, "edge_mean")
+
+
+# ============================================================================ DMM
+def test_dmm_mesh_graph_matches_autograd(dev):
+    from mmpde_amd.synth import build_models, fields
+
+    pde, _, _, _, dmm, _ = build_models("cy")
+    grid = pde.ori_grid
+    B = 3
+    u = fields(grid, B, 30)[:, 4]
+    ref_x, ref_y = refcpu.moving_mesh_tri(_sds(d=dmm)["d"], u, grid[None, :, 0].repeat(B, 1),
+                                         grid[None, :, 1].repeat(B, 1), grid)
+    ref = torch.cat((ref_x, ref_y), -1)
+    dmm.to(dev)
+    got = dmm.mesh(u.to(dev), grid.to(dev))
+    disp = (ref - grid.repeat(B, 1)).abs().max().item()
+    assert disp > 1e-3                                         # the mesh actually moves
+    _close(got, ref, 0.0, 2e-6, "dmm graph mesh")              # absolute, coords in [0,1]
+
+
+def test_dmm_mesh_array_matches_autograd(dev):
+    from mmpde_amd.synth import build_models, burgers_grid_points, fields
+
+    pde, _, _, _, dmm, gc = build_models("burgers")
+    B = 3
+    u = fields(burgers_grid_points(), B, 31).reshape(B, 31, 48, 48)[:, 4]
+    ox, oy = refcpu.moving_mesh(_sds(d=dmm)["d"], refcpu.PDEConst("burgers", [31, 48, 48]), u,
+                                48, 48)
+    ref = torch.cat((ox, oy), -1)
+    dmm.to(dev)
+    got = dmm.mesh(u.to(dev).contiguous(), gc.xi_grid_xy(48, 48, dev))
+    _close(got, ref, 0.0, 2e-6, "dmm array mesh")
+
+
+# ============================================================================ ItpNet
+@pytest.mark.parametrize("mode", ["1", "2"])
+def test_itp_interp_matches_oracle(dev, mode):
+    from mmpde_amd import ops
+    from mmpde_amd.synth import build_models
+
+    pde, _, _, itp, _, _ = build_models("cy")
+    B, N = 2, pde.ori_grid.shape[0]
+    torch.manual_seed(2)
+    src = pde.ori_grid.repeat(B, 1) + 0.01 * torch.randn(B * N, 2)
+    qry = pde.ori_grid.repeat(B, 1)
+    vals = torch.randn(B, N)
+    ref, idx = refcpu.interpolate(_sds(i=itp)["i"], vals, src[:, :1], src[:, 1:], qry[:, :1],
+                                  qry[:, 1:], mode, return_idx=True)
+    itp.to(dev)
+    got = ops.itp_interp(src.to(dev), vals.to(dev), qry.to(dev),
+                         idx.reshape(B * N, 30).int().to(dev), B, itp.packed(mode))
+    _close(got, ref, 2e-5, 1e-6, f"itp mode {mode}")
+
+
+@pytest.mark.parametrize("kind", ["cy", "burgers"])
+def test_res_cut_matches_oracle(dev, kind):
+    from mmpde_amd.synth import build_models
+
+    _, _, _, itp, _, _ = build_models(kind)
+    torch.manual_seed(4)
+    x = torch.randn(3, 2521) if kind == "cy" else torch.randn(3, 1, 48, 48)
+    ref = refcpu.itpnet(_sds(i=itp)["i"], None, None, "res_cut", data=x, burgers=kind != "cy")
+    itp.to(dev)
+    _close(itp(None, None, "res_cut", data=x.to(dev)), ref, 1e-5, 1e-6, f"res_cut {kind}")
+
+
+# ============================================================================ full step
+@pytest.mark.parametrize("kind", ["cy", "burgers"])
+def test_mmpde_step_matches_oracle(dev, kind):
+    """One MM-PDE step (train_helper_2d.py:479-488) through the rollout engine vs
+    the oracle; the oracle uses the engine's moved mesh (mesh_override) so the
+    kNN stages see identical coordinates -- the mesh itself is checked above."""
+    from mmpde_amd.rollout import MMPDERollout
+    from mmpde_amd.synth import build_models, burgers_grid_points, fields
+
+    pde, model, model_b, itp, dmm, gc = build_models(kind)
+    B, step = 2, 6
+    if kind == "cy":
+        data = fields(pde.ori_grid, B, 30)[:, step - 1:step]
+        opde = refcpu.PDEConst("cy", pde.grid_size, ori_grid=pde.ori_grid)
+    else:
+        data = fields(burgers_grid_points(), B, 31).reshape(B, 31, 48, 48)[:, step - 1:step]
+        opde = refcpu.PDEConst("burgers", pde.grid_size)
+    sds = _sds(model=model, model_b=model_b, itp=itp, dmm=dmm)
+    for m in (model, model_b, itp, dmm):
+        m.to(dev)
+    eng = MMPDERollout(kind, model, model_b, itp, dmm, gc, B, dev)
+    pred = eng.step(data[:, 0].to(dev), step)
+    ref, aux = refcpu.mmpde_step(opde, sds, data, data, [step] * B, mesh_override=eng.mesh.cpu())
+    assert torch.equal(eng.nbr_u.cpu().long(), aux["graph_uni"].nbr)
+    _close(pred, ref, 2e-5, 1e-6, f"mmpde step {kind}")
+
+
+def test_gnn_only_step_matches_oracle(dev):
+    from mmpde_amd.rollout import MMPDERollout
+    from mmpde_amd.synth import build_models, fields
+
+    pde, model, _, _, _, gc = build_models("cy", moving_mesh=False)
+    B, step = 3, 3
+    data = fields(pde.ori_grid, B, 30)[:, step - 1:step]
+    ref, _ = refcpu.mmpde_step(refcpu.PDEConst("cy", pde.grid_size, ori_grid=pde.ori_grid),
+                               _sds(model=model), data, data, [step] * B, moving_mesh=False)
+    model.to(dev)
+    eng = MMPDERollout("cy", model, None, None, None, gc, B, dev, moving_mesh=False)
+    _close(eng.step(data[:, 0].to(dev), step), ref, 2e-4, 1e-7, "gnn-only step")
+
+
+def test_graph_creator_api(dev):
+    """The drop-in GraphCreator path (create_graph / interpolate_pred) equals the engine."""
+    from mmpde_amd.rollout import MMPDERollout
+    from mmpde_amd.synth import build_models, fields
+
+    pde, model, model_b, itp, dmm, gc = build_models("cy")
+    for m in (model, model_b, itp, dmm):
+        m.to(dev)
+    B, step = 2, 4
+    u = fields(pde.ori_grid, B, 30)
+    data, labels = gc.create_data(u, [step] * B)
+    graph = gc.create_graph(itp, data, labels, [step] * B, dev, dmm)
+    graph_uni = gc.create_graph(itp, data, labels, [step] * B, dev, None)
+    pred = gc.interpolate_pred(itp, model_b(graph), graph, data, dev) + model(graph_uni)
+    eng = MMPDERollout("cy", model, model_b, itp, dmm, gc, B, dev)
+    pe = eng.step(data[:, 0].to(dev), step)
+    assert torch.equal(pred.reshape(-1), pe.reshape(-1))
+    ei = graph.edge_index
+    assert ei.dtype == torch.int64 and ei.shape == (2, B * 2521 * 35)
+    assert torch.equal(ei[0].reshape(-1, 35).int(), graph.nbr)
+
+
+# ============================================================================ full size
+def test_full_size_properties(dev):
+    """BASELINE config 4 size (16 x 2521 nodes): properties the oracle is too slow
+    to check end to end -- graph validity, determinism, finite rollout."""
+    from mmpde_amd import ops
+    from mmpde_amd.rollout import MMPDERollout
+    from mmpde_amd.synth import build_models, fields
+
+    pde, model, model_b, itp, dmm, gc = build_models("cy")
+    for m in (model, model_b, itp, dmm):
+        m.to(dev)
+    B, N = 16, 2521
+    eng = MMPDERollout("cy", model, model_b, itp, dmm, gc, B, dev)
+    u0 = fields(pde.ori_grid, B, 30)[:, 0].to(dev)
+    p1 = eng.step(u0, 1)
+    mesh = eng.mesh.clone()
+    p2 = eng.step(u0, 1)
+    assert torch.equal(p1, p2)                                  # bitwise deterministic
+    nbr = ops.knn_graph_nbr(mesh, B, 35).long().cpu()
+    rows = torch.arange(B * N)[:, None]
+    assert ((nbr // N) == rows // N).all()                      # within own trajectory
+    assert (nbr != rows).all()                                  # no self loops
+    m = mesh.cpu().double()
+    d = ((m[nbr] - m[:, None, :]) ** 2).sum(-1)
+    assert (d[:, 1:] >= d[:, :-1] - 1e-12).all()                # sorted by distance
+    # spot-check trajectory 11 against the oracle bit for bit
+    _, ref, _ = refcpu.knn_graph(mesh[11 * N:12 * N].cpu(), 35, 1)
+    assert torch.equal(nbr[11 * N:12 * N] - 11 * N, ref)
+    u = eng.rollout(u0, 1, 29)
+    assert torch.isfinite(u).all()
