@@ -263,14 +263,14 @@ __global__ __launch_bounds__(256) void head_kernel(const float *__restrict__ h, 
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        if (lane < 72) {
-            const int c = lane / 9, q = lane - c * 9;
+        for (int e = lane; e < 8 * 9; e += 64) {  // 72 outputs > 64 lanes
+            const int c = e / 9, q = e - c * 9;
             float v = sw2[384 + c];
             for (int ci = 0; ci < 4; ++ci) {
 #pragma unroll
                 for (int t = 0; t < 12; ++t) v += sw2[(c * 4 + ci) * 12 + t] * y1[wave][ci * 38 + 3 * q + t];
             }
-            y2[wave][lane] = fmaxf(v, 0.0f);
+            y2[wave][e] = fmaxf(v, 0.0f);
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();

@@ -87,9 +87,13 @@ int64_t knn_graph_oracle(const float *pos, int64_t batches, int64_t n_per, int k
                 insert_f(bd, bi, kk, d, j);
             }
             int64_t *row = nbr_out + (b * n_per + q) * k;
-            int w = 0, self_seen = 0;
+            int self_seen = 0;
+            for (int e = 0; e < kk; ++e) self_seen |= (bi[e] == q);
+            /* drop the self loop (mask row != col); without it the reference keeps
+             * k+1 edges -- here the first k, counted as degenerate */
+            int w = 0;
             for (int e = 0; e < kk && w < k; ++e) {
-                if (bi[e] == q && !self_seen) { self_seen = 1; continue; }
+                if (bi[e] == q) continue;
                 row[w++] = (bi[e] < 0) ? -1 : b * n_per + bi[e];
             }
             if (!self_seen || bi[kk - 1] < 0) degenerate++;

@@ -507,7 +507,7 @@ def mmpde_step(pde: PDEConst, sds, data, labels, steps, moving_mesh=True, mesh_o
                                  mesh_override=mesh_override,
                                  dmm_grid_edge_index=dmm_grid_edge_index)
         if graph_uni is None:
-            graph_uni = create_graph(pde, sds["itp"], data, labels, steps, dmm_sd=None)
+            graph_uni = create_graph(pde, sds.get("itp"), data, labels, steps, dmm_sd=None)
         out_u = mp_pde_solver(sds["model"], pde, graph_uni.x, graph_uni.pos, graph_uni.edge_index)
         if not moving_mesh:
             return out_u, {"graph_uni": graph_uni}

@@ -146,10 +146,10 @@ def test_gnn_layer_api_and_edge_index_input(dev):
                               ei.to(dev), None)
     _close(got, ref, 5e-5, 1e-6, "gnn layer")
 
-    class G:
-        x, pos, edge_index, nbr = u.to(dev), pos.to(dev), ei.to(dev), None
+    g = type("G", (), {"x": u.to(dev), "pos": pos.to(dev), "edge_index": ei.to(dev),
+                       "nbr": None})
     ref2 = refcpu.mp_pde_solver(sd, refcpu.PDEConst("cy", pde.grid_size), u, pos, ei)
-    _close(model(G()), ref2, 2e-4, 1e-7, "gnn edge_index input")
+    _close(model(g()), ref2, 2e-4, 1e-7, "gnn edge_index input")
 
 
 def test_edge_mean_vs_torch_fp32(dev):

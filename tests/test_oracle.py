@@ -56,12 +56,16 @@ def test_knn_graph_random_batches():
 
 
 def test_knn_graph_duplicates_are_degenerate():
-    pos = torch.zeros((40, 2))
-    pos[:, 0] = torch.arange(40) * 0.1
-    pos[5:] = pos[0]           # 35 copies of point 0 plus point 0 itself -> 36 at d=0
+    pos = torch.zeros((50, 2))
+    pos[:, 0] = torch.arange(50) * 0.1
+    pos[5:45] = pos[0]         # 41 coincident points {0, 5..44}
     _, nbr, deg = refcpu.knn_graph(pos, 35, 1)
-    assert deg >= 1
+    # the 36 nearest of each are {0, 5..39} (index order at d = 0): queries 40..44 lose
+    # their self loop -> ragged degree (36) in the reference
+    assert deg == 5
     assert (nbr >= 0).all()
+    assert 39 not in nbr[39].tolist()          # self dropped
+    assert nbr[40].tolist() == [0] + list(range(5, 39))
 
 
 # ----------------------------------------------------------------------------- kNN-30 query
