@@ -74,7 +74,7 @@ class HipEvents:
 
 
 class EdgeTracer:
-    """Hands out one GnnTrace (n_layers begin/end events) per GNN forward."""
+    """Hands out one GnnExec (n_layers begin/end events) per GNN forward."""
 
     def __init__(self, n_forwards, n_layers=6):
         from mmpde_amd import _lib
@@ -94,16 +94,17 @@ class EdgeTracer:
         base = 2 * self.L * i
         beg = (ctypes.c_void_p * self.L)(*self.pool.ev[base:base + self.L])
         end = (ctypes.c_void_p * self.L)(*self.pool.ev[base + self.L:base + 2 * self.L])
-        t = self._lib.GnnTrace(ctypes.cast(beg, ctypes.POINTER(ctypes.c_void_p)),
-                               ctypes.cast(end, ctypes.POINTER(ctypes.c_void_p)))
+        t = self._lib.GnnExec(ctypes.cast(beg, ctypes.POINTER(ctypes.c_void_p)),
+                              ctypes.cast(end, ctypes.POINTER(ctypes.c_void_p)), 0)
         self.traces.append((t, beg, end))
         return t
 
     def launch_times_ms(self):
+        """[(layer index, ms)] for every traced fused-layer launch."""
         out = []
         for _, beg, end in self.traces:
-            for a, b in zip(beg, end):
-                out.append(self.pool.elapsed_ms(a, b))
+            for l, (a, b) in enumerate(zip(beg, end)):
+                out.append((l, self.pool.elapsed_ms(a, b)))
         return out
 
 
@@ -156,6 +157,8 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="trajectories per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--edge-gemm", default="f32", choices=["f32", "f16x3"],
+                    help="message_net_2 arithmetic (include/mmpde_hip.h MMPDE_EDGE_GEMM_*)")
     args = ap.parse_args()
 
     from mmpde_amd import dist as D
@@ -176,6 +179,9 @@ def main():
     for m in (model, model_b, itp, dmm):
         if m is not None:
             m.to(device)
+    for m in (model, model_b):
+        if m is not None:
+            m.edge_gemm = args.edge_gemm
     if kind == "cy":
         pts, t_len = pde.ori_grid, 30
         u_all = fields(pts, total, t_len)[lo:hi]
@@ -207,20 +213,32 @@ def main():
     elapsed = D.max_over_ranks(local_s, device)
     finite = bool(torch.isfinite(u).all())
     launches = tracer.launch_times_ms()
-    edge_ms = sum(launches) / max(len(launches), 1)
     tracer.pool.close()
 
     if rank != 0:
         return
     n_local = (hi - lo) * n_nodes
-    flop_per_launch = n_local * gc.n * 2 * 128 * 128      # per target: k edges x 128x128 GEMV
-    achieved = flop_per_launch / (edge_ms * 1e-3) / 1e12
+    k = gc.n
+    # Algorithmic FLOP of one fused-layer launch (factored form):
+    # per node k edges x (128x128 message_net_2) + update_net_1 (257->128) +
+    # update_net_2 (128->128) + the next layer's message_net_1 node halves
+    # (128->256) on every layer but the last.
+    edge_f = k * 2 * 128 * 128
+    upd_f = 2 * 257 * 128 + 2 * 128 * 128
+    proj_f = 2 * 128 * 256
+    n_layers = 6
+    tot_flop = sum(n_local * (edge_f + upd_f + (proj_f if l < n_layers - 1 else 0))
+                   for l, _ in launches)
+    tot_ms = sum(ms for _, ms in launches)
+    launch_ms = tot_ms / max(len(launches), 1)
+    achieved = tot_flop / max(tot_ms * 1e-3, 1e-12) / 1e12
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", "edge_pmc_r01.json")
+    pmc = os.path.join(ROOT, "profiles", "fused_pmc_r01.json")
     if os.path.exists(pmc):
         with open(pmc) as f:
             rec = json.load(f)
-        if rec.get("workload") == args.config and rec.get("nodes") == n_local:
+        if (rec.get("workload") == args.config and rec.get("nodes") == n_local
+                and rec.get("edge_gemm") == args.edge_gemm):
             traffic = rec.get("hbm_bytes_per_launch")
     line = {
         "metric": METRIC if kind == "cy" else METRIC.replace("cylinder 2521-node mesh",
@@ -234,7 +252,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "f32" if args.edge_gemm == "f32" else "f32 (message_net_2 on fp16x3 split)",
         "data": "synthetic: seeded cy-synth 2521-node mesh / 48x48 grid, seeded sin-cos+noise "
                 "fields, seeded default-init weights (no dataset or checkpoint offline)",
         "config": {"workload": args.config, "baseline_config": cfg_name,
@@ -242,11 +260,13 @@ def main():
                    "nodes_per_trajectory": n_nodes, "neighbors": gc.n, "time_window": 1,
                    "parallelism": f"trajectory-shard x{world} (no data-path collective)",
                    "rollout": "autoregressive (pred -> next input)"},
-        "roofline": {"kernel": "edge_mean_kernel (GNN message_net_2 + mean, 12 launches/step)",
+        "roofline": {"kernel": "gnn_layer_fused_kernel (edge stage + update + next "
+                               "message_net_1, one launch per GNN layer, 12 per step)",
                      "bound": "mfma", "achieved": achieved, "peak": F32_MFMA_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved / F32_MFMA_PEAK_TFLOPS,
-                     "traffic": traffic, "launch_ms": edge_ms, "launches": len(launches),
-                     "flop_per_launch": flop_per_launch},
+                     "traffic": traffic, "launch_ms": launch_ms, "launches": len(launches),
+                     "flop_per_launch": tot_flop / max(len(launches), 1),
+                     "edge_gemm": args.edge_gemm},
         "finite": finite,
     }
     if world == 1 and not args.no_cpu_baseline:

@@ -169,20 +169,38 @@ int mmpde_gnn_forward(const float *u, const float *pos, int64_t n, int k, const 
                       const mmpde_gnn_head_params *head, void *workspace, float *out,
                       mmpde_stream_t stream);
 
-/* Same as mmpde_gnn_forward, plus optional instrumentation: when `trace` is
- * non-NULL, hipEventRecord(trace->edge_begin[l]) / (trace->edge_end[l]) are
- * issued on `stream` immediately before / after layer l's edge-stage kernel
- * (the dominant kernel), so a caller can time exactly that launch. */
+/* Arithmetic of the per-edge message_net_2 GEMM (the dominant work).
+ * F32   : v_mfma_f32_16x16x4_f32, exact fp32 products, fp32 accumulate
+ *         (bit-for-bit a k-ordered fmaf chain).
+ * F16X3 : fp32-emulating split GEMM (Ootomo & Yokota 2022 style): every fp32
+ *         operand x is scaled by a power of two (per weight column; per
+ *         neighbour slot for the activations) and split into fp16 hi + lo
+ *         (x = hi + lo to 2^-22 relative); the product uses hi*hi + hi*lo +
+ *         lo*hi on v_mfma_f32_16x16x32_f16 with fp32 accumulation.  Error vs
+ *         fp64 is measured beside F32 in tests/test_gpu_precision.py. */
+#define MMPDE_EDGE_GEMM_F32 0
+#define MMPDE_EDGE_GEMM_F16X3 1
+
+/* Execution options of mmpde_gnn_forward_ex (NULL = F32, no events). When
+ * edge_begin / edge_end are non-NULL, hipEventRecord(edge_begin[l]) /
+ * (edge_end[l]) are issued on `stream` immediately before / after layer l's
+ * fused layer kernel (edge stage + update + next layer's projections: the
+ * dominant kernel), so a caller can time exactly that launch. */
 typedef struct {
-    void *const *edge_begin; /* n_layers hipEvent_t */
-    void *const *edge_end;   /* n_layers hipEvent_t */
-} mmpde_gnn_trace;
+    void *const *edge_begin; /* n_layers hipEvent_t, or NULL */
+    void *const *edge_end;   /* n_layers hipEvent_t, or NULL */
+    int edge_gemm;           /* MMPDE_EDGE_GEMM_* */
+} mmpde_gnn_exec;
+
+/* Most layers mmpde_gnn_forward_ex accepts (sizes the workspace's packed
+ * weight region). */
+#define MMPDE_GNN_MAX_LAYERS 16
 
 int mmpde_gnn_forward_ex(const float *u, const float *pos, int64_t n, int k, const int32_t *nbr,
                          mmpde_gnn_scales sc, const mmpde_gnn_embed_params *emb,
                          const mmpde_gnn_layer_params *layers, int n_layers,
                          const mmpde_gnn_head_params *head, void *workspace, float *out,
-                         const mmpde_gnn_trace *trace, mmpde_stream_t stream);
+                         const mmpde_gnn_exec *exec, mmpde_stream_t stream);
 
 /* ------------------------------------------------------------------------
  * DMM mesh mover (reference mesh/dmm_model.py, data_creator_2d.py:88-137)

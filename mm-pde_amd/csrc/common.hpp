@@ -31,6 +31,22 @@ __device__ __forceinline__ int acc_row(int reg, int lane) {
     return (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
 }
 
+// v_mfma_f32_16x16x4_f32: lane l supplies A[l&15][l>>4] and B[l>>4][l&15];
+// D[4*(l>>4) + r][l&15] for register r (exact fp32, 32-cycle issue).
+__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// Blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, Workgroup
+// dispatch): remap so that each XCD walks a contiguous range of tiles (its L2
+// then holds the rows those tiles gather).  Bijective for any grid size; speed
+// only, never correctness.
+__device__ __forceinline__ int xcd_tile(int bid, int nb) {
+    const int q = nb >> 3, rem = nb & 7;
+    const int x = bid & 7, i = bid >> 3;
+    return x < rem ? x * (q + 1) + i : rem * (q + 1) + (x - rem) * q + i;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);

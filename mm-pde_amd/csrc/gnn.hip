@@ -233,6 +233,387 @@ __global__ __launch_bounds__(256, 2) void edge_mean_kernel(const float *__restri
 }
 
 // ---------------------------------------------------------------------------
+// Fused message-passing layer (the rollout's hot kernel): one launch per layer
+//   mean_i = (1/k) sum_e relu(W2 relu(a_i + b_nbr(i,e)) + b2)           edge stage
+//   v_i    = relu(U1 [h_i | mean_i | t_i] + c1)                         update_net_1
+//   h'_i   = BN(h_i + relu(U2 v_i + c2))                                update_net_2, BN
+//   a'_i, b'_i = next layer's message_net_1 halves of h'_i (NEXT only)  (see EpiProj)
+// (gnn_2d.py:53-69 twice over: this layer's update and the next layer's
+// message_net_1, so a layer costs one launch and h, a, b cross HBM once.)
+//
+// Workgroup = 16 target rows x 4 waves, v_mfma_f32_16x16x4_f32 throughout.
+// K index map for every 128-wide operand: lane l (row l&15, group g = l>>4)
+// holds k = 16 j + 4 g + t in component t of its float4 number j (j < 8), so a
+// row is read as 64-B contiguous pieces and MFMA step (j, t) consumes one float
+// per lane.  Edge stage: wave w takes neighbour slots e = w, w+4, ...; W2 sits
+// in LDS as the exact per-lane B image (64 KB, staged once per workgroup);
+// a_i stays in registers; b rows of the next slot are prefetched while the
+// current slot's 16x128x128 product runs.  Slot e of all 16 targets shares one
+// accumulator row, so per-target sums need no cross-lane traffic; the four
+// waves' partial sums meet in LDS (the then free W2 region), which also carries
+// the transposes between the epilogue GEMMs.  Deterministic: no atomics.
+// ---------------------------------------------------------------------------
+constexpr int FT = 16;    // target rows per workgroup
+constexpr int FRP = 132;  // padded LDS row (floats): conflict-free C-layout writes
+
+struct FusedLayerArgs {
+    const float *a, *b, *h;  // [n,128]: this layer's message_net_1 halves, layer input
+    const int32_t *nbr;      // [n,k] global source rows
+    int64_t n;
+    int k;
+    const float *w2, *b2;             // message_net_2.0 [128,128], [128]
+    const char *w2pk;                 // F16X3: packed W2 image + column scales
+    const float *u1, *c1;             // update_net_1.0 [128, ld_u1] (h | mean | t), [128]
+    int64_t ld_u1;
+    const float *u2, *c2;             // update_net_2.0 [128,128], [128]
+    const float *bn_w, *bn_b, *bn_rm, *bn_rv;
+    float eps;
+    float *h_out;
+    const float *w1n, *b1n;           // next layer message_net_1.0 [128, ld_w1n], [128]
+    int64_t ld_w1n;
+    float *a_out, *b_out;
+    const float *u, *pos;             // node input u [n], pos [n,3] = (t, x, y)
+    mmpde_gnn_scales sc;
+};
+
+__device__ __forceinline__ float4 relu4_add(float4 x, float4 y) {
+    return make_float4(fmaxf(x.x + y.x, 0.0f), fmaxf(x.y + y.y, 0.0f), fmaxf(x.z + y.z, 0.0f),
+                       fmaxf(x.w + y.w, 0.0f));
+}
+
+__device__ __forceinline__ float f4c(const float4 &v, int t) {
+    return t == 0 ? v.x : t == 1 ? v.y : t == 2 ? v.z : v.w;
+}
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// Power of two s with mx * s in [2^13, 2^14) (fp16 max 65504): the scale of
+// the F16X3 split.  mx zero / subnormal / inf / nan -> 1; clamped to
+// [2^-40, 2^40] so a scaled bias can never overflow fp32.
+__device__ __forceinline__ float split_scale(float mx) {
+    const int eb = (int)((__float_as_uint(mx) >> 23) & 0xff);
+    if (eb == 0 || eb == 255) return 1.0f;
+    const int se = min(max(267 - eb, 127 - 40), 127 + 40);
+    return __uint_as_float((uint32_t)se << 23);
+}
+
+// ---------------------------------------------------------------------------
+// F16X3 weight image of message_net_2 (per layer, once per forward): column
+// col is scaled by sw[col] = split_scale(max_k |W2[col, k]|) and split into
+// fp16 hi + lo, laid out as the exact per-lane B operand of
+// v_mfma_f32_16x16x32_f16: [ctile c][kstep s][hi|lo][lane][8 halves] with
+// lane = 16 g + (col & 15) holding k = 32 s + 8 g + j.  Followed by sw[128].
+// ---------------------------------------------------------------------------
+constexpr int kW2PackBytes = 65536 + 512;
+
+struct W2PackArgs {
+    const float *w2[MMPDE_GNN_MAX_LAYERS];
+};
+
+__global__ __launch_bounds__(128) void w2_pack_f16x3_kernel(W2PackArgs a, char *__restrict__ pack) {
+    __shared__ float red[2];
+    const int layer = blockIdx.y, col = blockIdx.x, k = threadIdx.x;
+    const float w = a.w2[layer][col * H + k];
+    const float m = wave_max(fabsf(w));
+    if ((k & 63) == 0) red[k >> 6] = m;
+    __syncthreads();
+    const float sw = split_scale(fmaxf(red[0], red[1]));
+    const float x = w * sw;
+    const _Float16 hi = (_Float16)x;
+    const _Float16 lo = (_Float16)(x - (float)hi);
+    const int c = col >> 4, s = k >> 5, g = (k >> 3) & 3, j = k & 7;
+    const int lane = 16 * g + (col & 15);
+    _Float16 *img = (_Float16 *)(pack + (int64_t)layer * kW2PackBytes);
+    img[(((c * 4 + s) * 2 + 0) * 64 + lane) * 8 + j] = hi;
+    img[(((c * 4 + s) * 2 + 1) * 64 + lane) * 8 + j] = lo;
+    if (k == 0) ((float *)(pack + (int64_t)layer * kW2PackBytes + 65536))[col] = sw;
+}
+
+template <bool NEXT, bool F16X3>
+__global__ __launch_bounds__(256, 2) void gnn_layer_fused_kernel(FusedLayerArgs p) {
+    __shared__ float4 lds4[8 * 8 * 64 + FT * FRP / 4];  // W2 image (64 KB) | a tile
+    float *lds = (float *)lds4;
+    float *lds_a = lds + 8 * 8 * 64 * 4;  // [16][FRP]: a rows of the tile
+    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int r = lane & 15, g = lane >> 4;
+    const int tile = xcd_tile(blockIdx.x, gridDim.x);
+    const int64_t tile0 = (int64_t)tile * FT;
+    const int64_t tgt = min(tile0 + r, p.n - 1);
+
+    if (F16X3) {
+        for (int e = threadIdx.x; e < 8 * 8 * 64; e += 256) lds4[e] = ((const float4 *)p.w2pk)[e];
+    } else {
+        for (int e = threadIdx.x; e < 8 * 8 * 64; e += 256) {
+            const int l = e & 63, j = (e >> 6) & 7, c = e >> 9;
+            lds4[e] = *(const float4 *)(p.w2 + (16 * c + (l & 15)) * H + 16 * j + 4 * (l >> 4));
+        }
+    }
+    for (int e = threadIdx.x; e < FT * 32; e += 256) {
+        const int row = e >> 5, c4 = e & 31;
+        const int64_t src = min(tile0 + row, p.n - 1);
+        *(float4 *)(lds_a + row * FRP + 4 * c4) = *(const float4 *)(p.a + src * H + 4 * c4);
+    }
+
+    float bias[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) bias[c] = p.b2[16 * c + r];
+    f32x4 S[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) S[c] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+
+    // Neighbour rows: slot e's b row is loaded one slot ahead, its index two
+    // slots ahead, so neither latency sits in front of the MFMAs.
+    // (clamped: a malformed caller table must not fault the GPU)
+    // k map of the b / a pieces: F32 float4 j holds k = 16 j + 4 g + t;
+    // F16X3 float4 i holds k = 32 (i >> 1) + 8 g + 4 (i & 1) + t.
+    const int32_t *nrow = p.nbr + tgt * p.k;
+    const uint32_t nmax = (uint32_t)(p.n - 1);
+    auto piece = [&](int i) { return F16X3 ? 32 * (i >> 1) + 8 * g + 4 * (i & 1) : 16 * i + 4 * g; };
+    float4 bv[8];
+    uint32_t src_next = 0;
+    if (wave < p.k) {
+        const int64_t src = min((uint32_t)nrow[wave], nmax);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) bv[i] = *(const float4 *)(p.b + src * H + piece(i));
+        if (wave + 4 < p.k) src_next = (uint32_t)nrow[wave + 4];
+    }
+    float bsw[8], isw[8];  // F16X3: bias * column scale, 1 / column scale
+    if (F16X3) {
+        const float *swp = (const float *)(p.w2pk + 65536);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const float sw = swp[16 * c + r];
+            bsw[c] = bias[c] * sw;
+            isw[c] = 1.0f / sw;
+        }
+    }
+    __syncthreads();
+    const float4 *wimg = lds4 + lane;
+    const float *arow = lds_a + r * FRP;
+
+    for (int e = wave; e < p.k; e += 4) {
+        // keep the W2 image in LDS: without this the compiler hoists the
+        // loop-invariant ds_reads out of the loop (256 VGPRs) and spills them
+        asm volatile("" ::: "memory");
+        float4 m[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) m[i] = relu4_add(*(const float4 *)(arow + piece(i)), bv[i]);
+        if (e + 4 < p.k) {
+            const int64_t src = min(src_next, nmax);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) bv[i] = *(const float4 *)(p.b + src * H + piece(i));
+            if (e + 8 < p.k) src_next = (uint32_t)nrow[e + 8];
+        }
+        f32x4 acc[8];
+        if (!F16X3) {
+#pragma unroll
+            for (int c = 0; c < 8; ++c) acc[c] = (f32x4){bias[c], bias[c], bias[c], bias[c]};
+            float4 w[8];
+#pragma unroll
+            for (int c = 0; c < 8; ++c) w[c] = wimg[c * 8 * 64];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                float4 wn[8];
+                if (j < 7) {
+#pragma unroll
+                    for (int c = 0; c < 8; ++c) wn[c] = wimg[(c * 8 + j + 1) * 64];
+                }
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+#pragma unroll
+                    for (int c = 0; c < 8; ++c) acc[c] = mfma16(f4c(m[j], t), f4c(w[c], t), acc[c]);
+                }
+                if (j < 7) {
+#pragma unroll
+                    for (int c = 0; c < 8; ++c) w[c] = wn[c];
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) S[c][q] += fmaxf(acc[c][q], 0.0f);
+            }
+        } else {
+            // slot scale: the largest message input of this neighbour slot
+            float mx = 0.0f;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) mx = fmaxf(fmaxf(fmaxf(mx, m[i].x), fmaxf(m[i].y, m[i].z)), m[i].w);
+            const float sc = split_scale(wave_max(mx));
+            const float isc = 1.0f / sc;
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const float bi = bsw[c] * sc;
+                acc[c] = (f32x4){bi, bi, bi, bi};
+            }
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) {
+                half8 hi, lo;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float x = f4c(m[2 * s4 + (j >> 2)], j & 3) * sc;
+                    const _Float16 h = (_Float16)x;
+                    hi[j] = h;
+                    lo[j] = (_Float16)(x - (float)h);
+                }
+                half8 wh[8], wl[8];
+#pragma unroll
+                for (int c = 0; c < 8; ++c) {
+                    const float4 a4 = wimg[((c * 4 + s4) * 2 + 0) * 64];
+                    const float4 b4 = wimg[((c * 4 + s4) * 2 + 1) * 64];
+                    wh[c] = *(const half8 *)&a4;
+                    wl[c] = *(const half8 *)&b4;
+                }
+#pragma unroll
+                for (int c = 0; c < 8; ++c) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi, wh[c], acc[c], 0, 0, 0);
+#pragma unroll
+                for (int c = 0; c < 8; ++c) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi, wl[c], acc[c], 0, 0, 0);
+#pragma unroll
+                for (int c = 0; c < 8; ++c) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(lo, wh[c], acc[c], 0, 0, 0);
+            }
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const float inv = isc * isw[c];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) S[c][q] = fmaf(fmaxf(acc[c][q], 0.0f), inv, S[c][q]);
+            }
+        }
+    }
+
+    // ---- cross-wave sum of the edge messages: red[wave][row][col] ----------
+    __syncthreads();  // every wave is done with the W2 image
+    float *red = lds;                      // 4 x 16 x FRP
+    float *vbuf = lds + 4 * FT * FRP;      // 16 x FRP
+    float *hbuf = vbuf + FT * FRP;         // 16 x FRP
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) red[(wave * FT + 4 * g + q) * FRP + 16 * c + r] = S[c][q];
+    }
+    __syncthreads();
+    const float kdiv = (float)p.k;
+
+    // ---- update_net_1: v = relu(U1 [h | mean | t] + c1), cols 32 w .. 32 w + 31
+    {
+        f32x4 acc[2] = {(f32x4){0.0f, 0.0f, 0.0f, 0.0f}, (f32x4){0.0f, 0.0f, 0.0f, 0.0f}};
+        const float *hrow = p.h + tgt * H + 4 * g;
+#pragma unroll 2
+        for (int j = 0; j < 8; ++j) {
+            const float4 hv = *(const float4 *)(hrow + 16 * j);
+            float4 mv = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const float4 x = *(const float4 *)(red + (w * FT + r) * FRP + 16 * j + 4 * g);
+                mv.x += x.x;
+                mv.y += x.y;
+                mv.z += x.z;
+                mv.w += x.w;
+            }
+            mv = make_float4(mv.x / kdiv, mv.y / kdiv, mv.z / kdiv, mv.w / kdiv);
+#pragma unroll
+            for (int cc = 0; cc < 2; ++cc) {
+                const float *wr = p.u1 + (int64_t)(32 * wave + 16 * cc + r) * p.ld_u1 + 16 * j + 4 * g;
+                const float4 wh = *(const float4 *)wr;
+                const float4 wm = *(const float4 *)(wr + 128);
+#pragma unroll
+                for (int t = 0; t < 4; ++t) acc[cc] = mfma16(f4c(hv, t), f4c(wh, t), acc[cc]);
+#pragma unroll
+                for (int t = 0; t < 4; ++t) acc[cc] = mfma16(f4c(mv, t), f4c(wm, t), acc[cc]);
+            }
+        }
+#pragma unroll
+        for (int cc = 0; cc < 2; ++cc) {
+            const int col = 32 * wave + 16 * cc + r;
+            const float wt = p.u1[(int64_t)col * p.ld_u1 + 256], bb = p.c1[col];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int64_t row = min(tile0 + 4 * g + q, p.n - 1);
+                const float pt = p.pos[row * 3 + 0] * p.sc.inv_tmax;
+                vbuf[(4 * g + q) * FRP + col] = fmaxf(acc[cc][q] + wt * pt + bb, 0.0f);
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- update_net_2 + residual + BatchNorm(eval) ----------------------------
+    {
+        f32x4 acc[2] = {(f32x4){0.0f, 0.0f, 0.0f, 0.0f}, (f32x4){0.0f, 0.0f, 0.0f, 0.0f}};
+#pragma unroll 2
+        for (int j = 0; j < 8; ++j) {
+            const float4 vv = *(const float4 *)(vbuf + r * FRP + 16 * j + 4 * g);
+#pragma unroll
+            for (int cc = 0; cc < 2; ++cc) {
+                const float4 w = *(const float4 *)(p.u2 + (32 * wave + 16 * cc + r) * H + 16 * j + 4 * g);
+#pragma unroll
+                for (int t = 0; t < 4; ++t) acc[cc] = mfma16(f4c(vv, t), f4c(w, t), acc[cc]);
+            }
+        }
+#pragma unroll
+        for (int cc = 0; cc < 2; ++cc) {
+            const int col = 32 * wave + 16 * cc + r;
+            const float bb = p.c2[col], rm = p.bn_rm[col], rv = p.bn_rv[col];
+            const float gw = p.bn_w[col], gb = p.bn_b[col];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int64_t row = tile0 + 4 * g + q;
+                const int64_t rowc = min(row, p.n - 1);
+                const float x = p.h[rowc * H + col] + fmaxf(acc[cc][q] + bb, 0.0f);
+                const float y = bn_eval(x, rm, rv, gw, gb, p.eps);
+                if (row < p.n) p.h_out[row * H + col] = y;
+                if (NEXT) hbuf[(4 * g + q) * FRP + col] = y;
+            }
+        }
+    }
+    if (!NEXT) return;
+    __syncthreads();
+
+    // ---- next layer's message_net_1 halves (EpiProj) -------------------------
+    {
+        f32x4 acc[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[c] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+        // tiles 0,1: a' cols 32w+16cc (W1n[:, 0:128]); tiles 2,3: b' (W1n[:, 128:256])
+#pragma unroll 2
+        for (int j = 0; j < 8; ++j) {
+            const float4 hv = *(const float4 *)(hbuf + r * FRP + 16 * j + 4 * g);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const int col = 32 * wave + 16 * (c & 1) + r;
+                const float4 w = *(const float4 *)(p.w1n + (int64_t)col * p.ld_w1n + 128 * (c >> 1) + 16 * j + 4 * g);
+#pragma unroll
+                for (int t = 0; t < 4; ++t) acc[c] = mfma16(f4c(hv, t), f4c(w, t), acc[c]);
+            }
+        }
+#pragma unroll
+        for (int cc = 0; cc < 2; ++cc) {
+            const int col = 32 * wave + 16 * cc + r;
+            const float *wc = p.w1n + (int64_t)col * p.ld_w1n;
+            const float wdu = wc[256], wdx = wc[257], wdy = wc[258], wt = wc[259];
+            const float bb = p.b1n[col];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int64_t row = tile0 + 4 * g + q;
+                if (row < p.n) {
+                    const float uu = p.u[row];
+                    const float px = p.pos[row * 3 + 1] * p.sc.inv_lx;
+                    const float py = p.pos[row * 3 + 2] * p.sc.inv_ly;
+                    const float pt = p.pos[row * 3 + 0] * p.sc.inv_tmax;
+                    const float node = wdu * uu + wdx * px + wdy * py;
+                    p.a_out[row * H + col] = acc[cc][q] + node + wt * pt + bb;
+                    p.b_out[row * H + col] = acc[2 + cc][q] - node;
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Conv1d head (gnn_2d.py:108-114,136-139): one wave per node.
 // 128 -> conv(1->4, k16, s3) 38 -> relu -> conv(4->8, k12, s3) 9 -> relu ->
 // conv(8->1, k8, s2) 1, times out_scale.
@@ -293,8 +674,9 @@ inline bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
 // C-ABI
 // ===========================================================================
 extern "C" int64_t mmpde_gnn_workspace_bytes(int64_t n) {
-    // h ping-pong (2) + a + b + mean + v  = 6 x [n,128] fp32
-    return 6 * n * H * (int64_t)sizeof(float);
+    // h, a, b ping-pong = 6 x [n,128] fp32 (the unfused per-layer API uses
+    // 4 of them as a, b, mean, v), then the F16X3 packed message_net_2 images
+    return 6 * n * H * (int64_t)sizeof(float) + (int64_t)MMPDE_GNN_MAX_LAYERS * kW2PackBytes;
 }
 
 extern "C" int mmpde_gnn_embed(const float *u, const float *pos, int64_t n,
@@ -386,31 +768,88 @@ extern "C" int mmpde_gnn_head(const float *h, int64_t n, const mmpde_gnn_head_pa
     return MMPDE_OK;
 }
 
+static int launch_fused_layer(const float *a, const float *b, const float *h, const float *u,
+                              const float *pos, int64_t n, int k, const int32_t *nbr,
+                              mmpde_gnn_scales sc, const mmpde_gnn_layer_params *p,
+                              const mmpde_gnn_layer_params *next, const char *w2pk,
+                              float *h_out, float *a_out, float *b_out, hipStream_t st) {
+    MMPDE_REQUIRE(p->upd1_ld >= 257 && (p->upd1_ld & 3) == 0 && aligned16(p->upd1_w));
+    MMPDE_REQUIRE(aligned16(p->msg2_w) && aligned16(p->upd2_w));
+    FusedLayerArgs f{a, b, h, nbr, n, k, p->msg2_w, p->msg2_b, w2pk, p->upd1_w, p->upd1_b,
+                     p->upd1_ld, p->upd2_w, p->upd2_b, p->bn_w, p->bn_b, p->bn_rm, p->bn_rv,
+                     p->eps, h_out, nullptr, nullptr, 0, a_out, b_out, u, pos, sc};
+    const dim3 grid(ceil_div(n, FT));
+    if (next) {
+        MMPDE_REQUIRE(next->msg1_ld >= 260 && (next->msg1_ld & 3) == 0 && aligned16(next->msg1_w));
+        f.w1n = next->msg1_w;
+        f.b1n = next->msg1_b;
+        f.ld_w1n = next->msg1_ld;
+    }
+#define MMPDE_FUSED(NX, SPLIT) \
+    hipLaunchKernelGGL((gnn_layer_fused_kernel<NX, SPLIT>), grid, dim3(256), 0, st, f)
+    if (next && w2pk) MMPDE_FUSED(true, true);
+    else if (next) MMPDE_FUSED(true, false);
+    else if (w2pk) MMPDE_FUSED(false, true);
+    else MMPDE_FUSED(false, false);
+#undef MMPDE_FUSED
+    MMPDE_RET_LAUNCH();
+    return MMPDE_OK;
+}
+
 extern "C" int mmpde_gnn_forward_ex(const float *u, const float *pos, int64_t n, int k,
                                     const int32_t *nbr, mmpde_gnn_scales sc,
                                     const mmpde_gnn_embed_params *emb,
                                     const mmpde_gnn_layer_params *layers, int n_layers,
                                     const mmpde_gnn_head_params *head, void *workspace,
-                                    float *out, const mmpde_gnn_trace *trace,
+                                    float *out, const mmpde_gnn_exec *exec,
                                     mmpde_stream_t stream) {
     MMPDE_REQUIRE(u && pos && nbr && emb && layers && head && workspace && out);
-    MMPDE_REQUIRE(n > 0 && k > 0 && n_layers >= 0);
+    MMPDE_REQUIRE(n > 0 && k > 0 && n_layers >= 0 && n_layers <= MMPDE_GNN_MAX_LAYERS);
+    MMPDE_REQUIRE(aligned16(workspace));
+    const int mode = exec ? exec->edge_gemm : MMPDE_EDGE_GEMM_F32;
+    MMPDE_REQUIRE(mode == MMPDE_EDGE_GEMM_F32 || mode == MMPDE_EDGE_GEMM_F16X3);
+    hipStream_t st = as_stream(stream);
     float *ws = (float *)workspace;
-    float *h0 = ws;
-    float *h1 = h0 + n * H;
-    float *lw = h1 + n * H;  // 4 x [n,128] layer scratch
-    int rc = mmpde_gnn_embed(u, pos, n, sc, emb, lw, h0, stream);
-    if (rc) return rc;
-    for (int l = 0; l < n_layers; ++l) {
-        hipEvent_t eb = trace ? (hipEvent_t)trace->edge_begin[l] : nullptr;
-        hipEvent_t ee = trace ? (hipEvent_t)trace->edge_end[l] : nullptr;
-        rc = gnn_layer_impl(h0, u, pos, n, k, nbr, sc, &layers[l], lw, h1, eb, ee, stream);
-        if (rc) return rc;
-        float *t = h0;
-        h0 = h1;
-        h1 = t;
+    float *hb[2] = {ws, ws + n * H};
+    float *ab[2] = {ws + 2 * n * H, ws + 3 * n * H};
+    float *bb[2] = {ws + 4 * n * H, ws + 5 * n * H};
+    char *pack = (char *)(ws + 6 * n * H);
+    if (mode == MMPDE_EDGE_GEMM_F16X3 && n_layers > 0) {
+        W2PackArgs pa{};
+        for (int l = 0; l < n_layers; ++l) {
+            MMPDE_REQUIRE(layers[l].msg2_w != nullptr);
+            pa.w2[l] = layers[l].msg2_w;
+        }
+        hipLaunchKernelGGL(w2_pack_f16x3_kernel, dim3(H, n_layers), dim3(128), 0, st, pa, pack);
+        MMPDE_RET_LAUNCH();
     }
-    return mmpde_gnn_head(h0, n, head, out, stream);
+    int rc = mmpde_gnn_embed(u, pos, n, sc, emb, ab[1], hb[0], stream);  // ab[1]: scratch
+    if (rc) return rc;
+    if (n_layers > 0) {
+        // layer 0's message_net_1 halves; later layers get theirs from the fused kernel
+        const mmpde_gnn_layer_params *p0 = &layers[0];
+        MMPDE_REQUIRE(p0->msg1_ld >= 260 && (p0->msg1_ld & 3) == 0 && aligned16(p0->msg1_w));
+        const int64_t ld = p0->msg1_ld;
+        GemmArgs g{n, hb[0], hb[0] + 64, H, p0->msg1_w, p0->msg1_w + 64, ld, 64};
+        EpiProj epi{ab[0], bb[0], p0->msg1_b, p0->msg1_w + 256, p0->msg1_w + 257,
+                    p0->msg1_w + 258, p0->msg1_w + 259, ld, u, pos, sc};
+        rc = launch_gemm<EpiProj, true>(g, 2, epi, st);
+        if (rc) return rc;
+    }
+    int cur = 0;
+    for (int l = 0; l < n_layers; ++l) {
+        hipEvent_t eb = exec && exec->edge_begin ? (hipEvent_t)exec->edge_begin[l] : nullptr;
+        hipEvent_t ee = exec && exec->edge_end ? (hipEvent_t)exec->edge_end[l] : nullptr;
+        if (eb && hipEventRecord(eb, st) != hipSuccess) return MMPDE_ERR_INVALID_ARG;
+        const mmpde_gnn_layer_params *next = l + 1 < n_layers ? &layers[l + 1] : nullptr;
+        const char *w2pk = mode == MMPDE_EDGE_GEMM_F16X3 ? pack + (int64_t)l * kW2PackBytes : nullptr;
+        rc = launch_fused_layer(ab[cur], bb[cur], hb[cur], u, pos, n, k, nbr, sc, &layers[l], next,
+                                w2pk, hb[cur ^ 1], ab[cur ^ 1], bb[cur ^ 1], st);
+        if (rc) return rc;
+        if (ee && hipEventRecord(ee, st) != hipSuccess) return MMPDE_ERR_INVALID_ARG;
+        cur ^= 1;
+    }
+    return mmpde_gnn_head(hb[cur], n, head, out, stream);
 }
 
 extern "C" int mmpde_gnn_forward(const float *u, const float *pos, int64_t n, int k,

@@ -4,12 +4,15 @@
 // mesh/dmm_model.py:228) and sklearn NearestNeighbors.kneighbors
 // (data_creator_2d.py:66-78).  One wave per query; the trajectory's point set
 // (<= 4096 points, <= 32 KB) is staged once per workgroup in LDS; every lane
-// keeps CPL candidate keys in registers.  The k-th smallest key is found by a
-// bitwise radix select (ballot + popcount per candidate, no data movement),
-// ties at the threshold are resolved in index order, the k winners are
-// compacted into a per-wave LDS list and ranked by (key, index).  The result
-// is exactly the (distance, index)-ordered list of the reference's insertion
-// sort, independent of scheduling.
+// keeps CPL candidate keys in registers.  Selection: U = the kk-th smallest of
+// the 64 per-lane minima (radix select over one value per lane: ballot +
+// popcount), which bounds the kk-th smallest key from above; the candidates
+// with key <= U (a few dozen on a mesh) are compacted into a per-wave LDS list
+// and ranked exhaustively by (key, index).  Point sets where that list would
+// overflow fall back to a full bitwise radix select over all keys with ties at
+// the threshold taken in index order.  Either way the result is exactly the
+// (distance, index)-ordered list of the reference's insertion sort,
+// independent of scheduling.
 //
 // Distance keys (must match oracle/knn_oracle.c bit for bit):
 //   graph: d2 = fmaf(dy, dy, dx*dx) in fp32  (torch_cluster under nvcc fmad)
@@ -23,6 +26,7 @@
 namespace {
 
 constexpr int kQueriesPerBlock = 16;  // 4 per wave
+constexpr int kCap = 512;             // LDS list of candidates with key <= U, per wave
 
 template <bool QUERY>
 struct KeyTraits;
@@ -67,8 +71,9 @@ __global__ __launch_bounds__(256) void knn_kernel(const float2 *__restrict__ pts
     typedef KeyTraits<QUERY> KT;
     typedef typename KT::key_t key_t;
     __shared__ float2 sP[CPL * 64];
-    __shared__ key_t sKey[4][64];
-    __shared__ int sIdx[4][64];
+    __shared__ key_t sKey[4][kCap];
+    __shared__ int sIdx[4][kCap];
+    __shared__ int sSel[4][64];
 
     const int b = blockIdx.y;
     const float2 *P = pts + (int64_t)b * n_src;
@@ -84,55 +89,100 @@ __global__ __launch_bounds__(256) void knn_kernel(const float2 *__restrict__ pts
     for (int qi = blockIdx.x * kQueriesPerBlock + wave; qi < q_end; qi += 4) {
         const float2 q = QUERY ? qry[(int64_t)b * n_q + qi] : sP[qi];
         key_t key[CPL];
+        key_t lmin = ~key_t(0);
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
             const int j = lane + 64 * c;
             key[c] = (j < n_src) ? KT::key(sP[j], q) : ~key_t(0);
+            lmin = key[c] < lmin ? key[c] : lmin;
         }
-        // Radix select: largest T with #(key < T) <= kk-1, i.e. the kk-th smallest key.
-        key_t T = 0;
+        // U = kk-th smallest of the 64 lane minima (radix select over one value
+        // per lane).  At least kk candidates have key <= U (one per lane whose
+        // minimum is <= U), so every key of the answer, ties included, is <= U:
+        // the answer is exactly the first kk of C = {key <= U} in (key, index)
+        // order.  C is small (~2 kk on a mesh), so it is compacted into LDS and
+        // ranked exhaustively.
+        key_t U = 0;
         for (int bit = KT::kTopBit; bit >= 0; --bit) {
-            const key_t Tc = T | (key_t(1) << bit);
-            int cnt = 0;
-#pragma unroll
-            for (int c = 0; c < CPL; ++c) cnt += __popcll(__ballot(key[c] < Tc));
-            if (cnt <= kk - 1) T = Tc;
+            const key_t Tc = U | (key_t(1) << bit);
+            if (__popcll(__ballot(lmin < Tc)) <= kk - 1) U = Tc;
         }
         int m = 0;
 #pragma unroll
-        for (int c = 0; c < CPL; ++c) m += __popcll(__ballot(key[c] < T));
-        const int need = kk - m;  // >= 1 candidates equal to T, taken in index order
-        int base = 0, eq_taken = 0;
-#pragma unroll
         for (int c = 0; c < CPL; ++c) {
-            const bool lt = key[c] < T;
-            const bool eq = key[c] == T;
-            const uint64_t em = __ballot(eq);
-            const int eqrank = eq_taken + __popcll(em & below);
-            const bool sel = lt || (eq && eqrank < need);
-            eq_taken += __popcll(em);
+            const bool sel = key[c] <= U;
             const uint64_t sm = __ballot(sel);
             if (sel) {
-                const int p = base + __popcll(sm & below);
-                sKey[wave][p] = key[c];
-                sIdx[wave][p] = lane + 64 * c;
+                const int pidx = m + __popcll(sm & below);
+                if (pidx < kCap) {
+                    sKey[wave][pidx] = key[c];
+                    sIdx[wave][pidx] = lane + 64 * c;
+                }
             }
-            base += __popcll(sm);
+            m += __popcll(sm);
         }
-        wave_lds_sync();
         key_t mk = ~key_t(0);
         int mi = 0x7fffffff;
-        if (lane < kk) {
-            mk = sKey[wave][lane];
-            mi = sIdx[wave][lane];
+        int rank = lane;
+        if (m <= kCap) {
+            wave_lds_sync();
+            for (int i = lane; i < m; i += 64) {
+                const key_t ki = sKey[wave][i];
+                const int ii = sIdx[wave][i];
+                int rk = 0;
+                for (int f = 0; f < m; ++f) {
+                    const key_t fk = sKey[wave][f];
+                    const int fi = sIdx[wave][f];
+                    rk += (fk < ki) || (fk == ki && fi < ii);
+                }
+                if (rk < kk) sSel[wave][rk] = ii;
+            }
+            wave_lds_sync();
+            if (lane < kk) mi = sSel[wave][lane];
+        } else {
+            // Fallback for adversarial point sets: full radix select on all keys.
+            key_t T = 0;
+            for (int bit = KT::kTopBit; bit >= 0; --bit) {
+                const key_t Tc = T | (key_t(1) << bit);
+                int cnt = 0;
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) cnt += __popcll(__ballot(key[c] < Tc));
+                if (cnt <= kk - 1) T = Tc;
+            }
+            int mlt = 0;
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) mlt += __popcll(__ballot(key[c] < T));
+            const int need = kk - mlt;  // >= 1 candidates equal to T, taken in index order
+            int base = 0, eq_taken = 0;
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const bool lt = key[c] < T;
+                const bool eq = key[c] == T;
+                const uint64_t em = __ballot(eq);
+                const int eqrank = eq_taken + __popcll(em & below);
+                const bool sel = lt || (eq && eqrank < need);
+                eq_taken += __popcll(em);
+                const uint64_t sm = __ballot(sel);
+                if (sel) {
+                    const int pidx = base + __popcll(sm & below);
+                    sKey[wave][pidx] = key[c];
+                    sIdx[wave][pidx] = lane + 64 * c;
+                }
+                base += __popcll(sm);
+            }
+            wave_lds_sync();
+            if (lane < kk) {
+                mk = sKey[wave][lane];
+                mi = sIdx[wave][lane];
+            }
+            rank = 0;
+            for (int f = 0; f < kk; ++f) {
+                const key_t fk = sKey[wave][f];
+                const int fi = sIdx[wave][f];
+                rank += (fk < mk) || (fk == mk && fi < mi);
+            }
         }
-        int rank = 0;
-        for (int f = 0; f < kk; ++f) {
-            const key_t fk = sKey[wave][f];
-            const int fi = sIdx[wave][f];
-            rank += (fk < mk) || (fk == mk && fi < mi);
-        }
-        wave_lds_sync();  // the next query overwrites sKey / sIdx
+        wave_lds_sync();  // the next query overwrites sKey / sIdx / sSel
         const int64_t row = ((int64_t)b * n_q + qi) * k;
         if (QUERY) {
             if (lane < kk) out[row + rank] = mi;

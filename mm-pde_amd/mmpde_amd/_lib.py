@@ -13,9 +13,11 @@ import os
 import torch
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libmmpde_hip.so")
-ABI_VERSION = 10000
+ABI_VERSION = 10100
 
 ACT_NONE, ACT_TANH, ACT_RELU = 0, 1, 2
+# message_net_2 edge GEMM arithmetic (include/mmpde_hip.h MMPDE_EDGE_GEMM_*)
+EDGE_GEMM = {"f32": 0, "f16x3": 1}
 
 _P = ctypes.c_void_p
 _I64 = ctypes.c_int64
@@ -55,8 +57,10 @@ class GnnHeadParams(ctypes.Structure):
 _P3 = _P * 3
 
 
-class GnnTrace(ctypes.Structure):
-    _fields_ = [("edge_begin", ctypes.POINTER(_P)), ("edge_end", ctypes.POINTER(_P))]
+class GnnExec(ctypes.Structure):
+    """mmpde_gnn_exec: optional per-layer hipEvents + the edge-GEMM arithmetic."""
+    _fields_ = [("edge_begin", ctypes.POINTER(_P)), ("edge_end", ctypes.POINTER(_P)),
+                ("edge_gemm", _I)]
 
 
 class DmmGraphBranch(ctypes.Structure):

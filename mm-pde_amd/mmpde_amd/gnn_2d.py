@@ -122,6 +122,9 @@ class MP_PDE_Solver_2D(nn.Module):  # noqa: N801 - reference name
             nn.Conv1d(8, 1, 8, stride=2))
         self._pack_key = None
         self._pack = None
+        # message_net_2 arithmetic: "f32" (exact fp32 MFMA) or "f16x3" (fp32
+        # emulated by scaled fp16 hi/lo splits; include/mmpde_hip.h)
+        self.edge_gemm = "f32"
 
     def __repr__(self):
         return "GNN"
@@ -169,7 +172,8 @@ class MP_PDE_Solver_2D(nn.Module):  # noqa: N801 - reference name
     def forward(self, data, out: torch.Tensor | None = None, workspace=None, trace=None):
         """gnn_2d.py:119-141 on one C-ABI call.  `data` needs .x [n,1], .pos [n,3]
         and either .nbr (int32 [n,k]) or a knn-style .edge_index.  `trace`: optional
-        _lib.GnnTrace of hipEvents recorded around each layer's edge kernel."""
+        _lib.GnnExec carrying hipEvents recorded around each layer's fused kernel
+        (its edge_gemm field is set from self.edge_gemm)."""
         self.check_supported()
         u, pos = data.x, data.pos
         L.require_device(u, pos)
@@ -185,9 +189,12 @@ class MP_PDE_Solver_2D(nn.Module):  # noqa: N801 - reference name
                                     dtype=torch.float32, device=u.device)
         if out is None:
             out = torch.empty((n, 1), dtype=torch.float32, device=u.device)
+        if trace is None:
+            trace = L.GnnExec(None, None, 0)
+        trace.edge_gemm = L.EDGE_GEMM[self.edge_gemm]
         L.check(L.lib().mmpde_gnn_forward_ex(
             L.ptr(u), L.ptr(pos), n, nbr.shape[1], L.ptr(nbr), sc, ctypes.byref(emb), arr,
             len(arr), ctypes.byref(head), L.ptr(workspace), L.ptr(out),
-            ctypes.byref(trace) if trace is not None else None, L.stream(u.device)),
+            ctypes.byref(trace), L.stream(u.device)),
             "mmpde_gnn_forward")
         return out

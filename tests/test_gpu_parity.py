@@ -74,6 +74,16 @@ def test_knn_graph_duplicates(dev):
     _graph_case(pos, 1, dev)
 
 
+def test_knn_graph_candidate_overflow_fallback(dev):
+    # > 512 points tie with the kk-th lane minimum: the LDS candidate list
+    # overflows and the kernel takes the full radix-select path.
+    torch.manual_seed(11)
+    pos = torch.rand(2 * 1500, 2)
+    pos[100:800] = pos[5]                                      # 701 coincident points
+    pos[1500 + 200:1500 + 1400] = 0.25                         # 1200 coincident points
+    _graph_case(pos, 2, dev)
+
+
 # ============================================================================ kNN-30 query
 def test_knn_query_sklearn_golden(dev):
     from mmpde_amd import ops
@@ -94,6 +104,18 @@ def test_knn_query_bit_exact(dev, ns, nq, B):
     qry[:3] = src[:3]                                          # zero-distance hits
     idx = ops.knn_query(src.to(dev), qry.to(dev), B, 30)
     ref = refcpu.knn_query(src, qry, B, 30)
+    assert torch.equal(idx.cpu().long().reshape(ref.shape), ref)
+
+
+def test_knn_query_candidate_overflow_fallback(dev):
+    from mmpde_amd import ops
+
+    torch.manual_seed(12)
+    src, qry = torch.rand(2 * 1000, 2), torch.rand(2 * 300, 2)
+    src[0:700] = 0.5                                           # 700 coincident sources
+    qry[0:100] = 0.5
+    idx = ops.knn_query(src.to(dev), qry.to(dev), 2, 30)
+    ref = refcpu.knn_query(src, qry, 2, 30)
     assert torch.equal(idx.cpu().long().reshape(ref.shape), ref)
 
 
