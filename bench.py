@@ -35,6 +35,7 @@ import torch  # noqa: E402
 
 METRIC = "MM-PDE rollout node-updates/sec, cylinder 2521-node mesh, 1/2/4/8 GPUs"
 F32_MFMA_PEAK_TFLOPS = 157.3          # MI355X_MICROARCH.md: dense fp32 matrix peak
+F16_MFMA_PEAK_TFLOPS = 2516.6         # 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz (~2.5 PF dense)
 HBM_PEAK_GBS = 8000.0
 CONFIGS = {
     # name: (kind, moving_mesh, default trajectories per GPU, BASELINE.json config)
@@ -157,8 +158,10 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="trajectories per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--edge-gemm", default="f32", choices=["f32", "f16x3"],
+    ap.add_argument("--edge-gemm", default="f16x3", choices=["f32", "f16x3"],
                     help="message_net_2 arithmetic (include/mmpde_hip.h MMPDE_EDGE_GEMM_*)")
+    ap.add_argument("--no-f32-exact", action="store_true",
+                    help="skip the second, exact-fp32-MFMA timed run reported as f32_exact")
     args = ap.parse_args()
 
     from mmpde_amd import dist as D
@@ -193,25 +196,40 @@ def main():
     n_gnn = 2 if moving else 1
     tracer = EdgeTracer(n_forwards=n_gnn * args.steps)
     eng.trace_hook = tracer
-    u = u_all[:, 0].to(device).contiguous()
+    u0 = u_all[:, 0].to(device).contiguous()
     n_t = t_len - 1
 
-    with torch.no_grad():
-        for i in range(args.warmup):
-            u = eng.step(u, 1 + i % n_t)
-        torch.cuda.synchronize(device)
-        D.barrier(device)
-        tracer.active = True
-        t0 = time.perf_counter()
-        for i in range(args.steps):
-            u = eng.step(u, 1 + (args.warmup + i) % n_t)
-        torch.cuda.synchronize(device)
-        D.barrier(device)
-        t1 = time.perf_counter()
-        tracer.active = False
-    local_s = t1 - t0
-    elapsed = D.max_over_ranks(local_s, device)
+    def timed_run(mode, trace):
+        """W warmup + K timed autoregressive steps from u0; returns (max-over-ranks
+        seconds, final state)."""
+        for m in (model, model_b):
+            if m is not None:
+                m.edge_gemm = mode
+        u = u0
+        with torch.no_grad():
+            for i in range(args.warmup):
+                u = eng.step(u, 1 + i % n_t)
+            torch.cuda.synchronize(device)
+            D.barrier(device)
+            tracer.active = trace
+            t0 = time.perf_counter()
+            for i in range(args.steps):
+                u = eng.step(u, 1 + (args.warmup + i) % n_t)
+            torch.cuda.synchronize(device)
+            D.barrier(device)
+            t1 = time.perf_counter()
+            tracer.active = False
+        return D.max_over_ranks(t1 - t0, device), u
+
+    elapsed, u = timed_run(args.edge_gemm, True)
     finite = bool(torch.isfinite(u).all())
+    exact = None
+    if not args.no_f32_exact and args.edge_gemm != "f32":
+        el32, u32 = timed_run("f32", False)
+        rel = ((u - u32).abs().max() / u32.abs().max().clamp_min(1e-30)).item()
+        exact = {"value": (hi - lo) * world * n_nodes * args.steps / el32,
+                 "ms_per_step": 1e3 * el32 / args.steps,
+                 "final_state_max_rel_diff_vs_main": rel}
     launches = tracer.launch_times_ms()
     tracer.pool.close()
 
@@ -232,14 +250,23 @@ def main():
     tot_ms = sum(ms for _, ms in launches)
     launch_ms = tot_ms / max(len(launches), 1)
     achieved = tot_flop / max(tot_ms * 1e-3, 1e-12) / 1e12
+    # Peak of the kernel's arithmetic mix: the time its MFMA work needs at the
+    # dense peaks (f32 edge GEMM: 157.3 TF; f16x3 edge GEMM: three fp16
+    # products per fp32 product at 2516.6 TF; epilogue GEMMs on f32 MFMA).
+    if args.edge_gemm == "f32":
+        peak = F32_MFMA_PEAK_TFLOPS
+    else:
+        t_ideal = sum(n_local * (3 * edge_f / (F16_MFMA_PEAK_TFLOPS * 1e12)
+                                 + (upd_f + (proj_f if l < n_layers - 1 else 0))
+                                 / (F32_MFMA_PEAK_TFLOPS * 1e12)) for l, _ in launches)
+        peak = tot_flop / t_ideal / 1e12
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "fused_pmc_r01.json")
     if os.path.exists(pmc):
         with open(pmc) as f:
             rec = json.load(f)
-        if (rec.get("workload") == args.config and rec.get("nodes") == n_local
-                and rec.get("edge_gemm") == args.edge_gemm):
-            traffic = rec.get("hbm_bytes_per_launch")
+        if rec.get("workload") == args.config and rec.get("nodes") == n_local:
+            traffic = rec.get("modes", {}).get(args.edge_gemm, {}).get("hbm_bytes_per_launch")
     line = {
         "metric": METRIC if kind == "cy" else METRIC.replace("cylinder 2521-node mesh",
                                                              "Burgers 48x48 grid"),
@@ -252,7 +279,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32" if args.edge_gemm == "f32" else "f32 (message_net_2 on fp16x3 split)",
+        "dtype": "f32" if args.edge_gemm == "f32" else "f32 (edge GEMM fp32-emulated by fp16x3 split, fp32 accumulate)",
         "data": "synthetic: seeded cy-synth 2521-node mesh / 48x48 grid, seeded sin-cos+noise "
                 "fields, seeded default-init weights (no dataset or checkpoint offline)",
         "config": {"workload": args.config, "baseline_config": cfg_name,
@@ -262,13 +289,15 @@ def main():
                    "rollout": "autoregressive (pred -> next input)"},
         "roofline": {"kernel": "gnn_layer_fused_kernel (edge stage + update + next "
                                "message_net_1, one launch per GNN layer, 12 per step)",
-                     "bound": "mfma", "achieved": achieved, "peak": F32_MFMA_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": achieved / F32_MFMA_PEAK_TFLOPS,
+                     "bound": "mfma", "achieved": achieved, "peak": peak,
+                     "unit": "TFLOP/s", "frac": achieved / peak,
                      "traffic": traffic, "launch_ms": launch_ms, "launches": len(launches),
                      "flop_per_launch": tot_flop / max(len(launches), 1),
                      "edge_gemm": args.edge_gemm},
         "finite": finite,
     }
+    if exact is not None:
+        line["f32_exact"] = exact
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(kind, moving, args.cpu_seconds)
     print(json.dumps(line), flush=True)

@@ -8,8 +8,13 @@
 
 namespace {
 
-constexpr int kCols = 4;  // output columns per wave
+constexpr int kKc = 256;  // K chunk staged in LDS
 
+// One wave per output column (4 per workgroup, so even N = 256 fills a few
+// hundred waves); the workgroup stages x[r0 : r0+MB, kc : kc+256] in LDS once
+// for its 4 columns, lanes stride K (k = kc + lane + 64 t) so every weight-row
+// load is a coalesced 256-B wave access for any row stride / alignment.  Each
+// weight is read exactly once; fixed summation order (deterministic).
 template <int MB>
 __global__ __launch_bounds__(256) void linear_skinny_kernel(const float *__restrict__ x,
                                                             int64_t ldx, int64_t m, int64_t k,
@@ -18,40 +23,42 @@ __global__ __launch_bounds__(256) void linear_skinny_kernel(const float *__restr
                                                             const float *__restrict__ b,
                                                             int64_t n, int act,
                                                             float *__restrict__ y, int64_t ldy) {
+    __shared__ float xs[MB][kKc];
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
-    const int64_t n0 = ((int64_t)blockIdx.x * 4 + wave) * kCols;
-    if (n0 >= n) return;
-    const float *wr[kCols];
-#pragma unroll
-    for (int j = 0; j < kCols; ++j) wr[j] = w + (n0 + j < n ? n0 + j : n - 1) * ldw;
+    const int64_t col = (int64_t)blockIdx.x * 4 + wave;
+    const bool colok = col < n;
+    const float *wr = w + (colok ? col : n - 1) * ldw;
     for (int64_t r0 = 0; r0 < m; r0 += MB) {
-        float acc[kCols][MB];
+        float acc[MB];
 #pragma unroll
-        for (int j = 0; j < kCols; ++j)
+        for (int i = 0; i < MB; ++i) acc[i] = 0.0f;
+        for (int64_t kc = 0; kc < k; kc += kKc) {
+            float wv[4];
 #pragma unroll
-            for (int i = 0; i < MB; ++i) acc[j][i] = 0.0f;
-        for (int64_t kk = lane; kk < k; kk += 64) {
-            float wv[kCols];
-#pragma unroll
-            for (int j = 0; j < kCols; ++j) wv[j] = wr[j][kk];
+            for (int t = 0; t < 4; ++t) {
+                const int64_t kg = kc + lane + 64 * t;
+                wv[t] = kg < k ? wr[kg] : 0.0f;
+            }
+            __syncthreads();  // previous chunk consumed
+            for (int e = threadIdx.x; e < MB * kKc; e += 256) {
+                const int i = e / kKc, kk = e % kKc;
+                const int64_t row = r0 + i, kg = kc + kk;
+                xs[i][kk] = (row < m && kg < k) ? x[row * ldx + kg] : 0.0f;
+            }
+            __syncthreads();
 #pragma unroll
             for (int i = 0; i < MB; ++i) {
-                const int64_t row = r0 + i;
-                const float xv = row < m ? x[row * ldx + kk] : 0.0f;
 #pragma unroll
-                for (int j = 0; j < kCols; ++j) acc[j][i] += xv * wv[j];
+                for (int t = 0; t < 4; ++t) acc[i] = fmaf(xs[i][lane + 64 * t], wv[t], acc[i]);
             }
         }
 #pragma unroll
-        for (int j = 0; j < kCols; ++j) {
-#pragma unroll
-            for (int i = 0; i < MB; ++i) {
-                const float v = wave_sum(acc[j][i]);
-                const int64_t row = r0 + i, col = n0 + j;
-                if (lane == 0 && row < m && col < n)
-                    y[row * ldy + col] = act_apply(v + (b ? b[col] : 0.0f), act);
-            }
+        for (int i = 0; i < MB; ++i) {
+            const float v = wave_sum(acc[i]);
+            const int64_t row = r0 + i;
+            if (lane == 0 && row < m && colok)
+                y[row * ldy + col] = act_apply(v + (b ? b[col] : 0.0f), act);
         }
     }
 }
@@ -107,17 +114,16 @@ extern "C" int mmpde_linear_skinny(const float *x, int64_t ldx, int64_t m, int64
     MMPDE_REQUIRE(x && w && y && m > 0 && k > 0 && n > 0 && m <= 4096);
     MMPDE_REQUIRE(ldx >= k && ldw >= k && ldy >= n && act >= 0 && act <= 2);
     hipStream_t st = as_stream(stream);
-    dim3 grid(ceil_div(n, 4 * kCols));
-    if (m <= 1)
-        hipLaunchKernelGGL((linear_skinny_kernel<1>), grid, dim3(256), 0, st, x, ldx, m, k, w, ldw, b, n, act, y, ldy);
-    else if (m <= 2)
-        hipLaunchKernelGGL((linear_skinny_kernel<2>), grid, dim3(256), 0, st, x, ldx, m, k, w, ldw, b, n, act, y, ldy);
-    else if (m <= 4)
-        hipLaunchKernelGGL((linear_skinny_kernel<4>), grid, dim3(256), 0, st, x, ldx, m, k, w, ldw, b, n, act, y, ldy);
-    else if (m <= 8)
-        hipLaunchKernelGGL((linear_skinny_kernel<8>), grid, dim3(256), 0, st, x, ldx, m, k, w, ldw, b, n, act, y, ldy);
-    else
-        hipLaunchKernelGGL((linear_skinny_kernel<16>), grid, dim3(256), 0, st, x, ldx, m, k, w, ldw, b, n, act, y, ldy);
+    dim3 grid(ceil_div(n, 4));
+#define MMPDE_SKINNY(MB) \
+    hipLaunchKernelGGL((linear_skinny_kernel<MB>), grid, dim3(256), 0, st, x, ldx, m, k, w, ldw, b, n, act, y, ldy)
+    if (m <= 1) MMPDE_SKINNY(1);
+    else if (m <= 2) MMPDE_SKINNY(2);
+    else if (m <= 4) MMPDE_SKINNY(4);
+    else if (m <= 8) MMPDE_SKINNY(8);
+    else if (m <= 16) MMPDE_SKINNY(16);
+    else MMPDE_SKINNY(32);
+#undef MMPDE_SKINNY
     MMPDE_RET_LAUNCH();
     return MMPDE_OK;
 }

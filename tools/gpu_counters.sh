@@ -6,7 +6,7 @@ set -u
 export TMPDIR=/tmp
 OUT=${PMC_OUT:-gpurun_out/ctr}
 REGEX=${PMC_REGEX:-gnn_layer_fused}
-ARGS=${PMC_BENCH_ARGS:---steps 2 --warmup 1 --no-cpu-baseline}
+ARGS=${PMC_BENCH_ARGS:---steps 2 --warmup 1 --no-cpu-baseline --no-f32-exact}
 mkdir -p "$OUT"
 i=0
 for grp in "$@"; do

@@ -7,8 +7,8 @@
 set -u
 export TMPDIR=/tmp
 OUT=${PMC_OUT:-gpurun_out/pmc}
-REGEX=${PMC_REGEX:-edge_}
-ARGS=${PMC_BENCH_ARGS:---steps 2 --warmup 1 --no-cpu-baseline}
+REGEX=${PMC_REGEX:-gnn_layer_fused}
+ARGS=${PMC_BENCH_ARGS:---steps 2 --warmup 1 --no-cpu-baseline --no-f32-exact}
 mkdir -p "$OUT"
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 ${PMC_TIMEOUT:-300} rocprofv3 --pmc $c --kernel-include-regex "$REGEX" \
