@@ -96,7 +96,7 @@ class EdgeTracer:
         beg = (ctypes.c_void_p * self.L)(*self.pool.ev[base:base + self.L])
         end = (ctypes.c_void_p * self.L)(*self.pool.ev[base + self.L:base + 2 * self.L])
         t = self._lib.GnnExec(ctypes.cast(beg, ctypes.POINTER(ctypes.c_void_p)),
-                              ctypes.cast(end, ctypes.POINTER(ctypes.c_void_p)), 0)
+                              ctypes.cast(end, ctypes.POINTER(ctypes.c_void_p)), 0, None)
         self.traces.append((t, beg, end))
         return t
 

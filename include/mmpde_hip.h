@@ -176,8 +176,10 @@ int mmpde_gnn_forward(const float *u, const float *pos, int64_t n, int k, const 
  *         operand x is scaled by a power of two (per weight column; per
  *         neighbour slot for the activations) and split into fp16 hi + lo
  *         (x = hi + lo to 2^-22 relative); the product uses hi*hi + hi*lo +
- *         lo*hi on v_mfma_f32_16x16x32_f16 with fp32 accumulation.  Error vs
- *         fp64 is measured beside F32 in tests/test_gpu_precision.py. */
+ *         lo*hi on v_mfma_f32_16x16x32_f16 with fp32 accumulation.  Applies
+ *         to every GEMM of the fused layer (edge message_net_2 and the node
+ *         GEMMs update_net_1/2, message_net_1).  Error vs fp64 is measured
+ *         beside F32 in tests/test_gpu_precision.py. */
 #define MMPDE_EDGE_GEMM_F32 0
 #define MMPDE_EDGE_GEMM_F16X3 1
 
@@ -190,11 +192,22 @@ typedef struct {
     void *const *edge_begin; /* n_layers hipEvent_t, or NULL */
     void *const *edge_end;   /* n_layers hipEvent_t, or NULL */
     int edge_gemm;           /* MMPDE_EDGE_GEMM_* */
+    const void *packed;      /* F16X3: weight images from mmpde_gnn_pack_f16x3 for these
+                                layers (caller-cached); NULL: packed per call into the
+                                workspace */
 } mmpde_gnn_exec;
 
 /* Most layers mmpde_gnn_forward_ex accepts (sizes the workspace's packed
  * weight region). */
 #define MMPDE_GNN_MAX_LAYERS 16
+
+/* F16X3 weight images (message_net_2, update_net_1, update_net_2 and
+ * message_net_1 of every layer, split into scaled fp16 hi/lo MFMA operand
+ * images + per-column scales).  Depends only on the weights: a caller packs
+ * once per parameter change and passes it as mmpde_gnn_exec.packed. */
+int64_t mmpde_gnn_pack_bytes(int n_layers);
+int mmpde_gnn_pack_f16x3(const mmpde_gnn_layer_params *layers, int n_layers, void *pack,
+                         mmpde_stream_t stream);
 
 int mmpde_gnn_forward_ex(const float *u, const float *pos, int64_t n, int k, const int32_t *nbr,
                          mmpde_gnn_scales sc, const mmpde_gnn_embed_params *emb,

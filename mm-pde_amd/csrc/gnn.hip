@@ -50,12 +50,14 @@ struct EpiProj {  // message_net_1 split (see header comment)
     int64_t ldw1;
     const float *u, *pos;
     mmpde_gnn_scales sc;
+    uint32_t *amax;  // nullable: range slot of the consumer layer ([0,64): |a|, [64,128): |b|)
     __device__ void operator()(const f32x16 &acc, int64_t row0, int col0, int lane, int64_t m,
                                int part) const {
         const int c = col0 + (lane & 31);
         const float wdu = w_du[c * ldw1], wdx = w_dx[c * ldw1], wdy = w_dy[c * ldw1];
         const float wt = w_t[c * ldw1], bb = b1[c];
         float *dst = part == 0 ? out_a : out_b;
+        float vmax = 0.0f;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int64_t row = row0 + acc_row(r, lane);
@@ -72,8 +74,10 @@ struct EpiProj {  // message_net_1 split (see header comment)
                     v = acc[r] - node;
                 }
                 dst[row * H + c] = v;
+                vmax = fmaxf(vmax, fabsf(v));
             }
         }
+        if (amax) amax_publish(vmax, amax + kAmaxShards * part);
     }
 };
 
@@ -262,7 +266,8 @@ struct FusedLayerArgs {
     int64_t n;
     int k;
     const float *w2, *b2;             // message_net_2.0 [128,128], [128]
-    const char *w2pk;                 // F16X3: packed W2 image + column scales
+    const char *pk;                   // F16X3: this layer's packed images (kLayerPack bytes)
+    const char *pkn;                  // F16X3: next layer's packed images (NEXT)
     const float *u1, *c1;             // update_net_1.0 [128, ld_u1] (h | mean | t), [128]
     int64_t ld_u1;
     const float *u2, *c2;             // update_net_2.0 [128,128], [128]
@@ -274,6 +279,8 @@ struct FusedLayerArgs {
     float *a_out, *b_out;
     const float *u, *pos;             // node input u [n], pos [n,3] = (t, x, y)
     mmpde_gnn_scales sc;
+    const uint32_t *amax_in;          // F16X3: range slot of a, b (this layer)
+    uint32_t *amax_out;               // F16X3 + NEXT: range slot of a', b'
 };
 
 __device__ __forceinline__ float4 relu4_add(float4 x, float4 y) {
@@ -287,12 +294,6 @@ __device__ __forceinline__ float f4c(const float4 &v, int t) {
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-    return v;
-}
-
 // Power of two s with mx * s in [2^13, 2^14) (fp16 max 65504): the scale of
 // the F16X3 split.  mx zero / subnormal / inf / nan -> 1; clamped to
 // [2^-40, 2^40] so a scaled bias can never overflow fp32.
@@ -303,43 +304,363 @@ __device__ __forceinline__ float split_scale(float mx) {
     return __uint_as_float((uint32_t)se << 23);
 }
 
-// ---------------------------------------------------------------------------
-// F16X3 weight image of message_net_2 (per layer, once per forward): column
-// col is scaled by sw[col] = split_scale(max_k |W2[col, k]|) and split into
-// fp16 hi + lo, laid out as the exact per-lane B operand of
-// v_mfma_f32_16x16x32_f16: [ctile c][kstep s][hi|lo][lane][8 halves] with
-// lane = 16 g + (col & 15) holding k = 32 s + 8 g + j.  Followed by sw[128].
-// ---------------------------------------------------------------------------
-constexpr int kW2PackBytes = 65536 + 512;
+// 1 / s for a power of two s from split_scale (exact).
+__device__ __forceinline__ float pow2_inv(float s) {
+    const uint32_t eb = (__float_as_uint(s) >> 23) & 0xff;
+    return __uint_as_float((254u - eb) << 23);
+}
 
-struct W2PackArgs {
-    const float *w2[MMPDE_GNN_MAX_LAYERS];
+// ---------------------------------------------------------------------------
+// F16X3 weight images (once per parameter change, mmpde_gnn_pack_f16x3).  A
+// B-operand matrix B[k][j] = W[row(j)][koff(j) + k] (K = 128 or 256) is packed
+// column by column: column j is scaled by sw[j] = split_scale(max_k |B[k][j]|)
+// and split into fp16 hi + lo, laid out as the exact per-lane B operand of
+// v_mfma_f32_16x16x32_f16: [ctile j/16][kstep K/32][hi|lo][lane][8 halves],
+// lane = 16 g + (j & 15) holding k = 32 s + 8 g + t; followed by sw[n_cols].
+// Per layer: message_net_2 (edge), update_net_1 (h | mean part), update_net_2
+// and message_net_1 as the two node halves (j < 128: W1[j, 0:128] -> a;
+// j >= 128: W1[j-128, 128:256] -> b).
+// ---------------------------------------------------------------------------
+constexpr int64_t kPkW2 = 0;                              // 128 x 128
+constexpr int64_t kPkU1 = kPkW2 + 65536 + 512;            // 128 x 256
+constexpr int64_t kPkU2 = kPkU1 + 131072 + 512;           // 128 x 128
+constexpr int64_t kPkW1 = kPkU2 + 65536 + 512;            // 256 x 128
+constexpr int64_t kLayerPack = kPkW1 + 131072 + 1024;     // bytes per layer (16-B multiple)
+static_assert(kLayerPack % 16 == 0, "pack alignment");
+// per layer: |a| and |b| range slots of kAmaxShards uint32 each
+constexpr int64_t kAmaxBytes = (int64_t)MMPDE_GNN_MAX_LAYERS * 2 * kAmaxShards * 4;
+
+struct PackSrc {
+    const float *w[MMPDE_GNN_MAX_LAYERS];
+    int64_t ld[MMPDE_GNN_MAX_LAYERS];
 };
 
-__global__ __launch_bounds__(128) void w2_pack_f16x3_kernel(W2PackArgs a, char *__restrict__ pack) {
-    __shared__ float red[2];
-    const int layer = blockIdx.y, col = blockIdx.x, k = threadIdx.x;
-    const float w = a.w2[layer][col * H + k];
+template <int K>
+__global__ __launch_bounds__(K) void pack_f16x3_kernel(PackSrc src, int half_split, int64_t img_off,
+                                                       int64_t n_cols, char *__restrict__ pack) {
+    __shared__ float red[K / 64];
+    const int layer = blockIdx.y, jcol = blockIdx.x, k = threadIdx.x;
+    const int row = half_split ? (jcol & 127) : jcol;
+    const int koff = half_split ? (jcol >> 7) * 128 : 0;
+    const float w = src.w[layer][(int64_t)row * src.ld[layer] + koff + k];
     const float m = wave_max(fabsf(w));
     if ((k & 63) == 0) red[k >> 6] = m;
     __syncthreads();
-    const float sw = split_scale(fmaxf(red[0], red[1]));
+    float mx = red[0];
+#pragma unroll
+    for (int i = 1; i < K / 64; ++i) mx = fmaxf(mx, red[i]);
+    const float sw = split_scale(mx);
     const float x = w * sw;
     const _Float16 hi = (_Float16)x;
     const _Float16 lo = (_Float16)(x - (float)hi);
-    const int c = col >> 4, s = k >> 5, g = (k >> 3) & 3, j = k & 7;
-    const int lane = 16 * g + (col & 15);
-    _Float16 *img = (_Float16 *)(pack + (int64_t)layer * kW2PackBytes);
-    img[(((c * 4 + s) * 2 + 0) * 64 + lane) * 8 + j] = hi;
-    img[(((c * 4 + s) * 2 + 1) * 64 + lane) * 8 + j] = lo;
-    if (k == 0) ((float *)(pack + (int64_t)layer * kW2PackBytes + 65536))[col] = sw;
+    const int c = jcol >> 4, s = k >> 5, g = (k >> 3) & 3, t = k & 7;
+    const int lane = 16 * g + (jcol & 15);
+    char *base = pack + (int64_t)layer * kLayerPack + img_off;
+    _Float16 *img = (_Float16 *)base;
+    img[(((c * (K / 32) + s) * 2 + 0) * 64 + lane) * 8 + t] = hi;
+    img[(((c * (K / 32) + s) * 2 + 1) * 64 + lane) * 8 + t] = lo;
+    if (k == 0) ((float *)(base + n_cols * K * 4))[jcol] = sw;
 }
 
-template <bool NEXT, bool F16X3>
+// B fragment (c, s, hi|lo) of a packed image with KS k-steps, as a half8.
+__device__ __forceinline__ half8 bfrag(const char *img, int KS, int c, int s, int hl, int lane) {
+    const float4 v = ((const float4 *)img)[((c * KS + s) * 2 + hl) * 64 + lane];
+    return *(const half8 *)&v;
+}
+
+// Scaled fp16 hi/lo split of 8 consecutive-k values.
+__device__ __forceinline__ void split8(const float4 &x0, const float4 &x1, float sc, half8 &hi,
+                                       half8 &lo) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        const float x = f4c(t < 4 ? x0 : x1, t & 3) * sc;
+        const _Float16 h = (_Float16)x;
+        hi[t] = h;
+        lo[t] = (_Float16)(x - (float)h);
+    }
+}
+
+// The same split as split8 with sc = 1 in 12 instructions: hi by v_cvt_pk_f16_f32
+// (RN), lo = RN_f16(x - f32(hi)) by v_fma_mix (x - hi is exact in f32, so
+// the result is bit-identical to split8; tools/ubench/split_check.hip).  The
+// trailing s_nop covers the VALU-write -> MFMA-operand hazard, which hipcc does
+// not pad for asm producers (cdna_hip_programming.md §5.7).
+__device__ __forceinline__ void split8_rn(const float4 &a, const float4 &b, half8 &hi, half8 &lo) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 h, l;
+    asm("v_cvt_pk_f16_f32 %0, %8, %9\n\t"
+        "v_cvt_pk_f16_f32 %1, %10, %11\n\t"
+        "v_cvt_pk_f16_f32 %2, %12, %13\n\t"
+        "v_cvt_pk_f16_f32 %3, %14, %15\n\t"
+        "v_fma_mixlo_f16 %4, %8, 1.0, -%0 op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixhi_f16 %4, %9, 1.0, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixlo_f16 %5, %10, 1.0, -%1 op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixhi_f16 %5, %11, 1.0, -%1 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixlo_f16 %6, %12, 1.0, -%2 op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixhi_f16 %6, %13, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixlo_f16 %7, %14, 1.0, -%3 op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixhi_f16 %7, %15, 1.0, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+        "s_nop 1"
+        : "=&v"(h.x), "=&v"(h.y), "=&v"(h.z), "=&v"(h.w), "=&v"(l.x), "=&v"(l.y), "=&v"(l.z),
+          "=&v"(l.w)
+        : "v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w));
+    hi = *(const half8 *)&h;
+    lo = *(const half8 *)&l;
+}
+
+__device__ __forceinline__ float absmax4(float m, const float4 &v) {
+    return fmaxf(fmaxf(fmaxf(m, fabsf(v.x)), fmaxf(fabsf(v.y), fabsf(v.z))), fabsf(v.w));
+}
+
+__device__ __forceinline__ f32x4 mfma_f16(const half8 &a, const half8 &b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+// ---- epilogue pieces shared by both arithmetic modes -------------------------
+// C layout of a 16x16 tile: lane (r = l & 15, g = l >> 4) holds column r of
+// rows 4 g + q.  Wave w owns output columns 32 w .. 32 w + 31 (two tiles).
+
+// v = relu(accH * sH + accM * sM + U1[:, 256] t + c1) -> vbuf (sH, sM: per-lane
+// unscale of the h / mean parts; 1 for the fp32 path, whose accH holds both).
+__device__ __forceinline__ void upd1_store(const FusedLayerArgs &p, const f32x4 &acc0,
+                                           const f32x4 &acc1, float s0, float s1, float *vbuf,
+                                           int64_t tile0, int wave, int lane) {
+    const int r = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+        const f32x4 &acc = cc ? acc1 : acc0;
+        const float sc = cc ? s1 : s0;
+        const int col = 32 * wave + 16 * cc + r;
+        const float wt = p.u1[(int64_t)col * p.ld_u1 + 256], bb = p.c1[col];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int64_t row = min(tile0 + 4 * g + q, p.n - 1);
+            const float pt = p.pos[row * 3 + 0] * p.sc.inv_tmax;
+            vbuf[(4 * g + q) * FRP + col] = fmaxf(acc[q] * sc + wt * pt + bb, 0.0f);
+        }
+    }
+}
+
+// h' = BN(h + relu(acc * inv + c2)); inv nullptr = 1 (fp32 path).
+template <bool NEXT>
+__device__ __forceinline__ void upd2_store(const FusedLayerArgs &p, const f32x4 *acc,
+                                           const float *inv, float *hbuf, int64_t tile0, int wave,
+                                           int lane) {
+    const int r = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+        const int col = 32 * wave + 16 * cc + r;
+        const float bb = p.c2[col], rm = p.bn_rm[col], rv = p.bn_rv[col];
+        const float gw = p.bn_w[col], gb = p.bn_b[col];
+        const float iv = inv ? inv[cc] : 1.0f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int64_t row = tile0 + 4 * g + q;
+            const int64_t rowc = min(row, p.n - 1);
+            const float x = p.h[rowc * H + col] + fmaxf(acc[cc][q] * iv + bb, 0.0f);
+            const float y = bn_eval(x, rm, rv, gw, gb, p.eps);
+            if (row < p.n) p.h_out[row * H + col] = y;
+            if (NEXT) hbuf[(4 * g + q) * FRP + col] = y;
+        }
+    }
+}
+
+// a' = acc[cc] * inv + node terms + t term + b1, b' = acc[2+cc] * inv - node terms.
+__device__ __forceinline__ void proj_store(const FusedLayerArgs &p, const f32x4 *acc,
+                                           const float *inv, int64_t tile0, int wave, int lane) {
+    const int r = lane & 15, g = lane >> 4;
+    float amx = 0.0f, bmx = 0.0f;
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+        const int col = 32 * wave + 16 * cc + r;
+        const float *wc = p.w1n + (int64_t)col * p.ld_w1n;
+        const float wdu = wc[256], wdx = wc[257], wdy = wc[258], wt = wc[259];
+        const float bb = p.b1n[col];
+        const float ia = inv ? inv[cc] : 1.0f, ib = inv ? inv[2 + cc] : 1.0f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int64_t row = tile0 + 4 * g + q;
+            if (row < p.n) {
+                const float uu = p.u[row];
+                const float px = p.pos[row * 3 + 1] * p.sc.inv_lx;
+                const float py = p.pos[row * 3 + 2] * p.sc.inv_ly;
+                const float pt = p.pos[row * 3 + 0] * p.sc.inv_tmax;
+                const float node = wdu * uu + wdx * px + wdy * py;
+                const float va = acc[cc][q] * ia + node + wt * pt + bb;
+                const float vb = acc[2 + cc][q] * ib - node;
+                p.a_out[row * H + col] = va;
+                p.b_out[row * H + col] = vb;
+                amx = fmaxf(amx, fabsf(va));
+                bmx = fmaxf(bmx, fabsf(vb));
+            }
+        }
+    }
+    if (p.amax_out) {
+        amax_publish(amx, p.amax_out);
+        amax_publish(bmx, p.amax_out + kAmaxShards);
+    }
+}
+
+// F16X3 epilogue: the three node GEMMs on split fp16 MFMA.  Every wave holds
+// the whole 16-row A tile, so the activation scales (wave_max) are uniform
+// across the workgroup; the h and mean parts of update_net_1 get their own
+// scales and accumulators.  k map: float4 number 2 s + u holds k = 32 s + 8 g
+// + 4 u + t (the 16x16x32 A fragment).
+template <bool NEXT>
+__device__ __forceinline__ void epilogue_f16x3(const FusedLayerArgs &p, const float *red,
+                                               float *vbuf, float *hbuf, int64_t tile0,
+                                               int64_t tgt, int wave, int lane) {
+    const int r = lane & 15, g = lane >> 4;
+    auto kp = [&](int i) { return 32 * (i >> 1) + 8 * g + 4 * (i & 1); };
+    // ---- update_net_1
+    {
+        float4 hA[8], mA[8];
+        float mh = 0.0f, mm = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            hA[i] = *(const float4 *)(p.h + tgt * H + kp(i));
+            mA[i] = *(const float4 *)(red + r * FRP + kp(i));
+            mh = absmax4(mh, hA[i]);
+            mm = absmax4(mm, mA[i]);
+        }
+        const float sh = split_scale(wave_max(mh)), sm = split_scale(wave_max(mm));
+        const char *img = p.pk + kPkU1;
+        const float *su = (const float *)(img + 131072);
+        f32x4 aH[2], aM[2];
+#pragma unroll
+        for (int cc = 0; cc < 2; ++cc) aH[cc] = aM[cc] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+            half8 hh, hl, mh8, ml8;
+            split8(hA[2 * s4], hA[2 * s4 + 1], sh, hh, hl);
+            split8(mA[2 * s4], mA[2 * s4 + 1], sm, mh8, ml8);
+            half8 bh[2], bl[2], ch[2], cl[2];
+#pragma unroll
+            for (int cc = 0; cc < 2; ++cc) {
+                bh[cc] = bfrag(img, 8, 2 * wave + cc, s4, 0, lane);
+                bl[cc] = bfrag(img, 8, 2 * wave + cc, s4, 1, lane);
+                ch[cc] = bfrag(img, 8, 2 * wave + cc, 4 + s4, 0, lane);
+                cl[cc] = bfrag(img, 8, 2 * wave + cc, 4 + s4, 1, lane);
+            }
+#pragma unroll
+            for (int cc = 0; cc < 2; ++cc) aH[cc] = mfma_f16(hh, bh[cc], aH[cc]);
+#pragma unroll
+            for (int cc = 0; cc < 2; ++cc) aM[cc] = mfma_f16(mh8, ch[cc], aM[cc]);
+#pragma unroll
+            for (int cc = 0; cc < 2; ++cc) aH[cc] = mfma_f16(hh, bl[cc], aH[cc]);
+#pragma unroll
+            for (int cc = 0; cc < 2; ++cc) aM[cc] = mfma_f16(mh8, cl[cc], aM[cc]);
+#pragma unroll
+            for (int cc = 0; cc < 2; ++cc) aH[cc] = mfma_f16(hl, bh[cc], aH[cc]);
+#pragma unroll
+            for (int cc = 0; cc < 2; ++cc) aM[cc] = mfma_f16(ml8, ch[cc], aM[cc]);
+        }
+        f32x4 acc[2];
+        float one[2];
+#pragma unroll
+        for (int cc = 0; cc < 2; ++cc) {
+            const float swc = su[32 * wave + 16 * cc + r];
+            const float ih = 1.0f / (sh * swc), im = 1.0f / (sm * swc);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[cc][q] = aH[cc][q] * ih + aM[cc][q] * im;
+            one[cc] = 1.0f;
+        }
+        upd1_store(p, acc[0], acc[1], one[0], one[1], vbuf, tile0, wave, lane);
+    }
+    __syncthreads();
+    // ---- update_net_2 + residual + BatchNorm
+    {
+        float4 vA[8];
+        float mv = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            vA[i] = *(const float4 *)(vbuf + r * FRP + kp(i));
+            mv = absmax4(mv, vA[i]);
+        }
+        const float sv = split_scale(wave_max(mv));
+        const char *img = p.pk + kPkU2;
+        const float *su = (const float *)(img + 65536);
+        f32x4 acc[2];
+#pragma unroll
+        for (int cc = 0; cc < 2; ++cc) acc[cc] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+            half8 vh, vl;
+            split8(vA[2 * s4], vA[2 * s4 + 1], sv, vh, vl);
+            half8 bh[2], bl[2];
+#pragma unroll
+            for (int cc = 0; cc < 2; ++cc) {
+                bh[cc] = bfrag(img, 4, 2 * wave + cc, s4, 0, lane);
+                bl[cc] = bfrag(img, 4, 2 * wave + cc, s4, 1, lane);
+            }
+#pragma unroll
+            for (int cc = 0; cc < 2; ++cc) acc[cc] = mfma_f16(vh, bh[cc], acc[cc]);
+#pragma unroll
+            for (int cc = 0; cc < 2; ++cc) acc[cc] = mfma_f16(vh, bl[cc], acc[cc]);
+#pragma unroll
+            for (int cc = 0; cc < 2; ++cc) acc[cc] = mfma_f16(vl, bh[cc], acc[cc]);
+        }
+        float inv[2];
+#pragma unroll
+        for (int cc = 0; cc < 2; ++cc) inv[cc] = 1.0f / (sv * su[32 * wave + 16 * cc + r]);
+        upd2_store<NEXT>(p, acc, inv, hbuf, tile0, wave, lane);
+    }
+    if (!NEXT) return;
+    __syncthreads();
+    // ---- next layer's message_net_1 node halves
+    {
+        float4 hA[8];
+        float mh = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            hA[i] = *(const float4 *)(hbuf + r * FRP + kp(i));
+            mh = absmax4(mh, hA[i]);
+        }
+        const float sh = split_scale(wave_max(mh));
+        const char *img = p.pkn + kPkW1;
+        const float *su = (const float *)(img + 131072);
+        f32x4 acc[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[c] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+        // image column tiles: a' cols 32 w + 16 cc -> tile 2 w + cc; b' -> 8 + 2 w + cc
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+            half8 xh, xl;
+            split8(hA[2 * s4], hA[2 * s4 + 1], sh, xh, xl);
+            half8 bh[4], bl[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const int ct = 8 * (c >> 1) + 2 * wave + (c & 1);
+                bh[c] = bfrag(img, 4, ct, s4, 0, lane);
+                bl[c] = bfrag(img, 4, ct, s4, 1, lane);
+            }
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc[c] = mfma_f16(xh, bh[c], acc[c]);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc[c] = mfma_f16(xh, bl[c], acc[c]);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc[c] = mfma_f16(xl, bh[c], acc[c]);
+        }
+        float inv[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            inv[c] = 1.0f / (sh * su[128 * (c >> 1) + 32 * wave + 16 * (c & 1) + r]);
+        proj_store(p, acc, inv, tile0, wave, lane);
+    }
+}
+
+// PHASES (profiling builds only, tools/ubench): bit 0 runs the edge loop,
+// bit 1 the epilogue, bit 2 skips the producer work of the edge loop, bit 3
+// its MFMAs; production launches use 3.
+template <bool NEXT, bool F16X3, int PHASES = 3>
 __global__ __launch_bounds__(256, 2) void gnn_layer_fused_kernel(FusedLayerArgs p) {
-    __shared__ float4 lds4[8 * 8 * 64 + FT * FRP / 4];  // W2 image (64 KB) | a tile
+    // LDS: [2 rounds][4 producer slots] A-operand images of 8 KB (the message
+    // inputs of one neighbour slot for the 16 targets, in per-lane fragment
+    // order) | the tile's a rows.  After the edge loop the slot region holds
+    // the epilogue scratch (mean, v, h').
+    __shared__ float4 lds4[2 * 4 * 512 + FT * FRP / 4];
     float *lds = (float *)lds4;
-    float *lds_a = lds + 8 * 8 * 64 * 4;  // [16][FRP]: a rows of the tile
+    float *lds_a = lds + 2 * 4 * 512 * 4;  // [16][FRP]
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
     const int r = lane & 15, g = lane >> 4;
@@ -347,157 +668,183 @@ __global__ __launch_bounds__(256, 2) void gnn_layer_fused_kernel(FusedLayerArgs 
     const int64_t tile0 = (int64_t)tile * FT;
     const int64_t tgt = min(tile0 + r, p.n - 1);
 
-    if (F16X3) {
-        for (int e = threadIdx.x; e < 8 * 8 * 64; e += 256) lds4[e] = ((const float4 *)p.w2pk)[e];
-    } else {
-        for (int e = threadIdx.x; e < 8 * 8 * 64; e += 256) {
-            const int l = e & 63, j = (e >> 6) & 7, c = e >> 9;
-            lds4[e] = *(const float4 *)(p.w2 + (16 * c + (l & 15)) * H + 16 * j + 4 * (l >> 4));
-        }
-    }
+    // F16X3: one power-of-two scale per launch for the message inputs
+    // m = relu(a_i + b_j) <= max|a| + max|b| (range slots published by the
+    // producer of a, b), so m * sc < 2^14 fits fp16 and the split keeps 22 bits.
+    float sc = 1.0f;
+    if (F16X3) sc = split_scale(amax_read(p.amax_in) + amax_read(p.amax_in + kAmaxShards));
     for (int e = threadIdx.x; e < FT * 32; e += 256) {
         const int row = e >> 5, c4 = e & 31;
         const int64_t src = min(tile0 + row, p.n - 1);
-        *(float4 *)(lds_a + row * FRP + 4 * c4) = *(const float4 *)(p.a + src * H + 4 * c4);
+        float4 v = *(const float4 *)(p.a + src * H + 4 * c4);
+        if (F16X3) v = make_float4(v.x * sc, v.y * sc, v.z * sc, v.w * sc);
+        *(float4 *)(lds_a + row * FRP + 4 * c4) = v;
     }
 
-    float bias[8];
+    // This wave's output columns 32 w .. 32 w + 31 (tiles cc = 0, 1): its
+    // message_net_2 B fragments stay in registers for the whole launch.
+    // F32: float4 wf[cc][j] = W2[col][16 j + 4 g + t];
+    // F16X3: wh/wl[cc][s4] = packed hi / lo half8 (k = 32 s4 + 8 g + t).
+    float4 wf[2][8];
+    half8 wh[2][4], wl[2][4];
+    float bias[2], bsc[2], inv[2];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) bias[c] = p.b2[16 * c + r];
-    f32x4 S[8];
+    for (int cc = 0; cc < 2; ++cc) {
+        const int col = 32 * wave + 16 * cc + r;
+        bias[cc] = p.b2[col];
+        if (F16X3) {
+            const char *img = p.pk + kPkW2;
 #pragma unroll
-    for (int c = 0; c < 8; ++c) S[c] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+            for (int s4 = 0; s4 < 4; ++s4) {
+                wh[cc][s4] = bfrag(img, 4, 2 * wave + cc, s4, 0, lane);
+                wl[cc][s4] = bfrag(img, 4, 2 * wave + cc, s4, 1, lane);
+            }
+            const float sw = ((const float *)(img + 65536))[col];
+            bsc[cc] = bias[cc] * sw * sc;
+            inv[cc] = pow2_inv(sw) * pow2_inv(sc);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) wf[cc][j] = *(const float4 *)(p.w2 + col * H + 16 * j + 4 * g);
+        }
+    }
+    f32x4 S[2] = {(f32x4){0.0f, 0.0f, 0.0f, 0.0f}, (f32x4){0.0f, 0.0f, 0.0f, 0.0f}};
 
-    // Neighbour rows: slot e's b row is loaded one slot ahead, its index two
-    // slots ahead, so neither latency sits in front of the MFMAs.
-    // (clamped: a malformed caller table must not fault the GPU)
-    // k map of the b / a pieces: F32 float4 j holds k = 16 j + 4 g + t;
+    // Producer role: wave w builds the A operand of neighbour slot 4 r + w in
+    // round r.  The loop is software-pipelined by one round: iteration r
+    // produces round r + 1 into the other LDS buffer while it multiplies
+    // round r, so the producer's gather/VALU work and the consumer's MFMAs of
+    // the same wave interleave.  Branch-free: slot indices past k are clamped
+    // (their products are discarded by a select).  b rows are loaded one round
+    // ahead of their production, indices two.  (clamped: a malformed caller
+    // table must not fault the GPU)
+    // k map of the b / a pieces: F32 float4 i holds k = 16 i + 4 g + t;
     // F16X3 float4 i holds k = 32 (i >> 1) + 8 g + 4 (i & 1) + t.
     const int32_t *nrow = p.nbr + tgt * p.k;
     const uint32_t nmax = (uint32_t)(p.n - 1);
+    const int kmax = p.k - 1;
     auto piece = [&](int i) { return F16X3 ? 32 * (i >> 1) + 8 * g + 4 * (i & 1) : 16 * i + 4 * g; };
     float4 bv[8];
-    uint32_t src_next = 0;
-    if (wave < p.k) {
-        const int64_t src = min((uint32_t)nrow[wave], nmax);
+    {
+        const int64_t src = min((uint32_t)nrow[min(wave, kmax)], nmax);
 #pragma unroll
         for (int i = 0; i < 8; ++i) bv[i] = *(const float4 *)(p.b + src * H + piece(i));
-        if (wave + 4 < p.k) src_next = (uint32_t)nrow[wave + 4];
     }
-    float bsw[8], isw[8];  // F16X3: bias * column scale, 1 / column scale
-    if (F16X3) {
-        const float *swp = (const float *)(p.w2pk + 65536);
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            const float sw = swp[16 * c + r];
-            bsw[c] = bias[c] * sw;
-            isw[c] = 1.0f / sw;
-        }
-    }
-    __syncthreads();
-    const float4 *wimg = lds4 + lane;
+    uint32_t src_next = (uint32_t)nrow[min(wave + 4, kmax)];
+    __syncthreads();  // a tile staged
     const float *arow = lds_a + r * FRP;
 
-    for (int e = wave; e < p.k; e += 4) {
-        // keep the W2 image in LDS: without this the compiler hoists the
-        // loop-invariant ds_reads out of the loop (256 VGPRs) and spills them
-        asm volatile("" ::: "memory");
+    auto produce = [&](int rd) {  // slot 4 rd + wave -> buffer rd & 1
+        const int e = 4 * rd + wave;
         float4 m[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) m[i] = relu4_add(*(const float4 *)(arow + piece(i)), bv[i]);
-        if (e + 4 < p.k) {
+        for (int i = 0; i < 8; ++i) {
+            const float4 av = *(const float4 *)(arow + piece(i));
+            if (F16X3)
+                m[i] = make_float4(fmaxf(fmaf(bv[i].x, sc, av.x), 0.0f), fmaxf(fmaf(bv[i].y, sc, av.y), 0.0f),
+                                   fmaxf(fmaf(bv[i].z, sc, av.z), 0.0f), fmaxf(fmaf(bv[i].w, sc, av.w), 0.0f));
+            else
+                m[i] = relu4_add(av, bv[i]);
+        }
+        {
             const int64_t src = min(src_next, nmax);
 #pragma unroll
             for (int i = 0; i < 8; ++i) bv[i] = *(const float4 *)(p.b + src * H + piece(i));
-            if (e + 8 < p.k) src_next = (uint32_t)nrow[e + 8];
+            src_next = (uint32_t)nrow[min(e + 8, kmax)];
         }
-        f32x4 acc[8];
-        if (!F16X3) {
-#pragma unroll
-            for (int c = 0; c < 8; ++c) acc[c] = (f32x4){bias[c], bias[c], bias[c], bias[c]};
-            float4 w[8];
-#pragma unroll
-            for (int c = 0; c < 8; ++c) w[c] = wimg[c * 8 * 64];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                float4 wn[8];
-                if (j < 7) {
-#pragma unroll
-                    for (int c = 0; c < 8; ++c) wn[c] = wimg[(c * 8 + j + 1) * 64];
-                }
-#pragma unroll
-                for (int t = 0; t < 4; ++t) {
-#pragma unroll
-                    for (int c = 0; c < 8; ++c) acc[c] = mfma16(f4c(m[j], t), f4c(w[c], t), acc[c]);
-                }
-                if (j < 7) {
-#pragma unroll
-                    for (int c = 0; c < 8; ++c) w[c] = wn[c];
-                }
-            }
-#pragma unroll
-            for (int c = 0; c < 8; ++c) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) S[c][q] += fmaxf(acc[c][q], 0.0f);
-            }
-        } else {
-            // slot scale: the largest message input of this neighbour slot
-            float mx = 0.0f;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) mx = fmaxf(fmaxf(fmaxf(mx, m[i].x), fmaxf(m[i].y, m[i].z)), m[i].w);
-            const float sc = split_scale(wave_max(mx));
-            const float isc = 1.0f / sc;
-#pragma unroll
-            for (int c = 0; c < 8; ++c) {
-                const float bi = bsw[c] * sc;
-                acc[c] = (f32x4){bi, bi, bi, bi};
-            }
+        float4 *dst = lds4 + (rd & 1) * 4 * 512 + wave * 512 + lane;
+        if (F16X3) {
 #pragma unroll
             for (int s4 = 0; s4 < 4; ++s4) {
                 half8 hi, lo;
+                split8_rn(m[2 * s4], m[2 * s4 + 1], hi, lo);
+                dst[(2 * s4 + 0) * 64] = *(const float4 *)&hi;
+                dst[(2 * s4 + 1) * 64] = *(const float4 *)&lo;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) dst[i * 64] = m[i];
+        }
+    };
+    auto consume = [&](int rd) {  // all 4 slots of buffer rd & 1
+        const float4 *slot = lds4 + (rd & 1) * 4 * 512 + lane;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float4 *src = slot + q * 512;
+            const bool valid = 4 * rd + q < p.k;
+            f32x4 acc[2] = {(f32x4){0.0f, 0.0f, 0.0f, 0.0f}, (f32x4){0.0f, 0.0f, 0.0f, 0.0f}};
+            if (F16X3) {
+#pragma unroll
+                for (int s4 = 0; s4 < 4; ++s4) {
+                    const float4 h4 = src[(2 * s4 + 0) * 64], l4 = src[(2 * s4 + 1) * 64];
+                    const half8 hi = *(const half8 *)&h4, lo = *(const half8 *)&l4;
+#pragma unroll
+                    for (int cc = 0; cc < 2; ++cc) acc[cc] = mfma_f16(hi, wh[cc][s4], acc[cc]);
+#pragma unroll
+                    for (int cc = 0; cc < 2; ++cc) acc[cc] = mfma_f16(hi, wl[cc][s4], acc[cc]);
+#pragma unroll
+                    for (int cc = 0; cc < 2; ++cc) acc[cc] = mfma_f16(lo, wh[cc][s4], acc[cc]);
+                }
+#pragma unroll
+                for (int cc = 0; cc < 2; ++cc) {
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        const float v = fmaf(fmaxf(acc[cc][t] + bsc[cc], 0.0f), inv[cc], S[cc][t]);
+                        S[cc][t] = valid ? v : S[cc][t];
+                    }
+                }
+            } else {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    const float x = f4c(m[2 * s4 + (j >> 2)], j & 3) * sc;
-                    const _Float16 h = (_Float16)x;
-                    hi[j] = h;
-                    lo[j] = (_Float16)(x - (float)h);
-                }
-                half8 wh[8], wl[8];
+                    const float4 mv = src[j * 64];
 #pragma unroll
-                for (int c = 0; c < 8; ++c) {
-                    const float4 a4 = wimg[((c * 4 + s4) * 2 + 0) * 64];
-                    const float4 b4 = wimg[((c * 4 + s4) * 2 + 1) * 64];
-                    wh[c] = *(const half8 *)&a4;
-                    wl[c] = *(const half8 *)&b4;
+                    for (int t = 0; t < 4; ++t) {
+#pragma unroll
+                        for (int cc = 0; cc < 2; ++cc) acc[cc] = mfma16(f4c(mv, t), f4c(wf[cc][j], t), acc[cc]);
+                    }
                 }
 #pragma unroll
-                for (int c = 0; c < 8; ++c) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi, wh[c], acc[c], 0, 0, 0);
+                for (int cc = 0; cc < 2; ++cc) {
 #pragma unroll
-                for (int c = 0; c < 8; ++c) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi, wl[c], acc[c], 0, 0, 0);
-#pragma unroll
-                for (int c = 0; c < 8; ++c) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(lo, wh[c], acc[c], 0, 0, 0);
-            }
-#pragma unroll
-            for (int c = 0; c < 8; ++c) {
-                const float inv = isc * isw[c];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) S[c][q] = fmaf(fmaxf(acc[c][q], 0.0f), inv, S[c][q]);
+                    for (int t = 0; t < 4; ++t) {
+                        const float v = S[cc][t] + fmaxf(acc[cc][t] + bias[cc], 0.0f);
+                        S[cc][t] = valid ? v : S[cc][t];
+                    }
+                }
             }
         }
+    };
+
+    const int rounds = (PHASES & 1) ? (p.k + 3) / 4 : 0;
+    if (rounds > 0) {
+        if (!(PHASES & 4)) produce(0);
+        __syncthreads();
+        for (int rd = 0; rd + 1 < rounds; ++rd) {  // one basic block: produce || consume
+            if (!(PHASES & 4)) produce(rd + 1);
+            if (!(PHASES & 8)) consume(rd);
+            __syncthreads();  // round rd consumed, round rd + 1 produced
+        }
+        if (!(PHASES & 8)) consume(rounds - 1);
     }
 
-    // ---- cross-wave sum of the edge messages: red[wave][row][col] ----------
-    __syncthreads();  // every wave is done with the W2 image
-    float *red = lds;                      // 4 x 16 x FRP
-    float *vbuf = lds + 4 * FT * FRP;      // 16 x FRP
+    // ---- mean of the messages -> red[row][col] (C layout: rows 4 g + t) -----
+    __syncthreads();  // every wave is done with the slots
+    float *red = lds;                      // 16 x FRP: mean
+    float *vbuf = lds + FT * FRP;          // 16 x FRP
     float *hbuf = vbuf + FT * FRP;         // 16 x FRP
+    const float kdiv = (float)p.k;
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
+    for (int cc = 0; cc < 2; ++cc) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) red[(wave * FT + 4 * g + q) * FRP + 16 * c + r] = S[c][q];
+        for (int t = 0; t < 4; ++t) red[(4 * g + t) * FRP + 32 * wave + 16 * cc + r] = S[cc][t] / kdiv;
     }
     __syncthreads();
-    const float kdiv = (float)p.k;
+
+    if constexpr (!(PHASES & 2)) {
+        return;
+    } else if constexpr (F16X3) {
+        epilogue_f16x3<NEXT>(p, red, vbuf, hbuf, tile0, tgt, wave, lane);
+        return;
+    }
 
     // ---- update_net_1: v = relu(U1 [h | mean | t] + c1), cols 32 w .. 32 w + 31
     {
@@ -506,16 +853,7 @@ __global__ __launch_bounds__(256, 2) void gnn_layer_fused_kernel(FusedLayerArgs 
 #pragma unroll 2
         for (int j = 0; j < 8; ++j) {
             const float4 hv = *(const float4 *)(hrow + 16 * j);
-            float4 mv = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-#pragma unroll
-            for (int w = 0; w < 4; ++w) {
-                const float4 x = *(const float4 *)(red + (w * FT + r) * FRP + 16 * j + 4 * g);
-                mv.x += x.x;
-                mv.y += x.y;
-                mv.z += x.z;
-                mv.w += x.w;
-            }
-            mv = make_float4(mv.x / kdiv, mv.y / kdiv, mv.z / kdiv, mv.w / kdiv);
+            const float4 mv = *(const float4 *)(red + r * FRP + 16 * j + 4 * g);
 #pragma unroll
             for (int cc = 0; cc < 2; ++cc) {
                 const float *wr = p.u1 + (int64_t)(32 * wave + 16 * cc + r) * p.ld_u1 + 16 * j + 4 * g;
@@ -527,17 +865,7 @@ __global__ __launch_bounds__(256, 2) void gnn_layer_fused_kernel(FusedLayerArgs 
                 for (int t = 0; t < 4; ++t) acc[cc] = mfma16(f4c(mv, t), f4c(wm, t), acc[cc]);
             }
         }
-#pragma unroll
-        for (int cc = 0; cc < 2; ++cc) {
-            const int col = 32 * wave + 16 * cc + r;
-            const float wt = p.u1[(int64_t)col * p.ld_u1 + 256], bb = p.c1[col];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int64_t row = min(tile0 + 4 * g + q, p.n - 1);
-                const float pt = p.pos[row * 3 + 0] * p.sc.inv_tmax;
-                vbuf[(4 * g + q) * FRP + col] = fmaxf(acc[cc][q] + wt * pt + bb, 0.0f);
-            }
-        }
+        upd1_store(p, acc[0], acc[1], 1.0f, 1.0f, vbuf, tile0, wave, lane);
     }
     __syncthreads();
 
@@ -554,21 +882,7 @@ __global__ __launch_bounds__(256, 2) void gnn_layer_fused_kernel(FusedLayerArgs 
                 for (int t = 0; t < 4; ++t) acc[cc] = mfma16(f4c(vv, t), f4c(w, t), acc[cc]);
             }
         }
-#pragma unroll
-        for (int cc = 0; cc < 2; ++cc) {
-            const int col = 32 * wave + 16 * cc + r;
-            const float bb = p.c2[col], rm = p.bn_rm[col], rv = p.bn_rv[col];
-            const float gw = p.bn_w[col], gb = p.bn_b[col];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int64_t row = tile0 + 4 * g + q;
-                const int64_t rowc = min(row, p.n - 1);
-                const float x = p.h[rowc * H + col] + fmaxf(acc[cc][q] + bb, 0.0f);
-                const float y = bn_eval(x, rm, rv, gw, gb, p.eps);
-                if (row < p.n) p.h_out[row * H + col] = y;
-                if (NEXT) hbuf[(4 * g + q) * FRP + col] = y;
-            }
-        }
+        upd2_store<NEXT>(p, acc, nullptr, hbuf, tile0, wave, lane);
     }
     if (!NEXT) return;
     __syncthreads();
@@ -590,26 +904,7 @@ __global__ __launch_bounds__(256, 2) void gnn_layer_fused_kernel(FusedLayerArgs 
                 for (int t = 0; t < 4; ++t) acc[c] = mfma16(f4c(hv, t), f4c(w, t), acc[c]);
             }
         }
-#pragma unroll
-        for (int cc = 0; cc < 2; ++cc) {
-            const int col = 32 * wave + 16 * cc + r;
-            const float *wc = p.w1n + (int64_t)col * p.ld_w1n;
-            const float wdu = wc[256], wdx = wc[257], wdy = wc[258], wt = wc[259];
-            const float bb = p.b1n[col];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int64_t row = tile0 + 4 * g + q;
-                if (row < p.n) {
-                    const float uu = p.u[row];
-                    const float px = p.pos[row * 3 + 1] * p.sc.inv_lx;
-                    const float py = p.pos[row * 3 + 2] * p.sc.inv_ly;
-                    const float pt = p.pos[row * 3 + 0] * p.sc.inv_tmax;
-                    const float node = wdu * uu + wdx * px + wdy * py;
-                    p.a_out[row * H + col] = acc[cc][q] + node + wt * pt + bb;
-                    p.b_out[row * H + col] = acc[2 + cc][q] - node;
-                }
-            }
-        }
+        proj_store(p, acc, nullptr, tile0, wave, lane);
     }
 }
 
@@ -675,8 +970,9 @@ inline bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
 // ===========================================================================
 extern "C" int64_t mmpde_gnn_workspace_bytes(int64_t n) {
     // h, a, b ping-pong = 6 x [n,128] fp32 (the unfused per-layer API uses
-    // 4 of them as a, b, mean, v), then the F16X3 packed message_net_2 images
-    return 6 * n * H * (int64_t)sizeof(float) + (int64_t)MMPDE_GNN_MAX_LAYERS * kW2PackBytes;
+    // 4 of them as a, b, mean, v), then room for per-call F16X3 weight images
+    return 6 * n * H * (int64_t)sizeof(float) + kAmaxBytes +
+           (int64_t)MMPDE_GNN_MAX_LAYERS * kLayerPack;
 }
 
 extern "C" int mmpde_gnn_embed(const float *u, const float *pos, int64_t n,
@@ -771,13 +1067,15 @@ extern "C" int mmpde_gnn_head(const float *h, int64_t n, const mmpde_gnn_head_pa
 static int launch_fused_layer(const float *a, const float *b, const float *h, const float *u,
                               const float *pos, int64_t n, int k, const int32_t *nbr,
                               mmpde_gnn_scales sc, const mmpde_gnn_layer_params *p,
-                              const mmpde_gnn_layer_params *next, const char *w2pk,
+                              const mmpde_gnn_layer_params *next, const char *pk,
+                              const char *pkn, const uint32_t *amax_in, uint32_t *amax_out,
                               float *h_out, float *a_out, float *b_out, hipStream_t st) {
     MMPDE_REQUIRE(p->upd1_ld >= 257 && (p->upd1_ld & 3) == 0 && aligned16(p->upd1_w));
     MMPDE_REQUIRE(aligned16(p->msg2_w) && aligned16(p->upd2_w));
-    FusedLayerArgs f{a, b, h, nbr, n, k, p->msg2_w, p->msg2_b, w2pk, p->upd1_w, p->upd1_b,
+    FusedLayerArgs f{a, b, h, nbr, n, k, p->msg2_w, p->msg2_b, pk, pkn, p->upd1_w, p->upd1_b,
                      p->upd1_ld, p->upd2_w, p->upd2_b, p->bn_w, p->bn_b, p->bn_rm, p->bn_rv,
-                     p->eps, h_out, nullptr, nullptr, 0, a_out, b_out, u, pos, sc};
+                     p->eps, h_out, nullptr, nullptr, 0, a_out, b_out, u, pos, sc, amax_in,
+                     amax_out};
     const dim3 grid(ceil_div(n, FT));
     if (next) {
         MMPDE_REQUIRE(next->msg1_ld >= 260 && (next->msg1_ld & 3) == 0 && aligned16(next->msg1_w));
@@ -787,11 +1085,43 @@ static int launch_fused_layer(const float *a, const float *b, const float *h, co
     }
 #define MMPDE_FUSED(NX, SPLIT) \
     hipLaunchKernelGGL((gnn_layer_fused_kernel<NX, SPLIT>), grid, dim3(256), 0, st, f)
-    if (next && w2pk) MMPDE_FUSED(true, true);
+    if (next && pk) MMPDE_FUSED(true, true);
     else if (next) MMPDE_FUSED(true, false);
-    else if (w2pk) MMPDE_FUSED(false, true);
+    else if (pk) MMPDE_FUSED(false, true);
     else MMPDE_FUSED(false, false);
 #undef MMPDE_FUSED
+    MMPDE_RET_LAUNCH();
+    return MMPDE_OK;
+}
+
+extern "C" int64_t mmpde_gnn_pack_bytes(int n_layers) {
+    return n_layers < 0 ? 0 : (int64_t)n_layers * kLayerPack;
+}
+
+extern "C" int mmpde_gnn_pack_f16x3(const mmpde_gnn_layer_params *layers, int n_layers,
+                                    void *pack, mmpde_stream_t stream) {
+    MMPDE_REQUIRE(layers && pack && n_layers > 0 && n_layers <= MMPDE_GNN_MAX_LAYERS);
+    MMPDE_REQUIRE(aligned16(pack));
+    hipStream_t st = as_stream(stream);
+    PackSrc w2{}, u1{}, u2{}, w1{};
+    for (int l = 0; l < n_layers; ++l) {
+        const mmpde_gnn_layer_params &q = layers[l];
+        MMPDE_REQUIRE(q.msg1_w && q.msg2_w && q.upd1_w && q.upd2_w);
+        MMPDE_REQUIRE(q.msg1_ld >= 260 && q.upd1_ld >= 257);
+        w2.w[l] = q.msg2_w;
+        w2.ld[l] = H;
+        u1.w[l] = q.upd1_w;
+        u1.ld[l] = q.upd1_ld;
+        u2.w[l] = q.upd2_w;
+        u2.ld[l] = H;
+        w1.w[l] = q.msg1_w;
+        w1.ld[l] = q.msg1_ld;
+    }
+    char *pk = (char *)pack;
+    hipLaunchKernelGGL(pack_f16x3_kernel<128>, dim3(128, n_layers), dim3(128), 0, st, w2, 0, kPkW2, (int64_t)128, pk);
+    hipLaunchKernelGGL(pack_f16x3_kernel<256>, dim3(128, n_layers), dim3(256), 0, st, u1, 0, kPkU1, (int64_t)128, pk);
+    hipLaunchKernelGGL(pack_f16x3_kernel<128>, dim3(128, n_layers), dim3(128), 0, st, u2, 0, kPkU2, (int64_t)128, pk);
+    hipLaunchKernelGGL(pack_f16x3_kernel<128>, dim3(256, n_layers), dim3(128), 0, st, w1, 1, kPkW1, (int64_t)256, pk);
     MMPDE_RET_LAUNCH();
     return MMPDE_OK;
 }
@@ -813,17 +1143,23 @@ extern "C" int mmpde_gnn_forward_ex(const float *u, const float *pos, int64_t n,
     float *hb[2] = {ws, ws + n * H};
     float *ab[2] = {ws + 2 * n * H, ws + 3 * n * H};
     float *bb[2] = {ws + 4 * n * H, ws + 5 * n * H};
-    char *pack = (char *)(ws + 6 * n * H);
+    const char *pack = nullptr;
+    // range slots of every layer's message inputs (F16X3 split scale)
+    uint32_t *amax = (uint32_t *)(ws + 6 * n * H);
+    int rc;
     if (mode == MMPDE_EDGE_GEMM_F16X3 && n_layers > 0) {
-        W2PackArgs pa{};
-        for (int l = 0; l < n_layers; ++l) {
-            MMPDE_REQUIRE(layers[l].msg2_w != nullptr);
-            pa.w2[l] = layers[l].msg2_w;
+        if (hipMemsetAsync(amax, 0, kAmaxBytes, st) != hipSuccess) return MMPDE_ERR_INVALID_ARG;
+        if (exec->packed) {
+            MMPDE_REQUIRE(aligned16(exec->packed));
+            pack = (const char *)exec->packed;
+        } else {
+            char *wpk = (char *)(ws + 6 * n * H) + kAmaxBytes;
+            rc = mmpde_gnn_pack_f16x3(layers, n_layers, wpk, stream);
+            if (rc) return rc;
+            pack = wpk;
         }
-        hipLaunchKernelGGL(w2_pack_f16x3_kernel, dim3(H, n_layers), dim3(128), 0, st, pa, pack);
-        MMPDE_RET_LAUNCH();
     }
-    int rc = mmpde_gnn_embed(u, pos, n, sc, emb, ab[1], hb[0], stream);  // ab[1]: scratch
+    rc = mmpde_gnn_embed(u, pos, n, sc, emb, ab[1], hb[0], stream);  // ab[1]: scratch
     if (rc) return rc;
     if (n_layers > 0) {
         // layer 0's message_net_1 halves; later layers get theirs from the fused kernel
@@ -832,7 +1168,7 @@ extern "C" int mmpde_gnn_forward_ex(const float *u, const float *pos, int64_t n,
         const int64_t ld = p0->msg1_ld;
         GemmArgs g{n, hb[0], hb[0] + 64, H, p0->msg1_w, p0->msg1_w + 64, ld, 64};
         EpiProj epi{ab[0], bb[0], p0->msg1_b, p0->msg1_w + 256, p0->msg1_w + 257,
-                    p0->msg1_w + 258, p0->msg1_w + 259, ld, u, pos, sc};
+                    p0->msg1_w + 258, p0->msg1_w + 259, ld, u, pos, sc, pack ? amax : nullptr};
         rc = launch_gemm<EpiProj, true>(g, 2, epi, st);
         if (rc) return rc;
     }
@@ -842,9 +1178,12 @@ extern "C" int mmpde_gnn_forward_ex(const float *u, const float *pos, int64_t n,
         hipEvent_t ee = exec && exec->edge_end ? (hipEvent_t)exec->edge_end[l] : nullptr;
         if (eb && hipEventRecord(eb, st) != hipSuccess) return MMPDE_ERR_INVALID_ARG;
         const mmpde_gnn_layer_params *next = l + 1 < n_layers ? &layers[l + 1] : nullptr;
-        const char *w2pk = mode == MMPDE_EDGE_GEMM_F16X3 ? pack + (int64_t)l * kW2PackBytes : nullptr;
+        const char *pk = pack ? pack + (int64_t)l * kLayerPack : nullptr;
+        const char *pkn = pack && next ? pack + (int64_t)(l + 1) * kLayerPack : nullptr;
+        const uint32_t *ain = pack ? amax + 2 * kAmaxShards * l : nullptr;
+        uint32_t *aout = pack && next ? amax + 2 * kAmaxShards * (l + 1) : nullptr;
         rc = launch_fused_layer(ab[cur], bb[cur], hb[cur], u, pos, n, k, nbr, sc, &layers[l], next,
-                                w2pk, hb[cur ^ 1], ab[cur ^ 1], bb[cur ^ 1], st);
+                                pk, pkn, ain, aout, hb[cur ^ 1], ab[cur ^ 1], bb[cur ^ 1], st);
         if (rc) return rc;
         if (ee && hipEventRecord(ee, st) != hipSuccess) return MMPDE_ERR_INVALID_ARG;
         cur ^= 1;

@@ -13,7 +13,7 @@ import os
 import torch
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libmmpde_hip.so")
-ABI_VERSION = 10100
+ABI_VERSION = 10200
 
 ACT_NONE, ACT_TANH, ACT_RELU = 0, 1, 2
 # message_net_2 edge GEMM arithmetic (include/mmpde_hip.h MMPDE_EDGE_GEMM_*)
@@ -60,7 +60,7 @@ _P3 = _P * 3
 class GnnExec(ctypes.Structure):
     """mmpde_gnn_exec: optional per-layer hipEvents + the edge-GEMM arithmetic."""
     _fields_ = [("edge_begin", ctypes.POINTER(_P)), ("edge_end", ctypes.POINTER(_P)),
-                ("edge_gemm", _I)]
+                ("edge_gemm", _I), ("packed", _P)]
 
 
 class DmmGraphBranch(ctypes.Structure):
@@ -102,6 +102,8 @@ _SIGS = {
     "mmpde_gnn_edge_mean": (_I, [_P, _P, _P, _I64, _I, _P, _P, _P, _P]),
     "mmpde_gnn_head": (_I, [_P, _I64, _P, _P, _P]),
     "mmpde_gnn_forward": (_I, [_P, _P, _I64, _I, _P, GnnScales, _P, _P, _I, _P, _P, _P, _P]),
+    "mmpde_gnn_pack_bytes": (_I64, [_I]),
+    "mmpde_gnn_pack_f16x3": (_I, [_P, _I, _P, _P]),
     "mmpde_gnn_forward_ex": (_I, [_P, _P, _I64, _I, _P, GnnScales, _P, _P, _I, _P, _P, _P, _P,
                                   _P]),
     "mmpde_dmm_workspace_bytes": (_I64, [_I64, _I64, _I, _I]),

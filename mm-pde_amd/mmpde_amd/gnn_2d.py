@@ -122,8 +122,9 @@ class MP_PDE_Solver_2D(nn.Module):  # noqa: N801 - reference name
             nn.Conv1d(8, 1, 8, stride=2))
         self._pack_key = None
         self._pack = None
-        # message_net_2 arithmetic: "f32" (exact fp32 MFMA) or "f16x3" (fp32
-        # emulated by scaled fp16 hi/lo splits; include/mmpde_hip.h)
+        self._f16x3 = None
+        # GEMM arithmetic of the fused layers: "f32" (exact fp32 MFMA) or "f16x3"
+        # (fp32 emulated by scaled fp16 hi/lo splits; include/mmpde_hip.h)
         self.edge_gemm = "f32"
 
     def __repr__(self):
@@ -159,7 +160,20 @@ class MP_PDE_Solver_2D(nn.Module):  # noqa: N801 - reference name
             arr = (L.GnnLayerParams * len(layer_params))(*layer_params)
             self._pack = ((self.scales(), emb, arr, head), f, [g._pack for g in self.gnn_layers])
             self._pack_key = key
+            self._f16x3 = None
         return self._pack[0]
+
+    def packed_f16x3(self, device):
+        """Split fp16 weight images of every layer (mmpde_gnn_pack_f16x3), rebuilt
+        when a parameter changes (device_params refresh)."""
+        _, _, arr, _ = self.device_params()
+        if self._f16x3 is None:
+            nb = L.lib().mmpde_gnn_pack_bytes(len(arr))
+            buf = torch.empty((nb // 4,), dtype=torch.float32, device=device)
+            L.check(L.lib().mmpde_gnn_pack_f16x3(arr, len(arr), L.ptr(buf), L.stream(device)),
+                    "mmpde_gnn_pack_f16x3")
+            self._f16x3 = buf
+        return self._f16x3
 
     def check_supported(self):
         if self.training:
@@ -190,8 +204,10 @@ class MP_PDE_Solver_2D(nn.Module):  # noqa: N801 - reference name
         if out is None:
             out = torch.empty((n, 1), dtype=torch.float32, device=u.device)
         if trace is None:
-            trace = L.GnnExec(None, None, 0)
+            trace = L.GnnExec(None, None, 0, None)
         trace.edge_gemm = L.EDGE_GEMM[self.edge_gemm]
+        trace.packed = (L.ptr(self.packed_f16x3(u.device)) if self.edge_gemm == "f16x3"
+                        else None)
         L.check(L.lib().mmpde_gnn_forward_ex(
             L.ptr(u), L.ptr(pos), n, nbr.shape[1], L.ptr(nbr), sc, ctypes.byref(emb), arr,
             len(arr), ctypes.byref(head), L.ptr(workspace), L.ptr(out),

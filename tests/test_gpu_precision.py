@@ -40,16 +40,19 @@ def test_edge_gemm_f16x3_vs_fp64(dev, kind):
     ref32 = refcpu.mp_pde_solver(sd, opde, u, pos, ei).reshape(-1).double()
     model.to(dev)
     g = _Nodes(u.to(dev), pos.to(dev), nbr.int().to(dev))
-    errs = {"cpu-f32": (ref32 - ref64).abs().max().item()}
+    outs = {"cpu-f32": ref32}
     for mode in ("f32", "f16x3"):
         model.edge_gemm = mode
-        out = model(g).reshape(-1).double().cpu()
-        errs[mode] = (out - ref64).abs().max().item()
+        outs[mode] = model(g).reshape(-1).double().cpu()
     model.edge_gemm = "f32"
+    errs = {m: (o - ref64).abs().max().item() for m, o in outs.items()}
+    rms = {m: (o - ref64).pow(2).mean().sqrt().item() for m, o in outs.items()}
     scale = ref64.abs().max().item()
-    print(f"{kind}: max|ref| {scale:.3e}; max|err vs fp64|: "
-          + ", ".join(f"{k} {v:.3e}" for k, v in errs.items()))
+    print(f"{kind}: max|ref| {scale:.3e}; vs fp64 max|err| / rms err: "
+          + ", ".join(f"{m} {errs[m]:.3e} / {rms[m]:.3e}" for m in outs)
+          + f"; f16x3 vs f32 max|diff| {(outs['f16x3'] - outs['f32']).abs().max().item():.3e}")
     assert errs["f16x3"] <= 4.0 * max(errs["f32"], errs["cpu-f32"]) + 1e-12
+    assert rms["f16x3"] <= 4.0 * max(rms["f32"], rms["cpu-f32"]) + 1e-12
     assert errs["f16x3"] <= 2e-4 * scale + 1e-7
 
 

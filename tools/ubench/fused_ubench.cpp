@@ -1,0 +1,147 @@
+// Phase breakdown of gnn_layer_fused_kernel (profiling aid, not shipped):
+// times the prologue-only / edge-only / epilogue-only / full variants of the
+// fused layer kernel on a cylinder-sized synthetic layer (n = 16 x 2521 rows,
+// k = 35 random in-trajectory neighbours), both arithmetic modes.
+//   make -C tools/ubench && tools/ubench/fused_ubench
+#include "../../mm-pde_amd/csrc/gnn.hip"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#define CK(x)                                                                     \
+    do {                                                                          \
+        hipError_t e_ = (x);                                                      \
+        if (e_ != hipSuccess) {                                                   \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            return 1;                                                             \
+        }                                                                         \
+    } while (0)
+
+static float *dev_random(size_t count, float lo, float hi, std::mt19937 &rng) {
+    std::uniform_real_distribution<float> d(lo, hi);
+    std::vector<float> h(count);
+    for (auto &v : h) v = d(rng);
+    float *p = nullptr;
+    if (hipMalloc(&p, count * 4) != hipSuccess) return nullptr;
+    hipMemcpy(p, h.data(), count * 4, hipMemcpyHostToDevice);
+    return p;
+}
+
+// Ceiling check: the edge loop's MFMA count (v_mfma_f32_16x16x32_f16, 2
+// accumulators, 12 per chain link) with register operands only.
+__global__ __launch_bounds__(256, 2) void mfma_only_kernel(const float4 *seed, int iters, float4 *out) {
+    const int lane = threadIdx.x & 63;
+    const float4 s0 = seed[lane], s1 = seed[lane + 64];
+    half8 a = *(const half8 *)&s0, b = *(const half8 *)&s1;
+    f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+        for (int j = 0; j < 12; ++j) {
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b, a, acc1, 0, 0, 0);
+        }
+    }
+    out[blockIdx.x * 256 + threadIdx.x] = make_float4(acc0[0] + acc1[0], acc0[1], acc0[2], acc1[3]);
+}
+
+template <bool NEXT, bool SPLIT, int PH>
+static float time_variant(const FusedLayerArgs &f, int64_t n, int iters) {
+    const dim3 grid(ceil_div(n, FT));
+    for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((gnn_layer_fused_kernel<NEXT, SPLIT, PH>), grid, dim3(256), 0, 0, f);
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    hipEventRecord(a, 0);
+    for (int i = 0; i < iters; ++i) hipLaunchKernelGGL((gnn_layer_fused_kernel<NEXT, SPLIT, PH>), grid, dim3(256), 0, 0, f);
+    hipEventRecord(b, 0);
+    hipEventSynchronize(b);
+    float ms = 0;
+    hipEventElapsedTime(&ms, a, b);
+    hipEventDestroy(a);
+    hipEventDestroy(b);
+    return 1e3f * ms / iters;
+}
+
+int main(int argc, char **argv) {
+    const int B = argc > 1 ? atoi(argv[1]) : 16, N = 2521, k = 35;
+    const int64_t n = (int64_t)B * N;
+    std::mt19937 rng(1);
+    float *a = dev_random(n * H, -1, 1, rng), *b = dev_random(n * H, -1, 1, rng);
+    float *h = dev_random(n * H, -1, 1, rng), *u = dev_random(n, -1, 1, rng);
+    float *pos = dev_random(n * 3, 0, 1, rng);
+    float *w1 = dev_random(128 * 260, -0.06f, 0.06f, rng), *b1 = dev_random(128, -0.06f, 0.06f, rng);
+    float *w2 = dev_random(128 * 128, -0.09f, 0.09f, rng), *b2 = dev_random(128, -0.09f, 0.09f, rng);
+    float *u1 = dev_random(128 * 260, -0.06f, 0.06f, rng), *c1 = dev_random(128, -0.06f, 0.06f, rng);
+    float *u2 = dev_random(128 * 128, -0.09f, 0.09f, rng), *c2 = dev_random(128, -0.09f, 0.09f, rng);
+    float *bnw = dev_random(128, 0.5f, 1.5f, rng), *bnb = dev_random(128, -0.1f, 0.1f, rng);
+    float *bnm = dev_random(128, -0.1f, 0.1f, rng), *bnv = dev_random(128, 0.5f, 1.5f, rng);
+    std::vector<int32_t> hn(n * k);
+    std::uniform_int_distribution<int> di(0, N - 1);
+    // argv[2]: "random" (default, in-trajectory random rows), "local" (rows of
+    // the same 16-row tile: gathers hit L1/L2), "self" (every edge = the target)
+    const char *pat = argc > 2 ? argv[2] : "random";
+    for (int64_t i = 0; i < n; ++i)
+        for (int e = 0; e < k; ++e) {
+            int64_t src = (i / N) * N + di(rng);
+            if (!strcmp(pat, "local")) src = std::min<int64_t>(n - 1, (i / 16) * 16 + (e % 16));
+            if (!strcmp(pat, "self")) src = i;
+            hn[i * k + e] = (int32_t)src;
+        }
+    printf("neighbour pattern: %s\n", pat);
+    int32_t *nbr;
+    CK(hipMalloc(&nbr, n * k * 4));
+    CK(hipMemcpy(nbr, hn.data(), n * k * 4, hipMemcpyHostToDevice));
+    float *ho, *ao, *bo;
+    CK(hipMalloc(&ho, n * H * 4));
+    CK(hipMalloc(&ao, n * H * 4));
+    CK(hipMalloc(&bo, n * H * 4));
+    mmpde_gnn_layer_params lp{w1, b1, w2, b2, u1, c1, u2, c2, bnw, bnb, bnm, bnv, 1e-5f, 260, 260};
+    mmpde_gnn_layer_params two[2] = {lp, lp};
+    char *pack;
+    CK(hipMalloc(&pack, mmpde_gnn_pack_bytes(2)));
+    if (mmpde_gnn_pack_f16x3(two, 2, pack, 0) != 0) return 1;
+    CK(hipDeviceSynchronize());
+    mmpde_gnn_scales sc{1.0f, 1.0f, 1.0f / 2.9f};
+    uint32_t *amax;
+    CK(hipMalloc(&amax, 4 * 2 * kAmaxShards * 4));
+    {   // range slots: |a|, |b| <= 1 for the uniform [-1, 1) inputs
+        std::vector<uint32_t> hs(4 * 2 * kAmaxShards, 0x3f800000u);
+        CK(hipMemcpy(amax, hs.data(), hs.size() * 4, hipMemcpyHostToDevice));
+    }
+    FusedLayerArgs f{a, b, h, nbr, n, k, w2, b2, pack, pack + kLayerPack, u1, c1, 260, u2, c2,
+                     bnw, bnb, bnm, bnv, 1e-5f, ho, w1, b1, 260, ao, bo, u, pos, sc,
+                     amax, amax + 2 * kAmaxShards};
+    const int it = 20;
+    printf("n=%lld k=%d  (us per launch)\n", (long long)n, k);
+    printf("f16x3: prologue %.1f  edge %.1f  epilogue %.1f  full %.1f\n",
+           time_variant<true, true, 0>(f, n, it), time_variant<true, true, 1>(f, n, it),
+           time_variant<true, true, 2>(f, n, it), time_variant<true, true, 3>(f, n, it));
+    printf("f16x3 edge loop: no-produce %.1f  no-mfma %.1f\n", time_variant<true, true, 5>(f, n, it),
+           time_variant<true, true, 9>(f, n, it));
+    printf("f32  : prologue %.1f  edge %.1f  epilogue %.1f  full %.1f\n",
+           time_variant<true, false, 0>(f, n, it), time_variant<true, false, 1>(f, n, it),
+           time_variant<true, false, 2>(f, n, it), time_variant<true, false, 3>(f, n, it));
+    {   // same MFMA count as the F16X3 edge loop: 2521 blocks x 4 waves x 9 rounds x 96
+        float4 *seed, *out;
+        CK(hipMalloc(&seed, 128 * 16));
+        CK(hipMemset(seed, 0x3c, 128 * 16));
+        CK(hipMalloc(&out, (size_t)ceil_div(n, FT) * 256 * 16));
+        const int nb = ceil_div(n, FT), iters = 9 * 96 / 24;
+        for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(mfma_only_kernel, dim3(nb), dim3(256), 0, 0, seed, iters, out);
+        hipEvent_t a0, b0;
+        hipEventCreate(&a0);
+        hipEventCreate(&b0);
+        hipEventRecord(a0, 0);
+        for (int i = 0; i < it; ++i) hipLaunchKernelGGL(mfma_only_kernel, dim3(nb), dim3(256), 0, 0, seed, iters, out);
+        hipEventRecord(b0, 0);
+        hipEventSynchronize(b0);
+        float ms = 0;
+        hipEventElapsedTime(&ms, a0, b0);
+        printf("mfma-only ceiling (edge-loop MFMA count, register operands): %.1f us\n", 1e3f * ms / it);
+    }
+    CK(hipGetLastError());
+    return 0;
+}
