@@ -1,65 +1,93 @@
 // Small dense helpers: skinny-M linear layers (res_cut MLP, DMM output_mlp /
 // fc layers, the per-trajectory branch . W contraction) and a direct 2-D
-// convolution (DMM ConvNet branch, Burgers res_cut).  These run at M = B
-// (<= 32 rows), where every weight is read exactly once: they are weight-
-// streaming (HBM-bound) kernels, one wave per 4 output columns, lanes striding K
-// so each weight row is read coalesced.
+// convolution (DMM ConvNet branch, Burgers res_cut).  The linears run at M = B
+// (<= 32 rows), where every weight is read exactly once: weight-streaming
+// (HBM-bound) kernels.
 #include "common.hpp"
 
 namespace {
 
-constexpr int kKc = 256;  // K chunk staged in LDS
+// y[r, c] = act(x[r, :k] . w[c, :k] + b[c]) for M = B <= a few dozen rows: a
+// weight-streaming GEMM (every weight read once).  One workgroup = one 16 x 16
+// output tile (16 rows of x, 16 weight rows) and kSkW waves.  K is walked in
+// chunks of 64 kSkW: the W and x tiles of a chunk are loaded cooperatively with
+// lanes on consecutive k (one wave-load = 256 contiguous bytes of one row, any
+// row stride or alignment -- res_cut's 2521-wide rows are not 16-B aligned) into
+// registers one chunk ahead, stored to LDS, and wave w multiplies k-range
+// [64 w, 64 w + 64) of the chunk with 16 v_mfma_f32_16x16x4_f32 (exact fp32
+// products; lane (r, g) holds k = 16 q + 4 g + t of float4 number q).  The
+// per-wave partial tiles meet in LDS in a fixed order (deterministic).
+constexpr int kSkW = 8;               // waves per workgroup
 
-// One wave per output column (4 per workgroup, so even N = 256 fills a few
-// hundred waves); the workgroup stages x[r0 : r0+MB, kc : kc+256] in LDS once
-// for its 4 columns, lanes stride K (k = kc + lane + 64 t) so every weight-row
-// load is a coalesced 256-B wave access for any row stride / alignment.  Each
-// weight is read exactly once; fixed summation order (deterministic).
-template <int MB>
-__global__ __launch_bounds__(256) void linear_skinny_kernel(const float *__restrict__ x,
-                                                            int64_t ldx, int64_t m, int64_t k,
-                                                            const float *__restrict__ w,
-                                                            int64_t ldw,
-                                                            const float *__restrict__ b,
-                                                            int64_t n, int act,
-                                                            float *__restrict__ y, int64_t ldy) {
-    __shared__ float xs[MB][kKc];
-    const int wave = threadIdx.x >> 6;
-    const int lane = threadIdx.x & 63;
-    const int64_t col = (int64_t)blockIdx.x * 4 + wave;
-    const bool colok = col < n;
-    const float *wr = w + (colok ? col : n - 1) * ldw;
-    for (int64_t r0 = 0; r0 < m; r0 += MB) {
-        float acc[MB];
+template <int kSkW>
+__global__ __launch_bounds__(kSkW * 64) void linear_skinny_kernel(const float *__restrict__ x,
+                                                                  int64_t ldx, int64_t m, int64_t k,
+                                                                  const float *__restrict__ w,
+                                                                  int64_t ldw,
+                                                                  const float *__restrict__ b,
+                                                                  int64_t n, int act,
+                                                                  float *__restrict__ y, int64_t ldy) {
+    constexpr int C = 64 * kSkW, LD = C + 4;
+    __shared__ float sw[16 * LD], sx[16 * LD];
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6;
+    const int lane = tid & 63;
+    const int r = lane & 15, g = lane >> 4;
+    const int64_t col0 = (int64_t)blockIdx.x * 16, row0 = (int64_t)blockIdx.y * 16;
+    const int K = (int)k;
+    const int nch = (K + C - 1) / C;
+    // loader role: rows i = 0..15 of both tiles at k = kc + tid
+    float lw[16], lx[16];
+    auto load = [&](int kc) {
+        const int kk = kc + tid;
+        const bool ok = kk < K;
+        const int o = ok ? kk : 0;
 #pragma unroll
-        for (int i = 0; i < MB; ++i) acc[i] = 0.0f;
-        for (int64_t kc = 0; kc < k; kc += kKc) {
-            float wv[4];
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const int64_t kg = kc + lane + 64 * t;
-                wv[t] = kg < k ? wr[kg] : 0.0f;
-            }
-            __syncthreads();  // previous chunk consumed
-            for (int e = threadIdx.x; e < MB * kKc; e += 256) {
-                const int i = e / kKc, kk = e % kKc;
-                const int64_t row = r0 + i, kg = kc + kk;
-                xs[i][kk] = (row < m && kg < k) ? x[row * ldx + kg] : 0.0f;
-            }
-            __syncthreads();
-#pragma unroll
-            for (int i = 0; i < MB; ++i) {
-#pragma unroll
-                for (int t = 0; t < 4; ++t) acc[i] = fmaf(xs[i][lane + 64 * t], wv[t], acc[i]);
-            }
+        for (int i = 0; i < 16; ++i) {
+            const float a = w[min(col0 + i, n - 1) * ldw + o];
+            const float c = x[min(row0 + i, m - 1) * ldx + o];
+            lw[i] = ok ? a : 0.0f;
+            lx[i] = ok ? c : 0.0f;
         }
+    };
+    f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+    load(0);
+    for (int c = 0; c < nch; ++c) {
+        if (c) __syncthreads();  // chunk c - 1 consumed
 #pragma unroll
-        for (int i = 0; i < MB; ++i) {
-            const float v = wave_sum(acc[i]);
-            const int64_t row = r0 + i;
-            if (lane == 0 && row < m && colok)
-                y[row * ldy + col] = act_apply(v + (b ? b[col] : 0.0f), act);
+        for (int i = 0; i < 16; ++i) {
+            sw[i * LD + tid] = lw[i];
+            sx[i * LD + tid] = lx[i];
         }
+        __syncthreads();
+        if (c + 1 < nch) load((c + 1) * C);
+        const float *aw = sw + r * LD + 64 * wave + 4 * g;
+        const float *ax = sx + r * LD + 64 * wave + 4 * g;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float4 wv = *(const float4 *)(aw + 16 * q);
+            const float4 xv = *(const float4 *)(ax + 16 * q);
+            acc = mfma16(xv.x, wv.x, acc);
+            acc = mfma16(xv.y, wv.y, acc);
+            acc = mfma16(xv.z, wv.z, acc);
+            acc = mfma16(xv.w, wv.w, acc);
+        }
+    }
+    __syncthreads();
+    f32x4 *part = (f32x4 *)sw;  // [wave][lane]
+    part[wave * 64 + lane] = acc;
+    __syncthreads();
+    if (wave != 0) return;
+    f32x4 s = part[lane];
+#pragma unroll
+    for (int v = 1; v < kSkW; ++v) s += part[v * 64 + lane];
+    const int64_t col = col0 + r;
+    if (col >= n) return;
+    const float bb = b ? b[col] : 0.0f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int64_t row = row0 + 4 * g + q;
+        if (row < m) y[row * ldy + col] = act_apply(s[q] + bb, act);
     }
 }
 
@@ -114,16 +142,9 @@ extern "C" int mmpde_linear_skinny(const float *x, int64_t ldx, int64_t m, int64
     MMPDE_REQUIRE(x && w && y && m > 0 && k > 0 && n > 0 && m <= 4096);
     MMPDE_REQUIRE(ldx >= k && ldw >= k && ldy >= n && act >= 0 && act <= 2);
     hipStream_t st = as_stream(stream);
-    dim3 grid(ceil_div(n, 4));
-#define MMPDE_SKINNY(MB) \
-    hipLaunchKernelGGL((linear_skinny_kernel<MB>), grid, dim3(256), 0, st, x, ldx, m, k, w, ldw, b, n, act, y, ldy)
-    if (m <= 1) MMPDE_SKINNY(1);
-    else if (m <= 2) MMPDE_SKINNY(2);
-    else if (m <= 4) MMPDE_SKINNY(4);
-    else if (m <= 8) MMPDE_SKINNY(8);
-    else if (m <= 16) MMPDE_SKINNY(16);
-    else MMPDE_SKINNY(32);
-#undef MMPDE_SKINNY
+    const dim3 grid((unsigned)ceil_div(n, 16), (unsigned)ceil_div(m, 16));
+    hipLaunchKernelGGL(linear_skinny_kernel<kSkW>, grid, dim3(kSkW * 64), 0, st, x, ldx, m, k, w, ldw, b,
+                       n, act, y, ldy);
     MMPDE_RET_LAUNCH();
     return MMPDE_OK;
 }
