@@ -75,13 +75,14 @@ class HipEvents:
 
 
 class EdgeTracer:
-    """Hands out one GnnExec (n_layers begin/end events) per GNN forward."""
+    """Hands out one GnnExec (n_layers edge-begin / edge-end / node-end events)
+    per GNN forward."""
 
     def __init__(self, n_forwards, n_layers=6):
         from mmpde_amd import _lib
 
         self.L = n_layers
-        self.pool = HipEvents(2 * n_forwards * n_layers)
+        self.pool = HipEvents(3 * n_forwards * n_layers)
         self.used = 0
         self.traces = []
         self._lib = _lib
@@ -92,20 +93,21 @@ class EdgeTracer:
             return None
         i = self.used
         self.used += 1
-        base = 2 * self.L * i
-        beg = (ctypes.c_void_p * self.L)(*self.pool.ev[base:base + self.L])
-        end = (ctypes.c_void_p * self.L)(*self.pool.ev[base + self.L:base + 2 * self.L])
-        t = self._lib.GnnExec(ctypes.cast(beg, ctypes.POINTER(ctypes.c_void_p)),
-                              ctypes.cast(end, ctypes.POINTER(ctypes.c_void_p)), 0, None)
-        self.traces.append((t, beg, end))
+        L = self.L
+        base = 3 * L * i
+        arr = [(ctypes.c_void_p * L)(*self.pool.ev[base + q * L:base + (q + 1) * L]) for q in range(3)]
+        cast = [ctypes.cast(a, ctypes.POINTER(ctypes.c_void_p)) for a in arr]
+        t = self._lib.GnnExec(cast[0], cast[1], 0, None, cast[2])
+        self.traces.append((t, arr))
         return t
 
     def launch_times_ms(self):
-        """[(layer index, ms)] for every traced fused-layer launch."""
+        """[(layer index, edge-stage ms, node-stage ms)] for every traced layer."""
         out = []
-        for _, beg, end in self.traces:
-            for l, (a, b) in enumerate(zip(beg, end)):
-                out.append((l, self.pool.elapsed_ms(a, b)))
+        for _, (beg, mid, end) in self.traces:
+            for l in range(self.L):
+                out.append((l, self.pool.elapsed_ms(beg[l], mid[l]),
+                            self.pool.elapsed_ms(mid[l], end[l])))
         return out
 
 
@@ -237,31 +239,21 @@ def main():
         return
     n_local = (hi - lo) * n_nodes
     k = gc.n
-    # Algorithmic FLOP of one fused-layer launch (factored form):
-    # per node k edges x (128x128 message_net_2) + update_net_1 (257->128) +
-    # update_net_2 (128->128) + the next layer's message_net_1 node halves
-    # (128->256) on every layer but the last.
-    edge_f = k * 2 * 128 * 128
-    upd_f = 2 * 257 * 128 + 2 * 128 * 128
-    proj_f = 2 * 128 * 256
-    n_layers = 6
-    tot_flop = sum(n_local * (edge_f + upd_f + (proj_f if l < n_layers - 1 else 0))
-                   for l, _ in launches)
-    tot_ms = sum(ms for _, ms in launches)
-    launch_ms = tot_ms / max(len(launches), 1)
-    achieved = tot_flop / max(tot_ms * 1e-3, 1e-12) / 1e12
-    # Peak of the kernel's arithmetic mix: the time its MFMA work needs at the
-    # dense peaks (f32 edge GEMM: 157.3 TF; f16x3 edge GEMM: three fp16
-    # products per fp32 product at 2516.6 TF; epilogue GEMMs on f32 MFMA).
-    if args.edge_gemm == "f32":
-        peak = F32_MFMA_PEAK_TFLOPS
-    else:
-        t_ideal = sum(n_local * (3 * edge_f / (F16_MFMA_PEAK_TFLOPS * 1e12)
-                                 + (upd_f + (proj_f if l < n_layers - 1 else 0))
-                                 / (F32_MFMA_PEAK_TFLOPS * 1e12)) for l, _ in launches)
-        peak = tot_flop / t_ideal / 1e12
+    # Dominant kernel = the edge stage (message_net_2 over every edge + mean),
+    # 12 launches per step.  Algorithmic FLOP per launch:
+    # n nodes x k edges x 2 x 128 x 128.
+    edge_f = n_local * k * 2 * 128 * 128
+    tot_ms = sum(e for _, e, _ in launches)
+    node_ms = sum(nd for _, _, nd in launches)
+    nl = max(len(launches), 1)
+    launch_ms = tot_ms / nl
+    achieved = edge_f * len(launches) / max(tot_ms * 1e-3, 1e-12) / 1e12
+    # Peak of the arithmetic the kernel runs: f32 -> dense fp32 MFMA peak;
+    # f16x3 -> each fp32 product is three fp16 MFMA products, so the
+    # fp32-equivalent peak is the dense fp16 MFMA peak / 3.
+    peak = F32_MFMA_PEAK_TFLOPS if args.edge_gemm == "f32" else F16_MFMA_PEAK_TFLOPS / 3
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", "fused_pmc_r01.json")
+    pmc = os.path.join(ROOT, "profiles", "edge_pmc_r01.json")
     if os.path.exists(pmc):
         with open(pmc) as f:
             rec = json.load(f)
@@ -287,13 +279,17 @@ def main():
                    "nodes_per_trajectory": n_nodes, "neighbors": gc.n, "time_window": 1,
                    "parallelism": f"trajectory-shard x{world} (no data-path collective)",
                    "rollout": "autoregressive (pred -> next input)"},
-        "roofline": {"kernel": "gnn_layer_fused_kernel (edge stage + update + next "
-                               "message_net_1, one launch per GNN layer, 12 per step)",
+        "roofline": {"kernel": "gnn_edge_kernel (message_net_2 over every edge + mean "
+                               "aggregation, one launch per GNN layer, 12 per step)",
                      "bound": "mfma", "achieved": achieved, "peak": peak,
                      "unit": "TFLOP/s", "frac": achieved / peak,
                      "traffic": traffic, "launch_ms": launch_ms, "launches": len(launches),
-                     "flop_per_launch": tot_flop / max(len(launches), 1),
-                     "edge_gemm": args.edge_gemm},
+                     "flop_per_launch": edge_f,
+                     "algorithmic_bytes_per_launch": n_local * (128 * 4 * 2 + k * 4 + 128 * 4),
+                     "edge_gemm": args.edge_gemm,
+                     "peak_basis": "dense fp32 MFMA" if args.edge_gemm == "f32" else
+                                   "dense fp16 MFMA / 3 (three fp16 products per fp32 product)"},
+        "node_stage_ms": node_ms / nl,
         "finite": finite,
     }
     if exact is not None:

@@ -177,17 +177,21 @@ int mmpde_gnn_forward(const float *u, const float *pos, int64_t n, int k, const 
  *         neighbour slot for the activations) and split into fp16 hi + lo
  *         (x = hi + lo to 2^-22 relative); the product uses hi*hi + hi*lo +
  *         lo*hi on v_mfma_f32_16x16x32_f16 with fp32 accumulation.  Applies
- *         to every GEMM of the fused layer (edge message_net_2 and the node
- *         GEMMs update_net_1/2, message_net_1).  Error vs fp64 is measured
+ *         to every GEMM of a layer (edge message_net_2 and the node
+ *         GEMMs update_net_1/2, message_net_1; activations scaled per
+ *         neighbour slot tile / per node row).  Error vs fp64 is measured
  *         beside F32 in tests/test_gpu_precision.py. */
 #define MMPDE_EDGE_GEMM_F32 0
 #define MMPDE_EDGE_GEMM_F16X3 1
 
-/* Execution options of mmpde_gnn_forward_ex (NULL = F32, no events). When
- * edge_begin / edge_end are non-NULL, hipEventRecord(edge_begin[l]) /
- * (edge_end[l]) are issued on `stream` immediately before / after layer l's
- * fused layer kernel (edge stage + update + next layer's projections: the
- * dominant kernel), so a caller can time exactly that launch. */
+/* Execution options of mmpde_gnn_forward_ex (NULL = F32, no events).  Each
+ * layer is two launches: the edge stage (message_net_2 over every edge + mean
+ * aggregation: the dominant kernel) and the node stage (update_net_1/2,
+ * residual, BatchNorm and the next layer's message_net_1 node halves).  When
+ * non-NULL, hipEventRecord(edge_begin[l]) / (edge_end[l]) / (node_end[l]) are
+ * issued on `stream` immediately before layer l's edge stage, between the two
+ * launches and after its node stage, so a caller can time exactly those
+ * launches. */
 typedef struct {
     void *const *edge_begin; /* n_layers hipEvent_t, or NULL */
     void *const *edge_end;   /* n_layers hipEvent_t, or NULL */
@@ -195,6 +199,7 @@ typedef struct {
     const void *packed;      /* F16X3: weight images from mmpde_gnn_pack_f16x3 for these
                                 layers (caller-cached); NULL: packed per call into the
                                 workspace */
+    void *const *node_end;   /* n_layers hipEvent_t, or NULL */
 } mmpde_gnn_exec;
 
 /* Most layers mmpde_gnn_forward_ex accepts (sizes the workspace's packed

@@ -47,6 +47,11 @@ __device__ __forceinline__ int xcd_tile(int bid, int nb) {
     return x < rem ? x * (q + 1) + i : rem * (q + 1) + (x - rem) * q + i;
 }
 
+// component t (compile-time after unrolling) of a float4
+__device__ __forceinline__ float f4c(const float4 &v, int t) {
+    return t == 0 ? v.x : t == 1 ? v.y : t == 2 ? v.z : v.w;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -15,7 +15,9 @@
 #include <vector>
 
 #include "common.hpp"
+#include "f16x3.hpp"
 #include "gemm.hpp"
+#include "layer.hpp"
 
 namespace {
 
@@ -237,678 +239,6 @@ __global__ __launch_bounds__(256, 2) void edge_mean_kernel(const float *__restri
 }
 
 // ---------------------------------------------------------------------------
-// Fused message-passing layer (the rollout's hot kernel): one launch per layer
-//   mean_i = (1/k) sum_e relu(W2 relu(a_i + b_nbr(i,e)) + b2)           edge stage
-//   v_i    = relu(U1 [h_i | mean_i | t_i] + c1)                         update_net_1
-//   h'_i   = BN(h_i + relu(U2 v_i + c2))                                update_net_2, BN
-//   a'_i, b'_i = next layer's message_net_1 halves of h'_i (NEXT only)  (see EpiProj)
-// (gnn_2d.py:53-69 twice over: this layer's update and the next layer's
-// message_net_1, so a layer costs one launch and h, a, b cross HBM once.)
-//
-// Workgroup = 16 target rows x 4 waves, v_mfma_f32_16x16x4_f32 throughout.
-// K index map for every 128-wide operand: lane l (row l&15, group g = l>>4)
-// holds k = 16 j + 4 g + t in component t of its float4 number j (j < 8), so a
-// row is read as 64-B contiguous pieces and MFMA step (j, t) consumes one float
-// per lane.  Edge stage: wave w takes neighbour slots e = w, w+4, ...; W2 sits
-// in LDS as the exact per-lane B image (64 KB, staged once per workgroup);
-// a_i stays in registers; b rows of the next slot are prefetched while the
-// current slot's 16x128x128 product runs.  Slot e of all 16 targets shares one
-// accumulator row, so per-target sums need no cross-lane traffic; the four
-// waves' partial sums meet in LDS (the then free W2 region), which also carries
-// the transposes between the epilogue GEMMs.  Deterministic: no atomics.
-// ---------------------------------------------------------------------------
-constexpr int FT = 16;    // target rows per workgroup
-constexpr int FRP = 132;  // padded LDS row (floats): conflict-free C-layout writes
-
-struct FusedLayerArgs {
-    const float *a, *b, *h;  // [n,128]: this layer's message_net_1 halves, layer input
-    const int32_t *nbr;      // [n,k] global source rows
-    int64_t n;
-    int k;
-    const float *w2, *b2;             // message_net_2.0 [128,128], [128]
-    const char *pk;                   // F16X3: this layer's packed images (kLayerPack bytes)
-    const char *pkn;                  // F16X3: next layer's packed images (NEXT)
-    const float *u1, *c1;             // update_net_1.0 [128, ld_u1] (h | mean | t), [128]
-    int64_t ld_u1;
-    const float *u2, *c2;             // update_net_2.0 [128,128], [128]
-    const float *bn_w, *bn_b, *bn_rm, *bn_rv;
-    float eps;
-    float *h_out;
-    const float *w1n, *b1n;           // next layer message_net_1.0 [128, ld_w1n], [128]
-    int64_t ld_w1n;
-    float *a_out, *b_out;
-    const float *u, *pos;             // node input u [n], pos [n,3] = (t, x, y)
-    mmpde_gnn_scales sc;
-    const uint32_t *amax_in;          // F16X3: range slot of a, b (this layer)
-    uint32_t *amax_out;               // F16X3 + NEXT: range slot of a', b'
-};
-
-__device__ __forceinline__ float4 relu4_add(float4 x, float4 y) {
-    return make_float4(fmaxf(x.x + y.x, 0.0f), fmaxf(x.y + y.y, 0.0f), fmaxf(x.z + y.z, 0.0f),
-                       fmaxf(x.w + y.w, 0.0f));
-}
-
-__device__ __forceinline__ float f4c(const float4 &v, int t) {
-    return t == 0 ? v.x : t == 1 ? v.y : t == 2 ? v.z : v.w;
-}
-
-typedef _Float16 half8 __attribute__((ext_vector_type(8)));
-
-// Power of two s with mx * s in [2^13, 2^14) (fp16 max 65504): the scale of
-// the F16X3 split.  mx zero / subnormal / inf / nan -> 1; clamped to
-// [2^-40, 2^40] so a scaled bias can never overflow fp32.
-__device__ __forceinline__ float split_scale(float mx) {
-    const int eb = (int)((__float_as_uint(mx) >> 23) & 0xff);
-    if (eb == 0 || eb == 255) return 1.0f;
-    const int se = min(max(267 - eb, 127 - 40), 127 + 40);
-    return __uint_as_float((uint32_t)se << 23);
-}
-
-// 1 / s for a power of two s from split_scale (exact).
-__device__ __forceinline__ float pow2_inv(float s) {
-    const uint32_t eb = (__float_as_uint(s) >> 23) & 0xff;
-    return __uint_as_float((254u - eb) << 23);
-}
-
-// ---------------------------------------------------------------------------
-// F16X3 weight images (once per parameter change, mmpde_gnn_pack_f16x3).  A
-// B-operand matrix B[k][j] = W[row(j)][koff(j) + k] (K = 128 or 256) is packed
-// column by column: column j is scaled by sw[j] = split_scale(max_k |B[k][j]|)
-// and split into fp16 hi + lo, laid out as the exact per-lane B operand of
-// v_mfma_f32_16x16x32_f16: [ctile j/16][kstep K/32][hi|lo][lane][8 halves],
-// lane = 16 g + (j & 15) holding k = 32 s + 8 g + t; followed by sw[n_cols].
-// Per layer: message_net_2 (edge), update_net_1 (h | mean part), update_net_2
-// and message_net_1 as the two node halves (j < 128: W1[j, 0:128] -> a;
-// j >= 128: W1[j-128, 128:256] -> b).
-// ---------------------------------------------------------------------------
-constexpr int64_t kPkW2 = 0;                              // 128 x 128
-constexpr int64_t kPkU1 = kPkW2 + 65536 + 512;            // 128 x 256
-constexpr int64_t kPkU2 = kPkU1 + 131072 + 512;           // 128 x 128
-constexpr int64_t kPkW1 = kPkU2 + 65536 + 512;            // 256 x 128
-constexpr int64_t kLayerPack = kPkW1 + 131072 + 1024;     // bytes per layer (16-B multiple)
-static_assert(kLayerPack % 16 == 0, "pack alignment");
-// per layer: |a| and |b| range slots of kAmaxShards uint32 each
-constexpr int64_t kAmaxBytes = (int64_t)MMPDE_GNN_MAX_LAYERS * 2 * kAmaxShards * 4;
-
-struct PackSrc {
-    const float *w[MMPDE_GNN_MAX_LAYERS];
-    int64_t ld[MMPDE_GNN_MAX_LAYERS];
-};
-
-template <int K>
-__global__ __launch_bounds__(K) void pack_f16x3_kernel(PackSrc src, int half_split, int64_t img_off,
-                                                       int64_t n_cols, char *__restrict__ pack) {
-    __shared__ float red[K / 64];
-    const int layer = blockIdx.y, jcol = blockIdx.x, k = threadIdx.x;
-    const int row = half_split ? (jcol & 127) : jcol;
-    const int koff = half_split ? (jcol >> 7) * 128 : 0;
-    const float w = src.w[layer][(int64_t)row * src.ld[layer] + koff + k];
-    const float m = wave_max(fabsf(w));
-    if ((k & 63) == 0) red[k >> 6] = m;
-    __syncthreads();
-    float mx = red[0];
-#pragma unroll
-    for (int i = 1; i < K / 64; ++i) mx = fmaxf(mx, red[i]);
-    const float sw = split_scale(mx);
-    const float x = w * sw;
-    const _Float16 hi = (_Float16)x;
-    const _Float16 lo = (_Float16)(x - (float)hi);
-    const int c = jcol >> 4, s = k >> 5, g = (k >> 3) & 3, t = k & 7;
-    const int lane = 16 * g + (jcol & 15);
-    char *base = pack + (int64_t)layer * kLayerPack + img_off;
-    _Float16 *img = (_Float16 *)base;
-    img[(((c * (K / 32) + s) * 2 + 0) * 64 + lane) * 8 + t] = hi;
-    img[(((c * (K / 32) + s) * 2 + 1) * 64 + lane) * 8 + t] = lo;
-    if (k == 0) ((float *)(base + n_cols * K * 4))[jcol] = sw;
-}
-
-// B fragment (c, s, hi|lo) of a packed image with KS k-steps, as a half8.
-__device__ __forceinline__ half8 bfrag(const char *img, int KS, int c, int s, int hl, int lane) {
-    const float4 v = ((const float4 *)img)[((c * KS + s) * 2 + hl) * 64 + lane];
-    return *(const half8 *)&v;
-}
-
-// Scaled fp16 hi/lo split of 8 consecutive-k values.
-__device__ __forceinline__ void split8(const float4 &x0, const float4 &x1, float sc, half8 &hi,
-                                       half8 &lo) {
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-        const float x = f4c(t < 4 ? x0 : x1, t & 3) * sc;
-        const _Float16 h = (_Float16)x;
-        hi[t] = h;
-        lo[t] = (_Float16)(x - (float)h);
-    }
-}
-
-// The same split as split8 with sc = 1 in 12 instructions: hi by v_cvt_pk_f16_f32
-// (RN), lo = RN_f16(x - f32(hi)) by v_fma_mix (x - hi is exact in f32, so
-// the result is bit-identical to split8; tools/ubench/split_check.hip).  The
-// trailing s_nop covers the VALU-write -> MFMA-operand hazard, which hipcc does
-// not pad for asm producers (cdna_hip_programming.md §5.7).
-__device__ __forceinline__ void split8_rn(const float4 &a, const float4 &b, half8 &hi, half8 &lo) {
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    u32x4 h, l;
-    asm("v_cvt_pk_f16_f32 %0, %8, %9\n\t"
-        "v_cvt_pk_f16_f32 %1, %10, %11\n\t"
-        "v_cvt_pk_f16_f32 %2, %12, %13\n\t"
-        "v_cvt_pk_f16_f32 %3, %14, %15\n\t"
-        "v_fma_mixlo_f16 %4, %8, 1.0, -%0 op_sel_hi:[0,0,1]\n\t"
-        "v_fma_mixhi_f16 %4, %9, 1.0, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
-        "v_fma_mixlo_f16 %5, %10, 1.0, -%1 op_sel_hi:[0,0,1]\n\t"
-        "v_fma_mixhi_f16 %5, %11, 1.0, -%1 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
-        "v_fma_mixlo_f16 %6, %12, 1.0, -%2 op_sel_hi:[0,0,1]\n\t"
-        "v_fma_mixhi_f16 %6, %13, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
-        "v_fma_mixlo_f16 %7, %14, 1.0, -%3 op_sel_hi:[0,0,1]\n\t"
-        "v_fma_mixhi_f16 %7, %15, 1.0, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
-        "s_nop 1"
-        : "=&v"(h.x), "=&v"(h.y), "=&v"(h.z), "=&v"(h.w), "=&v"(l.x), "=&v"(l.y), "=&v"(l.z),
-          "=&v"(l.w)
-        : "v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w));
-    hi = *(const half8 *)&h;
-    lo = *(const half8 *)&l;
-}
-
-__device__ __forceinline__ float absmax4(float m, const float4 &v) {
-    return fmaxf(fmaxf(fmaxf(m, fabsf(v.x)), fmaxf(fabsf(v.y), fabsf(v.z))), fabsf(v.w));
-}
-
-__device__ __forceinline__ f32x4 mfma_f16(const half8 &a, const half8 &b, f32x4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
-}
-
-// ---- epilogue pieces shared by both arithmetic modes -------------------------
-// C layout of a 16x16 tile: lane (r = l & 15, g = l >> 4) holds column r of
-// rows 4 g + q.  Wave w owns output columns 32 w .. 32 w + 31 (two tiles).
-
-// v = relu(accH * sH + accM * sM + U1[:, 256] t + c1) -> vbuf (sH, sM: per-lane
-// unscale of the h / mean parts; 1 for the fp32 path, whose accH holds both).
-__device__ __forceinline__ void upd1_store(const FusedLayerArgs &p, const f32x4 &acc0,
-                                           const f32x4 &acc1, float s0, float s1, float *vbuf,
-                                           int64_t tile0, int wave, int lane) {
-    const int r = lane & 15, g = lane >> 4;
-#pragma unroll
-    for (int cc = 0; cc < 2; ++cc) {
-        const f32x4 &acc = cc ? acc1 : acc0;
-        const float sc = cc ? s1 : s0;
-        const int col = 32 * wave + 16 * cc + r;
-        const float wt = p.u1[(int64_t)col * p.ld_u1 + 256], bb = p.c1[col];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int64_t row = min(tile0 + 4 * g + q, p.n - 1);
-            const float pt = p.pos[row * 3 + 0] * p.sc.inv_tmax;
-            vbuf[(4 * g + q) * FRP + col] = fmaxf(acc[q] * sc + wt * pt + bb, 0.0f);
-        }
-    }
-}
-
-// h' = BN(h + relu(acc * inv + c2)); inv nullptr = 1 (fp32 path).
-template <bool NEXT>
-__device__ __forceinline__ void upd2_store(const FusedLayerArgs &p, const f32x4 *acc,
-                                           const float *inv, float *hbuf, int64_t tile0, int wave,
-                                           int lane) {
-    const int r = lane & 15, g = lane >> 4;
-#pragma unroll
-    for (int cc = 0; cc < 2; ++cc) {
-        const int col = 32 * wave + 16 * cc + r;
-        const float bb = p.c2[col], rm = p.bn_rm[col], rv = p.bn_rv[col];
-        const float gw = p.bn_w[col], gb = p.bn_b[col];
-        const float iv = inv ? inv[cc] : 1.0f;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int64_t row = tile0 + 4 * g + q;
-            const int64_t rowc = min(row, p.n - 1);
-            const float x = p.h[rowc * H + col] + fmaxf(acc[cc][q] * iv + bb, 0.0f);
-            const float y = bn_eval(x, rm, rv, gw, gb, p.eps);
-            if (row < p.n) p.h_out[row * H + col] = y;
-            if (NEXT) hbuf[(4 * g + q) * FRP + col] = y;
-        }
-    }
-}
-
-// a' = acc[cc] * inv + node terms + t term + b1, b' = acc[2+cc] * inv - node terms.
-__device__ __forceinline__ void proj_store(const FusedLayerArgs &p, const f32x4 *acc,
-                                           const float *inv, int64_t tile0, int wave, int lane) {
-    const int r = lane & 15, g = lane >> 4;
-    float amx = 0.0f, bmx = 0.0f;
-#pragma unroll
-    for (int cc = 0; cc < 2; ++cc) {
-        const int col = 32 * wave + 16 * cc + r;
-        const float *wc = p.w1n + (int64_t)col * p.ld_w1n;
-        const float wdu = wc[256], wdx = wc[257], wdy = wc[258], wt = wc[259];
-        const float bb = p.b1n[col];
-        const float ia = inv ? inv[cc] : 1.0f, ib = inv ? inv[2 + cc] : 1.0f;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int64_t row = tile0 + 4 * g + q;
-            if (row < p.n) {
-                const float uu = p.u[row];
-                const float px = p.pos[row * 3 + 1] * p.sc.inv_lx;
-                const float py = p.pos[row * 3 + 2] * p.sc.inv_ly;
-                const float pt = p.pos[row * 3 + 0] * p.sc.inv_tmax;
-                const float node = wdu * uu + wdx * px + wdy * py;
-                const float va = acc[cc][q] * ia + node + wt * pt + bb;
-                const float vb = acc[2 + cc][q] * ib - node;
-                p.a_out[row * H + col] = va;
-                p.b_out[row * H + col] = vb;
-                amx = fmaxf(amx, fabsf(va));
-                bmx = fmaxf(bmx, fabsf(vb));
-            }
-        }
-    }
-    if (p.amax_out) {
-        amax_publish(amx, p.amax_out);
-        amax_publish(bmx, p.amax_out + kAmaxShards);
-    }
-}
-
-// F16X3 epilogue: the three node GEMMs on split fp16 MFMA.  Every wave holds
-// the whole 16-row A tile, so the activation scales (wave_max) are uniform
-// across the workgroup; the h and mean parts of update_net_1 get their own
-// scales and accumulators.  k map: float4 number 2 s + u holds k = 32 s + 8 g
-// + 4 u + t (the 16x16x32 A fragment).
-template <bool NEXT>
-__device__ __forceinline__ void epilogue_f16x3(const FusedLayerArgs &p, const float *red,
-                                               float *vbuf, float *hbuf, int64_t tile0,
-                                               int64_t tgt, int wave, int lane) {
-    const int r = lane & 15, g = lane >> 4;
-    auto kp = [&](int i) { return 32 * (i >> 1) + 8 * g + 4 * (i & 1); };
-    // ---- update_net_1
-    {
-        float4 hA[8], mA[8];
-        float mh = 0.0f, mm = 0.0f;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            hA[i] = *(const float4 *)(p.h + tgt * H + kp(i));
-            mA[i] = *(const float4 *)(red + r * FRP + kp(i));
-            mh = absmax4(mh, hA[i]);
-            mm = absmax4(mm, mA[i]);
-        }
-        const float sh = split_scale(wave_max(mh)), sm = split_scale(wave_max(mm));
-        const char *img = p.pk + kPkU1;
-        const float *su = (const float *)(img + 131072);
-        f32x4 aH[2], aM[2];
-#pragma unroll
-        for (int cc = 0; cc < 2; ++cc) aH[cc] = aM[cc] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) {
-            half8 hh, hl, mh8, ml8;
-            split8(hA[2 * s4], hA[2 * s4 + 1], sh, hh, hl);
-            split8(mA[2 * s4], mA[2 * s4 + 1], sm, mh8, ml8);
-            half8 bh[2], bl[2], ch[2], cl[2];
-#pragma unroll
-            for (int cc = 0; cc < 2; ++cc) {
-                bh[cc] = bfrag(img, 8, 2 * wave + cc, s4, 0, lane);
-                bl[cc] = bfrag(img, 8, 2 * wave + cc, s4, 1, lane);
-                ch[cc] = bfrag(img, 8, 2 * wave + cc, 4 + s4, 0, lane);
-                cl[cc] = bfrag(img, 8, 2 * wave + cc, 4 + s4, 1, lane);
-            }
-#pragma unroll
-            for (int cc = 0; cc < 2; ++cc) aH[cc] = mfma_f16(hh, bh[cc], aH[cc]);
-#pragma unroll
-            for (int cc = 0; cc < 2; ++cc) aM[cc] = mfma_f16(mh8, ch[cc], aM[cc]);
-#pragma unroll
-            for (int cc = 0; cc < 2; ++cc) aH[cc] = mfma_f16(hh, bl[cc], aH[cc]);
-#pragma unroll
-            for (int cc = 0; cc < 2; ++cc) aM[cc] = mfma_f16(mh8, cl[cc], aM[cc]);
-#pragma unroll
-            for (int cc = 0; cc < 2; ++cc) aH[cc] = mfma_f16(hl, bh[cc], aH[cc]);
-#pragma unroll
-            for (int cc = 0; cc < 2; ++cc) aM[cc] = mfma_f16(ml8, ch[cc], aM[cc]);
-        }
-        f32x4 acc[2];
-        float one[2];
-#pragma unroll
-        for (int cc = 0; cc < 2; ++cc) {
-            const float swc = su[32 * wave + 16 * cc + r];
-            const float ih = 1.0f / (sh * swc), im = 1.0f / (sm * swc);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) acc[cc][q] = aH[cc][q] * ih + aM[cc][q] * im;
-            one[cc] = 1.0f;
-        }
-        upd1_store(p, acc[0], acc[1], one[0], one[1], vbuf, tile0, wave, lane);
-    }
-    __syncthreads();
-    // ---- update_net_2 + residual + BatchNorm
-    {
-        float4 vA[8];
-        float mv = 0.0f;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            vA[i] = *(const float4 *)(vbuf + r * FRP + kp(i));
-            mv = absmax4(mv, vA[i]);
-        }
-        const float sv = split_scale(wave_max(mv));
-        const char *img = p.pk + kPkU2;
-        const float *su = (const float *)(img + 65536);
-        f32x4 acc[2];
-#pragma unroll
-        for (int cc = 0; cc < 2; ++cc) acc[cc] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) {
-            half8 vh, vl;
-            split8(vA[2 * s4], vA[2 * s4 + 1], sv, vh, vl);
-            half8 bh[2], bl[2];
-#pragma unroll
-            for (int cc = 0; cc < 2; ++cc) {
-                bh[cc] = bfrag(img, 4, 2 * wave + cc, s4, 0, lane);
-                bl[cc] = bfrag(img, 4, 2 * wave + cc, s4, 1, lane);
-            }
-#pragma unroll
-            for (int cc = 0; cc < 2; ++cc) acc[cc] = mfma_f16(vh, bh[cc], acc[cc]);
-#pragma unroll
-            for (int cc = 0; cc < 2; ++cc) acc[cc] = mfma_f16(vh, bl[cc], acc[cc]);
-#pragma unroll
-            for (int cc = 0; cc < 2; ++cc) acc[cc] = mfma_f16(vl, bh[cc], acc[cc]);
-        }
-        float inv[2];
-#pragma unroll
-        for (int cc = 0; cc < 2; ++cc) inv[cc] = 1.0f / (sv * su[32 * wave + 16 * cc + r]);
-        upd2_store<NEXT>(p, acc, inv, hbuf, tile0, wave, lane);
-    }
-    if (!NEXT) return;
-    __syncthreads();
-    // ---- next layer's message_net_1 node halves
-    {
-        float4 hA[8];
-        float mh = 0.0f;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            hA[i] = *(const float4 *)(hbuf + r * FRP + kp(i));
-            mh = absmax4(mh, hA[i]);
-        }
-        const float sh = split_scale(wave_max(mh));
-        const char *img = p.pkn + kPkW1;
-        const float *su = (const float *)(img + 131072);
-        f32x4 acc[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) acc[c] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
-        // image column tiles: a' cols 32 w + 16 cc -> tile 2 w + cc; b' -> 8 + 2 w + cc
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) {
-            half8 xh, xl;
-            split8(hA[2 * s4], hA[2 * s4 + 1], sh, xh, xl);
-            half8 bh[4], bl[4];
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const int ct = 8 * (c >> 1) + 2 * wave + (c & 1);
-                bh[c] = bfrag(img, 4, ct, s4, 0, lane);
-                bl[c] = bfrag(img, 4, ct, s4, 1, lane);
-            }
-#pragma unroll
-            for (int c = 0; c < 4; ++c) acc[c] = mfma_f16(xh, bh[c], acc[c]);
-#pragma unroll
-            for (int c = 0; c < 4; ++c) acc[c] = mfma_f16(xh, bl[c], acc[c]);
-#pragma unroll
-            for (int c = 0; c < 4; ++c) acc[c] = mfma_f16(xl, bh[c], acc[c]);
-        }
-        float inv[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-            inv[c] = 1.0f / (sh * su[128 * (c >> 1) + 32 * wave + 16 * (c & 1) + r]);
-        proj_store(p, acc, inv, tile0, wave, lane);
-    }
-}
-
-// PHASES (profiling builds only, tools/ubench): bit 0 runs the edge loop,
-// bit 1 the epilogue, bit 2 skips the producer work of the edge loop, bit 3
-// its MFMAs; production launches use 3.
-template <bool NEXT, bool F16X3, int PHASES = 3>
-__global__ __launch_bounds__(256, 2) void gnn_layer_fused_kernel(FusedLayerArgs p) {
-    // LDS: [2 rounds][4 producer slots] A-operand images of 8 KB (the message
-    // inputs of one neighbour slot for the 16 targets, in per-lane fragment
-    // order) | the tile's a rows.  After the edge loop the slot region holds
-    // the epilogue scratch (mean, v, h').
-    __shared__ float4 lds4[2 * 4 * 512 + FT * FRP / 4];
-    float *lds = (float *)lds4;
-    float *lds_a = lds + 2 * 4 * 512 * 4;  // [16][FRP]
-    const int wave = threadIdx.x >> 6;
-    const int lane = threadIdx.x & 63;
-    const int r = lane & 15, g = lane >> 4;
-    const int tile = xcd_tile(blockIdx.x, gridDim.x);
-    const int64_t tile0 = (int64_t)tile * FT;
-    const int64_t tgt = min(tile0 + r, p.n - 1);
-
-    // F16X3: one power-of-two scale per launch for the message inputs
-    // m = relu(a_i + b_j) <= max|a| + max|b| (range slots published by the
-    // producer of a, b), so m * sc < 2^14 fits fp16 and the split keeps 22 bits.
-    float sc = 1.0f;
-    if (F16X3) sc = split_scale(amax_read(p.amax_in) + amax_read(p.amax_in + kAmaxShards));
-    for (int e = threadIdx.x; e < FT * 32; e += 256) {
-        const int row = e >> 5, c4 = e & 31;
-        const int64_t src = min(tile0 + row, p.n - 1);
-        float4 v = *(const float4 *)(p.a + src * H + 4 * c4);
-        if (F16X3) v = make_float4(v.x * sc, v.y * sc, v.z * sc, v.w * sc);
-        *(float4 *)(lds_a + row * FRP + 4 * c4) = v;
-    }
-
-    // This wave's output columns 32 w .. 32 w + 31 (tiles cc = 0, 1): its
-    // message_net_2 B fragments stay in registers for the whole launch.
-    // F32: float4 wf[cc][j] = W2[col][16 j + 4 g + t];
-    // F16X3: wh/wl[cc][s4] = packed hi / lo half8 (k = 32 s4 + 8 g + t).
-    float4 wf[2][8];
-    half8 wh[2][4], wl[2][4];
-    float bias[2], bsc[2], inv[2];
-#pragma unroll
-    for (int cc = 0; cc < 2; ++cc) {
-        const int col = 32 * wave + 16 * cc + r;
-        bias[cc] = p.b2[col];
-        if (F16X3) {
-            const char *img = p.pk + kPkW2;
-#pragma unroll
-            for (int s4 = 0; s4 < 4; ++s4) {
-                wh[cc][s4] = bfrag(img, 4, 2 * wave + cc, s4, 0, lane);
-                wl[cc][s4] = bfrag(img, 4, 2 * wave + cc, s4, 1, lane);
-            }
-            const float sw = ((const float *)(img + 65536))[col];
-            bsc[cc] = bias[cc] * sw * sc;
-            inv[cc] = pow2_inv(sw) * pow2_inv(sc);
-        } else {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) wf[cc][j] = *(const float4 *)(p.w2 + col * H + 16 * j + 4 * g);
-        }
-    }
-    f32x4 S[2] = {(f32x4){0.0f, 0.0f, 0.0f, 0.0f}, (f32x4){0.0f, 0.0f, 0.0f, 0.0f}};
-
-    // Producer role: wave w builds the A operand of neighbour slot 4 r + w in
-    // round r.  The loop is software-pipelined by one round: iteration r
-    // produces round r + 1 into the other LDS buffer while it multiplies
-    // round r, so the producer's gather/VALU work and the consumer's MFMAs of
-    // the same wave interleave.  Branch-free: slot indices past k are clamped
-    // (their products are discarded by a select).  b rows are loaded one round
-    // ahead of their production, indices two.  (clamped: a malformed caller
-    // table must not fault the GPU)
-    // k map of the b / a pieces: F32 float4 i holds k = 16 i + 4 g + t;
-    // F16X3 float4 i holds k = 32 (i >> 1) + 8 g + 4 (i & 1) + t.
-    const int32_t *nrow = p.nbr + tgt * p.k;
-    const uint32_t nmax = (uint32_t)(p.n - 1);
-    const int kmax = p.k - 1;
-    auto piece = [&](int i) { return F16X3 ? 32 * (i >> 1) + 8 * g + 4 * (i & 1) : 16 * i + 4 * g; };
-    float4 bv[8];
-    {
-        const int64_t src = min((uint32_t)nrow[min(wave, kmax)], nmax);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) bv[i] = *(const float4 *)(p.b + src * H + piece(i));
-    }
-    uint32_t src_next = (uint32_t)nrow[min(wave + 4, kmax)];
-    __syncthreads();  // a tile staged
-    const float *arow = lds_a + r * FRP;
-
-    auto produce = [&](int rd) {  // slot 4 rd + wave -> buffer rd & 1
-        const int e = 4 * rd + wave;
-        float4 m[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const float4 av = *(const float4 *)(arow + piece(i));
-            if (F16X3)
-                m[i] = make_float4(fmaxf(fmaf(bv[i].x, sc, av.x), 0.0f), fmaxf(fmaf(bv[i].y, sc, av.y), 0.0f),
-                                   fmaxf(fmaf(bv[i].z, sc, av.z), 0.0f), fmaxf(fmaf(bv[i].w, sc, av.w), 0.0f));
-            else
-                m[i] = relu4_add(av, bv[i]);
-        }
-        {
-            const int64_t src = min(src_next, nmax);
-#pragma unroll
-            for (int i = 0; i < 8; ++i) bv[i] = *(const float4 *)(p.b + src * H + piece(i));
-            src_next = (uint32_t)nrow[min(e + 8, kmax)];
-        }
-        float4 *dst = lds4 + (rd & 1) * 4 * 512 + wave * 512 + lane;
-        if (F16X3) {
-#pragma unroll
-            for (int s4 = 0; s4 < 4; ++s4) {
-                half8 hi, lo;
-                split8_rn(m[2 * s4], m[2 * s4 + 1], hi, lo);
-                dst[(2 * s4 + 0) * 64] = *(const float4 *)&hi;
-                dst[(2 * s4 + 1) * 64] = *(const float4 *)&lo;
-            }
-        } else {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) dst[i * 64] = m[i];
-        }
-    };
-    auto consume = [&](int rd) {  // all 4 slots of buffer rd & 1
-        const float4 *slot = lds4 + (rd & 1) * 4 * 512 + lane;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const float4 *src = slot + q * 512;
-            const bool valid = 4 * rd + q < p.k;
-            f32x4 acc[2] = {(f32x4){0.0f, 0.0f, 0.0f, 0.0f}, (f32x4){0.0f, 0.0f, 0.0f, 0.0f}};
-            if (F16X3) {
-#pragma unroll
-                for (int s4 = 0; s4 < 4; ++s4) {
-                    const float4 h4 = src[(2 * s4 + 0) * 64], l4 = src[(2 * s4 + 1) * 64];
-                    const half8 hi = *(const half8 *)&h4, lo = *(const half8 *)&l4;
-#pragma unroll
-                    for (int cc = 0; cc < 2; ++cc) acc[cc] = mfma_f16(hi, wh[cc][s4], acc[cc]);
-#pragma unroll
-                    for (int cc = 0; cc < 2; ++cc) acc[cc] = mfma_f16(hi, wl[cc][s4], acc[cc]);
-#pragma unroll
-                    for (int cc = 0; cc < 2; ++cc) acc[cc] = mfma_f16(lo, wh[cc][s4], acc[cc]);
-                }
-#pragma unroll
-                for (int cc = 0; cc < 2; ++cc) {
-#pragma unroll
-                    for (int t = 0; t < 4; ++t) {
-                        const float v = fmaf(fmaxf(acc[cc][t] + bsc[cc], 0.0f), inv[cc], S[cc][t]);
-                        S[cc][t] = valid ? v : S[cc][t];
-                    }
-                }
-            } else {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const float4 mv = src[j * 64];
-#pragma unroll
-                    for (int t = 0; t < 4; ++t) {
-#pragma unroll
-                        for (int cc = 0; cc < 2; ++cc) acc[cc] = mfma16(f4c(mv, t), f4c(wf[cc][j], t), acc[cc]);
-                    }
-                }
-#pragma unroll
-                for (int cc = 0; cc < 2; ++cc) {
-#pragma unroll
-                    for (int t = 0; t < 4; ++t) {
-                        const float v = S[cc][t] + fmaxf(acc[cc][t] + bias[cc], 0.0f);
-                        S[cc][t] = valid ? v : S[cc][t];
-                    }
-                }
-            }
-        }
-    };
-
-    const int rounds = (PHASES & 1) ? (p.k + 3) / 4 : 0;
-    if (rounds > 0) {
-        if (!(PHASES & 4)) produce(0);
-        __syncthreads();
-        for (int rd = 0; rd + 1 < rounds; ++rd) {  // one basic block: produce || consume
-            if (!(PHASES & 4)) produce(rd + 1);
-            if (!(PHASES & 8)) consume(rd);
-            __syncthreads();  // round rd consumed, round rd + 1 produced
-        }
-        if (!(PHASES & 8)) consume(rounds - 1);
-    }
-
-    // ---- mean of the messages -> red[row][col] (C layout: rows 4 g + t) -----
-    __syncthreads();  // every wave is done with the slots
-    float *red = lds;                      // 16 x FRP: mean
-    float *vbuf = lds + FT * FRP;          // 16 x FRP
-    float *hbuf = vbuf + FT * FRP;         // 16 x FRP
-    const float kdiv = (float)p.k;
-#pragma unroll
-    for (int cc = 0; cc < 2; ++cc) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) red[(4 * g + t) * FRP + 32 * wave + 16 * cc + r] = S[cc][t] / kdiv;
-    }
-    __syncthreads();
-
-    if constexpr (!(PHASES & 2)) {
-        return;
-    } else if constexpr (F16X3) {
-        epilogue_f16x3<NEXT>(p, red, vbuf, hbuf, tile0, tgt, wave, lane);
-        return;
-    }
-
-    // ---- update_net_1: v = relu(U1 [h | mean | t] + c1), cols 32 w .. 32 w + 31
-    {
-        f32x4 acc[2] = {(f32x4){0.0f, 0.0f, 0.0f, 0.0f}, (f32x4){0.0f, 0.0f, 0.0f, 0.0f}};
-        const float *hrow = p.h + tgt * H + 4 * g;
-#pragma unroll 2
-        for (int j = 0; j < 8; ++j) {
-            const float4 hv = *(const float4 *)(hrow + 16 * j);
-            const float4 mv = *(const float4 *)(red + r * FRP + 16 * j + 4 * g);
-#pragma unroll
-            for (int cc = 0; cc < 2; ++cc) {
-                const float *wr = p.u1 + (int64_t)(32 * wave + 16 * cc + r) * p.ld_u1 + 16 * j + 4 * g;
-                const float4 wh = *(const float4 *)wr;
-                const float4 wm = *(const float4 *)(wr + 128);
-#pragma unroll
-                for (int t = 0; t < 4; ++t) acc[cc] = mfma16(f4c(hv, t), f4c(wh, t), acc[cc]);
-#pragma unroll
-                for (int t = 0; t < 4; ++t) acc[cc] = mfma16(f4c(mv, t), f4c(wm, t), acc[cc]);
-            }
-        }
-        upd1_store(p, acc[0], acc[1], 1.0f, 1.0f, vbuf, tile0, wave, lane);
-    }
-    __syncthreads();
-
-    // ---- update_net_2 + residual + BatchNorm(eval) ----------------------------
-    {
-        f32x4 acc[2] = {(f32x4){0.0f, 0.0f, 0.0f, 0.0f}, (f32x4){0.0f, 0.0f, 0.0f, 0.0f}};
-#pragma unroll 2
-        for (int j = 0; j < 8; ++j) {
-            const float4 vv = *(const float4 *)(vbuf + r * FRP + 16 * j + 4 * g);
-#pragma unroll
-            for (int cc = 0; cc < 2; ++cc) {
-                const float4 w = *(const float4 *)(p.u2 + (32 * wave + 16 * cc + r) * H + 16 * j + 4 * g);
-#pragma unroll
-                for (int t = 0; t < 4; ++t) acc[cc] = mfma16(f4c(vv, t), f4c(w, t), acc[cc]);
-            }
-        }
-        upd2_store<NEXT>(p, acc, nullptr, hbuf, tile0, wave, lane);
-    }
-    if (!NEXT) return;
-    __syncthreads();
-
-    // ---- next layer's message_net_1 halves (EpiProj) -------------------------
-    {
-        f32x4 acc[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) acc[c] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
-        // tiles 0,1: a' cols 32w+16cc (W1n[:, 0:128]); tiles 2,3: b' (W1n[:, 128:256])
-#pragma unroll 2
-        for (int j = 0; j < 8; ++j) {
-            const float4 hv = *(const float4 *)(hbuf + r * FRP + 16 * j + 4 * g);
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const int col = 32 * wave + 16 * (c & 1) + r;
-                const float4 w = *(const float4 *)(p.w1n + (int64_t)col * p.ld_w1n + 128 * (c >> 1) + 16 * j + 4 * g);
-#pragma unroll
-                for (int t = 0; t < 4; ++t) acc[c] = mfma16(f4c(hv, t), f4c(w, t), acc[c]);
-            }
-        }
-        proj_store(p, acc, nullptr, tile0, wave, lane);
-    }
-}
-
-// ---------------------------------------------------------------------------
 // Conv1d head (gnn_2d.py:108-114,136-139): one wave per node.
 // 128 -> conv(1->4, k16, s3) 38 -> relu -> conv(4->8, k12, s3) 9 -> relu ->
 // conv(8->1, k8, s2) 1, times out_scale.
@@ -1064,36 +394,6 @@ extern "C" int mmpde_gnn_head(const float *h, int64_t n, const mmpde_gnn_head_pa
     return MMPDE_OK;
 }
 
-static int launch_fused_layer(const float *a, const float *b, const float *h, const float *u,
-                              const float *pos, int64_t n, int k, const int32_t *nbr,
-                              mmpde_gnn_scales sc, const mmpde_gnn_layer_params *p,
-                              const mmpde_gnn_layer_params *next, const char *pk,
-                              const char *pkn, const uint32_t *amax_in, uint32_t *amax_out,
-                              float *h_out, float *a_out, float *b_out, hipStream_t st) {
-    MMPDE_REQUIRE(p->upd1_ld >= 257 && (p->upd1_ld & 3) == 0 && aligned16(p->upd1_w));
-    MMPDE_REQUIRE(aligned16(p->msg2_w) && aligned16(p->upd2_w));
-    FusedLayerArgs f{a, b, h, nbr, n, k, p->msg2_w, p->msg2_b, pk, pkn, p->upd1_w, p->upd1_b,
-                     p->upd1_ld, p->upd2_w, p->upd2_b, p->bn_w, p->bn_b, p->bn_rm, p->bn_rv,
-                     p->eps, h_out, nullptr, nullptr, 0, a_out, b_out, u, pos, sc, amax_in,
-                     amax_out};
-    const dim3 grid(ceil_div(n, FT));
-    if (next) {
-        MMPDE_REQUIRE(next->msg1_ld >= 260 && (next->msg1_ld & 3) == 0 && aligned16(next->msg1_w));
-        f.w1n = next->msg1_w;
-        f.b1n = next->msg1_b;
-        f.ld_w1n = next->msg1_ld;
-    }
-#define MMPDE_FUSED(NX, SPLIT) \
-    hipLaunchKernelGGL((gnn_layer_fused_kernel<NX, SPLIT>), grid, dim3(256), 0, st, f)
-    if (next && pk) MMPDE_FUSED(true, true);
-    else if (next) MMPDE_FUSED(true, false);
-    else if (pk) MMPDE_FUSED(false, true);
-    else MMPDE_FUSED(false, false);
-#undef MMPDE_FUSED
-    MMPDE_RET_LAUNCH();
-    return MMPDE_OK;
-}
-
 extern "C" int64_t mmpde_gnn_pack_bytes(int n_layers) {
     return n_layers < 0 ? 0 : (int64_t)n_layers * kLayerPack;
 }
@@ -1141,8 +441,7 @@ extern "C" int mmpde_gnn_forward_ex(const float *u, const float *pos, int64_t n,
     hipStream_t st = as_stream(stream);
     float *ws = (float *)workspace;
     float *hb[2] = {ws, ws + n * H};
-    float *ab[2] = {ws + 2 * n * H, ws + 3 * n * H};
-    float *bb[2] = {ws + 4 * n * H, ws + 5 * n * H};
+    float *wa = ws + 2 * n * H, *wb = ws + 3 * n * H, *wmean = ws + 4 * n * H;
     const char *pack = nullptr;
     // range slots of every layer's message inputs (F16X3 split scale)
     uint32_t *amax = (uint32_t *)(ws + 6 * n * H);
@@ -1159,7 +458,7 @@ extern "C" int mmpde_gnn_forward_ex(const float *u, const float *pos, int64_t n,
             pack = wpk;
         }
     }
-    rc = mmpde_gnn_embed(u, pos, n, sc, emb, ab[1], hb[0], stream);  // ab[1]: scratch
+    rc = mmpde_gnn_embed(u, pos, n, sc, emb, wmean, hb[0], stream);  // wmean: scratch
     if (rc) return rc;
     if (n_layers > 0) {
         // layer 0's message_net_1 halves; later layers get theirs from the fused kernel
@@ -1167,7 +466,7 @@ extern "C" int mmpde_gnn_forward_ex(const float *u, const float *pos, int64_t n,
         MMPDE_REQUIRE(p0->msg1_ld >= 260 && (p0->msg1_ld & 3) == 0 && aligned16(p0->msg1_w));
         const int64_t ld = p0->msg1_ld;
         GemmArgs g{n, hb[0], hb[0] + 64, H, p0->msg1_w, p0->msg1_w + 64, ld, 64};
-        EpiProj epi{ab[0], bb[0], p0->msg1_b, p0->msg1_w + 256, p0->msg1_w + 257,
+        EpiProj epi{wa, wb, p0->msg1_b, p0->msg1_w + 256, p0->msg1_w + 257,
                     p0->msg1_w + 258, p0->msg1_w + 259, ld, u, pos, sc, pack ? amax : nullptr};
         rc = launch_gemm<EpiProj, true>(g, 2, epi, st);
         if (rc) return rc;
@@ -1176,16 +475,21 @@ extern "C" int mmpde_gnn_forward_ex(const float *u, const float *pos, int64_t n,
     for (int l = 0; l < n_layers; ++l) {
         hipEvent_t eb = exec && exec->edge_begin ? (hipEvent_t)exec->edge_begin[l] : nullptr;
         hipEvent_t ee = exec && exec->edge_end ? (hipEvent_t)exec->edge_end[l] : nullptr;
-        if (eb && hipEventRecord(eb, st) != hipSuccess) return MMPDE_ERR_INVALID_ARG;
+        hipEvent_t ne = exec && exec->node_end ? (hipEvent_t)exec->node_end[l] : nullptr;
         const mmpde_gnn_layer_params *next = l + 1 < n_layers ? &layers[l + 1] : nullptr;
         const char *pk = pack ? pack + (int64_t)l * kLayerPack : nullptr;
         const char *pkn = pack && next ? pack + (int64_t)(l + 1) * kLayerPack : nullptr;
         const uint32_t *ain = pack ? amax + 2 * kAmaxShards * l : nullptr;
         uint32_t *aout = pack && next ? amax + 2 * kAmaxShards * (l + 1) : nullptr;
-        rc = launch_fused_layer(ab[cur], bb[cur], hb[cur], u, pos, n, k, nbr, sc, &layers[l], next,
-                                pk, pkn, ain, aout, hb[cur ^ 1], ab[cur ^ 1], bb[cur ^ 1], st);
+        if (eb && hipEventRecord(eb, st) != hipSuccess) return MMPDE_ERR_INVALID_ARG;
+        rc = launch_edge_stage(wa, wb, nbr, n, k, &layers[l], pk, ain, wmean, st);
         if (rc) return rc;
         if (ee && hipEventRecord(ee, st) != hipSuccess) return MMPDE_ERR_INVALID_ARG;
+        // a, b are rewritten in place: this layer's edge stage has consumed them
+        rc = launch_node_stage(hb[cur], wmean, u, pos, n, sc, &layers[l], next, pk, pkn, aout,
+                               hb[cur ^ 1], wa, wb, st);
+        if (rc) return rc;
+        if (ne && hipEventRecord(ne, st) != hipSuccess) return MMPDE_ERR_INVALID_ARG;
         cur ^= 1;
     }
     return mmpde_gnn_head(hb[cur], n, head, out, stream);

@@ -1,0 +1,732 @@
+// One message-passing layer of MP_PDE_Solver_2D (reference gnn_2d.py:53-69,
+// GNN_Layer_FS_2D.forward/message/update) as two launches:
+//
+//   edge stage  mean_i = (1/k) sum_e relu(W2 relu(a_i + b_nbr(i,e)) + b2)
+//   node stage  v_i = relu(U1 [h_i | mean_i | t_i] + c1)
+//               h'_i = BN(h_i + relu(U2 v_i + c2))
+//               a'_i, b'_i = next layer's message_net_1 node halves of h'_i
+//
+// a, b are message_net_1 factored exactly into a target half and a source half
+// (its 260-wide input is cat(h_i, h_j, u_i-u_j, x_i-x_j, y_i-y_j, t_i), so
+// W1 [h_i | h_j | du | dx | dy | t] = (W1a h_i + w.(u,x,y)_i + w_t t_i + b1)
+// + (W1b h_j - w.(u,x,y)_j)); the reference's [E, 260] edge concat never
+// exists and the only per-edge work is one 128x128 GEMM per edge.
+//
+// Edge stage (the dominant kernel): persistent, one 512-thread workgroup per
+// CU walking a contiguous (XCD-local) range of 16-target tiles.  Waves 4-7 are
+// producers: for neighbour slot e of a tile they gather the 16 source rows of
+// b, form m = relu(a_i + b_j) in registers and store it to an LDS ring as the
+// exact per-lane A operand (F16X3: scaled fp16 hi/lo halves).  Waves 0-3 are
+// consumers: each keeps 32 output columns of W2 in registers for the whole
+// launch and runs the MFMAs of every slot, accumulating relu(. + b2) per
+// target in registers (slot e of all 16 targets shares one accumulator row,
+// so no cross-lane traffic), and writes the mean after the tile's last slot.
+// A workgroup's waves land on SIMDs in the order 0,2,1,3 (MI355X_MICROARCH.md),
+// so waves w and w+4 share a SIMD: every SIMD pairs one MFMA stream with one
+// VALU/gather stream.  One barrier per round of 4 slots; producers run
+// ERING-1 rounds ahead, b rows are gathered two rounds before use.
+//
+// Node stage: 64 (or 32) rows per workgroup, 8 waves; every GEMM reads its
+// weight operand once per workgroup (wave w owns output column tile w for all
+// row blocks); activations are staged in LDS as MFMA operand images with
+// per-row power-of-two scales (F16X3).  No atomics anywhere: deterministic.
+#include "common.hpp"
+#include "f16x3.hpp"
+#include "layer.hpp"
+
+namespace {
+
+constexpr int LH = 128;   // hidden width
+constexpr int ET = 16;    // targets per edge tile
+constexpr int ESL = 4;    // neighbour slots per round
+constexpr int ERING = 3;  // LDS ring depth (rounds)
+constexpr int EPF = ERING - 1;
+constexpr int SLOT4 = 512;    // float4 per slot: 8 planes x 64 lanes = 8 KB
+constexpr int NLDA = LH + 4;  // a-tile LDS row stride (floats)
+
+// Contiguous XCD-local tile ranges (blocks b and b + 8 share an XCD): XCD x owns
+// tiles [lo, hi), its workgroups i = b >> 3 take lo + i + nW * j.  Bijective
+// for any grid; placement is used for speed only.
+__device__ __forceinline__ void tile_schedule(int bid, int G, int ntiles, int &first, int &stride,
+                                              int &count) {
+    const int x = bid & 7, i = bid >> 3;
+    const int q = G >> 3, rem = G & 7;
+    const int nW = q + (x < rem ? 1 : 0);
+    const int cum = x * q + min(x, rem);
+    const int lo = (int)((int64_t)ntiles * cum / G);
+    const int hi = (int)((int64_t)ntiles * (cum + nW) / G);
+    first = lo + i;
+    stride = nW;
+    count = first < hi ? (hi - first + stride - 1) / stride : 0;
+}
+
+struct EdgeArgs {
+    const float *a, *b;
+    const int32_t *nbr;
+    int64_t n;
+    int k, ntiles;
+    const float *w2, *b2;      // message_net_2.0 weight [128,128], bias
+    const char *pk;            // F16X3: this layer's packed images (column scales of W2)
+    const uint32_t *amax_in;   // F16X3: range slots of a, b
+    float *mean;               // [n, 128]
+    uint64_t *stamps;          // profiling builds (PH bit 10): per-round s_memtime of block 0
+};
+
+struct RoundCtr {  // (tile j, round rd) of a running round index
+    int j, rd;
+    __device__ void next(int rpt) {
+        if (++rd == rpt) {
+            rd = 0;
+            ++j;
+        }
+    }
+};
+
+#ifndef MMPDE_EDGE_NC
+#define MMPDE_EDGE_NC 2
+#endif
+constexpr int EDGE_NC = MMPDE_EDGE_NC;
+#ifndef MMPDE_EDGE_NP
+#define MMPDE_EDGE_NP 1
+#endif
+constexpr int EDGE_NP = MMPDE_EDGE_NP;
+
+// PH (profiling builds only, tools/ubench): bit 0 produce, bit 1 consume (MFMA),
+// bit 2 skip the gathers, bit 3 raise the consumer waves' issue priority, bit
+// 10 record per-round s_memtime stamps of block 0; production launches use EDGE_PH.
+#ifndef MMPDE_EDGE_PH
+#define MMPDE_EDGE_PH 11
+#endif
+constexpr int EDGE_PH = MMPDE_EDGE_PH;
+
+// Slot operand layout (v_mfma_f32_16x16x32_f16; F32: v_mfma_f32_16x16x4_f32): a
+// slot is the 16 x 128 message tile m[row][k] of one neighbour slot e of the
+// tile's 16 targets; lane l = 16 g + row holds 8 float4-sized pieces i < 8:
+//   F16X3 piece i: k = 32 (i >> 1) + 8 g + 4 (i & 1) + t -> pieces 2 s, 2 s + 1
+//         are the fp16 hi / lo halves of K step s (k = 32 s + 8 g + t, t < 8);
+//   F32   piece i: k = 16 i + 4 g + t (t < 4).
+// stored as 8 lane-contiguous 1 KB planes (8 KB per slot).
+//
+// Workgroup: 4 NC consumer waves + 4 producer waves (NC consumers per SIMD: a
+// workgroup's waves land on SIMDs in the order 0,2,1,3, so waves w, w + 4,
+// w + 8 share one).  Producer p builds slot ESL rd + p of round rd; consumer c
+// multiplies every slot by its 32 / NC output columns of W2 (held in
+// registers for the whole launch).  One barrier per round; producers run EPF
+// rounds ahead; b rows are gathered two rounds before use.
+template <bool F16X3, int PH = EDGE_PH, int NC = EDGE_NC, int NP = EDGE_NP>
+__global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(EdgeArgs p) {
+    constexpr int CT = 2 / NC;  // 16-column tiles per consumer wave
+    constexpr int NPC = 8 / NP;  // float4 pieces of a slot lane per producer wave
+    constexpr int NCT = 256 * NC;  // consumer threads
+    __shared__ float4 ring[ERING * ESL * SLOT4];  // [round % ERING][slot][plane][lane]
+    __shared__ float a_lds[2][ET * NLDA];        // a rows of tile j in [j & 1]
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const int r = lane & 15, g = lane >> 4;
+    const bool producer = wave >= 4 * NC;
+    int first, stride, nt;
+    tile_schedule(blockIdx.x, gridDim.x, p.ntiles, first, stride, nt);
+    const int k = p.k;
+    const int rpt = (k + ESL - 1) / ESL;
+    const int NR = nt * rpt;
+    const int NIT = NR + EPF;
+    const int NIT2 = (NIT + 1) & ~1;  // even: the producer's 2x-unrolled body has no tail test
+    const int64_t nmax = p.n - 1;
+    float sc = 1.0f;  // F16X3: m = relu(a + b) <= max|a| + max|b|, so m * sc < 2^14
+    if (F16X3) sc = split_scale(amax_read(p.amax_in) + amax_read(p.amax_in + kAmaxShards));
+    auto tile_row = [&](int j, int row) { return min((int64_t)(first + j * stride) * ET + row, nmax); };
+
+    // a tiles (scaled by sc for F16X3): the consumer waves stage tile j + 1 while
+    // the producers work on tile j, 2 / NC float4 per consumer thread.
+    auto a_fetch = [&](int j, float4 *v) {
+#pragma unroll
+        for (int u = 0; u < 2 / NC; ++u) {
+            const int e = tid + NCT * u, row = e >> 5, c4 = e & 31;
+            v[u] = *(const float4 *)(p.a + tile_row(j, row) * LH + 4 * c4);
+        }
+    };
+    auto a_store = [&](int j, const float4 *v) {
+#pragma unroll
+        for (int u = 0; u < 2 / NC; ++u) {
+            const int e = tid + NCT * u, row = e >> 5, c4 = e & 31;
+            float4 x = v[u];
+            if (F16X3) x = make_float4(x.x * sc, x.y * sc, x.z * sc, x.w * sc);
+            *(float4 *)(&a_lds[j & 1][row * NLDA + 4 * c4]) = x;
+        }
+    };
+    if (!producer && nt > 0) {
+        float4 v[2 / NC];
+        a_fetch(0, v);
+        a_store(0, v);
+    }
+    __syncthreads();
+
+    if (producer) {
+        // ------------------------------------------------------------ producer
+        // NP producers per slot (one per SIMD each): producer pidx builds
+        // pieces i0 .. i0 + NPC - 1 of slot pidx & 3 (F16X3: K steps
+        // i0 / 2 .. (i0 + NPC) / 2 - 1, hi and lo)
+        const int pidx = wave - 4 * NC;
+        const int pw = pidx & 3, i0 = (pidx >> 2) * NPC;
+        auto piece = [&](int i) {
+            const int ii = i0 + i;
+            return F16X3 ? 32 * (ii >> 1) + 8 * g + 4 * (ii & 1) : 16 * ii + 4 * g;
+        };
+        float4 acur[NPC], bv0[NPC], bv1[NPC];
+        // every round issues the same loads (clamped addresses past the end or
+        // past k): 1 index + 8 gathers
+        auto src_of = [&](const RoundCtr &c) -> uint32_t {
+            return (uint32_t)p.nbr[tile_row(c.j, r) * k + min(ESL * c.rd + pw, k - 1)];
+        };
+        auto gather = [&](float4 *dst, uint32_t src) {
+            const float *br = p.b + (int64_t)min(src, (uint32_t)nmax) * LH;  // clamped: a malformed table must not fault
+#pragma unroll
+            for (int i = 0; i < NPC; ++i) dst[i] = *(const float4 *)(br + piece(i));
+        };
+        RoundCtr cP{0, 0}, c2{0, 0}, c3{0, 0};
+        uint32_t s0, s1;  // neighbour index of the round gathered next into bv0 / bv1
+        // prologue in the loop's own load order (index of round R + 1, then the
+        // gathers of round R): idx0, idx1, gathers0, idx2, gathers1
+        {
+            const uint32_t i0 = src_of(c2);
+            c2.next(rpt);
+            const uint32_t i1 = src_of(c2);
+            c2.next(rpt);
+            gather(bv0, i0);
+            c3 = c2;
+            s0 = src_of(c3);
+            c3.next(rpt);
+            gather(bv1, i1);
+        }
+        int slot = 0;
+        // Branch-free rounds (a straight-line body keeps the compiler's
+        // vector-memory waits counted): past the end and for slots past k the
+        // producer still writes its ring slot (nobody reads it unmasked; after
+        // the last round the slot written is neither of the rounds still being
+        // consumed).
+        auto body = [&](int it, float4 *bv, uint32_t &s_use, uint32_t &s_fill) {
+            // the index of round it + 3 is this round's first load: a later use
+            // of a register only waits for the loads issued before it
+            s_fill = src_of(c3);
+            c3.next(rpt);
+            if (PH & 1) {
+                const float *ar = &a_lds[cP.j & 1][r * NLDA];
+#pragma unroll
+                for (int i = 0; i < NPC; ++i) acur[i] = *(const float4 *)(ar + piece(i));
+                float4 *dst = ring + (slot * ESL + pw) * SLOT4 + i0 * 64 + lane;
+#pragma unroll
+                for (int h2 = 0; h2 < NPC / 2; ++h2) {
+                    const float4 &a0 = acur[2 * h2], &a1 = acur[2 * h2 + 1];
+                    const float4 &b0 = bv[2 * h2], &b1 = bv[2 * h2 + 1];
+                    float4 m0, m1;
+                    if (F16X3) {
+                        m0 = make_float4(fmaxf(fmaf(b0.x, sc, a0.x), 0.0f), fmaxf(fmaf(b0.y, sc, a0.y), 0.0f),
+                                         fmaxf(fmaf(b0.z, sc, a0.z), 0.0f), fmaxf(fmaf(b0.w, sc, a0.w), 0.0f));
+                        m1 = make_float4(fmaxf(fmaf(b1.x, sc, a1.x), 0.0f), fmaxf(fmaf(b1.y, sc, a1.y), 0.0f),
+                                         fmaxf(fmaf(b1.z, sc, a1.z), 0.0f), fmaxf(fmaf(b1.w, sc, a1.w), 0.0f));
+                        half8 hi, lo;
+                        split8_rn(m0, m1, hi, lo);
+                        dst[(2 * h2 + 0) * 64] = *(const float4 *)&hi;
+                        dst[(2 * h2 + 1) * 64] = *(const float4 *)&lo;
+                    } else {
+                        m0 = make_float4(fmaxf(a0.x + b0.x, 0.0f), fmaxf(a0.y + b0.y, 0.0f),
+                                         fmaxf(a0.z + b0.z, 0.0f), fmaxf(a0.w + b0.w, 0.0f));
+                        m1 = make_float4(fmaxf(a1.x + b1.x, 0.0f), fmaxf(a1.y + b1.y, 0.0f),
+                                         fmaxf(a1.z + b1.z, 0.0f), fmaxf(a1.w + b1.w, 0.0f));
+                        dst[(2 * h2 + 0) * 64] = m0;
+                        dst[(2 * h2 + 1) * 64] = m1;
+                    }
+                }
+            }
+            cP.next(rpt);
+            // gather the round two ahead into the registers just consumed
+            if (!(PH & 4)) gather(bv, s_use);
+            c2.next(rpt);
+            slot = slot == ERING - 1 ? 0 : slot + 1;
+            if ((PH & 1024) && blockIdx.x == 0 && lane == 0 && it < 256)
+                p.stamps[2 * 256 * wave + 2 * it] = __builtin_amdgcn_s_memtime();
+            __syncthreads();
+            if ((PH & 1024) && blockIdx.x == 0 && lane == 0 && it < 256)
+                p.stamps[2 * 256 * wave + 2 * it + 1] = __builtin_amdgcn_s_memtime();
+        };
+        for (int it = 0; it < NIT2; it += 2) {
+            body(it, bv0, s0, s1);
+            body(it + 1, bv1, s1, s0);
+        }
+    } else {
+        // ------------------------------------------------------------ consumer
+        // this wave's output column tiles CT wave + cc (cc < CT)
+        float4 wf[CT][8];
+        half8 wh[CT][4], wl[CT][4];
+        float bias[CT], inv[CT];  // bias: added in the relu-sum (keeps the accumulator zero-initialised)
+#pragma unroll
+        for (int cc = 0; cc < CT; ++cc) {
+            const int col = 16 * (CT * wave + cc) + r;
+            float bb = p.b2[col];
+            if (F16X3) {
+                const char *img = p.pk + kPkW2;
+#pragma unroll
+                for (int s4 = 0; s4 < 4; ++s4) {
+                    wh[cc][s4] = bfrag(img, 4, CT * wave + cc, s4, 0, lane);
+                    wl[cc][s4] = bfrag(img, 4, CT * wave + cc, s4, 1, lane);
+                }
+                const float sw = ((const float *)(img + 65536))[col];
+                bb = bb * sw * sc;
+                inv[cc] = pow2_inv(sw) * pow2_inv(sc);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) wf[cc][j] = *(const float4 *)(p.w2 + col * LH + 16 * j + 4 * g);
+                inv[cc] = 1.0f;
+            }
+            bias[cc] = bb;
+        }
+        f32x4 S[CT];
+#pragma unroll
+        for (int cc = 0; cc < CT; ++cc) S[cc] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+        RoundCtr cC{0, 0};
+        int slot = 0;
+        const float kdiv = (float)k;
+        if (PH & 8) __builtin_amdgcn_s_setprio(1);
+        // The next half slot is read from LDS while the current one is
+        // multiplied (the next round's first half too: that round was
+        // completed by the previous barrier), and each slot's relu-sum update
+        // is issued after the next slot's first MFMAs.  Slots past k (last
+        // round) are multiplied but not summed.
+        const f32x4 zero4 = {0.0f, 0.0f, 0.0f, 0.0f};
+        // A operands stream through two half-slot register buffers (pieces
+        // 0-3 / 4-7 of a slot lane)
+        auto rd_half = [&](const float4 *src, int hf, float4 *x) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) x[i] = src[(4 * hf + i) * 64];
+        };
+        auto mma_half = [&](const float4 *x, int hf, f32x4 *acc) {
+            if (F16X3) {
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    const int s4 = 2 * hf + s;
+                    const half8 hi = *(const half8 *)&x[2 * s], lo = *(const half8 *)&x[2 * s + 1];
+#pragma unroll
+                    for (int cc = 0; cc < CT; ++cc) acc[cc] = mfma_f16(hi, wh[cc][s4], s4 == 0 ? zero4 : acc[cc]);
+#pragma unroll
+                    for (int cc = 0; cc < CT; ++cc) acc[cc] = mfma_f16(hi, wl[cc][s4], acc[cc]);
+#pragma unroll
+                    for (int cc = 0; cc < CT; ++cc) acc[cc] = mfma_f16(lo, wh[cc][s4], acc[cc]);
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int jj = 4 * hf + j;
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+#pragma unroll
+                        for (int cc = 0; cc < CT; ++cc)
+                            acc[cc] = mfma16(f4c(x[j], t), f4c(wf[cc][jj], t), jj == 0 && t == 0 ? zero4 : acc[cc]);
+                    }
+                }
+            }
+        };
+        auto sum_into = [&](const f32x4 *acc, bool valid) {
+#pragma unroll
+            for (int cc = 0; cc < CT; ++cc) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const float v = fmaf(fmaxf(acc[cc][t] + bias[cc], 0.0f), inv[cc], S[cc][t]);
+                    S[cc][t] = valid ? v : S[cc][t];
+                }
+            }
+        };
+        float4 xa[4], xb[4], an[2 / NC];
+        int js = 1;  // next a tile to stage: stored in iteration js * rpt - 1 (the
+                     // producers read it from iteration js * rpt), fetched up to two
+                     // iterations earlier but after the previous store
+        const int lead = min(2, rpt - 1);
+        for (int it = 0; it < NIT2; ++it) {
+            if (js < nt) {
+                const int ts = js * rpt - 1;
+                if (it == ts - lead) a_fetch(js, an);
+                if (it == ts) {
+                    a_store(js, an);
+                    ++js;
+                }
+            }
+            if (it >= EPF && it < NIT && (PH & 2)) {
+                const float4 *base = ring + slot * ESL * SLOT4 + lane;
+                const float4 *nbase = ring + (slot == ERING - 1 ? 0 : slot + 1) * ESL * SLOT4 + lane;
+                if (it == EPF) rd_half(base, 0, xa);
+                f32x4 accP[CT];
+#pragma unroll
+                for (int q = 0; q < ESL; ++q) {
+                    f32x4 accN[CT];
+                    rd_half(base + q * SLOT4, 1, xb);
+                    mma_half(xa, 0, accN);
+                    if (q > 0) sum_into(accP, ESL * cC.rd + q - 1 < k);
+                    if (q < ESL - 1) rd_half(base + (q + 1) * SLOT4, 0, xa);
+                    else if (it + 1 < NIT) rd_half(nbase, 0, xa);
+                    mma_half(xb, 1, accN);
+#pragma unroll
+                    for (int cc = 0; cc < CT; ++cc) accP[cc] = accN[cc];
+                }
+                sum_into(accP, ESL * cC.rd + ESL - 1 < k);
+                if (cC.rd == rpt - 1) {  // tile complete: mean = sum / k (PyG mean, fixed degree)
+                    const int64_t row0 = (int64_t)(first + cC.j * stride) * ET + 4 * g;
+#pragma unroll
+                    for (int cc = 0; cc < CT; ++cc) {
+                        const int col = 16 * (CT * wave + cc) + r;
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) {
+                            if (row0 + t < p.n) p.mean[(row0 + t) * LH + col] = S[cc][t] / kdiv;
+                        }
+                        S[cc] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+                    }
+                }
+                cC.next(rpt);
+                slot = slot == ERING - 1 ? 0 : slot + 1;
+            }
+            if ((PH & 1024) && blockIdx.x == 0 && lane == 0 && it < 256)
+                p.stamps[2 * 256 * wave + 2 * it] = __builtin_amdgcn_s_memtime();
+            __syncthreads();
+            if ((PH & 1024) && blockIdx.x == 0 && lane == 0 && it < 256)
+                p.stamps[2 * 256 * wave + 2 * it + 1] = __builtin_amdgcn_s_memtime();
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Node stage
+// ---------------------------------------------------------------------------
+struct NodeArgs {
+    const float *h, *mean;
+    int64_t n;
+    const float *u1, *c1;  // update_net_1.0 [128, ld_u1] (h | mean | t), bias
+    int64_t ld_u1;
+    const float *u2, *c2;  // update_net_2.0 [128, 128], bias
+    const float *bn_w, *bn_b, *bn_rm, *bn_rv;
+    float eps;
+    float *h_out;
+    const float *w1n, *b1n;  // next layer message_net_1.0 [128, ld_w1n], bias (NEXT)
+    int64_t ld_w1n;
+    float *a_out, *b_out;
+    const float *u, *pos;
+    mmpde_gnn_scales sc;
+    const char *pk, *pkn;  // F16X3 images: this layer (U1, U2), next layer (W1)
+    uint32_t *amax_out;
+};
+
+constexpr int NLD = 132;  // fp32 staging row stride (floats)
+
+// Operand images in LDS, per 16-row block rb and K step s (1 KB units of 64
+// lanes x 16 B): F16X3 [rb][s (32-wide)][hi|lo] with lane (r, g) holding
+// k = 32 s + 8 g + t; F32 [rb][s (16-wide)] with lane (r, g) holding k = 16 s + 4 g + t.
+// prep(): rows of 128 fp32 values (src, row stride lds) -> image at k offset
+// kofs (multiple of 128) of an image KT wide; F16X3 scales each row by a power
+// of two (its max |x| -> [2^13, 2^14)) and records it in rs[row].  8 lanes per row.
+template <bool F16X3, int ROWS>
+__device__ __forceinline__ void prep(const float *src, int64_t lds, int64_t row0, int64_t nrows_valid,
+                                     bool global, float4 *img, int KT, int kofs, float *rs,
+                                     float *copy = nullptr) {
+    for (int idx = threadIdx.x; idx < ROWS * 8; idx += 512) {
+        // a wave takes 8 rows x 8 parts, lane = 8 part + row: the 8 lanes of one
+        // ds_write_b128 group write 8 consecutive image rows (conflict-free)
+        const int row = (idx >> 6) * 8 + (idx & 7), part = (idx >> 3) & 7;
+        const int64_t srow = global ? min(row0 + row, nrows_valid - 1) : row;
+        const float *sp = src + srow * lds + 16 * part;
+        float4 x[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) x[q] = *(const float4 *)(sp + 4 * q);
+        if (copy) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) *(float4 *)(copy + row * NLD + 16 * part + 4 * q) = x[q];
+        }
+        const int rb = row >> 4, rr = row & 15;
+        if (F16X3) {
+            float m = 0.0f;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) m = absmax4(m, x[q]);
+            m = fmaxf(m, __shfl_xor(m, 8, 64));
+            m = fmaxf(m, __shfl_xor(m, 16, 64));
+            m = fmaxf(m, __shfl_xor(m, 32, 64));
+            const float s = split_scale(m);
+            if (part == 0) rs[row] = s;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) x[q] = make_float4(x[q].x * s, x[q].y * s, x[q].z * s, x[q].w * s);
+            const int KS = KT / 32;
+            const int ks = (kofs + 16 * part) >> 5;
+            const int g0 = 2 * (part & 1);
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+                half8 hi, lo;
+                split8_rn(x[2 * hh], x[2 * hh + 1], hi, lo);
+                float4 *d = img + ((rb * KS + ks) * 2) * 64 + 16 * (g0 + hh) + rr;
+                d[0] = *(const float4 *)&hi;
+                d[64] = *(const float4 *)&lo;
+            }
+        } else {
+            const int KJ = KT / 16;
+            const int j = (kofs >> 4) + part;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) img[(rb * KJ + j) * 64 + 16 * q + rr] = x[q];
+        }
+    }
+}
+
+// B operand fragments of NS K steps of column tile ct, loaded ahead of use.
+// F16X3: packed image (KSB 32-wide K steps per column tile) steps sb0 ..;
+// F32: fp32 weight row wrow (this lane's column), 16-wide steps from k = wk0.
+template <bool F16X3, int NS>
+struct BOps {
+    half8 h[F16X3 ? NS : 1], l[F16X3 ? NS : 1];
+    float4 w[F16X3 ? 1 : NS];
+    __device__ __forceinline__ void load(const char *bimg, int KSB, int ct, int sb0,
+                                         const float *wrow, int wk0, int lane) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            if (F16X3) {
+                h[s] = bfrag(bimg, KSB, ct, sb0 + s, 0, lane);
+                l[s] = bfrag(bimg, KSB, ct, sb0 + s, 1, lane);
+            } else {
+                w[s] = *(const float4 *)(wrow + wk0 + 16 * s + 4 * (lane >> 4));
+            }
+        }
+    }
+};
+
+// acc[rb] += A(image rows, K steps s0 .. s0 + NS of an image KT wide) x B.
+template <bool F16X3, int RB, int NS>
+__device__ __forceinline__ void gemm_tile(f32x4 *acc, const float4 *img, int KT, int s0,
+                                          const BOps<F16X3, NS> &B, int lane) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+            if (F16X3) {
+                const int KS = KT / 32;
+                const float4 h4 = img[((rb * KS + s0 + s) * 2) * 64 + lane];
+                const float4 l4 = img[((rb * KS + s0 + s) * 2 + 1) * 64 + lane];
+                const half8 ah = *(const half8 *)&h4, al = *(const half8 *)&l4;
+                acc[rb] = mfma_f16(ah, B.h[s], acc[rb]);
+                acc[rb] = mfma_f16(ah, B.l[s], acc[rb]);
+                acc[rb] = mfma_f16(al, B.h[s], acc[rb]);
+            } else {
+                const int KJ = KT / 16;
+                const float4 a = img[(rb * KJ + s0 + s) * 64 + lane];
+                acc[rb] = mfma16(a.x, B.w[s].x, acc[rb]);
+                acc[rb] = mfma16(a.y, B.w[s].y, acc[rb]);
+                acc[rb] = mfma16(a.z, B.w[s].z, acc[rb]);
+                acc[rb] = mfma16(a.w, B.w[s].w, acc[rb]);
+            }
+        }
+    }
+}
+
+template <bool NEXT, bool F16X3, int RB>
+__global__ __launch_bounds__(512, 1) void gnn_node_kernel(NodeArgs p) {
+    constexpr int ROWS = 16 * RB;
+    __shared__ float4 img[RB * 16 * 64];        // operand image, K = 256 (h | mean), then 128
+    __shared__ float stage[ROWS * NLD];         // fp32 v, then h'
+    __shared__ float hres[ROWS * NLD];          // fp32 h (residual)
+    __shared__ float rs[4][ROWS];               // row scales: h, mean, v, h'
+    __shared__ float rowv[4][ROWS];             // per row: t / tmax, x / Lx, y / Ly, u
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int r = lane & 15, g = lane >> 4;
+    const int64_t row0 = (int64_t)blockIdx.x * ROWS;
+    const int col = 16 * wave + r;  // this lane's output column (tile = wave)
+    constexpr int S1 = F16X3 ? 4 : 8;    // K steps per 128 columns of K
+    const float *wu1 = p.u1 + (int64_t)col * p.ld_u1, *wu2 = p.u2 + (int64_t)col * LH;
+    // everything the epilogues read from global memory is fetched up front
+    // (per-row node values to LDS, per-column constants to registers), so no
+    // epilogue waits on a memory round trip
+    if (tid < ROWS) {
+        const int64_t row = min(row0 + tid, p.n - 1);
+        rowv[0][tid] = p.pos[row * 3 + 0] * p.sc.inv_tmax;
+        rowv[1][tid] = p.pos[row * 3 + 1] * p.sc.inv_lx;
+        rowv[2][tid] = p.pos[row * 3 + 2] * p.sc.inv_ly;
+        rowv[3][tid] = p.u[row];
+    }
+    const float u1_wt = wu1[256], u1_b = p.c1[col];
+    const float u1_is = F16X3 ? pow2_inv(((const float *)(p.pk + kPkU1 + 131072))[col]) : 1.0f;
+    const float u2_b = p.c2[col], bn_rm = p.bn_rm[col], bn_rv = p.bn_rv[col];
+    const float bn_w = p.bn_w[col], bn_b = p.bn_b[col];
+    const float u2_is = F16X3 ? pow2_inv(((const float *)(p.pk + kPkU2 + 65536))[col]) : 1.0f;
+    const float *w1r = NEXT ? p.w1n + (int64_t)col * p.ld_w1n : nullptr;
+    float w1_du = 0.0f, w1_dx = 0.0f, w1_dy = 0.0f, w1_t = 0.0f, w1_b = 0.0f, w1_isa = 1.0f, w1_isb = 1.0f;
+    if (NEXT) {
+        w1_du = w1r[256];
+        w1_dx = w1r[257];
+        w1_dy = w1r[258];
+        w1_t = w1r[259];
+        w1_b = p.b1n[col];
+        if (F16X3) {
+            const float *su = (const float *)(p.pkn + kPkW1 + 131072);
+            w1_isa = pow2_inv(su[col]);
+            w1_isb = pow2_inv(su[128 + col]);
+        }
+    }
+    // weight operands of update_net_1 / _2 loaded first: their latency hides
+    // behind the activation staging
+    BOps<F16X3, S1> bH, bM, bU2;
+    bH.load(p.pk + kPkU1, 8, wave, 0, wu1, 0, lane);
+    bM.load(p.pk + kPkU1, 8, wave, S1, wu1, 128, lane);
+    bU2.load(p.pk + kPkU2, 4, wave, 0, wu2, 0, lane);
+
+    // ---- [h | mean] -> image (K = 256)
+    prep<F16X3, ROWS>(p.h, LH, row0, p.n, true, img, 256, 0, rs[0], hres);
+    prep<F16X3, ROWS>(p.mean, LH, row0, p.n, true, img, 256, 128, rs[1]);
+    __syncthreads();
+
+    // ---- update_net_1: v = relu(U1 [h | mean | t] + c1)
+    {
+        f32x4 aH[RB], aM[RB];
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) aH[rb] = aM[rb] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+        gemm_tile<F16X3, RB, S1>(aH, img, 256, 0, bH, lane);
+        gemm_tile<F16X3, RB, S1>(F16X3 ? aM : aH, img, 256, S1, bM, lane);
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int lr = 16 * rb + 4 * g + q;
+                float v = aH[rb][q];
+                if (F16X3) v = v * pow2_inv(rs[0][lr]) * u1_is + aM[rb][q] * pow2_inv(rs[1][lr]) * u1_is;
+                stage[lr * NLD + col] = fmaxf(v + u1_wt * rowv[0][lr] + u1_b, 0.0f);
+            }
+        }
+    }
+    __syncthreads();
+    prep<F16X3, ROWS>(stage, NLD, 0, ROWS, false, img, 128, 0, rs[2]);
+    __syncthreads();
+
+    // ---- update_net_2 + residual + BatchNorm(eval)
+    BOps<F16X3, S1> bA;
+    {
+        f32x4 acc[RB];
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) acc[rb] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+        gemm_tile<F16X3, RB, S1>(acc, img, 128, 0, bU2, lane);
+        // next layer's message_net_1 operands of a' (column tile wave)
+        if (NEXT) bA.load(p.pkn + kPkW1, 4, wave, 0, w1r, 0, lane);
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int lr = 16 * rb + 4 * g + q;
+                const int64_t row = row0 + lr;
+                float z = acc[rb][q];
+                if (F16X3) z = z * pow2_inv(rs[2][lr]) * u2_is;
+                const float x = hres[lr * NLD + col] + fmaxf(z + u2_b, 0.0f);
+                const float y = bn_eval(x, bn_rm, bn_rv, bn_w, bn_b, p.eps);
+                if (row < p.n) p.h_out[row * LH + col] = y;
+                if (NEXT) stage[lr * NLD + col] = y;
+            }
+        }
+    }
+    if constexpr (NEXT) {
+        __syncthreads();
+        prep<F16X3, ROWS>(stage, NLD, 0, ROWS, false, img, 128, 0, rs[3]);
+        __syncthreads();
+        // ---- next layer's message_net_1 node halves: a' (tile wave), b' (tile 8 + wave)
+        f32x4 aA[RB], aB[RB];
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) aA[rb] = aB[rb] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+        gemm_tile<F16X3, RB, S1>(aA, img, 128, 0, bA, lane);
+        {   // b' (column tile 8 + wave)
+            BOps<F16X3, S1> bB;
+            bB.load(p.pkn + kPkW1, 4, 8 + wave, 0, w1r, 128, lane);
+            gemm_tile<F16X3, RB, S1>(aB, img, 128, 0, bB, lane);
+        }
+        float amx = 0.0f, bmx = 0.0f;
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int lr = 16 * rb + 4 * g + q;
+                const int64_t row = row0 + lr;
+                if (row < p.n) {
+                    float za = aA[rb][q], zb = aB[rb][q];
+                    if (F16X3) {
+                        const float ir = pow2_inv(rs[3][lr]);
+                        za = za * ir * w1_isa;
+                        zb = zb * ir * w1_isb;
+                    }
+                    const float node = w1_du * rowv[3][lr] + w1_dx * rowv[1][lr] + w1_dy * rowv[2][lr];
+                    const float va = za + node + w1_t * rowv[0][lr] + w1_b;
+                    const float vb = zb - node;
+                    p.a_out[row * LH + col] = va;
+                    p.b_out[row * LH + col] = vb;
+                    amx = fmaxf(amx, fabsf(va));
+                    bmx = fmaxf(bmx, fabsf(vb));
+                }
+            }
+        }
+        if (p.amax_out) {
+            amax_publish(amx, p.amax_out);
+            amax_publish(bmx, p.amax_out + kAmaxShards);
+        }
+    }
+}
+
+inline bool al16(const void *q) { return ((uintptr_t)q & 15u) == 0; }
+
+int device_cus() {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+        return 256;
+    return cus;
+}
+
+}  // namespace
+
+// Node stage rows per workgroup (16 * RB)
+#ifndef MMPDE_NODE_RB
+#define MMPDE_NODE_RB 4
+#endif
+
+int launch_edge_stage(const float *a, const float *b, const int32_t *nbr, int64_t n, int k,
+                      const mmpde_gnn_layer_params *p, const char *pk, const uint32_t *amax_in,
+                      float *mean, hipStream_t st) {
+    MMPDE_REQUIRE(a && b && nbr && p && mean && n > 0 && k > 0 && n <= (int64_t)INT32_MAX);
+    MMPDE_REQUIRE(al16(a) && al16(b) && al16(p->msg2_w) && al16(mean));
+    MMPDE_REQUIRE(!pk || (amax_in && al16(pk)));
+    const int64_t ntiles = (n + ET - 1) / ET;
+    MMPDE_REQUIRE(ntiles * ((k + ESL - 1) / ESL) < (int64_t)INT32_MAX);
+    EdgeArgs e{a, b, nbr, n, k, (int)ntiles, p->msg2_w, p->msg2_b, pk, amax_in, mean, nullptr};
+    const int cus = device_cus();
+    const int grid = ntiles < cus ? (int)ntiles : cus;
+    const dim3 block(64 * (4 * EDGE_NC + 4 * EDGE_NP));
+    if (pk) hipLaunchKernelGGL(gnn_edge_kernel<true>, dim3(grid), block, 0, st, e);
+    else hipLaunchKernelGGL(gnn_edge_kernel<false>, dim3(grid), block, 0, st, e);
+    MMPDE_RET_LAUNCH();
+    return MMPDE_OK;
+}
+
+int launch_node_stage(const float *h, const float *mean, const float *u, const float *pos,
+                      int64_t n, mmpde_gnn_scales sc, const mmpde_gnn_layer_params *p,
+                      const mmpde_gnn_layer_params *next, const char *pk, const char *pkn,
+                      uint32_t *amax_out, float *h_out, float *a_out, float *b_out,
+                      hipStream_t st) {
+    MMPDE_REQUIRE(h && mean && u && pos && p && h_out && n > 0);
+    MMPDE_REQUIRE(al16(h) && al16(mean) && al16(h_out));
+    MMPDE_REQUIRE(p->upd1_ld >= 257 && (p->upd1_ld & 3) == 0 && al16(p->upd1_w) && al16(p->upd2_w));
+    MMPDE_REQUIRE(!pk || (al16(pk) && (!next || pkn)));
+    NodeArgs a{h, mean, n, p->upd1_w, p->upd1_b, p->upd1_ld, p->upd2_w, p->upd2_b, p->bn_w, p->bn_b,
+               p->bn_rm, p->bn_rv, p->eps, h_out, nullptr, nullptr, 0, a_out, b_out, u, pos, sc,
+               pk, pkn, amax_out};
+    if (next) {
+        MMPDE_REQUIRE(a_out && b_out && next->msg1_ld >= 260 && (next->msg1_ld & 3) == 0 &&
+                      al16(next->msg1_w));
+        a.w1n = next->msg1_w;
+        a.b1n = next->msg1_b;
+        a.ld_w1n = next->msg1_ld;
+    }
+    constexpr int RB = MMPDE_NODE_RB;
+    const dim3 grid((unsigned)ceil_div(n, 16 * RB));
+#define MMPDE_NODE(NX, SPLIT) \
+    hipLaunchKernelGGL((gnn_node_kernel<NX, SPLIT, RB>), grid, dim3(512), 0, st, a)
+    if (next && pk) MMPDE_NODE(true, true);
+    else if (next) MMPDE_NODE(true, false);
+    else if (pk) MMPDE_NODE(false, true);
+    else MMPDE_NODE(false, false);
+#undef MMPDE_NODE
+    MMPDE_RET_LAUNCH();
+    return MMPDE_OK;
+}

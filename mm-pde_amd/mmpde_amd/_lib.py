@@ -13,7 +13,7 @@ import os
 import torch
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libmmpde_hip.so")
-ABI_VERSION = 10200
+ABI_VERSION = 10300
 
 ACT_NONE, ACT_TANH, ACT_RELU = 0, 1, 2
 # message_net_2 edge GEMM arithmetic (include/mmpde_hip.h MMPDE_EDGE_GEMM_*)
@@ -60,7 +60,7 @@ _P3 = _P * 3
 class GnnExec(ctypes.Structure):
     """mmpde_gnn_exec: optional per-layer hipEvents + the edge-GEMM arithmetic."""
     _fields_ = [("edge_begin", ctypes.POINTER(_P)), ("edge_end", ctypes.POINTER(_P)),
-                ("edge_gemm", _I), ("packed", _P)]
+                ("edge_gemm", _I), ("packed", _P), ("node_end", ctypes.POINTER(_P))]
 
 
 class DmmGraphBranch(ctypes.Structure):

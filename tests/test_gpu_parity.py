@@ -351,3 +351,28 @@ def test_full_size_properties(dev):
     assert torch.equal(nbr[11 * N:12 * N] - 11 * N, ref)
     u = eng.rollout(u0, 1, 29)
     assert torch.isfinite(u).all()
+
+
+# ============================================================================ layer kernels: odd sizes
+@pytest.mark.parametrize("k", [1, 3, 4, 5, 8, 35])
+@pytest.mark.parametrize("mode", ["f32", "f16x3"])
+def test_gnn_forward_ragged_k(dev, k, mode):
+    """Degrees that leave partial rounds of neighbour slots (k % 4 != 0, k < 4)
+    and node counts that leave partial edge tiles / node tiles (3 x 37 rows),
+    in both arithmetic modes, against the oracle."""
+    from mmpde_amd.rollout import _Nodes
+    from mmpde_amd.synth import build_models
+
+    pde, model, _, _, _, _ = build_models("cy", moving_mesh=False, seed=3)
+    B, N = 3, 37
+    torch.manual_seed(k)
+    pts = torch.rand(B * N, 2)
+    pos = torch.cat((torch.full((B * N, 1), 0.7), pts), 1)
+    u = torch.randn(B * N, 1)
+    ei, nbr, _ = refcpu.knn_graph(pts, k, B)
+    opde = refcpu.PDEConst("cy", pde.grid_size, ori_grid=pde.ori_grid)
+    ref = refcpu.mp_pde_solver(_sds(m=model)["m"], opde, u, pos, ei)
+    model.to(dev)
+    model.edge_gemm = mode
+    out = model(_Nodes(u.to(dev), pos.to(dev), nbr.int().to(dev)))
+    _close(out, ref, 2e-4, 1e-7, f"gnn k={k} {mode}")

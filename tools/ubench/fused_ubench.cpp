@@ -1,10 +1,9 @@
-// Phase breakdown of gnn_layer_fused_kernel (profiling aid, not shipped):
-// times the prologue-only / edge-only / epilogue-only / full variants of the
-// fused layer kernel on a cylinder-sized synthetic layer (n = 16 x 2521 rows,
-// k = 35 random in-trajectory neighbours), both arithmetic modes.
-//   make -C tools/ubench && tools/ubench/fused_ubench
+// Timing of the layer kernels (profiling aid, not shipped): edge stage and
+// node stage variants on a cylinder-sized synthetic layer (n = B x 2521 rows,
+// k = 35 in-trajectory neighbours), both arithmetic modes.
+//   make -C tools/ubench && tools/ubench/fused_ubench [B] [random|local|self]
 #include "../../mm-pde_amd/csrc/gnn.hip"
-
+#include "../../mm-pde_amd/csrc/layer.hip"
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
@@ -47,15 +46,14 @@ __global__ __launch_bounds__(256, 2) void mfma_only_kernel(const float4 *seed, i
     out[blockIdx.x * 256 + threadIdx.x] = make_float4(acc0[0] + acc1[0], acc0[1], acc0[2], acc1[3]);
 }
 
-template <bool NEXT, bool SPLIT, int PH>
-static float time_variant(const FusedLayerArgs &f, int64_t n, int iters) {
-    const dim3 grid(ceil_div(n, FT));
-    for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((gnn_layer_fused_kernel<NEXT, SPLIT, PH>), grid, dim3(256), 0, 0, f);
+template <class F>
+static float time_it(F launch, int iters) {
+    for (int i = 0; i < 3; ++i) launch();
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
     hipEventRecord(a, 0);
-    for (int i = 0; i < iters; ++i) hipLaunchKernelGGL((gnn_layer_fused_kernel<NEXT, SPLIT, PH>), grid, dim3(256), 0, 0, f);
+    for (int i = 0; i < iters; ++i) launch();
     hipEventRecord(b, 0);
     hipEventSynchronize(b);
     float ms = 0;
@@ -111,36 +109,55 @@ int main(int argc, char **argv) {
         std::vector<uint32_t> hs(4 * 2 * kAmaxShards, 0x3f800000u);
         CK(hipMemcpy(amax, hs.data(), hs.size() * 4, hipMemcpyHostToDevice));
     }
-    FusedLayerArgs f{a, b, h, nbr, n, k, w2, b2, pack, pack + kLayerPack, u1, c1, 260, u2, c2,
-                     bnw, bnb, bnm, bnv, 1e-5f, ho, w1, b1, 260, ao, bo, u, pos, sc,
-                     amax, amax + 2 * kAmaxShards};
+    float *mean;
+    CK(hipMalloc(&mean, n * H * 4));
     const int it = 20;
+    const int64_t ntiles = (n + ET - 1) / ET;
+    int cus = device_cus();
+    const int grid_e = ntiles < cus ? (int)ntiles : cus;
+    uint64_t *stamps;
+    CK(hipMalloc(&stamps, 12 * 2 * 256 * 8));
+    CK(hipMemset(stamps, 0, 12 * 2 * 256 * 8));
+    EdgeArgs e32{a, b, nbr, n, k, (int)ntiles, w2, b2, nullptr, nullptr, mean, stamps};
+    EdgeArgs e16{a, b, nbr, n, k, (int)ntiles, w2, b2, pack, amax, mean, stamps};
+    NodeArgs nd{h, mean, n, u1, c1, 260, u2, c2, bnw, bnb, bnm, bnv, 1e-5f, ho, w1, b1, 260, ao, bo,
+                u, pos, sc, pack, pack + kLayerPack, amax + 2 * kAmaxShards};
     printf("n=%lld k=%d  (us per launch)\n", (long long)n, k);
-    printf("f16x3: prologue %.1f  edge %.1f  epilogue %.1f  full %.1f\n",
-           time_variant<true, true, 0>(f, n, it), time_variant<true, true, 1>(f, n, it),
-           time_variant<true, true, 2>(f, n, it), time_variant<true, true, 3>(f, n, it));
-    printf("f16x3 edge loop: no-produce %.1f  no-mfma %.1f\n", time_variant<true, true, 5>(f, n, it),
-           time_variant<true, true, 9>(f, n, it));
-    printf("f32  : prologue %.1f  edge %.1f  epilogue %.1f  full %.1f\n",
-           time_variant<true, false, 0>(f, n, it), time_variant<true, false, 1>(f, n, it),
-           time_variant<true, false, 2>(f, n, it), time_variant<true, false, 3>(f, n, it));
-    {   // same MFMA count as the F16X3 edge loop: 2521 blocks x 4 waves x 9 rounds x 96
+    auto edge = [&](auto kern, int nw, const EdgeArgs &ea) {
+        return time_it([&] { hipLaunchKernelGGL(kern, dim3(grid_e), dim3(64 * nw), 0, 0, ea); }, it);
+    };
+    printf("edge f16x3 NC1NP2 %.1f  prio %.1f | NC1NP1 %.1f | NC2NP2 %.1f | NC2NP1 %.1f | f32 NC1NP2 %.1f\n",
+           edge(gnn_edge_kernel<true, 3, 1, 2>, 12, e16), edge(gnn_edge_kernel<true, 11, 1, 2>, 12, e16),
+           edge(gnn_edge_kernel<true, 3, 1, 1>, 8, e16), edge(gnn_edge_kernel<true, 3, 2, 2>, 16, e16),
+           edge(gnn_edge_kernel<true, 3, 2, 1>, 12, e16), edge(gnn_edge_kernel<false, 3, 1, 2>, 12, e32));
+    printf("edge f16x3 NC1NP2 no-gather %.1f\n", edge(gnn_edge_kernel<true, 7, 1, 2>, 12, e16));
+    {   // per-round barrier arrival / release times of block 0 (waves 0..7, lane 0)
+        hipLaunchKernelGGL((gnn_edge_kernel<true, 1024 + 3, 1, 2>), dim3(grid_e), dim3(768), 0, 0, e16);
+        CK(hipDeviceSynchronize());
+        std::vector<uint64_t> st(12 * 2 * 256);
+        CK(hipMemcpy(st.data(), stamps, st.size() * 8, hipMemcpyDeviceToHost));
+        printf("round stamps (s_memtime, relative): it | arrive c0 c1 c2 c3 p0 p1 p2 p3 | release c0\n");
+        const uint64_t t0 = st[0];
+        for (int i = 0; i < 40; ++i) {
+            printf("%3d |", i);
+            for (int w : {0, 1, 2, 3, 4, 5, 8, 9}) printf(" %7lld", (long long)(st[2 * 256 * w + 2 * i] - t0));
+            printf(" | %7lld\n", (long long)(st[2 * i + 1] - t0));
+        }
+    }
+    printf("node f16x3 RB4 %.1f  RB2 %.1f  (last layer RB4 %.1f)  f32 RB4 %.1f\n",
+           time_it([&] { hipLaunchKernelGGL((gnn_node_kernel<true, true, 4>), dim3(ceil_div(n, 64)), dim3(512), 0, 0, nd); }, it),
+           time_it([&] { hipLaunchKernelGGL((gnn_node_kernel<true, true, 2>), dim3(ceil_div(n, 32)), dim3(512), 0, 0, nd); }, it),
+           time_it([&] { hipLaunchKernelGGL((gnn_node_kernel<false, true, 4>), dim3(ceil_div(n, 64)), dim3(512), 0, 0, nd); }, it),
+           time_it([&] { hipLaunchKernelGGL((gnn_node_kernel<true, false, 4>), dim3(ceil_div(n, 64)), dim3(512), 0, 0, nd); }, it));
+    {   // MFMA ceiling: the edge stage's MFMA count (16 x 16 x 32 f16), register operands
         float4 *seed, *out;
+        const int nb = (int)ntiles;
         CK(hipMalloc(&seed, 128 * 16));
         CK(hipMemset(seed, 0x3c, 128 * 16));
-        CK(hipMalloc(&out, (size_t)ceil_div(n, FT) * 256 * 16));
-        const int nb = ceil_div(n, FT), iters = 9 * 96 / 24;
-        for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(mfma_only_kernel, dim3(nb), dim3(256), 0, 0, seed, iters, out);
-        hipEvent_t a0, b0;
-        hipEventCreate(&a0);
-        hipEventCreate(&b0);
-        hipEventRecord(a0, 0);
-        for (int i = 0; i < it; ++i) hipLaunchKernelGGL(mfma_only_kernel, dim3(nb), dim3(256), 0, 0, seed, iters, out);
-        hipEventRecord(b0, 0);
-        hipEventSynchronize(b0);
-        float ms = 0;
-        hipEventElapsedTime(&ms, a0, b0);
-        printf("mfma-only ceiling (edge-loop MFMA count, register operands): %.1f us\n", 1e3f * ms / it);
+        CK(hipMalloc(&out, (size_t)nb * 256 * 16));
+        const int iters = 9 * 96 / 24;
+        printf("mfma-only ceiling (edge MFMA count, register operands, 2 waves/SIMD): %.1f us\n",
+               time_it([&] { hipLaunchKernelGGL(mfma_only_kernel, dim3(nb), dim3(256), 0, 0, seed, iters, out); }, it));
     }
     CK(hipGetLastError());
     return 0;
