@@ -458,19 +458,15 @@ extern "C" int mmpde_gnn_forward_ex(const float *u, const float *pos, int64_t n,
             pack = wpk;
         }
     }
-    rc = mmpde_gnn_embed(u, pos, n, sc, emb, wmean, hb[0], stream);  // wmean: scratch
-    if (rc) return rc;
     if (n_layers > 0) {
-        // layer 0's message_net_1 halves; later layers get theirs from the fused kernel
-        const mmpde_gnn_layer_params *p0 = &layers[0];
-        MMPDE_REQUIRE(p0->msg1_ld >= 260 && (p0->msg1_ld & 3) == 0 && aligned16(p0->msg1_w));
-        const int64_t ld = p0->msg1_ld;
-        GemmArgs g{n, hb[0], hb[0] + 64, H, p0->msg1_w, p0->msg1_w + 64, ld, 64};
-        EpiProj epi{wa, wb, p0->msg1_b, p0->msg1_w + 256, p0->msg1_w + 257,
-                    p0->msg1_w + 258, p0->msg1_w + 259, ld, u, pos, sc, pack ? amax : nullptr};
-        rc = launch_gemm<EpiProj, true>(g, 2, epi, st);
-        if (rc) return rc;
+        // embedding + layer 0's message_net_1 halves (later layers get theirs
+        // from the previous layer's node stage)
+        rc = launch_embed_stage(u, pos, n, sc, emb, &layers[0], pack, pack ? amax : nullptr, hb[0],
+                                wa, wb, st);
+    } else {
+        rc = mmpde_gnn_embed(u, pos, n, sc, emb, wmean, hb[0], stream);  // wmean: scratch
     }
+    if (rc) return rc;
     int cur = 0;
     for (int l = 0; l < n_layers; ++l) {
         hipEvent_t eb = exec && exec->edge_begin ? (hipEvent_t)exec->edge_begin[l] : nullptr;

@@ -518,6 +518,77 @@ __device__ __forceinline__ void gemm_tile(f32x4 *acc, const float4 *img, int KT,
     }
 }
 
+// Per-column constants of a message_net_1 node projection (weight row w1r of
+// this lane's column: node-term columns 256..259, bias, F16X3 unscale).
+struct W1C {
+    float du = 0.0f, dx = 0.0f, dy = 0.0f, t = 0.0f, b = 0.0f, isa = 1.0f, isb = 1.0f;
+    template <bool F16X3>
+    __device__ __forceinline__ void load(const float *w1r, const float *b1, const char *pk, int col) {
+        du = w1r[256];
+        dx = w1r[257];
+        dy = w1r[258];
+        t = w1r[259];
+        b = b1[col];
+        if (F16X3) {
+            const float *su = (const float *)(pk + kPkW1 + 131072);
+            isa = pow2_inv(su[col]);
+            isb = pow2_inv(su[128 + col]);
+        }
+    }
+};
+
+// message_net_1 node halves of the rows staged in img (K = 128, F16X3 row
+// scales rs): a = W1[:, :128] h + w.(u, x, y) + w_t t + b1 (column tile wave),
+// b = W1[:, 128:256] h - w.(u, x, y) (column tile 8 + wave); the epilogue of
+// gnn_2d.py:53-57's message_net_1 split (see the file header).  rowv: per-row
+// (t, x, y, u) planes of stride 16 RB.  bA: preloaded B operands of a.
+template <bool F16X3, int RB>
+__device__ __forceinline__ void proj_phase(const BOps<F16X3, F16X3 ? 4 : 8> &bA, const float4 *img,
+                                           const float *rs, const float *rowv, const W1C &w,
+                                           const char *pk, const float *w1r, int64_t row0,
+                                           int64_t n, float *a_out, float *b_out,
+                                           uint32_t *amax_out, int wave, int lane) {
+    constexpr int ROWS = 16 * RB, S1 = F16X3 ? 4 : 8;
+    const int col = 16 * wave + (lane & 15), g = lane >> 4;
+    f32x4 aA[RB], aB[RB];
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) aA[rb] = aB[rb] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+    gemm_tile<F16X3, RB, S1>(aA, img, 128, 0, bA, lane);
+    {
+        BOps<F16X3, S1> bB;
+        bB.load(pk + kPkW1, 4, 8 + wave, 0, w1r, 128, lane);
+        gemm_tile<F16X3, RB, S1>(aB, img, 128, 0, bB, lane);
+    }
+    float amx = 0.0f, bmx = 0.0f;
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int lr = 16 * rb + 4 * g + q;
+            const int64_t row = row0 + lr;
+            if (row < n) {
+                float za = aA[rb][q], zb = aB[rb][q];
+                if (F16X3) {
+                    const float ir = pow2_inv(rs[lr]);
+                    za = za * ir * w.isa;
+                    zb = zb * ir * w.isb;
+                }
+                const float node = w.du * rowv[3 * ROWS + lr] + w.dx * rowv[ROWS + lr] + w.dy * rowv[2 * ROWS + lr];
+                const float va = za + node + w.t * rowv[lr] + w.b;
+                const float vb = zb - node;
+                a_out[row * LH + col] = va;
+                b_out[row * LH + col] = vb;
+                amx = fmaxf(amx, fabsf(va));
+                bmx = fmaxf(bmx, fabsf(vb));
+            }
+        }
+    }
+    if (amax_out) {
+        amax_publish(amx, amax_out);
+        amax_publish(bmx, amax_out + kAmaxShards);
+    }
+}
+
 template <bool NEXT, bool F16X3, int RB>
 __global__ __launch_bounds__(512, 1) void gnn_node_kernel(NodeArgs p) {
     constexpr int ROWS = 16 * RB;
@@ -548,19 +619,8 @@ __global__ __launch_bounds__(512, 1) void gnn_node_kernel(NodeArgs p) {
     const float bn_w = p.bn_w[col], bn_b = p.bn_b[col];
     const float u2_is = F16X3 ? pow2_inv(((const float *)(p.pk + kPkU2 + 65536))[col]) : 1.0f;
     const float *w1r = NEXT ? p.w1n + (int64_t)col * p.ld_w1n : nullptr;
-    float w1_du = 0.0f, w1_dx = 0.0f, w1_dy = 0.0f, w1_t = 0.0f, w1_b = 0.0f, w1_isa = 1.0f, w1_isb = 1.0f;
-    if (NEXT) {
-        w1_du = w1r[256];
-        w1_dx = w1r[257];
-        w1_dy = w1r[258];
-        w1_t = w1r[259];
-        w1_b = p.b1n[col];
-        if (F16X3) {
-            const float *su = (const float *)(p.pkn + kPkW1 + 131072);
-            w1_isa = pow2_inv(su[col]);
-            w1_isb = pow2_inv(su[128 + col]);
-        }
-    }
+    W1C w1c;
+    if (NEXT) w1c.load<F16X3>(w1r, p.b1n, p.pkn, col);
     // weight operands of update_net_1 / _2 loaded first: their latency hides
     // behind the activation staging
     BOps<F16X3, S1> bH, bM, bU2;
@@ -623,45 +683,95 @@ __global__ __launch_bounds__(512, 1) void gnn_node_kernel(NodeArgs p) {
         __syncthreads();
         prep<F16X3, ROWS>(stage, NLD, 0, ROWS, false, img, 128, 0, rs[3]);
         __syncthreads();
-        // ---- next layer's message_net_1 node halves: a' (tile wave), b' (tile 8 + wave)
-        f32x4 aA[RB], aB[RB];
+        // ---- next layer's message_net_1 node halves
+        proj_phase<F16X3, RB>(bA, img, rs[3], &rowv[0][0], w1c, p.pkn, w1r, row0, p.n, p.a_out,
+                              p.b_out, p.amax_out, wave, lane);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Embedding + layer 0's message_net_1 halves in one launch (gnn_2d.py:99-106,
+// 122-131, then the first GNN layer's projections): per 64-row tile
+//   z  = relu(BN1(W0 [u, x/Lx, y/Ly, t/tmax] + b0))        (VALU, K = 4)
+//   h0 = BN4(W3 z + b3)                                     (exact fp32 MFMA)
+//   a0, b0 = layer 0's message_net_1 node halves of h0      (F16X3 or fp32)
+// ---------------------------------------------------------------------------
+struct EmbedArgs {
+    const float *u, *pos;
+    int64_t n;
+    mmpde_gnn_scales sc;
+    mmpde_gnn_embed_params e;
+    float *h_out;
+    const float *w1, *b1;  // layer 0 message_net_1.0 [128, ld_w1], bias
+    int64_t ld_w1;
+    float *a_out, *b_out;
+    const char *pk;        // F16X3: layer 0's packed images
+    uint32_t *amax_out;    // F16X3: layer 0's range slots
+};
+
+template <bool F16X3, int RB>
+__global__ __launch_bounds__(512, 1) void gnn_embed_kernel(EmbedArgs p) {
+    constexpr int ROWS = 16 * RB;
+    constexpr int S1 = F16X3 ? 4 : 8;
+    __shared__ float4 img[RB * 8 * 64];   // K = 128 operand image
+    __shared__ float stage[ROWS * NLD];   // fp32 z, then h0
+    __shared__ float rs[ROWS];            // h0 row scales
+    __shared__ float rowv[4][ROWS];       // per row: t / tmax, x / Lx, y / Ly, u
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int g = lane >> 4;
+    const int64_t row0 = (int64_t)blockIdx.x * ROWS;
+    const int col = 16 * wave + (lane & 15);
+    if (tid < ROWS) {
+        const int64_t row = min(row0 + tid, p.n - 1);
+        rowv[0][tid] = p.pos[row * 3 + 0] * p.sc.inv_tmax;
+        rowv[1][tid] = p.pos[row * 3 + 1] * p.sc.inv_lx;
+        rowv[2][tid] = p.pos[row * 3 + 2] * p.sc.inv_ly;
+        rowv[3][tid] = p.u[row];
+    }
+    const mmpde_gnn_embed_params &e = p.e;
+    BOps<false, 8> b3;  // embedding_mlp.3 weight row of this lane's column
+    b3.load(nullptr, 0, 0, 0, e.w3 + (int64_t)col * LH, 0, lane);
+    const float h_b = e.b3[col], h_rm = e.bn4_rm[col], h_rv = e.bn4_rv[col];
+    const float h_w = e.bn4_w[col], h_bb = e.bn4_b[col];
+    const float *w1r = p.w1 + (int64_t)col * p.ld_w1;
+    W1C w1c;
+    w1c.load<F16X3>(w1r, p.b1, p.pk, col);
+    // z: thread tid owns channel c = tid & 127 of rows (tid >> 7) + 4 i
+    const int c = tid & 127;
+    const float zw0 = e.w0[4 * c], zw1 = e.w0[4 * c + 1], zw2 = e.w0[4 * c + 2], zw3 = e.w0[4 * c + 3];
+    const float zb = e.b0[c], z_rm = e.bn1_rm[c], z_rv = e.bn1_rv[c], z_w = e.bn1_w[c], z_b = e.bn1_b[c];
+    __syncthreads();
+    for (int row = tid >> 7; row < ROWS; row += 4) {
+        const float v = zb + zw0 * rowv[3][row] + zw1 * rowv[1][row] + zw2 * rowv[2][row] + zw3 * rowv[0][row];
+        stage[row * NLD + c] = fmaxf(bn_eval(v, z_rm, z_rv, z_w, z_b, e.eps), 0.0f);
+    }
+    __syncthreads();
+    prep<false, ROWS>(stage, NLD, 0, ROWS, false, img, 128, 0, rs);
+    __syncthreads();
+    BOps<F16X3, S1> bA;
+    {
+        f32x4 acc[RB];
 #pragma unroll
-        for (int rb = 0; rb < RB; ++rb) aA[rb] = aB[rb] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
-        gemm_tile<F16X3, RB, S1>(aA, img, 128, 0, bA, lane);
-        {   // b' (column tile 8 + wave)
-            BOps<F16X3, S1> bB;
-            bB.load(p.pkn + kPkW1, 4, 8 + wave, 0, w1r, 128, lane);
-            gemm_tile<F16X3, RB, S1>(aB, img, 128, 0, bB, lane);
-        }
-        float amx = 0.0f, bmx = 0.0f;
+        for (int rb = 0; rb < RB; ++rb) acc[rb] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+        gemm_tile<false, RB, 8>(acc, img, 128, 0, b3, lane);
+        bA.load(p.pk + kPkW1, 4, wave, 0, w1r, 0, lane);
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int lr = 16 * rb + 4 * g + q;
                 const int64_t row = row0 + lr;
-                if (row < p.n) {
-                    float za = aA[rb][q], zb = aB[rb][q];
-                    if (F16X3) {
-                        const float ir = pow2_inv(rs[3][lr]);
-                        za = za * ir * w1_isa;
-                        zb = zb * ir * w1_isb;
-                    }
-                    const float node = w1_du * rowv[3][lr] + w1_dx * rowv[1][lr] + w1_dy * rowv[2][lr];
-                    const float va = za + node + w1_t * rowv[0][lr] + w1_b;
-                    const float vb = zb - node;
-                    p.a_out[row * LH + col] = va;
-                    p.b_out[row * LH + col] = vb;
-                    amx = fmaxf(amx, fabsf(va));
-                    bmx = fmaxf(bmx, fabsf(vb));
-                }
+                const float y = bn_eval(acc[rb][q] + h_b, h_rm, h_rv, h_w, h_bb, e.eps);
+                if (row < p.n) p.h_out[row * LH + col] = y;
+                stage[lr * NLD + col] = y;
             }
         }
-        if (p.amax_out) {
-            amax_publish(amx, p.amax_out);
-            amax_publish(bmx, p.amax_out + kAmaxShards);
-        }
     }
+    __syncthreads();
+    prep<F16X3, ROWS>(stage, NLD, 0, ROWS, false, img, 128, 0, rs);
+    __syncthreads();
+    proj_phase<F16X3, RB>(bA, img, rs, &rowv[0][0], w1c, p.pk, w1r, row0, p.n, p.a_out, p.b_out,
+                          p.amax_out, wave, lane);
 }
 
 inline bool al16(const void *q) { return ((uintptr_t)q & 15u) == 0; }
@@ -727,6 +837,24 @@ int launch_node_stage(const float *h, const float *mean, const float *u, const f
     else if (pk) MMPDE_NODE(false, true);
     else MMPDE_NODE(false, false);
 #undef MMPDE_NODE
+    MMPDE_RET_LAUNCH();
+    return MMPDE_OK;
+}
+
+int launch_embed_stage(const float *u, const float *pos, int64_t n, mmpde_gnn_scales sc,
+                       const mmpde_gnn_embed_params *e, const mmpde_gnn_layer_params *l0,
+                       const char *pk0, uint32_t *amax_out, float *h_out, float *a_out,
+                       float *b_out, hipStream_t st) {
+    MMPDE_REQUIRE(u && pos && e && l0 && h_out && a_out && b_out && n > 0);
+    MMPDE_REQUIRE(al16(e->w3) && al16(h_out) && al16(a_out) && al16(b_out));
+    MMPDE_REQUIRE(l0->msg1_ld >= 260 && (l0->msg1_ld & 3) == 0 && al16(l0->msg1_w));
+    MMPDE_REQUIRE(!pk0 || (al16(pk0) && amax_out));
+    EmbedArgs a{u, pos, n, sc, *e, h_out, l0->msg1_w, l0->msg1_b, l0->msg1_ld, a_out, b_out, pk0,
+                amax_out};
+    constexpr int RB = MMPDE_NODE_RB;
+    const dim3 grid((unsigned)ceil_div(n, 16 * RB));
+    if (pk0) hipLaunchKernelGGL((gnn_embed_kernel<true, RB>), grid, dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((gnn_embed_kernel<false, RB>), grid, dim3(512), 0, st, a);
     MMPDE_RET_LAUNCH();
     return MMPDE_OK;
 }

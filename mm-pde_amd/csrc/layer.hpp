@@ -19,3 +19,11 @@ int launch_node_stage(const float *h, const float *mean, const float *u, const f
                       const mmpde_gnn_layer_params *next, const char *pk, const char *pkn,
                       uint32_t *amax_out, float *h_out, float *a_out, float *b_out,
                       hipStream_t st);
+
+// Embedding (gnn_2d.py:99-106) + layer 0's message_net_1 node halves in one
+// launch: h_out = embedding_mlp(cat(u, x/Lx, y/Ly, t/tmax)), a_out / b_out as
+// launch_node_stage's.  F16X3 projection when pk0 (layer 0's images) != nullptr.
+int launch_embed_stage(const float *u, const float *pos, int64_t n, mmpde_gnn_scales sc,
+                       const mmpde_gnn_embed_params *e, const mmpde_gnn_layer_params *l0,
+                       const char *pk0, uint32_t *amax_out, float *h_out, float *a_out,
+                       float *b_out, hipStream_t st);
