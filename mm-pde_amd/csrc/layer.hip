@@ -413,6 +413,10 @@ struct NodeArgs {
 };
 
 constexpr int NLD = 132;  // fp32 staging row stride (floats)
+#ifndef MMPDE_NODE_WPE
+#define MMPDE_NODE_WPE 4
+#endif
+constexpr int NODE_WPE = MMPDE_NODE_WPE;  // node / embed launch bounds: waves per SIMD
 
 // Operand images in LDS, per 16-row block rb and K step s (1 KB units of 64
 // lanes x 16 B): F16X3 [rb][s (32-wide)][hi|lo] with lane (r, g) holding
@@ -590,7 +594,7 @@ __device__ __forceinline__ void proj_phase(const BOps<F16X3, F16X3 ? 4 : 8> &bA,
 }
 
 template <bool NEXT, bool F16X3, int RB>
-__global__ __launch_bounds__(512, 1) void gnn_node_kernel(NodeArgs p) {
+__global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs p) {
     constexpr int ROWS = 16 * RB;
     __shared__ float4 img[RB * 16 * 64];        // operand image, K = 256 (h | mean), then 128
     __shared__ float stage[ROWS * NLD];         // fp32 v, then h'
@@ -623,10 +627,15 @@ __global__ __launch_bounds__(512, 1) void gnn_node_kernel(NodeArgs p) {
     if (NEXT) w1c.load<F16X3>(w1r, p.b1n, p.pkn, col);
     // weight operands of update_net_1 / _2 loaded first: their latency hides
     // behind the activation staging
+    // (RB >= 4: all three up front; smaller tiles run several workgroups per
+    // CU, whose overlap hides the latency, so they load just before use)
+    constexpr bool PRE = RB >= 4;
     BOps<F16X3, S1> bH, bM, bU2;
     bH.load(p.pk + kPkU1, 8, wave, 0, wu1, 0, lane);
-    bM.load(p.pk + kPkU1, 8, wave, S1, wu1, 128, lane);
-    bU2.load(p.pk + kPkU2, 4, wave, 0, wu2, 0, lane);
+    if (PRE) {
+        bM.load(p.pk + kPkU1, 8, wave, S1, wu1, 128, lane);
+        bU2.load(p.pk + kPkU2, 4, wave, 0, wu2, 0, lane);
+    }
 
     // ---- [h | mean] -> image (K = 256)
     prep<F16X3, ROWS>(p.h, LH, row0, p.n, true, img, 256, 0, rs[0], hres);
@@ -639,6 +648,7 @@ __global__ __launch_bounds__(512, 1) void gnn_node_kernel(NodeArgs p) {
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) aH[rb] = aM[rb] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
         gemm_tile<F16X3, RB, S1>(aH, img, 256, 0, bH, lane);
+        if (!PRE) bM.load(p.pk + kPkU1, 8, wave, S1, wu1, 128, lane);
         gemm_tile<F16X3, RB, S1>(F16X3 ? aM : aH, img, 256, S1, bM, lane);
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) {
@@ -661,6 +671,7 @@ __global__ __launch_bounds__(512, 1) void gnn_node_kernel(NodeArgs p) {
         f32x4 acc[RB];
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) acc[rb] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+        if (!PRE) bU2.load(p.pk + kPkU2, 4, wave, 0, wu2, 0, lane);
         gemm_tile<F16X3, RB, S1>(acc, img, 128, 0, bU2, lane);
         // next layer's message_net_1 operands of a' (column tile wave)
         if (NEXT) bA.load(p.pkn + kPkW1, 4, wave, 0, w1r, 0, lane);
@@ -710,7 +721,7 @@ struct EmbedArgs {
 };
 
 template <bool F16X3, int RB>
-__global__ __launch_bounds__(512, 1) void gnn_embed_kernel(EmbedArgs p) {
+__global__ __launch_bounds__(512, NODE_WPE) void gnn_embed_kernel(EmbedArgs p) {
     constexpr int ROWS = 16 * RB;
     constexpr int S1 = F16X3 ? 4 : 8;
     __shared__ float4 img[RB * 8 * 64];   // K = 128 operand image
@@ -788,7 +799,7 @@ int device_cus() {
 
 // Node stage rows per workgroup (16 * RB)
 #ifndef MMPDE_NODE_RB
-#define MMPDE_NODE_RB 4
+#define MMPDE_NODE_RB 2
 #endif
 
 int launch_edge_stage(const float *a, const float *b, const int32_t *nbr, int64_t n, int k,
