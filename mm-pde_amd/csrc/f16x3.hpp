@@ -122,6 +122,40 @@ __device__ __forceinline__ void split8_rn(const float4 &a, const float4 &b, half
     lo = *(const half8 *)&l;
 }
 
+// relu + split of 8 consecutive-k values in 16 instructions, for inputs
+// scaled so that |x| < 2^11: hi = max(RTZ_f16(x), 0) (v_cvt_pkrtz + v_pk_max_f16),
+// lo = clamp01(RN_f16(x - hi_rtz)) by v_fma_mix ... clamp.  With round-toward-
+// zero hi, x - hi has the sign of x and |x - hi| < ulp(hi) <= 1, so the [0, 1]
+// clamp is exactly the relu of the low part: (hi, lo) is the split of
+// relu(x) (x = hi + lo to 2^-22 relative, like split8_rn).
+__device__ __forceinline__ void split8_relu_rtz(const float4 &a, const float4 &b, half8 &hi,
+                                                half8 &lo) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 h, l;
+    asm("v_cvt_pkrtz_f16_f32 %0, %8, %9\n\t"
+        "v_cvt_pkrtz_f16_f32 %1, %10, %11\n\t"
+        "v_cvt_pkrtz_f16_f32 %2, %12, %13\n\t"
+        "v_cvt_pkrtz_f16_f32 %3, %14, %15\n\t"
+        "v_fma_mixlo_f16 %4, %8, 1.0, -%0 op_sel_hi:[0,0,1] clamp\n\t"
+        "v_fma_mixhi_f16 %4, %9, 1.0, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1] clamp\n\t"
+        "v_fma_mixlo_f16 %5, %10, 1.0, -%1 op_sel_hi:[0,0,1] clamp\n\t"
+        "v_fma_mixhi_f16 %5, %11, 1.0, -%1 op_sel:[0,0,1] op_sel_hi:[0,0,1] clamp\n\t"
+        "v_fma_mixlo_f16 %6, %12, 1.0, -%2 op_sel_hi:[0,0,1] clamp\n\t"
+        "v_fma_mixhi_f16 %6, %13, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1] clamp\n\t"
+        "v_fma_mixlo_f16 %7, %14, 1.0, -%3 op_sel_hi:[0,0,1] clamp\n\t"
+        "v_fma_mixhi_f16 %7, %15, 1.0, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1] clamp\n\t"
+        "v_pk_max_f16 %0, %0, 0\n\t"
+        "v_pk_max_f16 %1, %1, 0\n\t"
+        "v_pk_max_f16 %2, %2, 0\n\t"
+        "v_pk_max_f16 %3, %3, 0\n\t"
+        "s_nop 1"
+        : "=&v"(h.x), "=&v"(h.y), "=&v"(h.z), "=&v"(h.w), "=&v"(l.x), "=&v"(l.y), "=&v"(l.z),
+          "=&v"(l.w)
+        : "v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w));
+    hi = *(const half8 *)&h;
+    lo = *(const half8 *)&l;
+}
+
 __device__ __forceinline__ float absmax4(float m, const float4 &v) {
     return fmaxf(fmaxf(fmaxf(m, fabsf(v.x)), fmaxf(fabsf(v.y), fabsf(v.z))), fabsf(v.w));
 }

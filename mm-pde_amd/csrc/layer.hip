@@ -132,8 +132,9 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
     const int NIT = NR + EPF;
     const int NIT2 = (NIT + 1) & ~1;  // even: the producer's 2x-unrolled body has no tail test
     const int64_t nmax = p.n - 1;
-    float sc = 1.0f;  // F16X3: m = relu(a + b) <= max|a| + max|b|, so m * sc < 2^14
-    if (F16X3) sc = split_scale(amax_read(p.amax_in) + amax_read(p.amax_in + kAmaxShards));
+    // F16X3: |a + b| <= max|a| + max|b|, scaled below 2^11 (split8_relu_rtz)
+    float sc = 1.0f;
+    if (F16X3) sc = 0.125f * split_scale(amax_read(p.amax_in) + amax_read(p.amax_in + kAmaxShards));
     auto tile_row = [&](int j, int row) { return min((int64_t)(first + j * stride) * ET + row, nmax); };
 
     // a tiles (scaled by sc for F16X3): the consumer waves stage tile j + 1 while
@@ -219,13 +220,13 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
                     const float4 &a0 = acur[2 * h2], &a1 = acur[2 * h2 + 1];
                     const float4 &b0 = bv[2 * h2], &b1 = bv[2 * h2 + 1];
                     float4 m0, m1;
-                    if (F16X3) {
-                        m0 = make_float4(fmaxf(fmaf(b0.x, sc, a0.x), 0.0f), fmaxf(fmaf(b0.y, sc, a0.y), 0.0f),
-                                         fmaxf(fmaf(b0.z, sc, a0.z), 0.0f), fmaxf(fmaf(b0.w, sc, a0.w), 0.0f));
-                        m1 = make_float4(fmaxf(fmaf(b1.x, sc, a1.x), 0.0f), fmaxf(fmaf(b1.y, sc, a1.y), 0.0f),
-                                         fmaxf(fmaf(b1.z, sc, a1.z), 0.0f), fmaxf(fmaf(b1.w, sc, a1.w), 0.0f));
+                    if (F16X3) {  // relu folded into the split (split8_relu_rtz)
+                        m0 = make_float4(fmaf(b0.x, sc, a0.x), fmaf(b0.y, sc, a0.y), fmaf(b0.z, sc, a0.z),
+                                         fmaf(b0.w, sc, a0.w));
+                        m1 = make_float4(fmaf(b1.x, sc, a1.x), fmaf(b1.y, sc, a1.y), fmaf(b1.z, sc, a1.z),
+                                         fmaf(b1.w, sc, a1.w));
                         half8 hi, lo;
-                        split8_rn(m0, m1, hi, lo);
+                        split8_relu_rtz(m0, m1, hi, lo);
                         dst[(2 * h2 + 0) * 64] = *(const float4 *)&hi;
                         dst[(2 * h2 + 1) * 64] = *(const float4 *)&lo;
                     } else {
@@ -258,7 +259,8 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
         // this wave's output column tiles CT wave + cc (cc < CT)
         float4 wf[CT][8];
         half8 wh[CT][4], wl[CT][4];
-        float bias[CT], inv[CT];  // bias: added in the relu-sum (keeps the accumulator zero-initialised)
+        f32x4 bias[CT];  // accumulator initial value (message_net_2 bias, scaled)
+        float inv[CT];
 #pragma unroll
         for (int cc = 0; cc < CT; ++cc) {
             const int col = 16 * (CT * wave + cc) + r;
@@ -278,7 +280,7 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
                 for (int j = 0; j < 8; ++j) wf[cc][j] = *(const float4 *)(p.w2 + col * LH + 16 * j + 4 * g);
                 inv[cc] = 1.0f;
             }
-            bias[cc] = bb;
+            bias[cc] = (f32x4){bb, bb, bb, bb};
         }
         f32x4 S[CT];
 #pragma unroll
@@ -292,7 +294,6 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
         // completed by the previous barrier), and each slot's relu-sum update
         // is issued after the next slot's first MFMAs.  Slots past k (last
         // round) are multiplied but not summed.
-        const f32x4 zero4 = {0.0f, 0.0f, 0.0f, 0.0f};
         // A operands stream through two half-slot register buffers (pieces
         // 0-3 / 4-7 of a slot lane)
         auto rd_half = [&](const float4 *src, int hf, float4 *x) {
@@ -306,7 +307,7 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
                     const int s4 = 2 * hf + s;
                     const half8 hi = *(const half8 *)&x[2 * s], lo = *(const half8 *)&x[2 * s + 1];
 #pragma unroll
-                    for (int cc = 0; cc < CT; ++cc) acc[cc] = mfma_f16(hi, wh[cc][s4], s4 == 0 ? zero4 : acc[cc]);
+                    for (int cc = 0; cc < CT; ++cc) acc[cc] = mfma_f16(hi, wh[cc][s4], s4 == 0 ? bias[cc] : acc[cc]);
 #pragma unroll
                     for (int cc = 0; cc < CT; ++cc) acc[cc] = mfma_f16(hi, wl[cc][s4], acc[cc]);
 #pragma unroll
@@ -320,19 +321,19 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
                     for (int t = 0; t < 4; ++t) {
 #pragma unroll
                         for (int cc = 0; cc < CT; ++cc)
-                            acc[cc] = mfma16(f4c(x[j], t), f4c(wf[cc][jj], t), jj == 0 && t == 0 ? zero4 : acc[cc]);
+                            acc[cc] = mfma16(f4c(x[j], t), f4c(wf[cc][jj], t), jj == 0 && t == 0 ? bias[cc] : acc[cc]);
                     }
                 }
             }
         };
+        // relu-sum of one slot; `valid` is wave-uniform (slots past k exist
+        // only in a tile's last round), so it is a branch, not a select
         auto sum_into = [&](const f32x4 *acc, bool valid) {
+            if (!valid) return;
 #pragma unroll
             for (int cc = 0; cc < CT; ++cc) {
 #pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    const float v = fmaf(fmaxf(acc[cc][t] + bias[cc], 0.0f), inv[cc], S[cc][t]);
-                    S[cc][t] = valid ? v : S[cc][t];
-                }
+                for (int t = 0; t < 4; ++t) S[cc][t] = fmaf(fmaxf(acc[cc][t], 0.0f), inv[cc], S[cc][t]);
             }
         };
         float4 xa[4], xb[4], an[2 / NC];
