@@ -28,8 +28,7 @@ def load(d, counter):
     return vals
 
 
-def main():
-    d, name = sys.argv[1], sys.argv[2]
+def summarise(d):
     fetch, write = load(d, "FETCH_SIZE"), load(d, "WRITE_SIZE")
     out = {}
     for k in sorted(set(fetch) | set(write)):
@@ -42,11 +41,32 @@ def main():
             rec["hbm_bytes_per_launch"] = (2.0 * fk + wk) * 1024.0
             rec["hbm_bytes_per_launch_uncorrected"] = (fk + wk) * 1024.0
         out[k] = rec
-    path = os.path.join(d, name + ".json")
-    with open(path, "w") as fh:
-        json.dump(out, fh, indent=1)
-    for k, v in out.items():
-        print(k[:90], json.dumps(v))
+    return out
+
+
+def main():
+    """pmc_summary.py OUT_NAME WORKLOAD NODES MODE=DIR [MODE=DIR ...]: one
+    record per arithmetic mode (bench.py --edge-gemm), as bench.py reads it for
+    roofline.traffic: {"workload", "nodes", "modes": {mode: {"hbm_bytes_per_launch",
+    "per_kernel"}}}.  Kernels of several template variants are averaged by
+    dispatch count."""
+    name, workload, nodes = sys.argv[1], sys.argv[2], int(sys.argv[3])
+    rec = {"workload": workload, "nodes": nodes,
+           "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), "
+                     "tools/gpu_pmc.sh; per-dispatch means; hbm = 2*FETCH_SIZE + WRITE_SIZE "
+                     "(gfx950 FETCH_SIZE half-count correction, MI355X_MICROARCH.md HBM)",
+           "modes": {}}
+    for arg in sys.argv[4:]:
+        mode, d = arg.split("=", 1)
+        per = summarise(d)
+        tot = sum(v["hbm_bytes_per_launch"] * v["dispatches"] for v in per.values()
+                  if "hbm_bytes_per_launch" in v)
+        cnt = sum(v["dispatches"] for v in per.values() if "hbm_bytes_per_launch" in v)
+        rec["modes"][mode] = {"hbm_bytes_per_launch": tot / max(cnt, 1), "per_kernel": per}
+    os.makedirs("gpurun_out/pmc", exist_ok=True)
+    with open(os.path.join("gpurun_out/pmc", name + ".json"), "w") as fh:
+        json.dump(rec, fh, indent=1)
+    print(json.dumps({m: v["hbm_bytes_per_launch"] for m, v in rec["modes"].items()}))
 
 
 if __name__ == "__main__":
