@@ -88,8 +88,10 @@ __global__ __launch_bounds__(256) void dmm_gnn_kernel(const float4 *__restrict__
         sC2[threadIdx.x] = c2[threadIdx.x];
     }
     __syncthreads();
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n_tot) return;
+    // four lanes per node: lane `sub` of the quad takes edges sub, sub + 4, ...
+    const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 2;
+    const int sub = threadIdx.x & 3;
+    if (i >= n_tot) return;  // whole quads leave together
     const int64_t b = i / n_per;
     const int64_t p = i - b * n_per;
     const float4 hi4 = h[i];
@@ -98,7 +100,7 @@ __global__ __launch_bounds__(256) void dmm_gnn_kernel(const float4 *__restrict__
     const float2 gi = grid[p];
     float sum[4] = {0.f, 0.f, 0.f, 0.f};
     const int32_t *nr = nbr + p * k;
-    for (int e = 0; e < k; ++e) {
+    for (int e = sub; e < k; e += 4) {
         const int64_t jl = min((uint32_t)nr[e], (uint32_t)(n_per - 1));
         const int64_t j = b * n_per + jl;
         const float4 hj4 = h[j];
@@ -121,6 +123,11 @@ __global__ __launch_bounds__(256) void dmm_gnn_kernel(const float4 *__restrict__
             sum[o] += tanhf(v);
         }
     }
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+        sum[o] += __shfl_xor(sum[o], 1, 64);
+        sum[o] += __shfl_xor(sum[o], 2, 64);
+    }
     float cat[8];
 #pragma unroll
     for (int o = 0; o < 4; ++o) {
@@ -142,7 +149,7 @@ __global__ __launch_bounds__(256) void dmm_gnn_kernel(const float4 *__restrict__
         for (int t = 0; t < 4; ++t) v += sV2[o * 4 + t] * up1[t];
         res[o] = bn_eval(hi[o] + tanhf(v), bnrm[o], bnrv[o], bnw[o], bnb[o], eps);
     }
-    h_out[i] = make_float4(res[0], res[1], res[2], res[3]);
+    if (sub == 0) h_out[i] = make_float4(res[0], res[1], res[2], res[3]);
 }
 
 // decoding_mlp DenseNet([4, 128, 1]) (dmm_model.py:173,209): d = W1 tanh(W0 h + b0) + b1
@@ -160,16 +167,20 @@ __global__ __launch_bounds__(256) void dmm_decode_kernel(const float4 *__restric
         sW1[threadIdx.x] = w1[threadIdx.x];
     }
     __syncthreads();
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n_tot) return;
+    // four lanes per node, lane `sub` of the quad takes hidden units sub, sub + 4, ...
+    const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 2;
+    const int sub = threadIdx.x & 3;
+    if (i >= n_tot) return;  // whole quads leave together
     const float4 hv = h[i];
     float acc = 0.0f;
-    for (int j = 0; j < 128; ++j) {
+    for (int j = sub; j < 128; j += 4) {
         const float z = tanhf(sB0[j] + sW0[4 * j] * hv.x + sW0[4 * j + 1] * hv.y +
                               sW0[4 * j + 2] * hv.z + sW0[4 * j + 3] * hv.w);
         acc += sW1[j] * z;
     }
-    out[i] = acc + b1[0];
+    acc += __shfl_xor(acc, 1, 64);
+    acc += __shfl_xor(acc, 2, 64);
+    if (sub == 0) out[i] = acc + b1[0];
 }
 
 // ---------------------------------------------------------------------------
@@ -235,8 +246,8 @@ __global__ __launch_bounds__(256) void jac_kernel(const float *__restrict__ s, i
     }
 }
 
-// mesh[b*N + n] = xi[n] + sum_k w_o[k] (1 - tanh^2(P[b,k] + Q[n,k])) J[n,k]; one wave
-// per grid point, looping over trajectories.
+// mesh[b*N + n] = xi[n] + sum_k w_o[k] (1 - tanh^2(P[b,k] + Q[n,k])) J[n,k]; one
+// workgroup per grid point, wave w taking trajectories w, w + 4, ...
 __global__ __launch_bounds__(256) void mesh_vjp_kernel(const float *__restrict__ P,
                                                        const float *__restrict__ Q,
                                                        const float2 *__restrict__ jac,
@@ -246,12 +257,11 @@ __global__ __launch_bounds__(256) void mesh_vjp_kernel(const float *__restrict__
                                                        int hidden, float2 *__restrict__ mesh) {
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
-    const int64_t nidx = (int64_t)blockIdx.x * 4 + wave;
-    if (nidx >= n_per) return;
+    const int64_t nidx = blockIdx.x;
     const float *q = Q + nidx * hidden;
     const float2 *jr = jac + nidx * hidden;
     const float2 x = xi[nidx];
-    for (int64_t b = 0; b < batches; ++b) {
+    for (int64_t b = wave; b < batches; b += 4) {
         const float *pb = P + b * hidden;
         float gx = 0.0f, gy = 0.0f;
         for (int kk = lane; kk < hidden; kk += 64) {
@@ -327,7 +337,7 @@ int dmm_head(const float *branch, const float *xi, int64_t batches, int64_t n_pe
     hipLaunchKernelGGL(jac_kernel, dim3((unsigned)n_per), dim3(256), 0, st, w.s, th, w.gt, Lp,
                        hd->t0_w, w.jac);
     MMPDE_RET_LAUNCH();
-    hipLaunchKernelGGL(mesh_vjp_kernel, dim3(ceil_div(n_per, 4)), dim3(256), 0, st, w.p, w.q,
+    hipLaunchKernelGGL(mesh_vjp_kernel, dim3((unsigned)n_per), dim3(256), 0, st, w.p, w.q,
                        w.jac, hd->o1_w, (const float2 *)xi, batches, n_per, Lp,
                        (float2 *)mesh_out);
     MMPDE_RET_LAUNCH();
@@ -365,12 +375,12 @@ extern "C" int mmpde_dmm_mesh_graph(const float *u, const float *grid, int64_t b
     float *om2 = om1 + batches * 512;
     float *branch = om2 + batches * 256;
     float *head_ws = branch + ((batches * hd->latent + 3) & ~int64_t(3));
-    const dim3 g1(ceil_div(nt, 256));
+    const dim3 g1(ceil_div(nt, 256)), g4(ceil_div(4 * nt, 256));  // g4: four lanes per node
     hipLaunchKernelGGL(dmm_embed_kernel, g1, dim3(256), 0, st, u, (const float2 *)grid, nt, n_per,
                        *br, h0);
     MMPDE_RET_LAUNCH();
     for (int l = 0; l < br->n_gnn_layers; ++l) {
-        hipLaunchKernelGGL(dmm_gnn_kernel, g1, dim3(256), 0, st, h0, u, (const float2 *)grid,
+        hipLaunchKernelGGL(dmm_gnn_kernel, g4, dim3(256), 0, st, h0, u, (const float2 *)grid,
                            grid_nbr, k, nt, n_per, br->g_msg1_w[l], br->g_msg1_b[l],
                            br->g_msg2_w[l], br->g_msg2_b[l], br->g_upd1_w[l], br->g_upd1_b[l],
                            br->g_upd2_w[l], br->g_upd2_b[l], br->g_bn_w[l], br->g_bn_b[l],
@@ -380,7 +390,7 @@ extern "C" int mmpde_dmm_mesh_graph(const float *u, const float *grid, int64_t b
         h0 = h1;
         h1 = t;
     }
-    hipLaunchKernelGGL(dmm_decode_kernel, g1, dim3(256), 0, st, h0, nt, br->dec0_w, br->dec0_b,
+    hipLaunchKernelGGL(dmm_decode_kernel, g4, dim3(256), 0, st, h0, nt, br->dec0_w, br->dec0_b,
                        br->dec1_w, br->dec1_b, dec);
     MMPDE_RET_LAUNCH();
     // output_mlp: Linear(N,512) tanh Linear(512,256) tanh Linear(256,L) on [B, N]
