@@ -4,13 +4,15 @@
 // mesh/dmm_model.py:228) and sklearn NearestNeighbors.kneighbors
 // (data_creator_2d.py:66-78).  One wave per query; the trajectory's point set
 // (<= 4096 points, <= 32 KB) is staged once per workgroup in LDS; every lane
-// keeps CPL candidate keys in registers.  Selection: U = the kk-th smallest of
-// the 64 per-lane minima (radix select over one value per lane: ballot +
-// popcount), which bounds the kk-th smallest key from above; the candidates
-// with key <= U (a few dozen on a mesh) are compacted into a per-wave LDS list
-// and ranked exhaustively by (key, index).  Point sets where that list would
-// overflow fall back to a full bitwise radix select over all keys with ties at
-// the threshold taken in index order.  Either way the result is exactly the
+// keeps CPL fp32 squared distances in registers.  Selection: U = the kk-th
+// smallest of the 64 per-lane minima (a 64-wide bitonic sort across the wave)
+// bounds the kk-th smallest key from above; the points with key <= U (a few
+// dozen on a mesh; for the fp64 query key, fp32 key <= U plus a proven
+// rounding margin) are compacted into a per-wave LDS list, their exact keys
+// formed, and sorted by (key, index) with a 128-wide two-per-lane bitonic
+// network.  Longer lists are ranked exhaustively; lists past kCap fall back to
+// a full bitwise radix select over all exact keys with ties at the threshold
+// taken in index order.  Every way the result is exactly the
 // (distance, index)-ordered list of the reference's insertion sort,
 // independent of scheduling.
 //
@@ -28,6 +30,15 @@ namespace {
 constexpr int kQueriesPerBlock = 16;  // 4 per wave
 constexpr int kCap = 512;             // LDS list of candidates with key <= U, per wave
 
+// fp32 squared distance as raw bits: the graph key, and the query's filter key.
+__device__ __forceinline__ uint32_t key_f32(float2 p, float2 q) {
+#pragma clang fp contract(off)
+    float dx = p.x - q.x;
+    float dy = p.y - q.y;
+    float a = dx * dx;
+    return __float_as_uint(fmaf(dy, dy, a));
+}
+
 template <bool QUERY>
 struct KeyTraits;
 
@@ -35,13 +46,9 @@ template <>
 struct KeyTraits<false> {
     typedef uint32_t key_t;
     static constexpr int kTopBit = 30;  // valid keys are < 2^31
-    __device__ static key_t key(float2 p, float2 q) {
-#pragma clang fp contract(off)
-        float dx = p.x - q.x;
-        float dy = p.y - q.y;
-        float a = dx * dx;
-        return __float_as_uint(fmaf(dy, dy, a));
-    }
+    __device__ static key_t key(float2 p, float2 q) { return key_f32(p, q); }
+    // the filter key is the key itself
+    __device__ static uint32_t filter_threshold(uint32_t u) { return u; }
 };
 
 template <>
@@ -56,11 +63,93 @@ struct KeyTraits<true> {
         double c = dy * dy;
         return (key_t)__double_as_longlong(a + c);
     }
+    // Candidates are filtered on the fp32 key f, whose relative error against
+    // the fp64 key is <= 2^-22 (<= 4 ulp: two rounded differences, two
+    // rounded products / one fma); an absolute 2^-126 covers denormal
+    // flushing.  If u is the kk-th smallest fp32 lane minimum, at least kk
+    // points have fp64 key <= u (1 + 2^-22) + 2^-126, hence so does every
+    // point of the answer, whose fp32 key is then <= u + ~9 ulp.  A 64-ulp
+    // margin over max(u, min normal) keeps every answer point a candidate.
+    __device__ static uint32_t filter_threshold(uint32_t u) {
+        return u >= 0x7f000000u ? 0xfffffffeu : (u < 0x00800000u ? 0x00800000u : u) + 64u;
+    }
 };
 
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
+}
+
+template <typename K>
+__device__ __forceinline__ K shfl_xor_key(K v, int m) {
+    if constexpr (sizeof(K) == 8) {
+        const uint32_t lo = __shfl_xor((uint32_t)v, m, 64);
+        const uint32_t hi = __shfl_xor((uint32_t)(v >> 32), m, 64);
+        return ((K)hi << 32) | lo;
+    } else {
+        return __shfl_xor(v, m, 64);
+    }
+}
+
+// Bitonic sort of one key per lane across the wave, ascending in lane order.
+template <typename K>
+__device__ __forceinline__ K wave_sort64(K v, int lane) {
+#pragma unroll
+    for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+        for (int j = size >> 1; j > 0; j >>= 1) {
+            const K o = shfl_xor_key(v, j);
+            const bool keep_min = ((lane & j) == 0) == ((lane & size) == 0);
+            v = keep_min ? (o < v ? o : v) : (o < v ? v : o);
+        }
+    }
+    return v;
+}
+
+__device__ __forceinline__ bool ki_less(uint32_t ka, int ia, uint32_t kb, int ib) {
+    // 31-bit keys and 12-bit indices: one 64-bit compare
+    return (((uint64_t)ka << 32) | (uint32_t)ia) < (((uint64_t)kb << 32) | (uint32_t)ib);
+}
+__device__ __forceinline__ bool ki_less(uint64_t ka, int ia, uint64_t kb, int ib) {
+    return ka < kb || (ka == kb && ia < ib);
+}
+
+// One compare-exchange step of the 128-wide network on register r of this
+// lane against lane ^ j (same register), keeping the min iff keep_min.
+template <typename K>
+__device__ __forceinline__ void cx_lane(K &k, int &i, int j, bool keep_min) {
+    const K ok = shfl_xor_key(k, j);
+    const int oi = __shfl_xor(i, j, 64);
+    const bool take = ki_less(ok, oi, k, i) == keep_min;
+    k = take ? ok : k;
+    i = take ? oi : i;
+}
+
+// Bitonic sort of 128 (key, index) pairs ordered lexicographically (the
+// reference's tie order), two per lane: element p lives in lane p & 63,
+// register p >> 6.  Ascending in p.
+template <typename K>
+__device__ __forceinline__ void wave_sort128(K &k0, int &i0, K &k1, int &i1, int lane) {
+#pragma unroll
+    for (int size = 2; size <= 128; size <<= 1) {
+#pragma unroll
+        for (int j = size >> 1; j > 0; j >>= 1) {
+            if (j == 64) {  // size == 128: partners are the lane's own two registers
+                const bool sw = ki_less(k1, i1, k0, i0);
+                const K tk = k0;
+                const int ti = i0;
+                k0 = sw ? k1 : k0;
+                i0 = sw ? i1 : i0;
+                k1 = sw ? tk : k1;
+                i1 = sw ? ti : i1;
+            } else {
+                // element p = lane (+64): ascending block iff (p & size) == 0
+                const bool lower = (lane & j) == 0;
+                cx_lane(k0, i0, j, lower == ((lane & size) == 0));
+                cx_lane(k1, i1, j, lower == (((lane + 64) & size) == 0));
+            }
+        }
+    }
 }
 
 template <int CPL, bool QUERY>
@@ -88,43 +177,54 @@ __global__ __launch_bounds__(256) void knn_kernel(const float2 *__restrict__ pts
 
     for (int qi = blockIdx.x * kQueriesPerBlock + wave; qi < q_end; qi += 4) {
         const float2 q = QUERY ? qry[(int64_t)b * n_q + qi] : sP[qi];
-        key_t key[CPL];
-        key_t lmin = ~key_t(0);
+        uint32_t fkey[CPL];
+        uint32_t lmin = ~0u;
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
             const int j = lane + 64 * c;
-            key[c] = (j < n_src) ? KT::key(sP[j], q) : ~key_t(0);
-            lmin = key[c] < lmin ? key[c] : lmin;
+            fkey[c] = (j < n_src) ? key_f32(sP[j], q) : ~0u;
+            lmin = fkey[c] < lmin ? fkey[c] : lmin;
         }
-        // U = kk-th smallest of the 64 lane minima (radix select over one value
-        // per lane).  At least kk candidates have key <= U (one per lane whose
-        // minimum is <= U), so every key of the answer, ties included, is <= U:
-        // the answer is exactly the first kk of C = {key <= U} in (key, index)
-        // order.  C is small (~2 kk on a mesh), so it is compacted into LDS and
-        // ranked exhaustively.
-        key_t U = 0;
-        for (int bit = KT::kTopBit; bit >= 0; --bit) {
-            const key_t Tc = U | (key_t(1) << bit);
-            if (__popcll(__ballot(lmin < Tc)) <= kk - 1) U = Tc;
-        }
+        // U = kk-th smallest of the 64 lane minima.  At least kk points have
+        // key <= U (one per lane whose minimum is <= U), so every key of the
+        // answer, ties included, is <= U: the answer is exactly the first kk
+        // of C = {key <= U} in (key, index) order.  (Query: the filter is on
+        // the fp32 key, with the margin of filter_threshold; exact fp64 keys
+        // are formed for C only.)  C is small (~2 kk on a mesh), so it is
+        // compacted into LDS and sorted.
+        const uint32_t thr = KT::filter_threshold(__shfl(wave_sort64(lmin, lane), kk - 1, 64));
         int m = 0;
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
-            const bool sel = key[c] <= U;
+            const bool sel = fkey[c] <= thr;
             const uint64_t sm = __ballot(sel);
             if (sel) {
                 const int pidx = m + __popcll(sm & below);
-                if (pidx < kCap) {
-                    sKey[wave][pidx] = key[c];
-                    sIdx[wave][pidx] = lane + 64 * c;
-                }
+                if (pidx < kCap) sIdx[wave][pidx] = lane + 64 * c;
             }
             m += __popcll(sm);
         }
         key_t mk = ~key_t(0);
         int mi = 0x7fffffff;
         int rank = lane;
-        if (m <= kCap) {
+        if (m <= 128) {
+            // Small candidate list (the common case): one 128-wide bitonic sort.
+            wave_lds_sync();
+            key_t k0 = ~key_t(0), k1 = ~key_t(0);
+            int i0 = 0x7fffffff, i1 = 0x7fffffff;
+            if (lane < m) {
+                i0 = sIdx[wave][lane];
+                k0 = KT::key(sP[i0], q);
+            }
+            if (lane + 64 < m) {
+                i1 = sIdx[wave][lane + 64];
+                k1 = KT::key(sP[i1], q);
+            }
+            wave_sort128(k0, i0, k1, i1, lane);
+            if (lane < kk) mi = i0;
+        } else if (m <= kCap) {
+            wave_lds_sync();
+            for (int i = lane; i < m; i += 64) sKey[wave][i] = KT::key(sP[sIdx[wave][i]], q);
             wave_lds_sync();
             for (int i = lane; i < m; i += 64) {
                 const key_t ki = sKey[wave][i];
@@ -140,24 +240,31 @@ __global__ __launch_bounds__(256) void knn_kernel(const float2 *__restrict__ pts
             wave_lds_sync();
             if (lane < kk) mi = sSel[wave][lane];
         } else {
-            // Fallback for adversarial point sets: full radix select on all keys.
+            // Fallback for adversarial point sets (hundreds of ties): full
+            // radix select on all exact keys, recomputed from LDS per use so
+            // that this rare path does not set the kernel's register budget.
+            auto key_at = [&](int c) -> key_t {
+                const int j = lane + 64 * c;
+                return (j < n_src) ? KT::key(sP[j], q) : ~key_t(0);
+            };
             key_t T = 0;
             for (int bit = KT::kTopBit; bit >= 0; --bit) {
                 const key_t Tc = T | (key_t(1) << bit);
                 int cnt = 0;
-#pragma unroll
-                for (int c = 0; c < CPL; ++c) cnt += __popcll(__ballot(key[c] < Tc));
+#pragma unroll 4
+                for (int c = 0; c < CPL; ++c) cnt += __popcll(__ballot(key_at(c) < Tc));
                 if (cnt <= kk - 1) T = Tc;
             }
             int mlt = 0;
-#pragma unroll
-            for (int c = 0; c < CPL; ++c) mlt += __popcll(__ballot(key[c] < T));
+#pragma unroll 4
+            for (int c = 0; c < CPL; ++c) mlt += __popcll(__ballot(key_at(c) < T));
             const int need = kk - mlt;  // >= 1 candidates equal to T, taken in index order
             int base = 0, eq_taken = 0;
-#pragma unroll
+#pragma unroll 4
             for (int c = 0; c < CPL; ++c) {
-                const bool lt = key[c] < T;
-                const bool eq = key[c] == T;
+                const key_t kc = key_at(c);
+                const bool lt = kc < T;
+                const bool eq = kc == T;
                 const uint64_t em = __ballot(eq);
                 const int eqrank = eq_taken + __popcll(em & below);
                 const bool sel = lt || (eq && eqrank < need);
@@ -165,7 +272,7 @@ __global__ __launch_bounds__(256) void knn_kernel(const float2 *__restrict__ pts
                 const uint64_t sm = __ballot(sel);
                 if (sel) {
                     const int pidx = base + __popcll(sm & below);
-                    sKey[wave][pidx] = key[c];
+                    sKey[wave][pidx] = kc;
                     sIdx[wave][pidx] = lane + 64 * c;
                 }
                 base += __popcll(sm);

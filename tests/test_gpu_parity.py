@@ -119,6 +119,28 @@ def test_knn_query_candidate_overflow_fallback(dev):
     assert torch.equal(idx.cpu().long().reshape(ref.shape), ref)
 
 
+@pytest.mark.parametrize("ring", [90, 400])
+def test_knn_query_fp32_filter_margin(dev, ring):
+    # `ring` sources at radius 0.1 (+- 1e-7 relative) from each query: their
+    # fp32 squared distances tie or misorder, only the fp64 keys separate
+    # them, so the candidate filter's rounding margin decides the answer.
+    # ring=90 takes the bitonic path, ring=400 the exhaustive-rank path.
+    from mmpde_amd import ops
+
+    g = torch.Generator().manual_seed(ring)
+    nq, nfar = 6, 1200
+    qry = 0.3 + 0.4 * torch.rand(nq, 2, generator=g)
+    src = []
+    for q in qry:
+        th = 2 * np.pi * torch.rand(ring, generator=g, dtype=torch.float64)
+        r = 0.1 * (1 + 1e-7 * torch.randn(ring, generator=g, dtype=torch.float64))
+        src.append(q.double() + torch.stack((r * th.cos(), r * th.sin()), 1))
+    src.append(0.5 + 2.0 * (torch.rand(nfar, 2, generator=g, dtype=torch.float64) - 0.5) + 0.3)
+    src = torch.cat(src).float()
+    idx = ops.knn_query(src.to(dev), qry.to(dev), 1, 30)
+    assert torch.equal(idx.cpu().long(), refcpu.knn_query(src, qry, 1, 30)[0])
+
+
 def test_knn_query_lattice_ties(dev):
     from mmpde_amd import ops
 
