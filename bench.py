@@ -14,8 +14,10 @@ data-path collective).  value = node-updates/s of the whole job
 
 Also reported (rank 0):
 * roofline: the dominant kernel (GNN edge stage, 12 launches per step) timed
-  live with hipEvents recorded on its own stream around every launch inside
-  the timed region; achieved = algorithmic FLOP per launch / mean launch time.
+  live with hipEvents recorded on its own stream around every launch, in a
+  second timed pass of the same K steps (an event record between launches
+  costs the stream ~10 us, so the pass that sets `value` records none);
+  achieved = algorithmic FLOP per launch / mean launch time.
 * cpu_baseline (N = 1 only): the CPU oracle (op-for-op restatement of the
   reference, oracle/refcpu.py) timed on a bounded sample on this host.
 """
@@ -223,7 +225,8 @@ def main():
             tracer.active = False
         return D.max_over_ranks(t1 - t0, device), u
 
-    elapsed, u = timed_run(args.edge_gemm, True)
+    elapsed, u = timed_run(args.edge_gemm, False)
+    elapsed_traced, _ = timed_run(args.edge_gemm, True)
     finite = bool(torch.isfinite(u).all())
     exact = None
     if not args.no_f32_exact and args.edge_gemm != "f32":
@@ -285,6 +288,7 @@ def main():
                      "unit": "TFLOP/s", "frac": achieved / peak,
                      "traffic": traffic, "launch_ms": launch_ms, "launches": len(launches),
                      "flop_per_launch": edge_f,
+                     "traced_pass_ms_per_step": 1e3 * elapsed_traced / args.steps,
                      "algorithmic_bytes_per_launch": n_local * (128 * 4 * 2 + k * 4 + 128 * 4),
                      "edge_gemm": args.edge_gemm,
                      "peak_basis": "dense fp32 MFMA" if args.edge_gemm == "f32" else

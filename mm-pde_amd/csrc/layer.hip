@@ -12,15 +12,18 @@
 // + (W1b h_j - w.(u,x,y)_j)); the reference's [E, 260] edge concat never
 // exists and the only per-edge work is one 128x128 GEMM per edge.
 //
-// Edge stage (the dominant kernel): persistent, one 512-thread workgroup per
-// CU walking a contiguous (XCD-local) range of 16-target tiles.  Waves 4-7 are
+// Edge stage (the dominant kernel): persistent, one 768-thread workgroup per
+// CU walking a contiguous (XCD-local) range of 16-target tiles.  Waves 8-11 are
 // producers: for neighbour slot e of a tile they gather the 16 source rows of
 // b, form m = relu(a_i + b_j) in registers and store it to an LDS ring as the
-// exact per-lane A operand (F16X3: scaled fp16 hi/lo halves).  Waves 0-3 are
-// consumers: each keeps 32 output columns of W2 in registers for the whole
-// launch and runs the MFMAs of every slot, accumulating relu(. + b2) per
-// target in registers (slot e of all 16 targets shares one accumulator row,
-// so no cross-lane traffic), and writes the mean after the tile's last slot.
+// exact per-lane A operand (F16X3: scaled fp16 hi/lo halves).  Waves 0-7 are
+// consumers: the two on one SIMD keep the same 32 output columns of W2 in
+// registers for the whole launch and split each round's slots (even / odd),
+// accumulating relu(. + b2) per target in registers (slot e of all 16 targets
+// shares one accumulator row, so no cross-lane traffic); after the tile's last
+// slot the odd-slot wave hands its sums to its partner through LDS, which
+// writes the mean.  Sharing columns rather than splitting them halves the
+// LDS operand reads (each slot is read by 4 waves, not 8).
 // A workgroup's waves land on SIMDs in the order 0,2,1,3 (MI355X_MICROARCH.md),
 // so waves w and w+4 share a SIMD: every SIMD pairs one MFMA stream with one
 // VALU/gather stream.  One barrier per round of 4 slots; producers run
@@ -91,11 +94,14 @@ constexpr int EDGE_NC = MMPDE_EDGE_NC;
 #endif
 constexpr int EDGE_NP = MMPDE_EDGE_NP;
 
-// PH (profiling builds only, tools/ubench): bit 0 produce, bit 1 consume (MFMA),
-// bit 2 skip the gathers, bit 3 raise the consumer waves' issue priority, bit
-// 10 record per-round s_memtime stamps of block 0; production launches use EDGE_PH.
+// PH: bit 0 produce, bit 1 consume (MFMA), bit 2 skip the gathers, bit 3 raise
+// the consumer waves' issue priority, bit 4 (NC == 2) split each round's slots
+// between the two consumer waves of a SIMD, which then own the same 32 output
+// columns (half the LDS operand reads of column-split waves), bit 10 record
+// per-round s_memtime stamps of block 0.  Bits other than 0, 1 and 4 are for
+// profiling builds (tools/ubench); production launches use EDGE_PH.
 #ifndef MMPDE_EDGE_PH
-#define MMPDE_EDGE_PH 11
+#define MMPDE_EDGE_PH 27
 #endif
 constexpr int EDGE_PH = MMPDE_EDGE_PH;
 
@@ -115,11 +121,15 @@ constexpr int EDGE_PH = MMPDE_EDGE_PH;
 // rounds ahead; b rows are gathered two rounds before use.
 template <bool F16X3, int PH = EDGE_PH, int NC = EDGE_NC, int NP = EDGE_NP>
 __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(EdgeArgs p) {
-    constexpr int CT = 2 / NC;  // 16-column tiles per consumer wave
+    constexpr bool SPLIT = NC == 2 && (PH & 16);
+    constexpr int CT = SPLIT ? 2 : 2 / NC;  // 16-column tiles per consumer wave
+    constexpr int SPW = SPLIT ? ESL / 2 : ESL;  // slots per consumer wave and round
     constexpr int NPC = 8 / NP;  // float4 pieces of a slot lane per producer wave
     constexpr int NCT = 256 * NC;  // consumer threads
     __shared__ float4 ring[ERING * ESL * SLOT4];  // [round % ERING][slot][plane][lane]
     __shared__ float a_lds[2][ET * NLDA];        // a rows of tile j in [j & 1]
+    // SPLIT: the odd-slot consumer's relu-sums of tile j, in [j & 1]
+    __shared__ float4 xS[SPLIT ? 2 * 4 * CT * 64 : 1];
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
     const int r = lane & 15, g = lane >> 4;
@@ -256,21 +266,25 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
         }
     } else {
         // ------------------------------------------------------------ consumer
-        // this wave's output column tiles CT wave + cc (cc < CT)
+        // this wave's output column tiles CT cg + cc (cc < CT); SPLIT: slots
+        // hs, hs + 2 of every round
+        const int cg = SPLIT ? (wave & 3) : wave;
+        const int hs = SPLIT ? (wave >> 2) : 0;
+        auto slotq = [&](int qq) { return SPLIT ? hs + 2 * qq : qq; };
         float4 wf[CT][8];
         half8 wh[CT][4], wl[CT][4];
         f32x4 bias[CT];  // accumulator initial value (message_net_2 bias, scaled)
         float inv[CT];
 #pragma unroll
         for (int cc = 0; cc < CT; ++cc) {
-            const int col = 16 * (CT * wave + cc) + r;
+            const int col = 16 * (CT * cg + cc) + r;
             float bb = p.b2[col];
             if (F16X3) {
                 const char *img = p.pk + kPkW2;
 #pragma unroll
                 for (int s4 = 0; s4 < 4; ++s4) {
-                    wh[cc][s4] = bfrag(img, 4, CT * wave + cc, s4, 0, lane);
-                    wl[cc][s4] = bfrag(img, 4, CT * wave + cc, s4, 1, lane);
+                    wh[cc][s4] = bfrag(img, 4, CT * cg + cc, s4, 0, lane);
+                    wl[cc][s4] = bfrag(img, 4, CT * cg + cc, s4, 1, lane);
                 }
                 const float sw = ((const float *)(img + 65536))[col];
                 bb = bb * sw * sc;
@@ -282,12 +296,35 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
             }
             bias[cc] = (f32x4){bb, bb, bb, bb};
         }
-        f32x4 S[CT];
+        const float kdiv = (float)k;
+        f32x4 S[CT], Ssave[CT];
 #pragma unroll
         for (int cc = 0; cc < CT; ++cc) S[cc] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+        int pend = -1;  // SPLIT, even-slot wave: tile whose mean waits for the partner's sums
+        auto write_mean = [&](int j, const f32x4 *T) {
+            const int64_t row0 = (int64_t)(first + j * stride) * ET + 4 * g;
+#pragma unroll
+            for (int cc = 0; cc < CT; ++cc) {
+                const int col = 16 * (CT * cg + cc) + r;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    if (row0 + t < p.n) p.mean[(row0 + t) * LH + col] = T[cc][t] / kdiv;
+                }
+            }
+        };
+        auto finish_pending = [&]() {  // after the barrier that follows the partner's store
+            if (SPLIT && pend >= 0) {
+#pragma unroll
+                for (int cc = 0; cc < CT; ++cc) {
+                    const float4 o = xS[(((pend & 1) * 4 + cg) * CT + cc) * 64 + lane];
+                    Ssave[cc] += (f32x4){o.x, o.y, o.z, o.w};
+                }
+                write_mean(pend, Ssave);
+                pend = -1;
+            }
+        };
         RoundCtr cC{0, 0};
         int slot = 0;
-        const float kdiv = (float)k;
         if (PH & 8) __builtin_amdgcn_s_setprio(1);
         // The next half slot is read from LDS while the current one is
         // multiplied (the next round's first half too: that round was
@@ -342,6 +379,7 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
                      // iterations earlier but after the previous store
         const int lead = min(2, rpt - 1);
         for (int it = 0; it < NIT2; ++it) {
+            finish_pending();
             if (js < nt) {
                 const int ts = js * rpt - 1;
                 if (it == ts - lead) a_fetch(js, an);
@@ -353,32 +391,36 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
             if (it >= EPF && it < NIT && (PH & 2)) {
                 const float4 *base = ring + slot * ESL * SLOT4 + lane;
                 const float4 *nbase = ring + (slot == ERING - 1 ? 0 : slot + 1) * ESL * SLOT4 + lane;
-                if (it == EPF) rd_half(base, 0, xa);
+                if (it == EPF) rd_half(base + slotq(0) * SLOT4, 0, xa);
                 f32x4 accP[CT];
 #pragma unroll
-                for (int q = 0; q < ESL; ++q) {
+                for (int qq = 0; qq < SPW; ++qq) {
                     f32x4 accN[CT];
-                    rd_half(base + q * SLOT4, 1, xb);
+                    rd_half(base + slotq(qq) * SLOT4, 1, xb);
                     mma_half(xa, 0, accN);
-                    if (q > 0) sum_into(accP, ESL * cC.rd + q - 1 < k);
-                    if (q < ESL - 1) rd_half(base + (q + 1) * SLOT4, 0, xa);
-                    else if (it + 1 < NIT) rd_half(nbase, 0, xa);
+                    if (qq > 0) sum_into(accP, ESL * cC.rd + slotq(qq - 1) < k);
+                    if (qq < SPW - 1) rd_half(base + slotq(qq + 1) * SLOT4, 0, xa);
+                    else if (it + 1 < NIT) rd_half(nbase + slotq(0) * SLOT4, 0, xa);
                     mma_half(xb, 1, accN);
 #pragma unroll
                     for (int cc = 0; cc < CT; ++cc) accP[cc] = accN[cc];
                 }
-                sum_into(accP, ESL * cC.rd + ESL - 1 < k);
+                sum_into(accP, ESL * cC.rd + slotq(SPW - 1) < k);
                 if (cC.rd == rpt - 1) {  // tile complete: mean = sum / k (PyG mean, fixed degree)
-                    const int64_t row0 = (int64_t)(first + cC.j * stride) * ET + 4 * g;
+                    if (!SPLIT) {
+                        write_mean(cC.j, S);
+                    } else if (hs == 1) {  // hand the odd slots' sums to the partner wave
 #pragma unroll
-                    for (int cc = 0; cc < CT; ++cc) {
-                        const int col = 16 * (CT * wave + cc) + r;
+                        for (int cc = 0; cc < CT; ++cc)
+                            xS[(((cC.j & 1) * 4 + cg) * CT + cc) * 64 + lane] =
+                                make_float4(S[cc][0], S[cc][1], S[cc][2], S[cc][3]);
+                    } else {
 #pragma unroll
-                        for (int t = 0; t < 4; ++t) {
-                            if (row0 + t < p.n) p.mean[(row0 + t) * LH + col] = S[cc][t] / kdiv;
-                        }
-                        S[cc] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+                        for (int cc = 0; cc < CT; ++cc) Ssave[cc] = S[cc];
+                        pend = cC.j;
                     }
+#pragma unroll
+                    for (int cc = 0; cc < CT; ++cc) S[cc] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
                 }
                 cC.next(rpt);
                 slot = slot == ERING - 1 ? 0 : slot + 1;
@@ -389,6 +431,7 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
             if ((PH & 1024) && blockIdx.x == 0 && lane == 0 && it < 256)
                 p.stamps[2 * 256 * wave + 2 * it + 1] = __builtin_amdgcn_s_memtime();
         }
+        finish_pending();  // the loop ends with a barrier
     }
 }
 

@@ -9,7 +9,10 @@
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-template <int MODE>  // bit 0: MFMA waves work, bit 1: VALU waves work, bit 2: VALU waves use fma_mix
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <int MODE>  // bit 0: MFMA waves work, bit 1: VALU waves work, bit 2: VALU waves use fma_mix,
+                     // bit 3: the MFMA stream is v_mfma_f32_32x32x16_f16 (same MAC count)
 __global__ __launch_bounds__(512, 1) void probe(float *out, int iters) {
     const int wave = threadIdx.x >> 6;
     float r = 0.0f;
@@ -20,15 +23,27 @@ __global__ __launch_bounds__(512, 1) void probe(float *out, int iters) {
                 a[i] = (_Float16)(threadIdx.x * 1e-3f + i);
                 b[i] = (_Float16)(1.0f / (i + 1));
             }
-            f32x4 c0 = {0, 0, 0, 0}, c1 = {0, 0, 0, 0};
-            for (int it = 0; it < iters; ++it) {
+            if (MODE & 8) {
+                f32x16 c0 = {}, c1 = {};
+                for (int it = 0; it < iters; ++it) {
 #pragma unroll
-                for (int j = 0; j < 12; ++j) {
-                    c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c0, 0, 0, 0);
-                    c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b, a, c1, 0, 0, 0);
+                    for (int j = 0; j < 6; ++j) {
+                        c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c0, 0, 0, 0);
+                        c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(b, a, c1, 0, 0, 0);
+                    }
                 }
+                r = c0[0] + c1[1];
+            } else {
+                f32x4 c0 = {0, 0, 0, 0}, c1 = {0, 0, 0, 0};
+                for (int it = 0; it < iters; ++it) {
+#pragma unroll
+                    for (int j = 0; j < 12; ++j) {
+                        c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c0, 0, 0, 0);
+                        c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b, a, c1, 0, 0, 0);
+                    }
+                }
+                r = c0[0] + c1[1];
             }
-            r = c0[0] + c1[1];
         }
     } else if (MODE & 2) {
         float x0 = threadIdx.x * 1e-3f, x1 = x0 + 1, x2 = x0 + 2, x3 = x0 + 3, s = 1.0001f;
@@ -81,5 +96,7 @@ int main() {
     const int iters = 4000;
     printf("us: mfma alone %.1f | valu alone %.1f (mix %.1f) | both %.1f (mix %.1f)\n", run<1>(out, iters),
            run<2>(out, iters), run<6>(out, iters), run<3>(out, iters), run<7>(out, iters));
+    printf("32x32x16: mfma alone %.1f | both %.1f (mix %.1f)\n", run<9>(out, iters), run<11>(out, iters),
+           run<15>(out, iters));
     return 0;
 }

@@ -1,3 +1,4 @@
+#include <cmath>
 // Timing of the layer kernels (profiling aid, not shipped): edge stage and
 // node stage variants on a cylinder-sized synthetic layer (n = B x 2521 rows,
 // k = 35 in-trajectory neighbours), both arithmetic modes.
@@ -131,6 +132,25 @@ int main(int argc, char **argv) {
            edge(gnn_edge_kernel<true, 3, 1, 1>, 8, e16), edge(gnn_edge_kernel<true, 3, 2, 2>, 16, e16),
            edge(gnn_edge_kernel<true, 3, 2, 1>, 12, e16), edge(gnn_edge_kernel<false, 3, 1, 2>, 12, e32));
     printf("edge f16x3 NC1NP2 no-gather %.1f\n", edge(gnn_edge_kernel<true, 7, 1, 2>, 12, e16));
+    printf("edge f16x3 slot-split NC2NP1 prio %.1f  noprio %.1f | NC2NP2 prio %.1f | column-split NC2NP1 prio %.1f\n",
+           edge(gnn_edge_kernel<true, 27, 2, 1>, 12, e16), edge(gnn_edge_kernel<true, 19, 2, 1>, 12, e16),
+           edge(gnn_edge_kernel<true, 27, 2, 2>, 16, e16), edge(gnn_edge_kernel<true, 11, 2, 1>, 12, e16));
+    printf("edge f16x3 slot-split NC2NP1: consume-only %.1f | no-gather %.1f | produce-only %.1f\n",
+           edge(gnn_edge_kernel<true, 26, 2, 1>, 12, e16), edge(gnn_edge_kernel<true, 31, 2, 1>, 12, e16),
+           edge(gnn_edge_kernel<true, 25, 2, 1>, 12, e16));
+    {   // slot-split vs column-split consumers: same sums, same order per target
+        std::vector<float> m0(n * H), m1(n * H);
+        hipLaunchKernelGGL((gnn_edge_kernel<true, 11, 2, 1>), dim3(grid_e), dim3(768), 0, 0, e16);
+        CK(hipMemcpy(m0.data(), mean, n * H * 4, hipMemcpyDeviceToHost));
+        hipLaunchKernelGGL((gnn_edge_kernel<true, 27, 2, 1>), dim3(grid_e), dim3(768), 0, 0, e16);
+        CK(hipMemcpy(m1.data(), mean, n * H * 4, hipMemcpyDeviceToHost));
+        double d = 0, mx = 0;
+        for (size_t i = 0; i < m0.size(); ++i) {
+            d = std::max(d, (double)std::fabs(m0[i] - m1[i]));
+            mx = std::max(mx, (double)std::fabs(m0[i]));
+        }
+        printf("slot-split vs column-split: max|diff| %.3e (max|mean| %.3e)\n", d, mx);
+    }
     {   // per-round barrier arrival / release times of block 0 (waves 0..7, lane 0)
         hipLaunchKernelGGL((gnn_edge_kernel<true, 1024 + 3, 1, 2>), dim3(grid_e), dim3(768), 0, 0, e16);
         CK(hipDeviceSynchronize());
