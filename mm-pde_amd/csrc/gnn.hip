@@ -239,56 +239,97 @@ __global__ __launch_bounds__(256, 2) void edge_mean_kernel(const float *__restri
 }
 
 // ---------------------------------------------------------------------------
-// Conv1d head (gnn_2d.py:108-114,136-139): one wave per node.
+// Conv1d head (gnn_2d.py:108-114,136-139):
 // 128 -> conv(1->4, k16, s3) 38 -> relu -> conv(4->8, k12, s3) 9 -> relu ->
 // conv(8->1, k8, s2) 1, times out_scale.
+// 64 nodes per 256-thread workgroup, one node per lane: the 64 h rows are
+// staged in LDS (row stride 129: a wave reading one column of 64 rows hits 64
+// distinct banks); wave c computes conv0 channel c (38 outputs, kept in
+// registers until every wave has read h, then written over the h rows), then
+// conv2 channels 2c, 2c+1 (9 outputs each) from all four conv0 channels, then
+// its share of conv4; the four partial sums meet in LDS.  Weights are
+// wave-uniform (scalar loads).  39 KB of LDS: several workgroups per CU.
 // ---------------------------------------------------------------------------
+constexpr int HN = 64;           // nodes per workgroup
+constexpr int HS = H + 1;        // h row stride (floats)
+constexpr int Y1S = 4 * 38 + 1;  // conv0 output row stride (floats)
+
 __global__ __launch_bounds__(256) void head_kernel(const float *__restrict__ h, int64_t n,
                                                    mmpde_gnn_head_params p,
                                                    float *__restrict__ out) {
-    __shared__ float sw0[64 + 4], sw2[384 + 8], sw4[64 + 1];
-    __shared__ float y1[4][4 * 38];
-    __shared__ float y2[4][8 * 9];
-    for (int i = threadIdx.x; i < 64; i += 256) sw0[i] = p.c0_w[i];
-    for (int i = threadIdx.x; i < 4; i += 256) sw0[64 + i] = p.c0_b[i];
-    for (int i = threadIdx.x; i < 384; i += 256) sw2[i] = p.c2_w[i];
-    for (int i = threadIdx.x; i < 8; i += 256) sw2[384 + i] = p.c2_b[i];
-    for (int i = threadIdx.x; i < 64; i += 256) sw4[i] = p.c4_w[i];
-    if (threadIdx.x == 0) sw4[64] = p.c4_b[0];
-    __syncthreads();
-    const int wave = threadIdx.x >> 6;
-    const int lane = threadIdx.x & 63;
-    for (int64_t i = (int64_t)blockIdx.x * 4 + wave; i < n; i += (int64_t)gridDim.x * 4) {
-        const float *hr = h + i * H;
-        for (int e = lane; e < 4 * 38; e += 64) {
-            const int c = e / 38, q = e - c * 38;
-            float v = sw0[64 + c];
-#pragma unroll
-            for (int t = 0; t < 16; ++t) v += sw0[c * 16 + t] * hr[3 * q + t];
-            y1[wave][e] = fmaxf(v, 0.0f);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        for (int e = lane; e < 8 * 9; e += 64) {  // 72 outputs > 64 lanes
-            const int c = e / 9, q = e - c * 9;
-            float v = sw2[384 + c];
-            for (int ci = 0; ci < 4; ++ci) {
-#pragma unroll
-                for (int t = 0; t < 12; ++t) v += sw2[(c * 4 + ci) * 12 + t] * y1[wave][ci * 38 + 3 * q + t];
-            }
-            y2[wave][e] = fmaxf(v, 0.0f);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        {
-            const int ci = lane >> 3, t = lane & 7;
-            float v = sw4[ci * 8 + t] * y2[wave][ci * 9 + t];
-            v = wave_sum(v);
-            if (lane == 0) out[i] = p.out_scale * (v + sw4[64]);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
+    __shared__ float sh[HN * (Y1S > HS ? Y1S : HS)];  // h rows (stride HS), then conv0 outputs (stride Y1S)
+    __shared__ float spart[4][HN];
+    float *const sy1 = sh;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int c = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int64_t node0 = (int64_t)blockIdx.x * HN;
+    for (int i = tid; i < HN * (H / 4); i += 256) {
+        const int row = i >> 5, c4 = i & 31;
+        const int64_t src = min(node0 + row, n - 1);
+        const float4 v = *(const float4 *)(h + src * H + 4 * c4);
+        float *d = sh + row * HS + 4 * c4;
+        d[0] = v.x;
+        d[1] = v.y;
+        d[2] = v.z;
+        d[3] = v.w;
     }
+    __syncthreads();
+    {   // conv0, channel c
+        float w[16], y[38];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) w[t] = p.c0_w[c * 16 + t];
+        const float b = p.c0_b[c];
+        const float *hr = sh + lane * HS;
+#pragma unroll
+        for (int q0 = 0; q0 < 38; q0 += 2) {
+            float x[19];
+#pragma unroll
+            for (int i = 0; i < 19; ++i) x[i] = hr[3 * q0 + i];
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq) {
+                float v = b;
+#pragma unroll
+                for (int t = 0; t < 16; ++t) v = fmaf(w[t], x[3 * qq + t], v);
+                y[q0 + qq] = fmaxf(v, 0.0f);
+            }
+        }
+        __syncthreads();  // every wave has read the h rows
+        float *yr = sy1 + lane * Y1S + c * 38;
+#pragma unroll
+        for (int q = 0; q < 38; ++q) yr[q] = y[q];
+    }
+    __syncthreads();
+    float part = 0.0f;
+#pragma unroll
+    for (int oo = 0; oo < 2; ++oo) {  // conv2 channel co = 2c + oo, then its conv4 terms
+        const int co = 2 * c + oo;
+        float acc[9];
+        const float b = p.c2_b[co];
+#pragma unroll
+        for (int q = 0; q < 9; ++q) acc[q] = b;
+#pragma unroll
+        for (int ci = 0; ci < 4; ++ci) {
+            float y[36];
+            const float *yr = sy1 + lane * Y1S + ci * 38;
+#pragma unroll
+            for (int i = 0; i < 36; ++i) y[i] = yr[i];
+            float w[12];
+#pragma unroll
+            for (int t = 0; t < 12; ++t) w[t] = p.c2_w[(co * 4 + ci) * 12 + t];
+#pragma unroll
+            for (int q = 0; q < 9; ++q) {
+#pragma unroll
+                for (int t = 0; t < 12; ++t) acc[q] = fmaf(w[t], y[3 * q + t], acc[q]);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < 8; ++t) part = fmaf(p.c4_w[co * 8 + t], fmaxf(acc[t], 0.0f), part);
+    }
+    spart[c][lane] = part;
+    __syncthreads();
+    if (c == 0 && node0 + lane < n)
+        out[node0 + lane] = p.out_scale * (p.c4_b[0] + ((spart[0][lane] + spart[1][lane]) +
+                                                        (spart[2][lane] + spart[3][lane])));
 }
 
 inline bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
@@ -386,10 +427,8 @@ extern "C" int mmpde_gnn_layer(const float *h_in, const float *u, const float *p
 extern "C" int mmpde_gnn_head(const float *h, int64_t n, const mmpde_gnn_head_params *p,
                               float *out, mmpde_stream_t stream) {
     MMPDE_REQUIRE(h && p && out && n > 0);
-    int blocks = ceil_div(n, 4);
-    if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(head_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), h, n, *p,
-                       out);
+    hipLaunchKernelGGL(head_kernel, dim3((unsigned)ceil_div(n, HN)), dim3(256), 0,
+                       as_stream(stream), h, n, *p, out);
     MMPDE_RET_LAUNCH();
     return MMPDE_OK;
 }
