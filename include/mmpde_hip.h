@@ -274,6 +274,25 @@ int mmpde_dmm_mesh_array(const float *u, const float *xi, int64_t batches, int64
                          const mmpde_dmm_array_branch *br, const mmpde_dmm_head *hd,
                          void *workspace, float *mesh_out, mmpde_stream_t stream);
 
+/* The grid side of the DMM head -- trunk(xi), Q = Wt.trunk and J = dQ/dxi
+ * (dmm_model.py:196-199's trunk and out_nn first layer) -- depends on xi and the
+ * weights only, not on u.  A rollout over a fixed grid prepares it once:
+ * cache >= mmpde_dmm_head_cache_bytes(N, hd->hidden) bytes (16-B aligned),
+ * workspace as for mmpde_dmm_mesh_*.  The _cached variants read it instead of
+ * recomputing it (same xi and weights required; results are identical). */
+int64_t mmpde_dmm_head_cache_bytes(int64_t n_per, int hidden);
+int mmpde_dmm_head_prepare(const float *xi, int64_t n_per, const mmpde_dmm_head *hd,
+                           void *workspace, void *cache, mmpde_stream_t stream);
+int mmpde_dmm_mesh_graph_cached(const float *u, const float *grid, int64_t batches,
+                                int64_t n_per, const int32_t *grid_nbr, int k,
+                                const mmpde_dmm_graph_branch *br, const mmpde_dmm_head *hd,
+                                const void *head_cache, void *workspace, float *mesh_out,
+                                mmpde_stream_t stream);
+int mmpde_dmm_mesh_array_cached(const float *u, const float *xi, int64_t batches, int64_t n_per,
+                                const mmpde_dmm_array_branch *br, const mmpde_dmm_head *hd,
+                                const void *head_cache, void *workspace, float *mesh_out,
+                                mmpde_stream_t stream);
+
 /* ------------------------------------------------------------------------
  * ItpNet interpolation (reference interpolate.py:77-93 + data_creator_2d.py:80-83)
  * ---------------------------------------------------------------------- */

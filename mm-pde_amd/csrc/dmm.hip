@@ -304,17 +304,11 @@ HeadWs carve_head(float *ws, int64_t batches, int64_t n_per, int latent, int hid
     return h;
 }
 
-// branch [B, L] -> mesh [B*N, 2]
-int dmm_head(const float *branch, const float *xi, int64_t batches, int64_t n_per,
-             const mmpde_dmm_head *hd, float *ws, float *mesh_out, hipStream_t st) {
+// Grid side of the head (a function of xi and the weights only): trunk, Q =
+// Wt . trunk [N, L'] and J = dQ/dxi [N, L'] (float2).
+int dmm_head_grid(const float *xi, int64_t n_per, const mmpde_dmm_head *hd, const HeadWs &w,
+                  float *q, float2 *jac, hipStream_t st) {
     const int L = hd->latent, Lp = hd->hidden, th = hd->th;
-    if (th < 1 || th > 64 || L % 8 != 0 || Lp % 128 != 0) return MMPDE_ERR_UNSUPPORTED;
-    HeadWs w = carve_head(ws, batches, n_per, L, Lp, th);
-    int rc;
-    // P = Wb . branch + b_o1 (Wb = out_nn.layers.0.weight[:, :L], row stride 2L)
-    rc = mmpde_linear_skinny(branch, L, batches, L, hd->o0_w, 2 * L, hd->o0_b, Lp,
-                             MMPDE_ACT_NONE, w.p, Lp, st);
-    if (rc) return rc;
     hipLaunchKernelGGL(trunk_kernel, dim3((unsigned)n_per), dim3(256), 0, st,
                        (const float2 *)xi, th, L, hd->t0_w, hd->t0_b, hd->t1_w, hd->t1_b, w.s,
                        w.trunk);
@@ -323,23 +317,50 @@ int dmm_head(const float *branch, const float *xi, int64_t batches, int64_t n_pe
     {
         const int kh = L / 2;
         GemmArgs g{n_per, w.trunk, w.trunk + kh, L, hd->o0_w + L, hd->o0_w + L + kh, 2 * L, kh};
-        EpiStore epi{w.q, Lp};
-        rc = launch_gemm(g, Lp / 128, epi, st);
+        EpiStore epi{q, Lp};
+        const int rc = launch_gemm(g, Lp / 128, epi, st);
         if (rc) return rc;
     }
     // Gt = (Wt . T1)^T = T1^T . Wt^T  ([th, L'])
     hipLaunchKernelGGL(transpose_kernel, dim3(ceil_div((int64_t)L * th, 256)), dim3(256), 0, st,
                        hd->t1_w, L, th, w.t1t);
     MMPDE_RET_LAUNCH();
-    rc = mmpde_linear_skinny(w.t1t, L, th, L, hd->o0_w + L, 2 * L, nullptr, Lp, MMPDE_ACT_NONE,
-                             w.gt, Lp, st);
+    const int rc = mmpde_linear_skinny(w.t1t, L, th, L, hd->o0_w + L, 2 * L, nullptr, Lp,
+                                       MMPDE_ACT_NONE, w.gt, Lp, st);
     if (rc) return rc;
     hipLaunchKernelGGL(jac_kernel, dim3((unsigned)n_per), dim3(256), 0, st, w.s, th, w.gt, Lp,
-                       hd->t0_w, w.jac);
+                       hd->t0_w, jac);
     MMPDE_RET_LAUNCH();
-    hipLaunchKernelGGL(mesh_vjp_kernel, dim3((unsigned)n_per), dim3(256), 0, st, w.p, w.q,
-                       w.jac, hd->o1_w, (const float2 *)xi, batches, n_per, Lp,
-                       (float2 *)mesh_out);
+    return MMPDE_OK;
+}
+
+bool head_ok(const mmpde_dmm_head *hd) {
+    return hd->th >= 1 && hd->th <= 64 && hd->latent % 8 == 0 && hd->hidden % 128 == 0;
+}
+
+// Head cache layout: Q [N, L'] then J [N, L'] float2.
+int64_t cache_floats(int64_t n_per, int hidden) { return 3 * n_per * hidden; }
+
+// branch [B, L] -> mesh [B*N, 2]; cache: a prepared grid side (or null: computed here)
+int dmm_head(const float *branch, const float *xi, int64_t batches, int64_t n_per,
+             const mmpde_dmm_head *hd, float *ws, const float *cache, float *mesh_out,
+             hipStream_t st) {
+    const int L = hd->latent, Lp = hd->hidden, th = hd->th;
+    if (!head_ok(hd)) return MMPDE_ERR_UNSUPPORTED;
+    HeadWs w = carve_head(ws, batches, n_per, L, Lp, th);
+    const float *q = cache ? cache : w.q;
+    const float2 *jac = cache ? (const float2 *)(cache + n_per * Lp) : w.jac;
+    int rc;
+    if (!cache) {
+        rc = dmm_head_grid(xi, n_per, hd, w, w.q, w.jac, st);
+        if (rc) return rc;
+    }
+    // P = Wb . branch + b_o1 (Wb = out_nn.layers.0.weight[:, :L], row stride 2L)
+    rc = mmpde_linear_skinny(branch, L, batches, L, hd->o0_w, 2 * L, hd->o0_b, Lp,
+                             MMPDE_ACT_NONE, w.p, Lp, st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(mesh_vjp_kernel, dim3((unsigned)n_per), dim3(256), 0, st, w.p, q, jac,
+                       hd->o1_w, (const float2 *)xi, batches, n_per, Lp, (float2 *)mesh_out);
     MMPDE_RET_LAUNCH();
     return MMPDE_OK;
 }
@@ -358,10 +379,34 @@ extern "C" int64_t mmpde_dmm_workspace_bytes(int64_t batches, int64_t n_per, int
            (int64_t)sizeof(float);
 }
 
+extern "C" int64_t mmpde_dmm_head_cache_bytes(int64_t n_per, int hidden) {
+    return n_per > 0 && hidden > 0 ? cache_floats(n_per, hidden) * (int64_t)sizeof(float) : 0;
+}
+
+extern "C" int mmpde_dmm_head_prepare(const float *xi, int64_t n_per, const mmpde_dmm_head *hd,
+                                      void *workspace, void *cache, mmpde_stream_t stream) {
+    MMPDE_REQUIRE(xi && hd && workspace && cache && n_per > 0 && al16(workspace) && al16(cache));
+    if (!head_ok(hd)) return MMPDE_ERR_UNSUPPORTED;
+    HeadWs w = carve_head((float *)workspace, 1, n_per, hd->latent, hd->hidden, hd->th);
+    float *q = (float *)cache;
+    return dmm_head_grid(xi, n_per, hd, w, q, (float2 *)(q + n_per * hd->hidden),
+                         as_stream(stream));
+}
+
 extern "C" int mmpde_dmm_mesh_graph(const float *u, const float *grid, int64_t batches,
                                     int64_t n_per, const int32_t *grid_nbr, int k,
                                     const mmpde_dmm_graph_branch *br, const mmpde_dmm_head *hd,
                                     void *workspace, float *mesh_out, mmpde_stream_t stream) {
+    return mmpde_dmm_mesh_graph_cached(u, grid, batches, n_per, grid_nbr, k, br, hd, nullptr,
+                                       workspace, mesh_out, stream);
+}
+
+extern "C" int mmpde_dmm_mesh_graph_cached(const float *u, const float *grid, int64_t batches,
+                                           int64_t n_per, const int32_t *grid_nbr, int k,
+                                           const mmpde_dmm_graph_branch *br,
+                                           const mmpde_dmm_head *hd, const void *head_cache,
+                                           void *workspace, float *mesh_out,
+                                           mmpde_stream_t stream) {
     MMPDE_REQUIRE(u && grid && grid_nbr && br && hd && workspace && mesh_out);
     MMPDE_REQUIRE(batches > 0 && n_per > k && k > 0 && br->n_gnn_layers >= 0 &&
                   br->n_gnn_layers <= 3 && al16(workspace));
@@ -403,13 +448,23 @@ extern "C" int mmpde_dmm_mesh_graph(const float *u, const float *grid, int64_t b
     rc = mmpde_linear_skinny(om2, 256, batches, 256, br->om4_w, 256, br->om4_b, hd->latent,
                              MMPDE_ACT_NONE, branch, hd->latent, stream);
     if (rc) return rc;
-    return dmm_head(branch, grid, batches, n_per, hd, head_ws, mesh_out, st);
+    return dmm_head(branch, grid, batches, n_per, hd, head_ws, (const float *)head_cache, mesh_out,
+                    st);
 }
 
 extern "C" int mmpde_dmm_mesh_array(const float *u, const float *xi, int64_t batches,
                                     int64_t n_per, const mmpde_dmm_array_branch *br,
                                     const mmpde_dmm_head *hd, void *workspace, float *mesh_out,
                                     mmpde_stream_t stream) {
+    return mmpde_dmm_mesh_array_cached(u, xi, batches, n_per, br, hd, nullptr, workspace, mesh_out,
+                                       stream);
+}
+
+extern "C" int mmpde_dmm_mesh_array_cached(const float *u, const float *xi, int64_t batches,
+                                           int64_t n_per, const mmpde_dmm_array_branch *br,
+                                           const mmpde_dmm_head *hd, const void *head_cache,
+                                           void *workspace, float *mesh_out,
+                                           mmpde_stream_t stream) {
     MMPDE_REQUIRE(u && xi && br && hd && workspace && mesh_out && batches > 0);
     MMPDE_REQUIRE((int64_t)br->s * br->s == n_per && al16(workspace));
     hipStream_t st = as_stream(stream);
@@ -448,5 +503,5 @@ extern "C" int mmpde_dmm_mesh_array(const float *u, const float *xi, int64_t bat
     rc = mmpde_linear_skinny(f2, 1024, batches, 1024, br->fc3_w, 1024, br->fc3_b, hd->latent,
                              MMPDE_ACT_NONE, branch, hd->latent, stream);
     if (rc) return rc;
-    return dmm_head(branch, xi, batches, n_per, hd, ws, mesh_out, st);
+    return dmm_head(branch, xi, batches, n_per, hd, ws, (const float *)head_cache, mesh_out, st);
 }

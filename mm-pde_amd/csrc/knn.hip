@@ -80,14 +80,49 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
+// v of lane ^ j without the LDS pipe (ds_bpermute's round trip would sit on
+// every step of the sorting networks): DPP quad_perm for j = 1, 2; DPP
+// row_shl / row_shr by j plus a select for j = 4, 8 (row_shl:j reads lane + j);
+// v_permlane16_swap / v_permlane32_swap of v with itself for j = 16, 32 (the
+// swap moves odd rows of its first operand with even rows of its second /
+// the upper half of the first with the lower half of the second).  j must fold
+// to a constant: the networks below are fully unrolled.
+__device__ __forceinline__ uint32_t xor_lane(uint32_t v, int j, int lane) {
+    const int x = (int)v;
+    switch (j) {
+    case 1:
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false);  // [1,0,3,2]
+    case 2:
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false);  // [2,3,0,1]
+    case 4: {
+        const int up = __builtin_amdgcn_update_dpp(0, x, 0x104, 0xF, 0xF, false);
+        const int dn = __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false);
+        return (uint32_t)((lane & 4) ? dn : up);
+    }
+    case 8: {
+        const int up = __builtin_amdgcn_update_dpp(0, x, 0x108, 0xF, 0xF, false);
+        const int dn = __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false);
+        return (uint32_t)((lane & 8) ? dn : up);
+    }
+    case 16: {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return (lane & 16) ? r[0] : r[1];
+    }
+    default: {  // 32
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return (lane & 32) ? r[0] : r[1];
+    }
+    }
+}
+
 template <typename K>
-__device__ __forceinline__ K shfl_xor_key(K v, int m) {
+__device__ __forceinline__ K shfl_xor_key(K v, int m, int lane) {
     if constexpr (sizeof(K) == 8) {
-        const uint32_t lo = __shfl_xor((uint32_t)v, m, 64);
-        const uint32_t hi = __shfl_xor((uint32_t)(v >> 32), m, 64);
+        const uint32_t lo = xor_lane((uint32_t)v, m, lane);
+        const uint32_t hi = xor_lane((uint32_t)(v >> 32), m, lane);
         return ((K)hi << 32) | lo;
     } else {
-        return __shfl_xor(v, m, 64);
+        return xor_lane(v, m, lane);
     }
 }
 
@@ -98,7 +133,7 @@ __device__ __forceinline__ K wave_sort64(K v, int lane) {
     for (int size = 2; size <= 64; size <<= 1) {
 #pragma unroll
         for (int j = size >> 1; j > 0; j >>= 1) {
-            const K o = shfl_xor_key(v, j);
+            const K o = shfl_xor_key(v, j, lane);
             const bool keep_min = ((lane & j) == 0) == ((lane & size) == 0);
             v = keep_min ? (o < v ? o : v) : (o < v ? v : o);
         }
@@ -117,9 +152,9 @@ __device__ __forceinline__ bool ki_less(uint64_t ka, int ia, uint64_t kb, int ib
 // One compare-exchange step of the 128-wide network on register r of this
 // lane against lane ^ j (same register), keeping the min iff keep_min.
 template <typename K>
-__device__ __forceinline__ void cx_lane(K &k, int &i, int j, bool keep_min) {
-    const K ok = shfl_xor_key(k, j);
-    const int oi = __shfl_xor(i, j, 64);
+__device__ __forceinline__ void cx_lane(K &k, int &i, int j, bool keep_min, int lane) {
+    const K ok = shfl_xor_key(k, j, lane);
+    const int oi = (int)xor_lane((uint32_t)i, j, lane);
     const bool take = ki_less(ok, oi, k, i) == keep_min;
     k = take ? ok : k;
     i = take ? oi : i;
@@ -145,8 +180,8 @@ __device__ __forceinline__ void wave_sort128(K &k0, int &i0, K &k1, int &i1, int
             } else {
                 // element p = lane (+64): ascending block iff (p & size) == 0
                 const bool lower = (lane & j) == 0;
-                cx_lane(k0, i0, j, lower == ((lane & size) == 0));
-                cx_lane(k1, i1, j, lower == (((lane + 64) & size) == 0));
+                cx_lane(k0, i0, j, lower == ((lane & size) == 0), lane);
+                cx_lane(k1, i1, j, lower == (((lane + 64) & size) == 0), lane);
             }
         }
     }

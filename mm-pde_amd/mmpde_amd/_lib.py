@@ -13,7 +13,7 @@ import os
 import torch
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libmmpde_hip.so")
-ABI_VERSION = 10300
+ABI_VERSION = 10400
 
 ACT_NONE, ACT_TANH, ACT_RELU = 0, 1, 2
 # message_net_2 edge GEMM arithmetic (include/mmpde_hip.h MMPDE_EDGE_GEMM_*)
@@ -109,6 +109,10 @@ _SIGS = {
     "mmpde_dmm_workspace_bytes": (_I64, [_I64, _I64, _I, _I]),
     "mmpde_dmm_mesh_graph": (_I, [_P, _P, _I64, _I64, _P, _I, _P, _P, _P, _P, _P]),
     "mmpde_dmm_mesh_array": (_I, [_P, _P, _I64, _I64, _P, _P, _P, _P, _P]),
+    "mmpde_dmm_head_cache_bytes": (_I64, [_I64, _I]),
+    "mmpde_dmm_head_prepare": (_I, [_P, _I64, _P, _P, _P, _P]),
+    "mmpde_dmm_mesh_graph_cached": (_I, [_P, _P, _I64, _I64, _P, _I, _P, _P, _P, _P, _P, _P]),
+    "mmpde_dmm_mesh_array_cached": (_I, [_P, _P, _I64, _I64, _P, _P, _P, _P, _P, _P]),
     "mmpde_itp_pack_bytes": (_I64, []),
     "mmpde_itp_pack": (_I, [_P, _P, _P]),
     "mmpde_itp_interp": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _P, _P, _P, _P]),

@@ -197,12 +197,32 @@ class DMM(nn.Module):
         return self._grid_cache[key]
 
     # ----------------------------------------------------------------- the API
+    def head_cache(self, xi: torch.Tensor, workspace: torch.Tensor | None = None) -> torch.Tensor:
+        """The grid side of the head (trunk(xi), Q, J = dQ/dxi): a function of xi
+        and the weights only, prepared once for a rollout over a fixed grid and
+        passed to mesh(..., head_cache=).  Recompute it after changing weights."""
+        L.require_device(xi)
+        _, hd = self.device_params()
+        xi = L.f32c(xi).reshape(-1, 2)
+        N = xi.shape[0]
+        if workspace is None:
+            nb = L.lib().mmpde_dmm_workspace_bytes(1, N, hd.latent, hd.hidden)
+            workspace = torch.empty((nb // 4,), dtype=torch.float32, device=xi.device)
+        cache = torch.empty((L.lib().mmpde_dmm_head_cache_bytes(N, hd.hidden) // 4,),
+                            dtype=torch.float32, device=xi.device)
+        L.check(L.lib().mmpde_dmm_head_prepare(L.ptr(xi), N, ctypes.byref(hd), L.ptr(workspace),
+                                               L.ptr(cache), L.stream(xi.device)),
+                "mmpde_dmm_head_prepare")
+        return cache
+
     def mesh(self, u: torch.Tensor, xi: torch.Tensor, out: torch.Tensor | None = None,
-             workspace: torch.Tensor | None = None) -> torch.Tensor:
+             workspace: torch.Tensor | None = None,
+             head_cache: torch.Tensor | None = None) -> torch.Tensor:
         """Moved mesh x = xi + d(phi)/d(xi) for every trajectory.
         u: graph mode [B, N] (values on the fixed grid), array mode [B, s, s];
         xi: [N, 2] grid shared by all trajectories (graph: self.ori_grid;
-        array: the np.meshgrid 'xy' grid of data_creator_2d.py:94-100).
+        array: the np.meshgrid 'xy' grid of data_creator_2d.py:94-100);
+        head_cache: head_cache(xi) of the same xi and weights, or None.
         Returns [B*N, 2] fp32."""
         L.require_device(u, xi)
         bp, hd = self.device_params()
@@ -214,15 +234,19 @@ class DMM(nn.Module):
             workspace = torch.empty((nb // 4,), dtype=torch.float32, device=u.device)
         if out is None:
             out = torch.empty((B * N, 2), dtype=torch.float32, device=u.device)
+        if head_cache is not None:
+            L.require_device(head_cache)
+            if head_cache.numel() * 4 < L.lib().mmpde_dmm_head_cache_bytes(N, hd.hidden):
+                raise ValueError("head_cache is smaller than mmpde_dmm_head_cache_bytes")
+        hc = L.ptr(head_cache) if head_cache is not None else None
         st = L.stream(u.device)
         if self.mode == "graph":
             nbr = self.grid_nbr(xi)
-            L.check(L.lib().mmpde_dmm_mesh_graph(L.ptr(u), L.ptr(xi), B, N, L.ptr(nbr),
-                                                 nbr.shape[1], ctypes.byref(bp), ctypes.byref(hd),
-                                                 L.ptr(workspace), L.ptr(out), st),
-                    "mmpde_dmm_mesh_graph")
+            L.check(L.lib().mmpde_dmm_mesh_graph_cached(
+                L.ptr(u), L.ptr(xi), B, N, L.ptr(nbr), nbr.shape[1], ctypes.byref(bp),
+                ctypes.byref(hd), hc, L.ptr(workspace), L.ptr(out), st), "mmpde_dmm_mesh_graph")
         else:
-            L.check(L.lib().mmpde_dmm_mesh_array(L.ptr(u), L.ptr(xi), B, N, ctypes.byref(bp),
-                                                 ctypes.byref(hd), L.ptr(workspace), L.ptr(out),
-                                                 st), "mmpde_dmm_mesh_array")
+            L.check(L.lib().mmpde_dmm_mesh_array_cached(
+                L.ptr(u), L.ptr(xi), B, N, ctypes.byref(bp), ctypes.byref(hd), hc,
+                L.ptr(workspace), L.ptr(out), st), "mmpde_dmm_mesh_array")
         return out

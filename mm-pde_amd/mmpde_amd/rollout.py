@@ -18,8 +18,10 @@ reads, so the rollout (which has no labels) does not compute it.
 
 Rollout: the prediction becomes the next step's input (u <- pred, t index + 1),
 which the reference itself never does (it only evaluates one-step losses,
-SURVEY.md §3); ``step`` is that one-step forward.  The fixed-grid graph
-(``nbr_u``) is built once at construction (it depends only on the grid).
+SURVEY.md §3); ``step`` is that one-step forward.  What depends only on the
+fixed grid and the weights is built once at construction: the fixed-grid graph
+(``nbr_u``) and the DMM head's grid side (trunk(xi), Q, J; ``dmm_cache``).
+Changing weights after construction needs a new engine.
 """
 from __future__ import annotations
 
@@ -66,6 +68,8 @@ class MMPDERollout:
                 self.xi = self.grid
             for mode in ("1", "2") if kind == "burgers" else ("2",):
                 itp.packed(mode)
+            # the DMM head's grid side depends on xi and the weights only
+            self.dmm_cache = dmm.head_cache(self.xi, workspace=self.ws_dmm)
 
     def _trace(self):
         return self.trace_hook() if self.trace_hook is not None else None
@@ -82,7 +86,8 @@ class MMPDERollout:
         if not self.moving_mesh:
             return self.model(_Nodes(u_flat, self.pos_u, self.nbr_u), out=self.out_u,
                               workspace=self.ws_gnn, trace=self._trace()).reshape(u.shape)
-        mesh = self.dmm.mesh(u, self.xi, out=self.mesh, workspace=self.ws_dmm)
+        mesh = self.dmm.mesh(u, self.xi, out=self.mesh, workspace=self.ws_dmm,
+                             head_cache=self.dmm_cache)
         self.pos_m[:, 1:3] = mesh
         self._set_t(self.pos_m, step_idx)
         nbr_m = ops.knn_graph_nbr(mesh, B, self.gc.n)

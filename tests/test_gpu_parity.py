@@ -248,6 +248,27 @@ def test_dmm_mesh_array_matches_autograd(dev):
     _close(got, ref, 0.0, 2e-6, "dmm array mesh")
 
 
+@pytest.mark.parametrize("kind", ["cy", "burgers"])
+def test_dmm_head_cache_identical(dev, kind):
+    """A prepared grid-side head (trunk, Q, J of the fixed xi) gives the same mesh,
+    bit for bit, as computing it inside the call."""
+    from mmpde_amd.synth import build_models, burgers_grid_points, fields
+
+    pde, _, _, _, dmm, gc = build_models(kind)
+    B = 4
+    dmm.to(dev)
+    if kind == "cy":
+        xi = pde.ori_grid.to(dev)
+        u = fields(pde.ori_grid, B, 30)[:, 7].to(dev).contiguous()
+    else:
+        xi = gc.xi_grid_xy(48, 48, dev)
+        u = fields(burgers_grid_points(), B, 31).reshape(B, 31, 48, 48)[:, 7].to(dev).contiguous()
+    cache = dmm.head_cache(xi)
+    a = dmm.mesh(u, xi)
+    b = dmm.mesh(u, xi, head_cache=cache)
+    assert torch.equal(a, b)
+
+
 # ============================================================================ ItpNet
 @pytest.mark.parametrize("mode", ["1", "2"])
 def test_itp_interp_matches_oracle(dev, mode):
