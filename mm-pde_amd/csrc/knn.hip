@@ -160,6 +160,18 @@ __device__ __forceinline__ void cx_lane(K &k, int &i, int j, bool keep_min, int 
     i = take ? oi : i;
 }
 
+// Bitonic sort of 64 (key, index) pairs, one per lane, ordered
+// lexicographically (the reference's tie order).  Ascending in lane.
+template <typename K>
+__device__ __forceinline__ void wave_sort64_ki(K &k, int &i, int lane) {
+#pragma unroll
+    for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+        for (int j = size >> 1; j > 0; j >>= 1)
+            cx_lane(k, i, j, ((lane & j) == 0) == ((lane & size) == 0), lane);
+    }
+}
+
 // Bitonic sort of 128 (key, index) pairs ordered lexicographically (the
 // reference's tie order), two per lane: element p lives in lane p & 63,
 // register p >> 6.  Ascending in p.
@@ -242,8 +254,20 @@ __global__ __launch_bounds__(256) void knn_kernel(const float2 *__restrict__ pts
         key_t mk = ~key_t(0);
         int mi = 0x7fffffff;
         int rank = lane;
-        if (m <= 128) {
-            // Small candidate list (the common case): one 128-wide bitonic sort.
+        if (m <= 64) {
+            // The common case (a mesh point's list holds ~1.5 kk): one pair per
+            // lane, one 64-wide bitonic sort.
+            wave_lds_sync();
+            key_t k0 = ~key_t(0);
+            int i0 = 0x7fffffff;
+            if (lane < m) {
+                i0 = sIdx[wave][lane];
+                k0 = KT::key(sP[i0], q);
+            }
+            wave_sort64_ki(k0, i0, lane);
+            if (lane < kk) mi = i0;
+        } else if (m <= 128) {
+            // Two pairs per lane, one 128-wide bitonic sort.
             wave_lds_sync();
             key_t k0 = ~key_t(0), k1 = ~key_t(0);
             int i0 = 0x7fffffff, i1 = 0x7fffffff;
