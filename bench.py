@@ -15,8 +15,9 @@ data-path collective).  value = node-updates/s of the whole job
 Also reported (rank 0):
 * roofline: the dominant kernel (GNN edge stage, 12 launches per step) timed
   live with hipEvents recorded on its own stream around every launch, in a
-  second timed pass of the same K steps (an event record between launches
-  costs the stream ~10 us, so the pass that sets `value` records none);
+  second timed pass of the same K steps run on ONE stream (the pass that sets
+  `value` runs the fixed-grid model on a side stream beside the moving-mesh
+  chain, where two edge kernels can share the GPU, and records no events);
   achieved = algorithmic FLOP per launch / mean launch time.
 * cpu_baseline (N = 1 only): the CPU oracle (op-for-op restatement of the
   reference, oracle/refcpu.py) timed on a bounded sample on this host.
@@ -205,10 +206,11 @@ def main():
 
     def timed_run(mode, trace):
         """W warmup + K timed autoregressive steps from u0; returns (max-over-ranks
-        seconds, final state)."""
+        seconds, final state).  trace: record the edge-kernel events, one stream."""
         for m in (model, model_b):
             if m is not None:
                 m.edge_gemm = mode
+        eng.overlap = not trace
         u = u0
         with torch.no_grad():
             for i in range(args.warmup):

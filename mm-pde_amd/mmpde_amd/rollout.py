@@ -41,6 +41,9 @@ class MMPDERollout:
         self.device = torch.device(device)
         self.moving_mesh = moving_mesh
         self.trace_hook = None   # callable() -> _lib.GnnTrace | None, one per GNN forward
+        # run the fixed-grid model beside the moving-mesh chain (False: one stream,
+        # e.g. to time single kernels without a concurrent neighbour)
+        self.overlap = True
         gc = graph_creator
         self.grid = gc.uniform_grid(self.device).contiguous()           # [N, 2]
         self.N = N = self.grid.shape[0]
@@ -70,6 +73,10 @@ class MMPDERollout:
                 itp.packed(mode)
             # the DMM head's grid side depends on xi and the weights only
             self.dmm_cache = dmm.head_cache(self.xi, workspace=self.ws_dmm)
+            # the fixed-grid model depends on u only: it runs on a side stream,
+            # with its own workspace, beside the moving-mesh chain
+            self.side = torch.cuda.Stream(self.device)
+            self.ws_gnn_u = torch.empty_like(self.ws_gnn)
 
     def _trace(self):
         return self.trace_hook() if self.trace_hook is not None else None
@@ -86,6 +93,13 @@ class MMPDERollout:
         if not self.moving_mesh:
             return self.model(_Nodes(u_flat, self.pos_u, self.nbr_u), out=self.out_u,
                               workspace=self.ws_gnn, trace=self._trace()).reshape(u.shape)
+        cur = torch.cuda.current_stream(self.device)
+        side = self.side if self.overlap else cur
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            u.record_stream(side)
+            out_u = self.model(_Nodes(u_flat, self.pos_u, self.nbr_u), out=self.out_u,
+                               workspace=self.ws_gnn_u, trace=self._trace())
         mesh = self.dmm.mesh(u, self.xi, out=self.mesh, workspace=self.ws_dmm,
                              head_cache=self.dmm_cache)
         self.pos_m[:, 1:3] = mesh
@@ -103,8 +117,7 @@ class MMPDERollout:
         idx2 = ops.knn_query(mesh, self.grid_rep, B, 30)
         interp = ops.itp_interp(mesh, out_b, self.grid_rep, idx2, B, self.itp.packed("2"),
                                 addend=res)
-        out_u = self.model(_Nodes(u_flat, self.pos_u, self.nbr_u), out=self.out_u,
-                           workspace=self.ws_gnn, trace=self._trace())
+        cur.wait_stream(side)
         return torch.add(interp, out_u.reshape(-1)).reshape(u.shape)
 
     def rollout(self, u0: torch.Tensor, start_step: int, n_steps: int):
