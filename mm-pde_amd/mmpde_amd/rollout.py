@@ -77,6 +77,10 @@ class MMPDERollout:
             # with its own workspace, beside the moving-mesh chain
             self.side = torch.cuda.Stream(self.device)
             self.ws_gnn_u = torch.empty_like(self.ws_gnn)
+            # the kNN-30 query onto the fixed grid and res_cut need only the mesh
+            # and u: a second side stream runs them beside the moved-mesh graph
+            # and model_b
+            self.side2 = torch.cuda.Stream(self.device)
 
     def _trace(self):
         return self.trace_hook() if self.trace_hook is not None else None
@@ -102,19 +106,28 @@ class MMPDERollout:
                                workspace=self.ws_gnn_u, trace=self._trace())
         mesh = self.dmm.mesh(u, self.xi, out=self.mesh, workspace=self.ws_dmm,
                              head_cache=self.dmm_cache)
+        side2 = self.side2 if self.overlap else cur
+        side2.wait_stream(cur)
+        with torch.cuda.stream(side2):
+            u.record_stream(side2)
+            idx2 = ops.knn_query(mesh, self.grid_rep, B, 30)
+            if self.kind == "burgers":
+                res = self.itp.res_cut(u.reshape(B, 1, self.s, self.s)).reshape(-1)
+            else:
+                res = self.itp.res_cut(u.reshape(B, N)).reshape(-1)
+            idx2.record_stream(cur)
+            res.record_stream(cur)
         self.pos_m[:, 1:3] = mesh
         self._set_t(self.pos_m, step_idx)
         nbr_m = ops.knn_graph_nbr(mesh, B, self.gc.n)
         if self.kind == "burgers":
             idx1 = ops.knn_query(self.grid_rep, mesh, B, 30)
             u_m = ops.itp_interp(self.grid_rep, u_flat, mesh, idx1, B, self.itp.packed("1"))
-            res = self.itp.res_cut(u.reshape(B, 1, self.s, self.s)).reshape(-1)
         else:
             u_m = u_flat
-            res = self.itp.res_cut(u.reshape(B, N)).reshape(-1)
         out_b = self.model_b(_Nodes(u_m, self.pos_m, nbr_m), out=self.out_b,
                              workspace=self.ws_gnn, trace=self._trace())
-        idx2 = ops.knn_query(mesh, self.grid_rep, B, 30)
+        cur.wait_stream(side2)
         interp = ops.itp_interp(mesh, out_b, self.grid_rep, idx2, B, self.itp.packed("2"),
                                 addend=res)
         cur.wait_stream(side)
