@@ -95,7 +95,8 @@ constexpr int EDGE_NC = MMPDE_EDGE_NC;
 constexpr int EDGE_NP = MMPDE_EDGE_NP;
 
 // PH: bit 0 produce, bit 1 consume (MFMA), bit 2 skip the gathers, bit 3 raise
-// the consumer waves' issue priority, bit 4 (NC == 2) split each round's slots
+// the consumer waves' issue priority, bit 5 replace the producer's split by a
+// bare conversion, bit 6 store one ring piece in four (both timing only), bit 4 (NC == 2) split each round's slots
 // between the two consumer waves of a SIMD, which then own the same 32 output
 // columns (half the LDS operand reads of column-split waves), bit 10 record
 // per-round s_memtime stamps of block 0.  Bits other than 0, 1 and 4 are for
@@ -225,6 +226,7 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
 #pragma unroll
                 for (int i = 0; i < NPC; ++i) acur[i] = *(const float4 *)(ar + piece(i));
                 float4 *dst = ring + (slot * ESL + pw) * SLOT4 + i0 * 64 + lane;
+                uint32_t fold = 0;
 #pragma unroll
                 for (int h2 = 0; h2 < NPC / 2; ++h2) {
                     const float4 &a0 = acur[2 * h2], &a1 = acur[2 * h2 + 1];
@@ -236,9 +238,24 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
                         m1 = make_float4(fmaf(b1.x, sc, a1.x), fmaf(b1.y, sc, a1.y), fmaf(b1.z, sc, a1.z),
                                          fmaf(b1.w, sc, a1.w));
                         half8 hi, lo;
-                        split8_relu_rtz(m0, m1, hi, lo);
-                        dst[(2 * h2 + 0) * 64] = *(const float4 *)&hi;
-                        dst[(2 * h2 + 1) * 64] = *(const float4 *)&lo;
+                        if (PH & 32) {  // profiling: conversion only, no split (wrong values)
+                            const uint32_t w[4] = {
+                                __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(m0.x, m0.y)),
+                                __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(m0.z, m0.w)),
+                                __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(m1.x, m1.y)),
+                                __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(m1.z, m1.w))};
+                            hi = *(const half8 *)w;
+                            lo = hi;
+                        } else {
+                            split8_relu_rtz(m0, m1, hi, lo);
+                        }
+                        if (!(PH & 64) || h2 == 0) {
+                            dst[(2 * h2 + 0) * 64] = *(const float4 *)&hi;
+                            dst[(2 * h2 + 1) * 64] = *(const float4 *)&lo;
+                        } else {  // profiling: one store in four, the rest folded (kept live)
+                            const uint32_t *hw = (const uint32_t *)&hi, *lw = (const uint32_t *)&lo;
+                            fold ^= hw[0] ^ hw[1] ^ hw[2] ^ hw[3] ^ lw[0] ^ lw[1] ^ lw[2] ^ lw[3];
+                        }
                     } else {
                         m0 = make_float4(fmaxf(a0.x + b0.x, 0.0f), fmaxf(a0.y + b0.y, 0.0f),
                                          fmaxf(a0.z + b0.z, 0.0f), fmaxf(a0.w + b0.w, 0.0f));
@@ -248,6 +265,7 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
                         dst[(2 * h2 + 1) * 64] = m1;
                     }
                 }
+                if ((PH & 64) && fold == 0x9e3779b9u) dst[64] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             }
             cP.next(rpt);
             // gather the round two ahead into the registers just consumed
@@ -430,6 +448,11 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
             __syncthreads();
             if ((PH & 1024) && blockIdx.x == 0 && lane == 0 && it < 256)
                 p.stamps[2 * 256 * wave + 2 * it + 1] = __builtin_amdgcn_s_memtime();
+            if ((PH & 1024) && blockIdx.x == 0 && tid == 0 && (it == 0 || it == NIT2 - 1)) {
+                // shader clock vs the 100 MHz constant clock, first / last round
+                p.stamps[12 * 2 * 256 + (it ? 2 : 0)] = __builtin_amdgcn_s_memtime();
+                p.stamps[12 * 2 * 256 + (it ? 3 : 1)] = __builtin_amdgcn_s_memrealtime();
+            }
         }
         finish_pending();  // the loop ends with a barrier
     }

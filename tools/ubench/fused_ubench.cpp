@@ -117,8 +117,8 @@ int main(int argc, char **argv) {
     int cus = device_cus();
     const int grid_e = ntiles < cus ? (int)ntiles : cus;
     uint64_t *stamps;
-    CK(hipMalloc(&stamps, 12 * 2 * 256 * 8));
-    CK(hipMemset(stamps, 0, 12 * 2 * 256 * 8));
+    CK(hipMalloc(&stamps, (12 * 2 * 256 + 4) * 8));
+    CK(hipMemset(stamps, 0, (12 * 2 * 256 + 4) * 8));
     EdgeArgs e32{a, b, nbr, n, k, (int)ntiles, w2, b2, nullptr, nullptr, mean, stamps};
     EdgeArgs e16{a, b, nbr, n, k, (int)ntiles, w2, b2, pack, amax, mean, stamps};
     NodeArgs nd{h, mean, n, u1, c1, 260, u2, c2, bnw, bnb, bnm, bnv, 1e-5f, ho, w1, b1, 260, ao, bo,
@@ -135,9 +135,13 @@ int main(int argc, char **argv) {
     printf("edge f16x3 slot-split NC2NP1 prio %.1f  noprio %.1f | NC2NP2 prio %.1f | column-split NC2NP1 prio %.1f\n",
            edge(gnn_edge_kernel<true, 27, 2, 1>, 12, e16), edge(gnn_edge_kernel<true, 19, 2, 1>, 12, e16),
            edge(gnn_edge_kernel<true, 27, 2, 2>, 16, e16), edge(gnn_edge_kernel<true, 11, 2, 1>, 12, e16));
-    printf("edge f16x3 slot-split NC2NP1: consume-only %.1f | no-gather %.1f | produce-only %.1f\n",
+    printf("edge f16x3 slot-split NC2NP1: consume-only %.1f | no-gather %.1f | produce-only %.1f | "
+           "cvt-only producer %.1f (no gather %.1f)\n",
            edge(gnn_edge_kernel<true, 26, 2, 1>, 12, e16), edge(gnn_edge_kernel<true, 31, 2, 1>, 12, e16),
-           edge(gnn_edge_kernel<true, 25, 2, 1>, 12, e16));
+           edge(gnn_edge_kernel<true, 25, 2, 1>, 12, e16), edge(gnn_edge_kernel<true, 27 + 32, 2, 1>, 12, e16),
+           edge(gnn_edge_kernel<true, 31 + 32, 2, 1>, 12, e16));
+    printf("edge f16x3 slot-split NC2NP1: quarter ring stores %.1f (no gather %.1f)\n",
+           edge(gnn_edge_kernel<true, 27 + 64, 2, 1>, 12, e16), edge(gnn_edge_kernel<true, 31 + 64, 2, 1>, 12, e16));
     {   // slot-split vs column-split consumers: same sums, same order per target
         std::vector<float> m0(n * H), m1(n * H);
         hipLaunchKernelGGL((gnn_edge_kernel<true, 11, 2, 1>), dim3(grid_e), dim3(768), 0, 0, e16);
@@ -152,10 +156,16 @@ int main(int argc, char **argv) {
         printf("slot-split vs column-split: max|diff| %.3e (max|mean| %.3e)\n", d, mx);
     }
     {   // per-round barrier arrival / release times of block 0 (waves 0..7, lane 0)
-        hipLaunchKernelGGL((gnn_edge_kernel<true, 1024 + 3, 1, 2>), dim3(grid_e), dim3(768), 0, 0, e16);
+        hipLaunchKernelGGL((gnn_edge_kernel<true, 1024 + 27, 2, 1>), dim3(grid_e), dim3(768), 0, 0, e16);
         CK(hipDeviceSynchronize());
-        std::vector<uint64_t> st(12 * 2 * 256);
+        std::vector<uint64_t> st(12 * 2 * 256 + 4);
         CK(hipMemcpy(st.data(), stamps, st.size() * 8, hipMemcpyDeviceToHost));
+        {
+            const double dt = (double)(st[12 * 2 * 256 + 2] - st[12 * 2 * 256]);
+            const double dr = (double)(st[12 * 2 * 256 + 3] - st[12 * 2 * 256 + 1]);
+            printf("edge kernel shader clock (block 0, s_memtime / s_memrealtime at 100 MHz): %.0f MHz over %.1f us\n",
+                   dr > 0 ? 100.0 * dt / dr : 0.0, dr / 100.0);
+        }
         printf("round stamps (s_memtime, relative): it | arrive c0 c1 c2 c3 p0 p1 p2 p3 | release c0\n");
         const uint64_t t0 = st[0];
         for (int i = 0; i < 40; ++i) {
