@@ -96,7 +96,8 @@ constexpr int EDGE_NP = MMPDE_EDGE_NP;
 
 // PH: bit 0 produce, bit 1 consume (MFMA), bit 2 skip the gathers, bit 3 raise
 // the consumer waves' issue priority, bit 5 replace the producer's split by a
-// bare conversion, bit 6 store one ring piece in four (both timing only), bit 4 (NC == 2) split each round's slots
+// bare conversion, bit 6 store one ring piece in four (both timing only), bit 7
+// re-read the tile's a rows every round, bit 4 (NC == 2) split each round's slots
 // between the two consumer waves of a SIMD, which then own the same 32 output
 // columns (half the LDS operand reads of column-split waves), bit 10 record
 // per-round s_memtime stamps of block 0.  Bits other than 0, 1 and 4 are for
@@ -222,9 +223,13 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
             s_fill = src_of(c3);
             c3.next(rpt);
             if (PH & 1) {
-                const float *ar = &a_lds[cP.j & 1][r * NLDA];
+                // the a rows of a tile are the same for all its rounds: read them
+                // from LDS once per tile (PH bit 7: every round)
+                if ((PH & 128) || cP.rd == 0) {
+                    const float *ar = &a_lds[cP.j & 1][r * NLDA];
 #pragma unroll
-                for (int i = 0; i < NPC; ++i) acur[i] = *(const float4 *)(ar + piece(i));
+                    for (int i = 0; i < NPC; ++i) acur[i] = *(const float4 *)(ar + piece(i));
+                }
                 float4 *dst = ring + (slot * ESL + pw) * SLOT4 + i0 * 64 + lane;
                 uint32_t fold = 0;
 #pragma unroll

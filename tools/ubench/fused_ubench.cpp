@@ -140,6 +140,8 @@ int main(int argc, char **argv) {
            edge(gnn_edge_kernel<true, 26, 2, 1>, 12, e16), edge(gnn_edge_kernel<true, 31, 2, 1>, 12, e16),
            edge(gnn_edge_kernel<true, 25, 2, 1>, 12, e16), edge(gnn_edge_kernel<true, 27 + 32, 2, 1>, 12, e16),
            edge(gnn_edge_kernel<true, 31 + 32, 2, 1>, 12, e16));
+    printf("edge f16x3 slot-split NC2NP1: a rows re-read every round %.1f\n",
+           edge(gnn_edge_kernel<true, 27 + 128, 2, 1>, 12, e16));
     printf("edge f16x3 slot-split NC2NP1: quarter ring stores %.1f (no gather %.1f)\n",
            edge(gnn_edge_kernel<true, 27 + 64, 2, 1>, 12, e16), edge(gnn_edge_kernel<true, 31 + 64, 2, 1>, 12, e16));
     {   // slot-split vs column-split consumers: same sums, same order per target
@@ -154,6 +156,16 @@ int main(int argc, char **argv) {
             mx = std::max(mx, (double)std::fabs(m0[i]));
         }
         printf("slot-split vs column-split: max|diff| %.3e (max|mean| %.3e)\n", d, mx);
+    }
+    {   // shader clock of the consume-only variant (ring operands never written)
+        hipLaunchKernelGGL((gnn_edge_kernel<true, 1024 + 26, 2, 1>), dim3(grid_e), dim3(768), 0, 0, e16);
+        CK(hipDeviceSynchronize());
+        std::vector<uint64_t> c(4);
+        CK(hipMemcpy(c.data(), stamps + 12 * 2 * 256, 4 * 8, hipMemcpyDeviceToHost));
+        const double dr = (double)(c[3] - c[1]);
+        printf("consume-only shader clock: %.0f MHz over %.1f us\n",
+               dr > 0 ? 100.0 * (double)(c[2] - c[0]) / dr : 0.0, dr / 100.0);
+        fflush(stdout);
     }
     {   // per-round barrier arrival / release times of block 0 (waves 0..7, lane 0)
         hipLaunchKernelGGL((gnn_edge_kernel<true, 1024 + 27, 2, 1>), dim3(grid_e), dim3(768), 0, 0, e16);
