@@ -70,6 +70,19 @@ int mmpde_knn_graph(const float *pos, int64_t batches, int64_t n_per, int k,
 int mmpde_knn_query(const float *src, const float *qry, int64_t batches, int64_t n_src,
                     int64_t n_qry, int k, int32_t *idx_out, mmpde_stream_t stream);
 
+/* torch_cluster.radius_graph(pos, r, batch, loop=False, max_num_neighbors)
+ * (data_creator_2d.py:257-258, connect_edge='radius'; r at :195 / :226) for
+ * `batches` equal contiguous segments of n_per points, CUDA semantics: each
+ * query keeps the first max_num_neighbors + 1 points of its segment in index
+ * order with squared distance (fmaf(dy, dy, dx*dx), fp32) < (float)(r*r),
+ * itself included, then the self loop is dropped.
+ * nbr_out [n, max_num_neighbors + 1] int32 global source indices ascending,
+ * padded with -1; degree_out [n] entries kept per row -- pass both to
+ * mmpde_gnn_forward_ex (k = max_num_neighbors + 1, exec->degree). */
+int mmpde_radius_graph(const float *pos, int64_t batches, int64_t n_per, float r,
+                       int max_num_neighbors, int32_t *nbr_out, int32_t *degree_out,
+                       mmpde_stream_t stream);
+
 /* PyG edge_index (int64 [2, n*k]) from a target-major neighbour table.
  * Row 0 = source (nbr), row 1 = target. (data_creator_2d.py:260-262) */
 int mmpde_edge_index_from_nbr(const int32_t *nbr, int64_t n, int k, int64_t *edge_index,
@@ -200,6 +213,10 @@ typedef struct {
                                 layers (caller-cached); NULL: packed per call into the
                                 workspace */
     void *const *node_end;   /* n_layers hipEvent_t, or NULL */
+    const int32_t *degree;   /* [n] in-degree of every target for a ragged nbr table (row i
+                                holds degree[i] sources, the rest of its k entries are
+                                ignored; PyG mean = sum / max(degree, 1)), e.g. from
+                                mmpde_radius_graph; NULL: every row holds k */
 } mmpde_gnn_exec;
 
 /* Most layers mmpde_gnn_forward_ex accepts (sizes the workspace's packed

@@ -517,7 +517,8 @@ extern "C" int mmpde_gnn_forward_ex(const float *u, const float *pos, int64_t n,
         const uint32_t *ain = pack ? amax + 2 * kAmaxShards * l : nullptr;
         uint32_t *aout = pack && next ? amax + 2 * kAmaxShards * (l + 1) : nullptr;
         if (eb && hipEventRecord(eb, st) != hipSuccess) return MMPDE_ERR_INVALID_ARG;
-        rc = launch_edge_stage(wa, wb, nbr, n, k, &layers[l], pk, ain, wmean, st);
+        rc = launch_edge_stage(wa, wb, nbr, exec ? exec->degree : nullptr, n, k, &layers[l], pk,
+                               ain, wmean, st);
         if (rc) return rc;
         if (ee && hipEventRecord(ee, st) != hipSuccess) return MMPDE_ERR_INVALID_ARG;
         // a, b are rewritten in place: this layer's edge stage has consumed them

@@ -396,6 +396,40 @@ int launch_knn(const float *pts, const float *qry, int64_t batches, int64_t n_sr
     return MMPDE_ERR_UNSUPPORTED;
 }
 
+// torch_cluster radius_graph(x, r, batch, loop=False, max_num_neighbors)
+// (reference data_creator_2d.py:257-258): radius(x, x, ..., max_num_neighbors
+// + 1) scans the query's segment in index order and keeps the first w = max_nn
+// + 1 points with d2 < r2 (the query itself included), then the self loop is
+// dropped.  One wave per query, 64 candidates per step, ballot order = index
+// order; stops once w points were taken.  nbr [n, w] global sources ascending,
+// padded with -1; deg [n] = entries kept (w - 1 or w).
+__global__ __launch_bounds__(256) void radius_kernel(const float2 *__restrict__ pts, int n_per,
+                                                     float r2, int w, int32_t *__restrict__ nbr,
+                                                     int32_t *__restrict__ deg) {
+    const int b = blockIdx.y;
+    const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (q >= n_per) return;  // wave-uniform: no barrier below
+    const float2 *P = pts + (int64_t)b * n_per;
+    const float2 qp = P[q];
+    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    int32_t *row = nbr + ((int64_t)b * n_per + q) * w;
+    int taken = 0, kept = 0;
+    for (int j0 = 0; j0 < n_per && taken < w; j0 += 64) {
+        const int j = j0 + lane;
+        const bool hit = j < n_per && key_f32(P[j], qp) < __float_as_uint(r2);
+        const uint64_t hm = __ballot(hit);
+        const bool take = hit && taken + __popcll(hm & below) < w;
+        const uint64_t tm = __ballot(take);
+        const uint64_t km = __ballot(take && j != q);  // self loop dropped
+        if (take && j != q) row[kept + __popcll(km & below)] = b * n_per + j;
+        taken += __popcll(tm);
+        kept += __popcll(km);
+    }
+    for (int e = kept + lane; e < w; e += 64) row[e] = -1;
+    if (lane == 0) deg[(int64_t)b * n_per + q] = kept;
+}
+
 __global__ void edge_index_kernel(const int32_t *__restrict__ nbr, int64_t n, int k,
                                   int64_t *__restrict__ ei) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -421,6 +455,21 @@ extern "C" int mmpde_knn_query(const float *src, const float *qry, int64_t batch
     MMPDE_REQUIRE(src && qry && idx_out);
     return launch_knn<true>(src, qry, batches, n_src, n_qry, k, idx_out, nullptr,
                             as_stream(stream));
+}
+
+extern "C" int mmpde_radius_graph(const float *pos, int64_t batches, int64_t n_per, float r,
+                                  int max_num_neighbors, int32_t *nbr_out, int32_t *degree_out,
+                                  mmpde_stream_t stream) {
+    MMPDE_REQUIRE(pos && nbr_out && degree_out);
+    MMPDE_REQUIRE(batches > 0 && batches <= 65535 && n_per > 0 && n_per <= INT32_MAX &&
+                  batches * n_per <= INT32_MAX && max_num_neighbors > 0 && r > 0.0f);
+    // torch_cluster squares r on the host in double and hands the kernel a float
+    const float r2 = (float)((double)r * (double)r);
+    hipLaunchKernelGGL(radius_kernel, dim3((unsigned)ceil_div(n_per, 4), (unsigned)batches),
+                       dim3(256), 0, as_stream(stream), (const float2 *)pos, (int)n_per, r2,
+                       max_num_neighbors + 1, nbr_out, degree_out);
+    MMPDE_RET_LAUNCH();
+    return MMPDE_OK;
 }
 
 extern "C" int mmpde_edge_index_from_nbr(const int32_t *nbr, int64_t n, int k,

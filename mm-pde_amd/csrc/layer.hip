@@ -73,6 +73,7 @@ struct EdgeArgs {
     const uint32_t *amax_in;   // F16X3: range slots of a, b
     float *mean;               // [n, 128]
     uint64_t *stamps;          // profiling builds (PH bit 10): per-round s_memtime of block 0
+    const int32_t *deg;        // RAGGED: in-degree of every target (nbr row entries past it are ignored)
 };
 
 struct RoundCtr {  // (tile j, round rd) of a running round index
@@ -121,7 +122,9 @@ constexpr int EDGE_PH = MMPDE_EDGE_PH;
 // multiplies every slot by its 32 / NC output columns of W2 (held in
 // registers for the whole launch).  One barrier per round; producers run EPF
 // rounds ahead; b rows are gathered two rounds before use.
-template <bool F16X3, int PH = EDGE_PH, int NC = EDGE_NC, int NP = EDGE_NP>
+// RAGGED: target i averages over its first deg[i] table entries (PyG / torch_scatter
+// mean over a variable in-degree: sum / max(deg, 1)); otherwise over all k.
+template <bool F16X3, int PH = EDGE_PH, int NC = EDGE_NC, int NP = EDGE_NP, bool RAGGED = false>
 __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(EdgeArgs p) {
     constexpr bool SPLIT = NC == 2 && (PH & 16);
     constexpr int CT = SPLIT ? 2 : 2 / NC;  // 16-column tiles per consumer wave
@@ -320,6 +323,7 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
             bias[cc] = (f32x4){bb, bb, bb, bb};
         }
         const float kdiv = (float)k;
+        int dg[4] = {k, k, k, k};  // RAGGED: in-degree of this lane's rows 4 g + t of the tile
         f32x4 S[CT], Ssave[CT];
 #pragma unroll
         for (int cc = 0; cc < CT; ++cc) S[cc] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
@@ -331,7 +335,8 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
                 const int col = 16 * (CT * cg + cc) + r;
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
-                    if (row0 + t < p.n) p.mean[(row0 + t) * LH + col] = T[cc][t] / kdiv;
+                    const float div = RAGGED ? (float)max(dg[t], 1) : kdiv;
+                    if (row0 + t < p.n) p.mean[(row0 + t) * LH + col] = T[cc][t] / div;
                 }
             }
         };
@@ -386,14 +391,19 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
                 }
             }
         };
-        // relu-sum of one slot; `valid` is wave-uniform (slots past k exist
-        // only in a tile's last round), so it is a branch, not a select
-        auto sum_into = [&](const f32x4 *acc, bool valid) {
-            if (!valid) return;
+        // relu-sum of slot e; e < k is wave-uniform (slots past k exist only
+        // in a tile's last round), so it is a branch, not a select; RAGGED adds
+        // the per-row e < deg select
+        auto sum_into = [&](const f32x4 *acc, int e) {
+            if (e >= k) return;
 #pragma unroll
             for (int cc = 0; cc < CT; ++cc) {
 #pragma unroll
-                for (int t = 0; t < 4; ++t) S[cc][t] = fmaf(fmaxf(acc[cc][t], 0.0f), inv[cc], S[cc][t]);
+                for (int t = 0; t < 4; ++t) {
+                    float v = fmaxf(acc[cc][t], 0.0f);
+                    if (RAGGED) v = e < dg[t] ? v : 0.0f;
+                    S[cc][t] = fmaf(v, inv[cc], S[cc][t]);
+                }
             }
         };
         float4 xa[4], xb[4], an[2 / NC];
@@ -415,21 +425,25 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
                 const float4 *base = ring + slot * ESL * SLOT4 + lane;
                 const float4 *nbase = ring + (slot == ERING - 1 ? 0 : slot + 1) * ESL * SLOT4 + lane;
                 if (it == EPF) rd_half(base + slotq(0) * SLOT4, 0, xa);
+                if (RAGGED && cC.rd == 0) {  // a new tile (after finish_pending used the last one's)
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) dg[t] = p.deg[tile_row(cC.j, 4 * g + t)];
+                }
                 f32x4 accP[CT];
 #pragma unroll
                 for (int qq = 0; qq < SPW; ++qq) {
                     f32x4 accN[CT];
                     rd_half(base + slotq(qq) * SLOT4, 1, xb);
                     mma_half(xa, 0, accN);
-                    if (qq > 0) sum_into(accP, ESL * cC.rd + slotq(qq - 1) < k);
+                    if (qq > 0) sum_into(accP, ESL * cC.rd + slotq(qq - 1));
                     if (qq < SPW - 1) rd_half(base + slotq(qq + 1) * SLOT4, 0, xa);
                     else if (it + 1 < NIT) rd_half(nbase + slotq(0) * SLOT4, 0, xa);
                     mma_half(xb, 1, accN);
 #pragma unroll
                     for (int cc = 0; cc < CT; ++cc) accP[cc] = accN[cc];
                 }
-                sum_into(accP, ESL * cC.rd + slotq(SPW - 1) < k);
-                if (cC.rd == rpt - 1) {  // tile complete: mean = sum / k (PyG mean, fixed degree)
+                sum_into(accP, ESL * cC.rd + slotq(SPW - 1));
+                if (cC.rd == rpt - 1) {  // tile complete: mean = sum / degree (PyG mean)
                     if (!SPLIT) {
                         write_mean(cC.j, S);
                     } else if (hs == 1) {  // hand the odd slots' sums to the partner wave
@@ -874,20 +888,25 @@ int device_cus() {
 #define MMPDE_NODE_RB 2
 #endif
 
-int launch_edge_stage(const float *a, const float *b, const int32_t *nbr, int64_t n, int k,
-                      const mmpde_gnn_layer_params *p, const char *pk, const uint32_t *amax_in,
-                      float *mean, hipStream_t st) {
+int launch_edge_stage(const float *a, const float *b, const int32_t *nbr, const int32_t *deg,
+                      int64_t n, int k, const mmpde_gnn_layer_params *p, const char *pk,
+                      const uint32_t *amax_in, float *mean, hipStream_t st) {
     MMPDE_REQUIRE(a && b && nbr && p && mean && n > 0 && k > 0 && n <= (int64_t)INT32_MAX);
     MMPDE_REQUIRE(al16(a) && al16(b) && al16(p->msg2_w) && al16(mean));
     MMPDE_REQUIRE(!pk || (amax_in && al16(pk)));
     const int64_t ntiles = (n + ET - 1) / ET;
     MMPDE_REQUIRE(ntiles * ((k + ESL - 1) / ESL) < (int64_t)INT32_MAX);
-    EdgeArgs e{a, b, nbr, n, k, (int)ntiles, p->msg2_w, p->msg2_b, pk, amax_in, mean, nullptr};
+    EdgeArgs e{a, b, nbr, n, k, (int)ntiles, p->msg2_w, p->msg2_b, pk, amax_in, mean, nullptr, deg};
     const int cus = device_cus();
     const int grid = ntiles < cus ? (int)ntiles : cus;
     const dim3 block(64 * (4 * EDGE_NC + 4 * EDGE_NP));
-    if (pk) hipLaunchKernelGGL(gnn_edge_kernel<true>, dim3(grid), block, 0, st, e);
-    else hipLaunchKernelGGL(gnn_edge_kernel<false>, dim3(grid), block, 0, st, e);
+    if (deg) {
+        if (pk) hipLaunchKernelGGL((gnn_edge_kernel<true, EDGE_PH, EDGE_NC, EDGE_NP, true>), dim3(grid), block, 0, st, e);
+        else hipLaunchKernelGGL((gnn_edge_kernel<false, EDGE_PH, EDGE_NC, EDGE_NP, true>), dim3(grid), block, 0, st, e);
+    } else {
+        if (pk) hipLaunchKernelGGL(gnn_edge_kernel<true>, dim3(grid), block, 0, st, e);
+        else hipLaunchKernelGGL(gnn_edge_kernel<false>, dim3(grid), block, 0, st, e);
+    }
     MMPDE_RET_LAUNCH();
     return MMPDE_OK;
 }

@@ -4,11 +4,12 @@
 #include "common.hpp"
 
 // Edge stage: mean[i] = (1/k) sum_e relu(W2 relu(a_i + b_nbr(i,e)) + b2)
-// (message_net_2 + PyG mean aggregation).  F16X3: pk = this layer's packed
-// images, amax_in = range slots of a, b (both required).
-int launch_edge_stage(const float *a, const float *b, const int32_t *nbr, int64_t n, int k,
-                      const mmpde_gnn_layer_params *p, const char *pk, const uint32_t *amax_in,
-                      float *mean, hipStream_t st);
+// (message_net_2 + PyG mean aggregation); with deg != nullptr the sum runs
+// over e < deg[i] and divides by max(deg[i], 1).  F16X3: pk = this layer's
+// packed images, amax_in = range slots of a, b (both required).
+int launch_edge_stage(const float *a, const float *b, const int32_t *nbr, const int32_t *deg,
+                      int64_t n, int k, const mmpde_gnn_layer_params *p, const char *pk,
+                      const uint32_t *amax_in, float *mean, hipStream_t st);
 
 // Node stage: h' = BN(h + relu(U2 relu(U1 [h | mean | t] + c1) + c2)) and, when
 // next != nullptr, the next layer's message_net_1 node halves a', b' (and,

@@ -13,7 +13,7 @@ import os
 import torch
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libmmpde_hip.so")
-ABI_VERSION = 10400
+ABI_VERSION = 10500
 
 ACT_NONE, ACT_TANH, ACT_RELU = 0, 1, 2
 # message_net_2 edge GEMM arithmetic (include/mmpde_hip.h MMPDE_EDGE_GEMM_*)
@@ -60,7 +60,8 @@ _P3 = _P * 3
 class GnnExec(ctypes.Structure):
     """mmpde_gnn_exec: optional per-layer hipEvents + the edge-GEMM arithmetic."""
     _fields_ = [("edge_begin", ctypes.POINTER(_P)), ("edge_end", ctypes.POINTER(_P)),
-                ("edge_gemm", _I), ("packed", _P), ("node_end", ctypes.POINTER(_P))]
+                ("edge_gemm", _I), ("packed", _P), ("node_end", ctypes.POINTER(_P)),
+                ("degree", _P)]
 
 
 class DmmGraphBranch(ctypes.Structure):
@@ -110,6 +111,7 @@ _SIGS = {
     "mmpde_dmm_mesh_graph": (_I, [_P, _P, _I64, _I64, _P, _I, _P, _P, _P, _P, _P]),
     "mmpde_dmm_mesh_array": (_I, [_P, _P, _I64, _I64, _P, _P, _P, _P, _P]),
     "mmpde_dmm_head_cache_bytes": (_I64, [_I64, _I]),
+    "mmpde_radius_graph": (_I, [_P, _I64, _I64, _F, _I, _P, _P, _P]),
     "mmpde_dmm_head_prepare": (_I, [_P, _I64, _P, _P, _P, _P]),
     "mmpde_dmm_mesh_graph_cached": (_I, [_P, _P, _I64, _I64, _P, _I, _P, _P, _P, _P, _P, _P]),
     "mmpde_dmm_mesh_array_cached": (_I, [_P, _P, _I64, _I64, _P, _P, _P, _P, _P, _P]),

@@ -68,6 +68,19 @@ class GraphCreator_FS_2D(nn.Module):  # noqa: N801 - reference name
         g = torch.tensor(np.array(np.meshgrid(gx, gy)), dtype=torch.float)
         return g.reshape(2, -1).permute(1, 0).contiguous().to(device)
 
+    def radius(self) -> float:
+        """connect_edge='radius' cut-off, data_creator_2d.py:187-195 / :221-226:
+        neighbors * |(dx, dy)| + 1e-4 of the uniform linspace grid (cylinder:
+        nx = ny = int(sqrt(N))), computed in fp32 as the reference does."""
+        if self._is_array():
+            _, nx, ny = self.pde.grid_size
+        else:
+            nx = ny = int(np.sqrt(self.pde.grid_size[1]))
+        x = torch.linspace(0, self.pde.Lx, nx)
+        y = torch.linspace(0, self.pde.Ly, ny)
+        dx, dy = x[1] - x[0], y[1] - y[0]
+        return float(self.n * torch.sqrt(dx ** 2 + dy ** 2) + 0.0001)
+
     def fixed_graph_nbr(self, grid: torch.Tensor, batches: int) -> torch.Tensor:
         """kNN-k table of `batches` copies of the fixed grid (cached)."""
         key = (grid.data_ptr(), grid._version, str(grid.device), batches, self.n)
@@ -116,7 +129,7 @@ class GraphCreator_FS_2D(nn.Module):  # noqa: N801 - reference name
         return ops.itp_interp(src, u.reshape(-1), qry, idx, nu, itp_model.packed(mode))
 
     # ------------------------------------------------------------------ graph
-    def _graph(self, u_nodes, mesh, t_nodes, labels_nodes, nbr, B, n):
+    def _graph(self, u_nodes, mesh, t_nodes, labels_nodes, nbr, B, n, deg=None):
         pos = torch.cat((t_nodes[:, None], mesh), 1).contiguous()
         batch = torch.arange(B, device=mesh.device).repeat_interleave(n)
         g = Data(x=u_nodes, edge_index=None)
@@ -124,12 +137,13 @@ class GraphCreator_FS_2D(nn.Module):  # noqa: N801 - reference name
         g.pos = pos
         g.batch = batch
         g.nbr = nbr
+        g.deg = deg
         return g
 
     def create_graph(self, itp_model, data, labels, steps, device, mesh_model=None):
-        """data_creator_2d.py:157-267 (connect_edge 'knn')."""
-        if self.e != "knn":
-            raise NotImplementedError("connect_edge='radius' is a §8(f) 'next' row")
+        """data_creator_2d.py:157-267 (connect_edge 'knn' or 'radius')."""
+        if self.e not in ("knn", "radius"):
+            raise ValueError(f"connect_edge {self.e!r}: knn | radius")
         data = data.to(device)
         labels = labels.to(device)
         B = data.shape[0]
@@ -168,11 +182,15 @@ class GraphCreator_FS_2D(nn.Module):  # noqa: N801 - reference name
         u_nodes = data.reshape(B, self.tw, n).permute(0, 2, 1).reshape(B * n, self.tw)
         y_nodes = labels.reshape(B, self.tw, n).permute(0, 2, 1).reshape(B * n, self.tw)
         t_nodes = t[list(steps)].to(device).repeat_interleave(n)
-        if mesh_model is None:
+        deg = None
+        if self.e == "radius":   # torch_cluster default max_num_neighbors = 32
+            nbr, deg = ops.radius_graph_nbr(mesh.contiguous(), B, self.radius(), 32)
+        elif mesh_model is None:
             nbr = self.fixed_graph_nbr(grid, B)
         else:
             nbr = ops.knn_graph_nbr(mesh, B, self.n)
-        return self._graph(u_nodes.contiguous(), mesh.contiguous(), t_nodes, y_nodes, nbr, B, n)
+        return self._graph(u_nodes.contiguous(), mesh.contiguous(), t_nodes, y_nodes, nbr, B, n,
+                           deg)
 
     def interpolate_pred(self, itp_model, pred, graph, data, device):
         """data_creator_2d.py:270-305: moved-mesh prediction -> fixed grid (kNN-30 of

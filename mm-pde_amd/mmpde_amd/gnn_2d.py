@@ -15,7 +15,7 @@ import torch
 from torch import nn
 
 from . import _lib as L
-from .ops import nbr_from_edge_index
+from .ops import nbr_from_edge_index, nbr_table_from_edge_index
 
 
 class BatchNorm(nn.Module):
@@ -185,7 +185,8 @@ class MP_PDE_Solver_2D(nn.Module):  # noqa: N801 - reference name
     # ----------------------------------------------------------------- forward
     def forward(self, data, out: torch.Tensor | None = None, workspace=None, trace=None):
         """gnn_2d.py:119-141 on one C-ABI call.  `data` needs .x [n,1], .pos [n,3]
-        and either .nbr (int32 [n,k]) or a knn-style .edge_index.  `trace`: optional
+        and either .nbr (int32 [n,k], plus .deg [n] for a ragged table such as the
+        radius graph's) or a PyG .edge_index (any in-degrees).  `trace`: optional
         _lib.GnnExec carrying hipEvents recorded around each layer's fused kernel
         (its edge_gemm field is set from self.edge_gemm)."""
         self.check_supported()
@@ -193,8 +194,12 @@ class MP_PDE_Solver_2D(nn.Module):  # noqa: N801 - reference name
         L.require_device(u, pos)
         n = u.shape[0]
         nbr = getattr(data, "nbr", None)
+        deg = getattr(data, "deg", None) if nbr is not None else None
         if nbr is None:
-            nbr = nbr_from_edge_index(data.edge_index, n)
+            nbr, deg = nbr_table_from_edge_index(data.edge_index, n)
+        if deg is not None:
+            L.require_device(deg)
+            deg = deg.to(torch.int32).contiguous()
         u = L.f32c(u).reshape(-1)
         pos = L.f32c(pos)
         sc, emb, arr, head = self.device_params()
@@ -206,6 +211,7 @@ class MP_PDE_Solver_2D(nn.Module):  # noqa: N801 - reference name
         if trace is None:
             trace = L.GnnExec(None, None, 0, None)
         trace.edge_gemm = L.EDGE_GEMM[self.edge_gemm]
+        trace.degree = L.ptr(deg)
         trace.packed = (L.ptr(self.packed_f16x3(u.device)) if self.edge_gemm == "f16x3"
                         else None)
         L.check(L.lib().mmpde_gnn_forward_ex(

@@ -21,6 +21,7 @@ class Data:
         self.pos = None
         self.batch = None
         self.nbr = None
+        self.deg = None   # ragged graphs (radius): in-degree per target, nbr rows padded
         for k, v in kwargs.items():
             setattr(self, k, v)
 
@@ -29,7 +30,7 @@ class Data:
         """PyG edge_index, materialised lazily from ``nbr`` (int64 widening kernel)."""
         if self._edge_index is None and self.nbr is not None:
             from .ops import edge_index_from_nbr
-            self._edge_index = edge_index_from_nbr(self.nbr)
+            self._edge_index = edge_index_from_nbr(self.nbr, self.deg)
         return self._edge_index
 
     @edge_index.setter
@@ -41,7 +42,7 @@ class Data:
         return None if self.x is None else self.x.shape[0]
 
     def to(self, device):
-        for k in ("x", "_edge_index", "y", "pos", "batch", "nbr"):
+        for k in ("x", "_edge_index", "y", "pos", "batch", "nbr", "deg"):
             v = getattr(self, k)
             if isinstance(v, torch.Tensor):
                 setattr(self, k, v.to(device))

@@ -27,7 +27,34 @@ def knn_graph_nbr(pos: torch.Tensor, batches: int, k: int, count_degenerate: boo
     return (nbr, deg) if count_degenerate else nbr
 
 
-def edge_index_from_nbr(nbr: torch.Tensor) -> torch.Tensor:
+def radius_graph_nbr(pos: torch.Tensor, batches: int, r: float, max_num_neighbors: int = 32):
+    """torch_cluster.radius_graph(pos, r, batch, loop=False, max_num_neighbors) for
+    `batches` equal contiguous segments (reference data_creator_2d.py:257-258),
+    CUDA semantics (first max_num_neighbors + 1 in index order within r, self
+    dropped).  Returns (nbr int32 [n, max_num_neighbors + 1] global sources,
+    padded with -1; degree int32 [n])."""
+    L.require_device(pos)
+    pos = L.f32c(pos).reshape(-1, 2)
+    n = pos.shape[0]
+    if n % batches:
+        raise ValueError("pos rows must split into equal batch segments")
+    w = max_num_neighbors + 1
+    nbr = torch.empty((n, w), dtype=torch.int32, device=pos.device)
+    deg = torch.empty((n,), dtype=torch.int32, device=pos.device)
+    L.check(L.lib().mmpde_radius_graph(L.ptr(pos), batches, n // batches, float(r),
+                                       max_num_neighbors, L.ptr(nbr), L.ptr(deg),
+                                       L.stream(pos.device)), "mmpde_radius_graph")
+    return nbr, deg
+
+
+def edge_index_from_nbr(nbr: torch.Tensor, degree: torch.Tensor | None = None) -> torch.Tensor:
+    """PyG edge_index int64 [2, E] (row 0 source, row 1 target) of a target-major
+    table; with `degree`, row i contributes its first degree[i] entries."""
+    if degree is not None:
+        n, k = nbr.shape
+        keep = torch.arange(k, device=nbr.device)[None, :] < degree[:, None].long()
+        tgt = torch.arange(n, device=nbr.device)[:, None].expand(n, k)
+        return torch.stack((nbr.long()[keep], tgt[keep]))
     """PyG edge_index int64 [2, n*k] (row 0 source, row 1 target)."""
     L.require_device(nbr)
     n, k = nbr.shape
@@ -40,7 +67,7 @@ def edge_index_from_nbr(nbr: torch.Tensor) -> torch.Tensor:
 def nbr_from_edge_index(edge_index: torch.Tensor, n: int) -> torch.Tensor:
     """Recover the fixed-degree target-major table from a PyG edge_index whose
     targets are grouped (the layout knn_graph produces).  Raises on ragged
-    degree (only possible for degenerate point sets)."""
+    degree (use nbr_table_from_edge_index)."""
     e = edge_index.shape[1]
     if e % n:
         raise ValueError("edge_index has ragged in-degree; fixed-degree kernels need k*n edges")
@@ -49,6 +76,28 @@ def nbr_from_edge_index(edge_index: torch.Tensor, n: int) -> torch.Tensor:
     if not bool(torch.equal(edge_index[1], tgt)):
         raise ValueError("edge_index targets are not grouped as knn_graph emits them")
     return edge_index[0].reshape(n, k).to(torch.int32).contiguous()
+
+
+def nbr_table_from_edge_index(edge_index: torch.Tensor, n: int):
+    """Any PyG edge_index -> (nbr int32 [n, k], degree int32 [n] or None).  A
+    grouped fixed-degree graph gives degree None; otherwise the in-edges of every
+    target (stable order) fill its row, padded with -1, k = max in-degree."""
+    e = edge_index.shape[1]
+    if e % n == 0:
+        k = e // n
+        tgt = torch.arange(n, device=edge_index.device).repeat_interleave(k)
+        if bool(torch.equal(edge_index[1], tgt)):
+            return edge_index[0].reshape(n, k).to(torch.int32).contiguous(), None
+    src, tgt = edge_index[0].long(), edge_index[1].long()
+    order = torch.argsort(tgt, stable=True)
+    src, tgt = src[order], tgt[order]
+    deg = torch.bincount(tgt, minlength=n)
+    k = max(int(deg.max().item()) if e else 0, 1)
+    start = torch.cumsum(deg, 0) - deg
+    slot = torch.arange(e, device=edge_index.device) - start[tgt]
+    nbr = torch.full((n, k), -1, dtype=torch.int32, device=edge_index.device)
+    nbr[tgt, slot] = src.to(torch.int32)
+    return nbr, deg.to(torch.int32)
 
 
 def knn_query(src: torch.Tensor, qry: torch.Tensor, batches: int, k: int) -> torch.Tensor:

@@ -33,6 +33,18 @@
  *    to its heap; we fix (rdist, index) ascending.  Queries may coincide with a
  *    source point (distance 0); no self exclusion.
  *
+ * 3. radius_graph_oracle -- restates torch_cluster 1.5.9 `radius_graph(x, r,
+ *    batch, loop=False, max_num_neighbors=32)` (reference data_creator_2d.py:
+ *    257-258, connect_edge='radius'; r from :195 / :226), CUDA path (the
+ *    reference runs on cuda:0).  Published algorithm: radius_graph calls
+ *    radius(x, x, r, batch, batch, max_num_neighbors + 1); its kernel scans the
+ *    query's segment in index order, appends every point with squared distance
+ *    (accumulated as in knn_graph: fmaf(dy, dy, dx*dx)) strictly below r*r
+ *    (squared in double on the host, handed to the kernel as float) and stops
+ *    after max_num_neighbors + 1 points; radius_graph then masks the self loop.
+ *    Output: nbr [n, max_nn + 1] global sources in scan order padded with -1,
+ *    deg [n] = entries kept.
+ *
  * Parity status: torch_cluster boundary is "parity unpinned" (no reference
  * fixture exists, running the reference was denied -- SURVEY.md §8(c));
  * the sklearn boundary is pinned against sklearn 1.7.2 fixtures on tie-free
@@ -145,4 +157,26 @@ int64_t knn_query_oracle(const float *src, const float *qry, int64_t batches,
     free(bd);
     free(bi);
     return 0;
+}
+
+/* pos: [batches*n_per, 2]; nbr_out [batches*n_per, max_nn+1]; deg_out [batches*n_per] */
+void radius_graph_oracle(const float *pos, int64_t batches, int64_t n_per, float r, int max_nn,
+                         int64_t *nbr_out, int64_t *deg_out) {
+    const float r2 = (float)((double)r * (double)r);
+    const int w = max_nn + 1;
+    for (int64_t b = 0; b < batches; ++b) {
+        const float *P = pos + 2 * b * n_per;
+        for (int64_t q = 0; q < n_per; ++q) {
+            int64_t *row = nbr_out + (b * n_per + q) * w;
+            int taken = 0, kept = 0;
+            for (int64_t j = 0; j < n_per && taken < w; ++j) {
+                if (d2_graph(P[2 * q], P[2 * q + 1], P[2 * j], P[2 * j + 1]) < r2) {
+                    taken++;
+                    if (j != q) row[kept++] = b * n_per + j;
+                }
+            }
+            deg_out[b * n_per + q] = kept;
+            for (int e = kept; e < w; ++e) row[e] = -1;
+        }
+    }
 }

@@ -54,6 +54,10 @@ def _lib():
         lib.knn_query_oracle.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                          ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
                                          ctypes.c_void_p]
+        lib.radius_graph_oracle.restype = None
+        lib.radius_graph_oracle.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                            ctypes.c_float, ctypes.c_int, ctypes.c_void_p,
+                                            ctypes.c_void_p]
         _LIB = lib
     return _LIB
 
@@ -96,6 +100,26 @@ def knn_graph(x: torch.Tensor, k: int, batches: int):
     tgt = torch.arange(n, dtype=torch.int64).repeat_interleave(k)
     edge_index = torch.stack([nbr.reshape(-1), tgt])
     return edge_index, nbr, int(deg)
+
+
+def radius_graph(x: torch.Tensor, r: float, batches: int, max_num_neighbors: int = 32):
+    """torch_cluster.radius_graph(x, r, batch, loop=False, max_num_neighbors), CUDA
+    semantics, equal contiguous batch segments (reference data_creator_2d.py:257-258).
+    Returns (edge_index [2, E] int64 target-major, nbr [n, max_nn+1] int64 padded
+    with -1, deg [n] int64)."""
+    x = x.detach().to(torch.float32).contiguous().cpu()
+    n = x.shape[0]
+    n_per = n // batches
+    assert n_per * batches == n
+    w = max_num_neighbors + 1
+    nbr = torch.empty((n, w), dtype=torch.int64)
+    deg = torch.empty((n,), dtype=torch.int64)
+    _lib().radius_graph_oracle(x.data_ptr(), batches, n_per, r, max_num_neighbors,
+                               nbr.data_ptr(), deg.data_ptr())
+    keep = torch.arange(w)[None, :] < deg[:, None]
+    tgt = torch.arange(n)[:, None].expand(n, w)
+    edge_index = torch.stack([nbr[keep], tgt[keep]])
+    return edge_index, nbr, deg
 
 
 def knn_query(src: torch.Tensor, qry: torch.Tensor, batches: int, k: int):
