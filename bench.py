@@ -167,6 +167,9 @@ def main():
                     help="message_net_2 arithmetic (include/mmpde_hip.h MMPDE_EDGE_GEMM_*)")
     ap.add_argument("--no-f32-exact", action="store_true",
                     help="skip the second, exact-fp32-MFMA timed run reported as f32_exact")
+    ap.add_argument("--serial", action="store_true",
+                    help="one stream in every pass (per-kernel profiles without concurrent "
+                         "kernels sharing the GPU)")
     args = ap.parse_args()
 
     from mmpde_amd import dist as D
@@ -210,7 +213,7 @@ def main():
         for m in (model, model_b):
             if m is not None:
                 m.edge_gemm = mode
-        eng.overlap = not trace
+        eng.overlap = not (trace or args.serial)
         u = u0
         with torch.no_grad():
             for i in range(args.warmup):

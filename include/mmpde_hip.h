@@ -109,11 +109,14 @@ int mmpde_conv2d(const float *x, int64_t batches, int cin, int h, int w, const f
                  const float *residual, int act, float *y, mmpde_stream_t stream);
 
 /* ------------------------------------------------------------------------
- * MP_PDE_Solver_2D (reference gnn_2d.py:19-141), hidden width 128, tw = 1.
- * Node inputs: u [n] fp32 (data.x), pos [n, 3] fp32 = (t, x, y) (data.pos).
+ * MP_PDE_Solver_2D (reference gnn_2d.py:19-141), hidden width 128.
+ * Node inputs: u [n, tw] fp32 (data.x), pos [n, 3] fp32 = (t, x, y) (data.pos).
+ * time_window tw (1 .. 16) is supported by mmpde_gnn_forward[_ex]; the
+ * per-stage entry points (mmpde_gnn_embed / _layer) take tw = 1.
  * ---------------------------------------------------------------------- */
 typedef struct {
     float inv_lx, inv_ly, inv_tmax; /* 1/pde.Lx, 1/pde.Ly, 1/pde.tmax (gnn_2d.py:122-124) */
+    int tw;                         /* time_window: channels of u (0 is read as 1) */
 } mmpde_gnn_scales;
 
 typedef struct {
@@ -144,7 +147,10 @@ typedef struct {
     /* output_mlp Conv1d(1,4,16,s3) ReLU Conv1d(4,8,12,s3) ReLU Conv1d(8,1,8,s2)
      * (gnn_2d.py:108-114) */
     const float *c0_w, *c0_b, *c2_w, *c2_b, *c4_w, *c4_b;
-    float out_scale; /* cumsum(ones(1,tw) * pde.dt * 0.1) for tw = 1 (gnn_2d.py:137-139) */
+    float out_scale;          /* tw = 1: pde.dt * 0.1 (gnn_2d.py:137-139) */
+    const float *out_scales;  /* tw > 1: cumsum(ones(1, tw) * pde.dt * 0.1), tw device floats;
+                                 out[n, tw] = out_scales[c] * output_mlp(h) */
+    int tw;                   /* 0 or 1: out[n] = out_scale * output_mlp(h) */
 } mmpde_gnn_head_params;
 
 /* Bytes of device workspace mmpde_gnn_forward needs for n nodes. */

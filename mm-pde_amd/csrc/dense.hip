@@ -126,7 +126,7 @@ __global__ __launch_bounds__(256) void conv2d_kernel(const float *__restrict__ x
 
 }  // namespace
 
-extern "C" int mmpde_version(void) { return 10500; }
+extern "C" int mmpde_version(void) { return 10600; }
 
 extern "C" const char *mmpde_status_string(int status) {
     if (status == MMPDE_OK) return "ok";

@@ -327,9 +327,15 @@ __global__ __launch_bounds__(256) void head_kernel(const float *__restrict__ h, 
     }
     spart[c][lane] = part;
     __syncthreads();
-    if (c == 0 && node0 + lane < n)
-        out[node0 + lane] = p.out_scale * (p.c4_b[0] + ((spart[0][lane] + spart[1][lane]) +
-                                                        (spart[2][lane] + spart[3][lane])));
+    if (c == 0 && node0 + lane < n) {
+        const float diff = p.c4_b[0] + ((spart[0][lane] + spart[1][lane]) +
+                                        (spart[2][lane] + spart[3][lane]));
+        if (p.tw <= 1) {
+            out[node0 + lane] = p.out_scale * diff;
+        } else {  // out [n, tw] = cumsum(dt) * diff (gnn_2d.py:137-141)
+            for (int t = 0; t < p.tw; ++t) out[(node0 + lane) * p.tw + t] = p.out_scales[t] * diff;
+        }
+    }
 }
 
 inline bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
@@ -350,6 +356,7 @@ extern "C" int mmpde_gnn_embed(const float *u, const float *pos, int64_t n,
                                mmpde_gnn_scales sc, const mmpde_gnn_embed_params *p,
                                float *workspace, float *h_out, mmpde_stream_t stream) {
     MMPDE_REQUIRE(u && pos && p && workspace && h_out && n > 0);
+    MMPDE_REQUIRE(sc.tw <= 1);  // the per-stage entry points take one u channel
     hipStream_t st = as_stream(stream);
     hipLaunchKernelGGL(embed0_kernel, dim3(ceil_div(n * H, 256)), dim3(256), 0, st, u, pos, n,
                        sc, *p, workspace);
@@ -420,13 +427,14 @@ extern "C" int mmpde_gnn_layer(const float *h_in, const float *u, const float *p
                                int k, const int32_t *nbr, mmpde_gnn_scales sc,
                                const mmpde_gnn_layer_params *p, float *workspace,
                                float *h_out, mmpde_stream_t stream) {
+    MMPDE_REQUIRE(sc.tw <= 1);  // the per-stage entry points take one u channel
     return gnn_layer_impl(h_in, u, pos, n, k, nbr, sc, p, workspace, h_out, nullptr, nullptr,
                           stream);
 }
 
 extern "C" int mmpde_gnn_head(const float *h, int64_t n, const mmpde_gnn_head_params *p,
                               float *out, mmpde_stream_t stream) {
-    MMPDE_REQUIRE(h && p && out && n > 0);
+    MMPDE_REQUIRE(h && p && out && n > 0 && p->tw <= 16 && (p->tw <= 1 || p->out_scales));
     hipLaunchKernelGGL(head_kernel, dim3((unsigned)ceil_div(n, HN)), dim3(256), 0,
                        as_stream(stream), h, n, *p, out);
     MMPDE_RET_LAUNCH();
@@ -475,6 +483,9 @@ extern "C" int mmpde_gnn_forward_ex(const float *u, const float *pos, int64_t n,
     MMPDE_REQUIRE(u && pos && nbr && emb && layers && head && workspace && out);
     MMPDE_REQUIRE(n > 0 && k > 0 && n_layers >= 0 && n_layers <= MMPDE_GNN_MAX_LAYERS);
     MMPDE_REQUIRE(aligned16(workspace));
+    const int tw = sc.tw > 1 ? sc.tw : 1;
+    MMPDE_REQUIRE(tw <= 16 && (head->tw > 1 ? head->tw : 1) == tw && (n_layers > 0 || tw == 1));
+    for (int l = 0; l < n_layers; ++l) MMPDE_REQUIRE(layers[l].msg1_ld >= 259 + tw);
     const int mode = exec ? exec->edge_gemm : MMPDE_EDGE_GEMM_F32;
     MMPDE_REQUIRE(mode == MMPDE_EDGE_GEMM_F32 || mode == MMPDE_EDGE_GEMM_F16X3);
     hipStream_t st = as_stream(stream);

@@ -608,16 +608,20 @@ __device__ __forceinline__ void gemm_tile(f32x4 *acc, const float4 *img, int KT,
     }
 }
 
+constexpr int MAX_TW = 16;  // time_window (u channels) of the fused kernels
+
 // Per-column constants of a message_net_1 node projection (weight row w1r of
-// this lane's column: node-term columns 256..259, bias, F16X3 unscale).
+// this lane's column: node-term columns 256 .. 256 + tw - 1 (u_i - u_j, du holds
+// the first), 256 + tw (x), 257 + tw (y), 258 + tw (t), bias, F16X3 unscale).
 struct W1C {
     float du = 0.0f, dx = 0.0f, dy = 0.0f, t = 0.0f, b = 0.0f, isa = 1.0f, isb = 1.0f;
     template <bool F16X3>
-    __device__ __forceinline__ void load(const float *w1r, const float *b1, const char *pk, int col) {
+    __device__ __forceinline__ void load(const float *w1r, const float *b1, const char *pk, int col,
+                                         int tw) {
         du = w1r[256];
-        dx = w1r[257];
-        dy = w1r[258];
-        t = w1r[259];
+        dx = w1r[256 + tw];
+        dy = w1r[257 + tw];
+        t = w1r[258 + tw];
         b = b1[col];
         if (F16X3) {
             const float *su = (const float *)(pk + kPkW1 + 131072);
@@ -631,11 +635,11 @@ struct W1C {
 // scales rs): a = W1[:, :128] h + w.(u, x, y) + w_t t + b1 (column tile wave),
 // b = W1[:, 128:256] h - w.(u, x, y) (column tile 8 + wave); the epilogue of
 // gnn_2d.py:53-57's message_net_1 split (see the file header).  rowv: per-row
-// (t, x, y, u) planes of stride 16 RB.  bA: preloaded B operands of a.
+// (t, x, y, u_0 .. u_{tw-1}) planes of stride 16 RB.  bA: preloaded B operands of a.
 template <bool F16X3, int RB>
 __device__ __forceinline__ void proj_phase(const BOps<F16X3, F16X3 ? 4 : 8> &bA, const float4 *img,
                                            const float *rs, const float *rowv, const W1C &w,
-                                           const char *pk, const float *w1r, int64_t row0,
+                                           const char *pk, const float *w1r, int tw, int64_t row0,
                                            int64_t n, float *a_out, float *b_out,
                                            uint32_t *amax_out, int wave, int lane) {
     constexpr int ROWS = 16 * RB, S1 = F16X3 ? 4 : 8;
@@ -663,7 +667,9 @@ __device__ __forceinline__ void proj_phase(const BOps<F16X3, F16X3 ? 4 : 8> &bA,
                     za = za * ir * w.isa;
                     zb = zb * ir * w.isb;
                 }
-                const float node = w.du * rowv[3 * ROWS + lr] + w.dx * rowv[ROWS + lr] + w.dy * rowv[2 * ROWS + lr];
+                float node = w.du * rowv[3 * ROWS + lr];
+                for (int c = 1; c < tw; ++c) node += w1r[256 + c] * rowv[(3 + c) * ROWS + lr];
+                node = node + w.dx * rowv[ROWS + lr] + w.dy * rowv[2 * ROWS + lr];
                 const float va = za + node + w.t * rowv[lr] + w.b;
                 const float vb = zb - node;
                 a_out[row * LH + col] = va;
@@ -686,11 +692,12 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs p) {
     __shared__ float stage[ROWS * NLD];         // fp32 v, then h'
     __shared__ float hres[ROWS * NLD];          // fp32 h (residual)
     __shared__ float rs[4][ROWS];               // row scales: h, mean, v, h'
-    __shared__ float rowv[4][ROWS];             // per row: t / tmax, x / Lx, y / Ly, u
+    __shared__ float rowv[3 + MAX_TW][ROWS];    // per row: t / tmax, x / Lx, y / Ly, u_0 .. u_{tw-1}
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int r = lane & 15, g = lane >> 4;
     const int64_t row0 = (int64_t)blockIdx.x * ROWS;
     const int col = 16 * wave + r;  // this lane's output column (tile = wave)
+    const int tw = p.sc.tw > 1 ? p.sc.tw : 1;
     constexpr int S1 = F16X3 ? 4 : 8;    // K steps per 128 columns of K
     const float *wu1 = p.u1 + (int64_t)col * p.ld_u1, *wu2 = p.u2 + (int64_t)col * LH;
     // everything the epilogues read from global memory is fetched up front
@@ -701,7 +708,7 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs p) {
         rowv[0][tid] = p.pos[row * 3 + 0] * p.sc.inv_tmax;
         rowv[1][tid] = p.pos[row * 3 + 1] * p.sc.inv_lx;
         rowv[2][tid] = p.pos[row * 3 + 2] * p.sc.inv_ly;
-        rowv[3][tid] = p.u[row];
+        for (int c = 0; c < tw; ++c) rowv[3 + c][tid] = p.u[row * tw + c];
     }
     const float u1_wt = wu1[256], u1_b = p.c1[col];
     const float u1_is = F16X3 ? pow2_inv(((const float *)(p.pk + kPkU1 + 131072))[col]) : 1.0f;
@@ -710,7 +717,7 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs p) {
     const float u2_is = F16X3 ? pow2_inv(((const float *)(p.pk + kPkU2 + 65536))[col]) : 1.0f;
     const float *w1r = NEXT ? p.w1n + (int64_t)col * p.ld_w1n : nullptr;
     W1C w1c;
-    if (NEXT) w1c.load<F16X3>(w1r, p.b1n, p.pkn, col);
+    if (NEXT) w1c.load<F16X3>(w1r, p.b1n, p.pkn, col, tw);
     // weight operands of update_net_1 / _2 loaded first: their latency hides
     // behind the activation staging
     // (RB >= 4: all three up front; smaller tiles run several workgroups per
@@ -781,7 +788,7 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs p) {
         prep<F16X3, ROWS>(stage, NLD, 0, ROWS, false, img, 128, 0, rs[3]);
         __syncthreads();
         // ---- next layer's message_net_1 node halves
-        proj_phase<F16X3, RB>(bA, img, rs[3], &rowv[0][0], w1c, p.pkn, w1r, row0, p.n, p.a_out,
+        proj_phase<F16X3, RB>(bA, img, rs[3], &rowv[0][0], w1c, p.pkn, w1r, tw, row0, p.n, p.a_out,
                               p.b_out, p.amax_out, wave, lane);
     }
 }
@@ -813,17 +820,18 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_embed_kernel(EmbedArgs p) {
     __shared__ float4 img[RB * 8 * 64];   // K = 128 operand image
     __shared__ float stage[ROWS * NLD];   // fp32 z, then h0
     __shared__ float rs[ROWS];            // h0 row scales
-    __shared__ float rowv[4][ROWS];       // per row: t / tmax, x / Lx, y / Ly, u
+    __shared__ float rowv[3 + MAX_TW][ROWS];  // per row: t / tmax, x / Lx, y / Ly, u_0 .. u_{tw-1}
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int g = lane >> 4;
     const int64_t row0 = (int64_t)blockIdx.x * ROWS;
     const int col = 16 * wave + (lane & 15);
+    const int tw = p.sc.tw > 1 ? p.sc.tw : 1;
     if (tid < ROWS) {
         const int64_t row = min(row0 + tid, p.n - 1);
         rowv[0][tid] = p.pos[row * 3 + 0] * p.sc.inv_tmax;
         rowv[1][tid] = p.pos[row * 3 + 1] * p.sc.inv_lx;
         rowv[2][tid] = p.pos[row * 3 + 2] * p.sc.inv_ly;
-        rowv[3][tid] = p.u[row];
+        for (int c = 0; c < tw; ++c) rowv[3 + c][tid] = p.u[row * tw + c];
     }
     const mmpde_gnn_embed_params &e = p.e;
     BOps<false, 8> b3;  // embedding_mlp.3 weight row of this lane's column
@@ -832,14 +840,18 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_embed_kernel(EmbedArgs p) {
     const float h_w = e.bn4_w[col], h_bb = e.bn4_b[col];
     const float *w1r = p.w1 + (int64_t)col * p.ld_w1;
     W1C w1c;
-    w1c.load<F16X3>(w1r, p.b1, p.pk, col);
-    // z: thread tid owns channel c = tid & 127 of rows (tid >> 7) + 4 i
+    w1c.load<F16X3>(w1r, p.b1, p.pk, col, tw);
+    // z: thread tid owns channel c = tid & 127 of rows (tid >> 7) + 4 i;
+    // embedding_mlp.0 weight [128, tw + 3] over (u_0 .. u_{tw-1}, x, y, t)
     const int c = tid & 127;
-    const float zw0 = e.w0[4 * c], zw1 = e.w0[4 * c + 1], zw2 = e.w0[4 * c + 2], zw3 = e.w0[4 * c + 3];
+    const float *zwr = e.w0 + (int64_t)c * (tw + 3);
+    const float zw0 = zwr[0], zw1 = zwr[tw], zw2 = zwr[tw + 1], zw3 = zwr[tw + 2];
     const float zb = e.b0[c], z_rm = e.bn1_rm[c], z_rv = e.bn1_rv[c], z_w = e.bn1_w[c], z_b = e.bn1_b[c];
     __syncthreads();
     for (int row = tid >> 7; row < ROWS; row += 4) {
-        const float v = zb + zw0 * rowv[3][row] + zw1 * rowv[1][row] + zw2 * rowv[2][row] + zw3 * rowv[0][row];
+        float v = zb + zw0 * rowv[3][row];
+        for (int ch = 1; ch < tw; ++ch) v += zwr[ch] * rowv[3 + ch][row];
+        v = v + zw1 * rowv[1][row] + zw2 * rowv[2][row] + zw3 * rowv[0][row];
         stage[row * NLD + c] = fmaxf(bn_eval(v, z_rm, z_rv, z_w, z_b, e.eps), 0.0f);
     }
     __syncthreads();
@@ -867,8 +879,8 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_embed_kernel(EmbedArgs p) {
     __syncthreads();
     prep<F16X3, ROWS>(stage, NLD, 0, ROWS, false, img, 128, 0, rs);
     __syncthreads();
-    proj_phase<F16X3, RB>(bA, img, rs, &rowv[0][0], w1c, p.pk, w1r, row0, p.n, p.a_out, p.b_out,
-                          p.amax_out, wave, lane);
+    proj_phase<F16X3, RB>(bA, img, rs, &rowv[0][0], w1c, p.pk, w1r, tw, row0, p.n, p.a_out,
+                          p.b_out, p.amax_out, wave, lane);
 }
 
 inline bool al16(const void *q) { return ((uintptr_t)q & 15u) == 0; }

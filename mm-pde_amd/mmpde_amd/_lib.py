@@ -13,7 +13,7 @@ import os
 import torch
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libmmpde_hip.so")
-ABI_VERSION = 10500
+ABI_VERSION = 10600
 
 ACT_NONE, ACT_TANH, ACT_RELU = 0, 1, 2
 # message_net_2 edge GEMM arithmetic (include/mmpde_hip.h MMPDE_EDGE_GEMM_*)
@@ -35,7 +35,7 @@ class MmpdeError(RuntimeError):
 
 # --------------------------------------------------------------------------- structs
 class GnnScales(ctypes.Structure):
-    _fields_ = [("inv_lx", _F), ("inv_ly", _F), ("inv_tmax", _F)]
+    _fields_ = [("inv_lx", _F), ("inv_ly", _F), ("inv_tmax", _F), ("tw", _I)]
 
 
 class GnnEmbedParams(ctypes.Structure):
@@ -51,7 +51,7 @@ class GnnLayerParams(ctypes.Structure):
 
 class GnnHeadParams(ctypes.Structure):
     _fields_ = [(n, _P) for n in ("c0_w", "c0_b", "c2_w", "c2_b", "c4_w", "c4_b")] + \
-        [("out_scale", _F)]
+        [("out_scale", _F), ("out_scales", _P), ("tw", _I)]
 
 
 _P3 = _P * 3

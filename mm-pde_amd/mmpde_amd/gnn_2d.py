@@ -69,9 +69,15 @@ class GNN_Layer_FS_2D(nn.Module):  # noqa: N801 - reference name
             u1 = f[4]
             u1p = torch.zeros((u1.shape[0], 260), dtype=torch.float32, device=u1.device)
             u1p[:, :u1.shape[1]] = u1          # row stride 260 keeps rows 16-B aligned
-            keep = f[:4] + [u1p] + f[5:]
+            w1 = f[0]
+            if w1.shape[1] % 4:                # 259 + tw columns: pad rows to 16 B too
+                w1p = torch.zeros((w1.shape[0], (w1.shape[1] + 3) & ~3), dtype=torch.float32,
+                                  device=w1.device)
+                w1p[:, :w1.shape[1]] = w1
+                w1 = w1p
+            keep = [w1] + f[1:4] + [u1p] + f[5:]
             p = L.GnnLayerParams(*[t.data_ptr() for t in keep], float(self.norm.module.eps),
-                                 f[0].shape[1], 260)
+                                 w1.shape[1], 260)
             self._pack, self._pack_key = (p, keep), key
         return self._pack[0]
 
@@ -131,16 +137,20 @@ class MP_PDE_Solver_2D(nn.Module):  # noqa: N801 - reference name
         return "GNN"
 
     # ----------------------------------------------------------------- packing
-    def out_scale(self) -> float:
-        """cumsum(ones(1, tw) * pde.dt * 0.1) evaluated exactly as gnn_2d.py:137-138
-        (fp32, on the host); tw = 1 -> one scalar."""
+    def out_scales(self) -> torch.Tensor:
+        """cumsum(ones(1, tw) * pde.dt * 0.1) evaluated as gnn_2d.py:137-138 (fp32,
+        on the host): [tw]."""
         dt = torch.ones(1, self.time_window) * self.pde.dt * 0.1
-        return float(torch.cumsum(dt, dim=1)[0, -1])
+        return torch.cumsum(dt, dim=1)[0]
+
+    def out_scale(self) -> float:
+        """The tw = 1 head scale (pde.dt * 0.1)."""
+        return float(self.out_scales()[0])
 
     def scales(self) -> L.GnnScales:
         one = torch.ones((), dtype=torch.float32)
         return L.GnnScales(float(one / self.pde.Lx), float(one / self.pde.Ly),
-                           float(one / self.pde.tmax))
+                           float(one / self.pde.tmax), self.time_window)
 
     def device_params(self):
         """(scales, embed, layer array, head) ctypes blocks, cached by parameter
@@ -156,7 +166,10 @@ class MP_PDE_Solver_2D(nn.Module):  # noqa: N801 - reference name
         if key != self._pack_key:
             f = [L.f32c(t) for t in ts]
             emb = L.GnnEmbedParams(*[t.data_ptr() for t in f[:12]], float(e[1].eps))
-            head = L.GnnHeadParams(*[t.data_ptr() for t in f[12:]], self.out_scale())
+            scl = self.out_scales().to(f[12].device)
+            f.append(scl)                      # kept alive with the parameter block
+            head = L.GnnHeadParams(*[t.data_ptr() for t in f[12:18]], self.out_scale(),
+                                   scl.data_ptr(), self.time_window)
             arr = (L.GnnLayerParams * len(layer_params))(*layer_params)
             self._pack = ((self.scales(), emb, arr, head), f, [g._pack for g in self.gnn_layers])
             self._pack_key = key
@@ -178,8 +191,9 @@ class MP_PDE_Solver_2D(nn.Module):  # noqa: N801 - reference name
     def check_supported(self):
         if self.training:
             raise NotImplementedError("training-mode forward is out of scope; call .eval()")
-        if self.hidden_features != 128 or self.time_window != 1 or len(self.eq_variables):
-            raise NotImplementedError("HIP solver supports hidden 128, time_window 1, no "
+        if self.hidden_features != 128 or not 1 <= self.time_window <= 16 or \
+                len(self.eq_variables):
+            raise NotImplementedError("HIP solver supports hidden 128, time_window 1..16, no "
                                       "extra equation variables (reference defaults)")
 
     # ----------------------------------------------------------------- forward
@@ -207,7 +221,7 @@ class MP_PDE_Solver_2D(nn.Module):  # noqa: N801 - reference name
             workspace = torch.empty((L.lib().mmpde_gnn_workspace_bytes(n) // 4,),
                                     dtype=torch.float32, device=u.device)
         if out is None:
-            out = torch.empty((n, 1), dtype=torch.float32, device=u.device)
+            out = torch.empty((n, self.time_window), dtype=torch.float32, device=u.device)
         if trace is None:
             trace = L.GnnExec(None, None, 0, None)
         trace.edge_gemm = L.EDGE_GEMM[self.edge_gemm]
