@@ -277,6 +277,51 @@ __global__ __launch_bounds__(256) void mesh_vjp_kernel(const float *__restrict__
     }
 }
 
+// The same VJP with one wave per grid point and every trajectory: Q[n], J[n]
+// and w_o are read once per grid point into registers (KPL = hidden / 64 per
+// lane), P (all trajectories) once per workgroup into LDS; per-lane partial
+// sums and the wave reduction are those of mesh_vjp_kernel (identical results).
+template <int KPL>
+__global__ __launch_bounds__(256) void mesh_vjp_wave_kernel(const float *__restrict__ P,
+                                                            const float *__restrict__ Q,
+                                                            const float2 *__restrict__ jac,
+                                                            const float *__restrict__ wo,
+                                                            const float2 *__restrict__ xi,
+                                                            int batches, int n_per,
+                                                            float2 *__restrict__ mesh) {
+    extern __shared__ float sP[];  // [batches][64 KPL]
+    constexpr int HID = 64 * KPL;
+    for (int i = threadIdx.x; i < batches * HID; i += 256) sP[i] = P[i];
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int nidx = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (nidx >= n_per) return;  // wave-uniform, after the only barrier
+    float q[KPL], w[KPL];
+    float2 jj[KPL];
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) {
+        const int kk = lane + 64 * i;
+        q[i] = Q[(int64_t)nidx * HID + kk];
+        jj[i] = jac[(int64_t)nidx * HID + kk];
+        w[i] = wo[kk];
+    }
+    const float2 x = xi[nidx];
+    for (int b = 0; b < batches; ++b) {
+        const float *pb = sP + b * HID;
+        float gx = 0.0f, gy = 0.0f;
+#pragma unroll
+        for (int i = 0; i < KPL; ++i) {
+            const float t = tanhf(pb[lane + 64 * i] + q[i]);
+            const float g = w[i] * (1.0f - t * t);
+            gx += g * jj[i].x;
+            gy += g * jj[i].y;
+        }
+        gx = wave_sum(gx);
+        gy = wave_sum(gy);
+        if (lane == 0) mesh[(int64_t)b * n_per + nidx] = make_float2(gx + x.x, gy + x.y);
+    }
+}
+
 struct HeadWs {
     float *trunk, *s, *q, *t1t, *gt, *p;
     float2 *jac;
@@ -359,8 +404,15 @@ int dmm_head(const float *branch, const float *xi, int64_t batches, int64_t n_pe
     rc = mmpde_linear_skinny(branch, L, batches, L, hd->o0_w, 2 * L, hd->o0_b, Lp,
                              MMPDE_ACT_NONE, w.p, Lp, st);
     if (rc) return rc;
-    hipLaunchKernelGGL(mesh_vjp_kernel, dim3((unsigned)n_per), dim3(256), 0, st, w.p, q, jac,
-                       hd->o1_w, (const float2 *)xi, batches, n_per, Lp, (float2 *)mesh_out);
+    const size_t lds = (size_t)batches * Lp * sizeof(float);
+    if (Lp == 512 && lds <= 65536) {
+        hipLaunchKernelGGL(mesh_vjp_wave_kernel<8>, dim3((unsigned)ceil_div(n_per, 4)), dim3(256),
+                           lds, st, w.p, q, jac, hd->o1_w, (const float2 *)xi, (int)batches,
+                           (int)n_per, (float2 *)mesh_out);
+    } else {
+        hipLaunchKernelGGL(mesh_vjp_kernel, dim3((unsigned)n_per), dim3(256), 0, st, w.p, q, jac,
+                           hd->o1_w, (const float2 *)xi, batches, n_per, Lp, (float2 *)mesh_out);
+    }
     MMPDE_RET_LAUNCH();
     return MMPDE_OK;
 }
