@@ -240,16 +240,31 @@ __global__ __launch_bounds__(256) void knn_kernel(const float2 *__restrict__ pts
         // are formed for C only.)  C is small (~2 kk on a mesh), so it is
         // compacted into LDS and sorted.
         const uint32_t thr = KT::filter_threshold(__shfl(wave_sort64(lmin, lane), kk - 1, 64));
-        int m = 0;
+        // Compaction (order is free: the list is sorted or ranked next): every
+        // lane's candidates as a bit mask, the wave's exclusive prefix of their
+        // counts from the counts' bit planes (ballot + mbcnt, no LDS), then each
+        // lane writes its own few entries.
+        uint64_t cm = 0;
 #pragma unroll
-        for (int c = 0; c < CPL; ++c) {
-            const bool sel = fkey[c] <= thr;
-            const uint64_t sm = __ballot(sel);
-            if (sel) {
-                const int pidx = m + __popcll(sm & below);
-                if (pidx < kCap) sIdx[wave][pidx] = lane + 64 * c;
-            }
-            m += __popcll(sm);
+        for (int c = 0; c < CPL; ++c) cm |= (uint64_t)(fkey[c] <= thr) << c;
+        const int cnt = __popcll(cm);
+        int m = 0, pidx = 0;
+#pragma unroll
+        for (int bit = 0; bit < 6; ++bit) {  // cnt <= CPL <= 64 < 2^7: bit 6 only for 64
+            const uint64_t plane = __ballot((cnt >> bit) & 1);
+            m += __popcll(plane) << bit;
+            pidx += __popcll(plane & below) << bit;
+        }
+        {
+            const uint64_t plane = __ballot(cnt >> 6);
+            m += __popcll(plane) << 6;
+            pidx += __popcll(plane & below) << 6;
+        }
+        while (cm) {
+            const int c = __builtin_ctzll(cm);
+            cm &= cm - 1;
+            if (pidx < kCap) sIdx[wave][pidx] = lane + 64 * c;
+            ++pidx;
         }
         key_t mk = ~key_t(0);
         int mi = 0x7fffffff;
