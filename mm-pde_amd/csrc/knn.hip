@@ -28,7 +28,7 @@
 namespace {
 
 constexpr int kQueriesPerBlock = 16;  // 4 per wave
-constexpr int kCap = 512;             // LDS list of candidates with key <= U, per wave
+constexpr int kCap = 256;             // LDS list of candidates with key <= U, per wave
 
 // fp32 squared distance as raw bits: the graph key, and the query's filter key.
 __device__ __forceinline__ uint32_t key_f32(float2 p, float2 q) {
