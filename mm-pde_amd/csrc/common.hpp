@@ -97,4 +97,17 @@ __device__ __forceinline__ float bn_eval(float v, float rm, float rv, float w, f
     return (v - rm) / sqrtf(rv + eps) * w + b;
 }
 
+// BatchNorm (eval) folded per channel as PyTorch's CPU kernel applies it
+// (alpha = w / sqrt(rv + eps), beta = b - rm alpha, y = x alpha + beta): two
+// constants per channel instead of a division per element.
+struct BnAffine {
+    float a = 1.0f, c = 0.0f;
+    __device__ __forceinline__ void set(float rm, float rv, float w, float b, float eps) {
+        const float invstd = 1.0f / sqrtf(rv + eps);
+        a = invstd * w;
+        c = b - rm * a;
+    }
+    __device__ __forceinline__ float operator()(float x) const { return fmaf(x, a, c); }
+};
+
 static inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }

@@ -712,8 +712,9 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs p) {
     }
     const float u1_wt = wu1[256], u1_b = p.c1[col];
     const float u1_is = F16X3 ? pow2_inv(((const float *)(p.pk + kPkU1 + 131072))[col]) : 1.0f;
-    const float u2_b = p.c2[col], bn_rm = p.bn_rm[col], bn_rv = p.bn_rv[col];
-    const float bn_w = p.bn_w[col], bn_b = p.bn_b[col];
+    const float u2_b = p.c2[col];
+    BnAffine bn;
+    bn.set(p.bn_rm[col], p.bn_rv[col], p.bn_w[col], p.bn_b[col], p.eps);
     const float u2_is = F16X3 ? pow2_inv(((const float *)(p.pk + kPkU2 + 65536))[col]) : 1.0f;
     const float *w1r = NEXT ? p.w1n + (int64_t)col * p.ld_w1n : nullptr;
     W1C w1c;
@@ -777,7 +778,7 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs p) {
                 float z = acc[rb][q];
                 if (F16X3) z = z * pow2_inv(rs[2][lr]) * u2_is;
                 const float x = hres[lr * NLD + col] + fmaxf(z + u2_b, 0.0f);
-                const float y = bn_eval(x, bn_rm, bn_rv, bn_w, bn_b, p.eps);
+                const float y = bn(x);
                 if (row < p.n) p.h_out[row * LH + col] = y;
                 if (NEXT) stage[lr * NLD + col] = y;
             }
@@ -836,8 +837,9 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_embed_kernel(EmbedArgs p) {
     const mmpde_gnn_embed_params &e = p.e;
     BOps<false, 8> b3;  // embedding_mlp.3 weight row of this lane's column
     b3.load(nullptr, 0, 0, 0, e.w3 + (int64_t)col * LH, 0, lane);
-    const float h_b = e.b3[col], h_rm = e.bn4_rm[col], h_rv = e.bn4_rv[col];
-    const float h_w = e.bn4_w[col], h_bb = e.bn4_b[col];
+    const float h_b = e.b3[col];
+    BnAffine bn4;
+    bn4.set(e.bn4_rm[col], e.bn4_rv[col], e.bn4_w[col], e.bn4_b[col], e.eps);
     const float *w1r = p.w1 + (int64_t)col * p.ld_w1;
     W1C w1c;
     w1c.load<F16X3>(w1r, p.b1, p.pk, col, tw);
@@ -846,13 +848,15 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_embed_kernel(EmbedArgs p) {
     const int c = tid & 127;
     const float *zwr = e.w0 + (int64_t)c * (tw + 3);
     const float zw0 = zwr[0], zw1 = zwr[tw], zw2 = zwr[tw + 1], zw3 = zwr[tw + 2];
-    const float zb = e.b0[c], z_rm = e.bn1_rm[c], z_rv = e.bn1_rv[c], z_w = e.bn1_w[c], z_b = e.bn1_b[c];
+    const float zb = e.b0[c];
+    BnAffine bn1;
+    bn1.set(e.bn1_rm[c], e.bn1_rv[c], e.bn1_w[c], e.bn1_b[c], e.eps);
     __syncthreads();
     for (int row = tid >> 7; row < ROWS; row += 4) {
         float v = zb + zw0 * rowv[3][row];
         for (int ch = 1; ch < tw; ++ch) v += zwr[ch] * rowv[3 + ch][row];
         v = v + zw1 * rowv[1][row] + zw2 * rowv[2][row] + zw3 * rowv[0][row];
-        stage[row * NLD + c] = fmaxf(bn_eval(v, z_rm, z_rv, z_w, z_b, e.eps), 0.0f);
+        stage[row * NLD + c] = fmaxf(bn1(v), 0.0f);
     }
     __syncthreads();
     prep<false, ROWS>(stage, NLD, 0, ROWS, false, img, 128, 0, rs);
@@ -870,7 +874,7 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_embed_kernel(EmbedArgs p) {
             for (int q = 0; q < 4; ++q) {
                 const int lr = 16 * rb + 4 * g + q;
                 const int64_t row = row0 + lr;
-                const float y = bn_eval(acc[rb][q] + h_b, h_rm, h_rv, h_w, h_bb, e.eps);
+                const float y = bn4(acc[rb][q] + h_b);
                 if (row < p.n) p.h_out[row * LH + col] = y;
                 stage[lr * NLD + col] = y;
             }

@@ -451,3 +451,44 @@ def test_graph_replay_matches_eager(dev, kind):
     for i, s in enumerate(range(4, 8)):
         u = eng.graph_step(u, s)
         assert torch.equal(u, ref[i]), f"{kind} graph step {s}: max|diff| {(u - ref[i]).abs().max()}"
+
+
+# ============================================================================ full size vs oracle
+@pytest.mark.parametrize("edge_gemm", ["f16x3", "f32"])
+def test_full_size_step_matches_oracle_sampled(dev, edge_gemm):
+    """BASELINE config 4 at its full size (16 trajectories x 2521 nodes, the
+    bench's launch geometry: 2521 edge tiles per layer over the persistent grid)
+    against the oracle on sampled trajectories (first, middle, last; trajectories
+    are independent, so the oracle on a subset is the full oracle restricted):
+    the DMM mesh against autograd, the moved-mesh kNN-35 rows bit for bit and the
+    step output at the parity tolerance."""
+    from mmpde_amd import ops
+    from mmpde_amd.rollout import MMPDERollout
+    from mmpde_amd.synth import build_models, fields
+
+    pde, model, model_b, itp, dmm, gc = build_models("cy")
+    grid = pde.ori_grid
+    B, N, step = 16, grid.shape[0], 7
+    data = fields(grid, B, 30)[:, step - 1:step]
+    sds = _sds(model=model, model_b=model_b, itp=itp, dmm=dmm)
+    for m in (model, model_b, itp, dmm):
+        m.to(dev)
+    model.edge_gemm = model_b.edge_gemm = edge_gemm
+    eng = MMPDERollout("cy", model, model_b, itp, dmm, gc, B, dev)
+    pred = eng.step(data[:, 0].to(dev), step).cpu().reshape(B, N)
+    mesh = eng.mesh.cpu().reshape(B, N, 2)
+    nbr = ops.knn_graph_nbr(eng.mesh, B, 35).long().cpu().reshape(B, N, 35)
+    pick = [0, 7, 15]
+    sub = data[pick]
+    ref_x, ref_y = refcpu.moving_mesh_tri(sds["dmm"], sub.reshape(len(pick), -1),
+                                          grid[None, :, 0].repeat(len(pick), 1),
+                                          grid[None, :, 1].repeat(len(pick), 1), grid)
+    ref_mesh = torch.cat((ref_x, ref_y), -1).reshape(len(pick), N, 2)
+    _close(mesh[pick], ref_mesh, 1e-5, 1e-6, "full-size DMM mesh")
+    for i, b in enumerate(pick):
+        _, ref_nbr, _ = refcpu.knn_graph(mesh[b], 35, 1)
+        assert torch.equal(nbr[b] - b * N, ref_nbr), f"kNN-35 rows of trajectory {b}"
+    opde = refcpu.PDEConst("cy", [30, N], ori_grid=grid)
+    ref, _ = refcpu.mmpde_step(opde, sds, sub, sub, [step] * len(pick),
+                               mesh_override=mesh[pick].reshape(-1, 2))
+    _close(pred[pick], ref, 2.5e-5, 1e-7, f"full-size mmpde step {edge_gemm}")
