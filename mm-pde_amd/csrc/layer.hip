@@ -513,8 +513,9 @@ constexpr int NODE_WPE = MMPDE_NODE_WPE;  // node / embed launch bounds: waves p
 template <bool F16X3, int ROWS>
 __device__ __forceinline__ void prep(const float *src, int64_t lds, int64_t row0, int64_t nrows_valid,
                                      bool global, float4 *img, int KT, int kofs, float *rs,
-                                     float *copy = nullptr) {
-    for (int idx = threadIdx.x; idx < ROWS * 8; idx += 512) {
+                                     float *copy = nullptr, int t0 = -1, int nthr = 512) {
+    // threads t0 .. t0 + nthr (default: the whole workgroup) share the rows
+    for (int idx = t0 < 0 ? (int)threadIdx.x : (int)threadIdx.x - t0; idx < ROWS * 8; idx += nthr) {
         // a wave takes 8 rows x 8 parts, lane = 8 part + row: the 8 lanes of one
         // ds_write_b128 group write 8 consecutive image rows (conflict-free)
         const int row = (idx >> 6) * 8 + (idx & 7), part = (idx >> 3) & 7;
@@ -732,8 +733,13 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs p) {
     }
 
     // ---- [h | mean] -> image (K = 256)
-    prep<F16X3, ROWS>(p.h, LH, row0, p.n, true, img, 256, 0, rs[0], hres);
-    prep<F16X3, ROWS>(p.mean, LH, row0, p.n, true, img, 256, 128, rs[1]);
+    if constexpr (ROWS * 8 <= 256) {  // h on waves 0-3, mean on waves 4-7 at once
+        if (tid < 256) prep<F16X3, ROWS>(p.h, LH, row0, p.n, true, img, 256, 0, rs[0], hres, 0, 256);
+        else prep<F16X3, ROWS>(p.mean, LH, row0, p.n, true, img, 256, 128, rs[1], nullptr, 256, 256);
+    } else {
+        prep<F16X3, ROWS>(p.h, LH, row0, p.n, true, img, 256, 0, rs[0], hres);
+        prep<F16X3, ROWS>(p.mean, LH, row0, p.n, true, img, 256, 128, rs[1]);
+    }
     __syncthreads();
 
     // ---- update_net_1: v = relu(U1 [h | mean | t] + c1)
