@@ -433,12 +433,15 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
 #pragma unroll
                 for (int qq = 0; qq < SPW; ++qq) {
                     f32x4 accN[CT];
+                    // slots past k (a tile's last round only; wave-uniform) skip
+                    // their MFMAs and free the SIMD for the partner wave
+                    const bool live = ESL * cC.rd + slotq(qq) < k;
                     rd_half(base + slotq(qq) * SLOT4, 1, xb);
-                    mma_half(xa, 0, accN);
+                    if (live) mma_half(xa, 0, accN);
                     if (qq > 0) sum_into(accP, ESL * cC.rd + slotq(qq - 1));
                     if (qq < SPW - 1) rd_half(base + slotq(qq + 1) * SLOT4, 0, xa);
                     else if (it + 1 < NIT) rd_half(nbase + slotq(0) * SLOT4, 0, xa);
-                    mma_half(xb, 1, accN);
+                    if (live) mma_half(xb, 1, accN);
 #pragma unroll
                     for (int cc = 0; cc < CT; ++cc) accP[cc] = accN[cc];
                 }
