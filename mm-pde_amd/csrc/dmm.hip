@@ -9,8 +9,9 @@
 // and the two autograd.grad calls of the reference reduce to the analytic VJP
 //     d(phi)/d(xi)(b, n) = sum_k w_o[k] (1 - tanh^2 z_k) J[n, k, :],
 //     J[n] = (Wt T1) diag(1 - s_n^2) T0,  s_n = tanh(T0 xi_n + t0b)   [L', 2]
-// (trunk = DenseNet[2, th, L]: T0 [th, 2], T1 [L, th]).  Q and J are recomputed
-// every call from the weights (no cross-call caching).
+// (trunk = DenseNet[2, th, L]: T0 [th, 2], T1 [L, th]).  Q and J depend only on the
+// grid and the weights: mmpde_dmm_head_prepare computes them once into a caller-owned
+// cache that later calls reuse; without a cache they are computed inside the call.
 #include "common.hpp"
 #include "gemm.hpp"
 

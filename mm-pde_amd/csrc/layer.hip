@@ -32,7 +32,9 @@
 // Node stage: 64 (or 32) rows per workgroup, 8 waves; every GEMM reads its
 // weight operand once per workgroup (wave w owns output column tile w for all
 // row blocks); activations are staged in LDS as MFMA operand images with
-// per-row power-of-two scales (F16X3).  No atomics anywhere: deterministic.
+// per-row power-of-two scales (F16X3).  The only atomics are the F16X3 range
+// slots (amax_publish: atomicMax of non-negative floats), whose result does
+// not depend on order, so every output is deterministic.
 #include "common.hpp"
 #include "f16x3.hpp"
 #include "layer.hpp"

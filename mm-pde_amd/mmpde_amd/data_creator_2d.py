@@ -83,12 +83,16 @@ class GraphCreator_FS_2D(nn.Module):  # noqa: N801 - reference name
 
     def fixed_graph_nbr(self, grid: torch.Tensor, batches: int) -> torch.Tensor:
         """kNN-k table of `batches` copies of the fixed grid (cached)."""
-        key = (grid.data_ptr(), grid._version, str(grid.device), batches, self.n)
-        nbr = self._fixed_graph_cache.get(key)
-        if nbr is None:
-            nbr = ops.knn_graph_nbr(grid.repeat(batches, 1), batches, self.n)
-            self._fixed_graph_cache = {key: nbr}
-        return nbr
+        # keyed on the grid's content (create_graph builds a fresh grid tensor
+        # every call, so an address key could match a different grid allocated
+        # at a freed address): the host copy of the grid is compared exactly
+        host = grid.detach().to("cpu", torch.float32).contiguous()
+        key = (tuple(host.shape), str(grid.device), batches, self.n)
+        hit = self._fixed_graph_cache.get(key)
+        if hit is None or not torch.equal(hit[0], host):
+            hit = (host, ops.knn_graph_nbr(grid.repeat(batches, 1), batches, self.n))
+            self._fixed_graph_cache = {key: hit}
+        return hit[1]
 
     # ------------------------------------------------------------------ data
     def create_data(self, datapoints, steps):

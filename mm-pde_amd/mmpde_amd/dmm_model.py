@@ -191,10 +191,15 @@ class DMM(nn.Module):
         """kNN-35 table of the fixed grid (reference dmm_model.py:222-234 builds it
         every call on B identical copies; it depends only on the grid, so it is
         built once per grid here).  LOCAL indices [N, k] int32."""
-        key = (grid.data_ptr(), grid._version, str(grid.device), k)
-        if key not in self._grid_cache:
-            self._grid_cache = {key: knn_graph_nbr(grid, 1, k)}
-        return self._grid_cache[key]
+        # the entry holds the grid tensor itself, so its storage cannot be freed
+        # and reused by another grid while the entry lives: (address, version,
+        # shape) then identifies the content
+        key = (grid.data_ptr(), grid._version, tuple(grid.shape), str(grid.device), k)
+        hit = self._grid_cache.get(key)
+        if hit is None:
+            hit = (grid, knn_graph_nbr(grid, 1, k))
+            self._grid_cache = {key: hit}
+        return hit[1]
 
     # ----------------------------------------------------------------- the API
     def head_cache(self, xi: torch.Tensor, workspace: torch.Tensor | None = None) -> torch.Tensor:

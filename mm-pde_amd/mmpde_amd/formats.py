@@ -13,9 +13,16 @@
   ``mesh/data/burgers_192.npy`` ([traj, T, 192, 192]; mmpde.py:171).
 
 Every file is read by loaders that execute nothing from it:
-``torch.load(weights_only=True)`` with ``argparse.Namespace`` as the only extra
-allowed global, and ``numpy.load(allow_pickle=False)``.  A file that needs any
-other global is refused (``pickle.UnpicklingError``).
+``torch.load(weights_only=True)`` with a data-only allowlist, and
+``numpy.load(allow_pickle=False)``.  The allowlist is ``argparse.Namespace``
+(the ``args`` entry) plus the numpy reconstructors a numpy value pickles to:
+the DMM checkpoint's ``train_std`` / ``train_minmax`` / ``test_*`` lists hold
+``np.mean(...)`` scalars (mesh/dmm_utils.py:734-737 append the values that
+``evaluate`` / ``evaluate_tri`` return, :1232,1284), which pickle as
+``numpy.core.multiarray.scalar`` (numpy 1.x files; ``numpy._core`` under numpy
+2) + ``numpy.dtype`` + the dtype's class.  Those rebuild a number from its
+bytes and call nothing else; object / void / string dtypes are not on the list.
+A file that needs any other global is refused (``pickle.UnpicklingError``).
 """
 from __future__ import annotations
 
@@ -27,9 +34,36 @@ import torch
 from .dmm_model import DMM
 
 
+def _numpy_data_globals():
+    """(callable, pickled name) pairs for numpy scalars / arrays / numeric dtypes,
+    under both the numpy 1.x (``numpy.core``) and numpy 2.x (``numpy._core``)
+    module paths the reference's checkpoints may name."""
+    try:
+        from numpy._core import multiarray as ma
+    except ImportError:  # numpy 1.x
+        from numpy.core import multiarray as ma
+    out = [np.dtype, np.ndarray]
+    for mod in ("numpy.core.multiarray", "numpy._core.multiarray"):
+        out.append((ma.scalar, f"{mod}.scalar"))
+        out.append((ma._reconstruct, f"{mod}._reconstruct"))
+    numeric = ("Bool", "Int8", "Int16", "Int32", "Int64", "UInt8", "UInt16", "UInt32", "UInt64",
+               "Float16", "Float32", "Float64", "LongDouble", "Complex64", "Complex128",
+               "LongLong", "ULongLong", "Byte", "UByte", "Short", "UShort", "Int", "UInt",
+               "Long", "ULong")
+    dts = getattr(np, "dtypes", None)
+    if dts is not None:
+        seen = set()
+        for name in numeric:
+            cls = getattr(dts, name + "DType", None)
+            if cls is not None and cls not in seen:
+                seen.add(cls)
+                out.append(cls)
+    return out
+
+
 def load_reference_file(path, map_location="cpu"):
     """torch.load of a reference checkpoint / dataset file without executing code."""
-    with torch.serialization.safe_globals([argparse.Namespace]):
+    with torch.serialization.safe_globals([argparse.Namespace] + _numpy_data_globals()):
         return torch.load(path, map_location=map_location, weights_only=True)
 
 

@@ -9,6 +9,21 @@ import torch
 
 from . import _lib as L
 
+# kNN kernels stage one trajectory's points in LDS and keep its distances in
+# registers (csrc/knn.hip): at most this many points per trajectory
+# (include/mmpde_hip.h mmpde_knn_graph / mmpde_knn_query).  The reference's
+# benchmarked grids are 2521 (cy) and 48 x 48 = 2304 (burgers); burgers at the
+# PDE's own default 96 x 96 (PDEs.py:27) exceeds it.
+KNN_MAX_POINTS = 4096
+
+
+def _knn_points_check(n_per: int, k: int, what: str):
+    if n_per > KNN_MAX_POINTS:
+        raise ValueError(f"{what}: {n_per} points per trajectory; the HIP kNN kernels take at "
+                         f"most {KNN_MAX_POINTS} (run --base_resolution <= 64 x 64)")
+    if k > 63:
+        raise ValueError(f"{what}: k = {k}; the HIP kNN kernels take k <= 63")
+
 
 def knn_graph_nbr(pos: torch.Tensor, batches: int, k: int, count_degenerate: bool = False):
     """torch_cluster.knn_graph(pos, k, batch, loop=False) for `batches` equal
@@ -20,6 +35,7 @@ def knn_graph_nbr(pos: torch.Tensor, batches: int, k: int, count_degenerate: boo
     n = pos.shape[0]
     if n % batches:
         raise ValueError("pos rows must split into equal batch segments")
+    _knn_points_check(n // batches, k, "knn_graph")
     nbr = torch.empty((n, k), dtype=torch.int32, device=pos.device)
     deg = torch.zeros((1,), dtype=torch.int32, device=pos.device) if count_degenerate else None
     L.check(L.lib().mmpde_knn_graph(L.ptr(pos), batches, n // batches, k, L.ptr(nbr),
@@ -108,6 +124,7 @@ def knn_query(src: torch.Tensor, qry: torch.Tensor, batches: int, k: int) -> tor
     src = L.f32c(src).reshape(-1, 2)
     qry = L.f32c(qry).reshape(-1, 2)
     ns, nq = src.shape[0] // batches, qry.shape[0] // batches
+    _knn_points_check(ns, k, "knn_query")
     idx = torch.empty((batches * nq, k), dtype=torch.int32, device=src.device)
     L.check(L.lib().mmpde_knn_query(L.ptr(src), L.ptr(qry), batches, ns, nq, k, L.ptr(idx),
                                     L.stream(src.device)), "mmpde_knn_query")

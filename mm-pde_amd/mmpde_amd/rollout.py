@@ -1,6 +1,6 @@
 """Autoregressive MM-PDE rollout engine (the benchmarked hot path).
 
-One step is the forward of train_helper_2d.py:479-488 (test_timestep_losses),
+One step is the forward of train_helper_2d.py:174-185 (test_timestep_losses),
 composed directly on the C-ABI with every buffer preallocated:
 
     pred = interpolate_pred(itp, model_b(graph_moved), graph_moved, data) + model(graph_uni)

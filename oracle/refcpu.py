@@ -522,7 +522,7 @@ def interpolate_pred(pde: PDEConst, itp_sd, pred, graph, data, return_idx=False)
 
 def mmpde_step(pde: PDEConst, sds, data, labels, steps, moving_mesh=True, mesh_override=None,
                graph_uni=None, dmm_grid_edge_index=None):
-    """One MM-PDE forward step, train_helper_2d.py:479-488 (test_timestep_losses):
+    """One MM-PDE forward step, train_helper_2d.py:174-185 (test_timestep_losses):
     pred = interpolate_pred(itp, model_b(graph), graph, data) + model(graph_uni).
     sds = dict(model=..., model_b=..., itp=..., dmm=...) state dicts."""
     with torch.no_grad():

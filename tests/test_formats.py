@@ -33,14 +33,37 @@ def _dmm_args(kind):
                               out_layers=[1024, 512, 1], lr_adam=2e-4, rf=True)
 
 
+def _evaluate_stat(seed):
+    """What mesh/dmm_utils.py:1228-1232 (evaluate_tri) / :1280-1284 (evaluate)
+    return: np.mean over a list of 0-d float32 arrays (torch -> .numpy()), an
+    np.float32 scalar."""
+    g = torch.Generator().manual_seed(seed)
+    per_traj = [torch.std(torch.rand(50, generator=g)).cpu().detach().numpy() for _ in range(4)]
+    return np.mean(per_traj)
+
+
+def _dmm_checkpoint_dict(dmm, kind):
+    """The dict mesh/dmm_utils.py:772-782 saves: loss lists of .item() floats
+    (:555-557), the argparse args, and per-epoch lists of np.mean scalars
+    (:734-737)."""
+    return {"model_state_dict": dmm.state_dict(), "loss_in": [0.5, 0.25],
+            "loss_bound": [1.0, 0.5], "loss_convex": [0.0, 0.0], "args": _dmm_args(kind),
+            "train_std": [_evaluate_stat(1), _evaluate_stat(2)],
+            "train_minmax": [_evaluate_stat(3)], "test_std": [_evaluate_stat(4)],
+            "test_minmax": [np.float64(_evaluate_stat(5))]}
+
+
 @pytest.mark.parametrize("kind", ["cy", "burgers"])
 def test_dmm_checkpoint_round_trip(tmp_path, kind):
     pde, _, _, _, dmm, _ = build_models(kind, seed=3)
     path = tmp_path / f"{kind}_checkpoint"
-    torch.save({"model_state_dict": dmm.state_dict(), "loss_in": [0.5, 0.25],
-                "loss_bound": [torch.tensor(1.0)], "loss_convex": [], "args": _dmm_args(kind),
-                "train_std": [0.1], "train_minmax": [0.2], "test_std": [0.3],
-                "test_minmax": [0.4]}, path)
+    ck = _dmm_checkpoint_dict(dmm, kind)
+    assert isinstance(ck["train_std"][0], np.float32)
+    torch.save(ck, path)
+    back = formats.load_reference_file(path)
+    for key in ("train_std", "train_minmax", "test_std", "test_minmax"):
+        assert [type(v) for v in back[key]] == [type(v) for v in ck[key]]
+        assert back[key] == ck[key]
     if kind == "cy":
         got = formats.load_dmm_checkpoint(path, "cy", grid=pde.ori_grid)
     else:
@@ -80,6 +103,43 @@ def test_loader_refuses_code_in_files(tmp_path):
     torch.save({"model_state_dict": {}, "args": _NotAllowed()}, path)
     with pytest.raises(pickle.UnpicklingError):
         formats.load_reference_file(path)
+
+
+def test_loader_refuses_object_arrays(tmp_path):
+    """The numpy allowlist is data only: an object-dtype array (whose elements
+    would be arbitrary pickled objects) is still refused."""
+    path = tmp_path / "objarr"
+    torch.save({"train_std": np.array([1, "x"], dtype=object)}, path)
+    with pytest.raises(pickle.UnpicklingError):
+        formats.load_reference_file(path)
+
+
+def _rename_pickled_module(path, old: bytes, new: bytes):
+    """Rewrite the GLOBAL opcodes of a torch.save zip's data.pkl (protocol 2: text
+    'module\\nname\\n') -- here to produce the numpy 1.x module path
+    ('numpy.core.multiarray') that checkpoints written by the reference's
+    environment (env.yml pins numpy 1.x) carry."""
+    import zipfile
+
+    with zipfile.ZipFile(path) as z:
+        items = [(i, z.read(i.filename)) for i in z.infolist()]
+    with zipfile.ZipFile(path, "w", zipfile.ZIP_STORED) as z:
+        for info, data in items:
+            if info.filename.endswith("data.pkl"):
+                assert old in data
+                data = data.replace(old, new)
+            z.writestr(info, data)
+
+
+def test_numpy1_module_paths(tmp_path):
+    path = tmp_path / "cy_checkpoint_np1"
+    torch.save({"args": _dmm_args("cy"), "train_std": [_evaluate_stat(7)],
+                "test_minmax": [np.float64(0.25)]}, path)
+    _rename_pickled_module(path, b"numpy._core.multiarray\n", b"numpy.core.multiarray\n")
+    back = formats.load_reference_file(path)
+    assert back["train_std"] == [_evaluate_stat(7)]
+    assert isinstance(back["train_std"][0], np.float32)
+    assert back["test_minmax"] == [0.25]
 
 
 def test_cylinder_data(tmp_path):
