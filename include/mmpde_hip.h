@@ -100,6 +100,13 @@ int mmpde_linear_skinny(const float *x, int64_t ldx, int64_t m, int64_t k, const
                         int64_t ldw, const float *b, int64_t n, int act, float *y,
                         int64_t ldy, mmpde_stream_t stream);
 
+/* out[b] = mean_i (pred[b, i] - labels[b, i])^2 per trajectory b (n_per values
+ * each): the loss of mmpde.py:33-36 (MSELoss) kept per trajectory for the
+ * sharded teacher-forced evaluation (train_helper_2d.py:184-185,193-198).
+ * Fixed summation order per trajectory: independent of `batches`. */
+int mmpde_traj_mse(const float *pred, const float *labels, int64_t batches, int64_t n_per,
+                   float *out, mmpde_stream_t stream);
+
 /* Direct 2-D convolution, NCHW fp32, square kernel ks, zero padding pad,
  * stride 1 or 2, fused act(conv + bias [+ residual]).  residual nullable,
  * same shape as the output.  ConvNet branch (mesh/dmm_model.py:53-57,65-81)

@@ -124,9 +124,42 @@ __global__ __launch_bounds__(256) void conv2d_kernel(const float *__restrict__ x
     y[e] = act_apply(acc, act);
 }
 
+// Per-trajectory mean squared error: one workgroup per trajectory, every thread
+// sums a fixed strided subset in index order, then a fixed LDS tree: the
+// result depends only on that trajectory's values (not on how many
+// trajectories share the launch), so a sharded evaluation reproduces the
+// single-process losses bit for bit.
+__global__ __launch_bounds__(256) void traj_mse_kernel(const float *__restrict__ pred,
+                                                       const float *__restrict__ lab, int64_t n_per,
+                                                       float *__restrict__ out) {
+    __shared__ float red[256];
+    const int64_t base = (int64_t)blockIdx.x * n_per;
+    float s = 0.0f;
+    for (int64_t i = threadIdx.x; i < n_per; i += 256) {
+        const float d = pred[base + i] - lab[base + i];
+        s = fmaf(d, d, s);
+    }
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[blockIdx.x] = red[0] / (float)n_per;
+}
+
 }  // namespace
 
-extern "C" int mmpde_version(void) { return 10600; }
+extern "C" int mmpde_version(void) { return 10700; }
+
+extern "C" int mmpde_traj_mse(const float *pred, const float *labels, int64_t batches, int64_t n_per,
+                              float *out, mmpde_stream_t stream) {
+    MMPDE_REQUIRE(pred && labels && out && batches > 0 && n_per > 0 && batches <= INT32_MAX);
+    hipLaunchKernelGGL(traj_mse_kernel, dim3((unsigned)batches), dim3(256), 0, as_stream(stream), pred,
+                       labels, n_per, out);
+    MMPDE_RET_LAUNCH();
+    return MMPDE_OK;
+}
 
 extern "C" const char *mmpde_status_string(int status) {
     if (status == MMPDE_OK) return "ok";

@@ -45,7 +45,21 @@ def shard_range(total: int, rank: int, world: int):
 
 
 def per_trajectory_mse(pred: torch.Tensor, labels: torch.Tensor, batches: int) -> torch.Tensor:
-    """MSE of each trajectory (mmpde.py:33-36 applied per trajectory)."""
+    """MSE of each trajectory (mmpde.py:33-36 applied per trajectory).  Device
+    tensors go through mmpde_traj_mse (fixed summation order per trajectory, so
+    the value does not depend on how trajectories are sharded); host tensors
+    (the gloo tests) use torch."""
+    if pred.is_cuda:
+        from . import _lib as L
+
+        p = L.f32c(pred).reshape(-1)
+        q = L.f32c(labels.to(pred.device)).reshape(-1)
+        if p.numel() != q.numel() or p.numel() % batches:
+            raise ValueError("pred / labels must hold `batches` equal trajectories")
+        out = torch.empty((batches,), dtype=torch.float32, device=pred.device)
+        L.check(L.lib().mmpde_traj_mse(L.ptr(p), L.ptr(q), batches, p.numel() // batches,
+                                       L.ptr(out), L.stream(pred.device)), "mmpde_traj_mse")
+        return out
     d = (pred.reshape(batches, -1) - labels.reshape(batches, -1)).float()
     return (d * d).mean(dim=1)
 

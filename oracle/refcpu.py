@@ -544,3 +544,21 @@ def mmpde_step(pde: PDEConst, sds, data, labels, steps, moving_mesh=True, mesh_o
 def mse(pred, labels):
     """mmpde.py:33-36."""
     return torch.nn.MSELoss()(pred, labels.reshape(-1, 1))
+
+
+def test_timestep_losses(pde: PDEConst, sds, u, steps, moving_mesh=True, tw=1):
+    """train_helper_2d.py:137-200 with the whole test set as one batch: for each
+    step (mmpde.py:139, filter :167-168), create_data -> the MM-PDE step ->
+    MSELoss(pred, labels) (mmpde.py:33-36).  Returns (per-step loss [S],
+    per-trajectory MSE [S, B])."""
+    B = u.shape[0]
+    per_step, per_traj = [], []
+    for s in steps:
+        if s != tw and s % tw != 0:
+            continue
+        data, labels = create_data(u, [s] * B, tw)
+        pred, _ = mmpde_step(pde, sds, data, labels, [s] * B, moving_mesh=moving_mesh)
+        per_step.append(mse(pred, labels))
+        d = pred.reshape(B, -1) - labels.reshape(B, -1)
+        per_traj.append((d * d).mean(1))
+    return torch.stack(per_step), torch.stack(per_traj)

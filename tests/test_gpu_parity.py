@@ -500,3 +500,57 @@ def test_full_size_step_matches_oracle_sampled(dev, edge_gemm):
     out_b = eng.out_b.cpu().reshape(B, N)[pick]
     _close(out_u, aux["out_u"], 1e-5, 1e-9, f"full-size model(graph_uni) {edge_gemm}")
     _close(out_b, aux["out_b"], 1e-5, 1e-9, f"full-size model_b(graph) {edge_gemm}")
+
+
+def test_full_size_burgers_step_properties_and_oracle(dev):
+    """BASELINE config 2 at its full size (32 trajectories x 48 x 48 nodes,
+    array-mode DMM, mode-'1' interpolation onto the moved mesh, Conv2d res_cut):
+    kNN validity on every trajectory's moved mesh, bitwise determinism, a finite
+    30-step autoregressive rollout, and the step against the oracle on sampled
+    trajectories (mesh vs autograd, moved-mesh kNN-35 rows bit for bit, each GNN
+    against its own range, the summed step)."""
+    from mmpde_amd import ops
+    from mmpde_amd.rollout import MMPDERollout
+    from mmpde_amd.synth import build_models, burgers_grid_points, fields
+
+    pde, model, model_b, itp, dmm, gc = build_models("burgers")
+    B, s, step = 32, 48, 11
+    N = s * s
+    u_all = fields(burgers_grid_points(), B, 31).reshape(B, 31, s, s)
+    data = u_all[:, step - 1:step]
+    sds = _sds(model=model, model_b=model_b, itp=itp, dmm=dmm)
+    for m in (model, model_b, itp, dmm):
+        m.to(dev)
+    for m in (model, model_b):
+        m.edge_gemm = "f16x3"
+    eng = MMPDERollout("burgers", model, model_b, itp, dmm, gc, B, dev)
+    u0 = data[:, 0].to(dev).contiguous()
+    p1 = eng.step(u0, step)
+    mesh = eng.mesh.clone()
+    out_u, out_b = eng.out_u.clone(), eng.out_b.clone()
+    p2 = eng.step(u0, step)
+    assert torch.equal(p1, p2)                                  # bitwise deterministic
+    nbr = ops.knn_graph_nbr(mesh, B, 35).long().cpu()
+    rows = torch.arange(B * N)[:, None]
+    assert ((nbr // N) == rows // N).all() and (nbr != rows).all()
+    m = mesh.cpu().double()
+    d = ((m[nbr] - m[:, None, :]) ** 2).sum(-1)
+    # sorted by the fp32 key (fmaf(dy, dy, dx*dx)): in fp64 the near-uniform grid's
+    # near-ties may swap by an fp32 rounding (exact order: oracle rows below)
+    assert (d[:, 1:] >= d[:, :-1] * (1 - 1e-6)).all()
+    pick = [0, 13, 31]
+    mesh_c = mesh.cpu().reshape(B, N, 2)
+    opde = refcpu.PDEConst("burgers", [31, s, s])
+    sub = data[pick]
+    ox, oy = refcpu.moving_mesh(sds["dmm"], opde, sub.reshape(len(pick), s, s), s, s)
+    _close(mesh_c[pick], torch.cat((ox, oy), -1), 0.0, 2e-6, "full-size burgers DMM mesh")
+    for b in pick:
+        _, ref_nbr, _ = refcpu.knn_graph(mesh_c[b], 35, 1)
+        assert torch.equal(nbr.reshape(B, N, 35)[b] - b * N, ref_nbr), f"kNN-35 rows of {b}"
+    ref, aux = refcpu.mmpde_step(opde, sds, sub, sub, [step] * len(pick),
+                                 mesh_override=mesh_c[pick].reshape(-1, 2))
+    _close(p1.cpu().reshape(B, N)[pick], ref, 2.5e-5, 1e-7, "full-size burgers step")
+    _close(out_u.cpu().reshape(B, N)[pick], aux["out_u"], 1e-5, 1e-9, "full-size burgers model")
+    _close(out_b.cpu().reshape(B, N)[pick], aux["out_b"], 1e-5, 1e-9, "full-size burgers model_b")
+    u = eng.rollout(u0, 1, 30)
+    assert torch.isfinite(u).all()
