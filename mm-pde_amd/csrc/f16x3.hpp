@@ -156,6 +156,19 @@ __device__ __forceinline__ void split8_relu_rtz(const float4 &a, const float4 &b
     lo = *(const half8 *)&l;
 }
 
+// split8_relu_rtz for one pair of values (4 instructions), for schedules that
+// spread a slot's split between MFMAs.  No trailing s_nop: the caller
+// guarantees that no MFMA reads hi / lo within the next two instructions (the
+// wave kernel consumes them one slot later).
+__device__ __forceinline__ void split2_relu_rtz(float x0, float x1, uint32_t &hi, uint32_t &lo) {
+    asm("v_cvt_pkrtz_f16_f32 %0, %2, %3\n\t"
+        "v_fma_mixlo_f16 %1, %2, 1.0, -%0 op_sel_hi:[0,0,1] clamp\n\t"
+        "v_fma_mixhi_f16 %1, %3, 1.0, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1] clamp\n\t"
+        "v_pk_max_f16 %0, %0, 0"
+        : "=&v"(hi), "=&v"(lo)
+        : "v"(x0), "v"(x1));
+}
+
 __device__ __forceinline__ float absmax4(float m, const float4 &v) {
     return fmaxf(fmaxf(fmaxf(m, fabsf(v.x)), fmaxf(fabsf(v.y), fabsf(v.z))), fabsf(v.w));
 }

@@ -22,6 +22,9 @@
 namespace {
 
 constexpr int H = 128;  // hidden width (gnn_2d.py:77)
+// [n, H] fp32 buffers of the forward workspace: h ping-pong, a, b, and 4 for the
+// edge stage's mean parts (the first doubles as the mean)
+constexpr int kGnnBufs = 8;
 
 // ---------------------------------------------------------------------------
 // Embedding first half: z = relu(BN1(W0 [u, x/Lx, y/Ly, t/tmax] + b0)), one thread
@@ -346,9 +349,10 @@ inline bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
 // C-ABI
 // ===========================================================================
 extern "C" int64_t mmpde_gnn_workspace_bytes(int64_t n) {
-    // h, a, b ping-pong = 6 x [n,128] fp32 (the unfused per-layer API uses
-    // 4 of them as a, b, mean, v), then room for per-call F16X3 weight images
-    return 6 * n * H * (int64_t)sizeof(float) + kAmaxBytes +
+    // h ping-pong, a, b and up to 4 edge-stage mean parts = 8 x [n,128] fp32
+    // (the unfused per-layer API uses 4 of them as a, b, mean, v), then the
+    // F16X3 range slots and room for per-call weight images
+    return kGnnBufs * n * H * (int64_t)sizeof(float) + kAmaxBytes +
            (int64_t)MMPDE_GNN_MAX_LAYERS * kLayerPack;
 }
 
@@ -494,7 +498,7 @@ extern "C" int mmpde_gnn_forward_ex(const float *u, const float *pos, int64_t n,
     float *wa = ws + 2 * n * H, *wb = ws + 3 * n * H, *wmean = ws + 4 * n * H;
     const char *pack = nullptr;
     // range slots of every layer's message inputs (F16X3 split scale)
-    uint32_t *amax = (uint32_t *)(ws + 6 * n * H);
+    uint32_t *amax = (uint32_t *)(ws + kGnnBufs * n * H);
     int rc;
     if (mode == MMPDE_EDGE_GEMM_F16X3 && n_layers > 0) {
         if (hipMemsetAsync(amax, 0, kAmaxBytes, st) != hipSuccess) return MMPDE_ERR_INVALID_ARG;
@@ -502,7 +506,7 @@ extern "C" int mmpde_gnn_forward_ex(const float *u, const float *pos, int64_t n,
             MMPDE_REQUIRE(aligned16(exec->packed));
             pack = (const char *)exec->packed;
         } else {
-            char *wpk = (char *)(ws + 6 * n * H) + kAmaxBytes;
+            char *wpk = (char *)(ws + kGnnBufs * n * H) + kAmaxBytes;
             rc = mmpde_gnn_pack_f16x3(layers, n_layers, wpk, stream);
             if (rc) return rc;
             pack = wpk;
@@ -528,12 +532,13 @@ extern "C" int mmpde_gnn_forward_ex(const float *u, const float *pos, int64_t n,
         const uint32_t *ain = pack ? amax + 2 * kAmaxShards * l : nullptr;
         uint32_t *aout = pack && next ? amax + 2 * kAmaxShards * (l + 1) : nullptr;
         if (eb && hipEventRecord(eb, st) != hipSuccess) return MMPDE_ERR_INVALID_ARG;
+        int parts = 1;
         rc = launch_edge_stage(wa, wb, nbr, exec ? exec->degree : nullptr, n, k, &layers[l], pk,
-                               ain, wmean, st);
+                               ain, wmean, n * H, kGnnBufs - 4, &parts, st);
         if (rc) return rc;
         if (ee && hipEventRecord(ee, st) != hipSuccess) return MMPDE_ERR_INVALID_ARG;
         // a, b are rewritten in place: this layer's edge stage has consumed them
-        rc = launch_node_stage(hb[cur], wmean, u, pos, n, sc, &layers[l], next, pk, pkn, aout,
+        rc = launch_node_stage(hb[cur], wmean, parts, n * H, u, pos, n, sc, &layers[l], next, pk, pkn, aout,
                                hb[cur ^ 1], wa, wb, st);
         if (rc) return rc;
         if (ne && hipEventRecord(ne, st) != hipSuccess) return MMPDE_ERR_INVALID_ARG;

@@ -138,7 +138,10 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
     // SPLIT: the odd-slot consumer's relu-sums of tile j, in [j & 1]
     __shared__ float4 xS[SPLIT ? 2 * 4 * CT * 64 : 1];
     const int tid = threadIdx.x;
-    const int wave = tid >> 6, lane = tid & 63;
+    // wave index in an SGPR: every role / slot / liveness test below is then a
+    // scalar branch (a VGPR wave index made `live` divergent: exec-masked MFMA
+    // blocks and accumulator copies at every slot)
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int r = lane & 15, g = lane >> 4;
     const bool producer = wave >= 4 * NC;
     int first, stride, nt;
@@ -185,6 +188,7 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
         // pieces i0 .. i0 + NPC - 1 of slot pidx & 3 (F16X3: K steps
         // i0 / 2 .. (i0 + NPC) / 2 - 1, hi and lo)
         const int pidx = wave - 4 * NC;
+        if (PH & 2048) __builtin_amdgcn_s_setprio(2);  // profiling: producers first
         const int pw = pidx & 3, i0 = (pidx >> 2) * NPC;
         auto piece = [&](int i) {
             const int ii = i0 + i;
@@ -330,6 +334,8 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
 #pragma unroll
         for (int cc = 0; cc < CT; ++cc) S[cc] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
         int pend = -1;  // SPLIT, even-slot wave: tile whose mean waits for the partner's sums
+        // T: relu-sums in the scaled domain (F16X3: x sw[col] sc, powers of two);
+        // inv undoes the scale exactly before the division by the degree
         auto write_mean = [&](int j, const f32x4 *T) {
             const int64_t row0 = (int64_t)(first + j * stride) * ET + 4 * g;
 #pragma unroll
@@ -338,7 +344,7 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
                     const float div = RAGGED ? (float)max(dg[t], 1) : kdiv;
-                    if (row0 + t < p.n) p.mean[(row0 + t) * LH + col] = T[cc][t] / div;
+                    if (row0 + t < p.n) p.mean[(row0 + t) * LH + col] = T[cc][t] * inv[cc] / div;
                 }
             }
         };
@@ -396,15 +402,17 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
         // relu-sum of slot e; e < k is wave-uniform (slots past k exist only
         // in a tile's last round), so it is a branch, not a select; RAGGED adds
         // the per-row e < deg select
+        // (relu as v_med3(x, 0, max): one instruction, where fmaxf adds a NaN-
+        // quieting canonicalize; the column scale is applied once, in write_mean)
         auto sum_into = [&](const f32x4 *acc, int e) {
             if (e >= k) return;
 #pragma unroll
             for (int cc = 0; cc < CT; ++cc) {
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
-                    float v = fmaxf(acc[cc][t], 0.0f);
+                    float v = __builtin_amdgcn_fmed3f(acc[cc][t], 0.0f, 3.402823466e38f);
                     if (RAGGED) v = e < dg[t] ? v : 0.0f;
-                    S[cc][t] = fmaf(v, inv[cc], S[cc][t]);
+                    S[cc][t] += v;
                 }
             }
         };
@@ -431,23 +439,22 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
 #pragma unroll
                     for (int t = 0; t < 4; ++t) dg[t] = p.deg[tile_row(cC.j, 4 * g + t)];
                 }
-                f32x4 accP[CT];
+                // Straight-line round: every slot is multiplied (a slot past k, in
+                // a tile's last round only, holds a duplicate of the last
+                // neighbour and is not summed) and the next round's first half
+                // slot is read even after the last round (in-bounds, unused):
+                // no branch joins, so the accumulators need no copies.
+                f32x4 acc[SPW][CT];
 #pragma unroll
                 for (int qq = 0; qq < SPW; ++qq) {
-                    f32x4 accN[CT];
-                    // slots past k (a tile's last round only; wave-uniform) skip
-                    // their MFMAs and free the SIMD for the partner wave
-                    const bool live = ESL * cC.rd + slotq(qq) < k;
                     rd_half(base + slotq(qq) * SLOT4, 1, xb);
-                    if (live) mma_half(xa, 0, accN);
-                    if (qq > 0) sum_into(accP, ESL * cC.rd + slotq(qq - 1));
+                    mma_half(xa, 0, acc[qq]);
+                    if (qq > 0) sum_into(acc[qq - 1], ESL * cC.rd + slotq(qq - 1));
                     if (qq < SPW - 1) rd_half(base + slotq(qq + 1) * SLOT4, 0, xa);
-                    else if (it + 1 < NIT) rd_half(nbase + slotq(0) * SLOT4, 0, xa);
-                    if (live) mma_half(xb, 1, accN);
-#pragma unroll
-                    for (int cc = 0; cc < CT; ++cc) accP[cc] = accN[cc];
+                    else rd_half(nbase + slotq(0) * SLOT4, 0, xa);
+                    mma_half(xb, 1, acc[qq]);
                 }
-                sum_into(accP, ESL * cC.rd + slotq(SPW - 1));
+                sum_into(acc[SPW - 1], ESL * cC.rd + slotq(SPW - 1));
                 if (cC.rd == rpt - 1) {  // tile complete: mean = sum / degree (PyG mean)
                     if (!SPLIT) {
                         write_mean(cC.j, S);
@@ -501,6 +508,8 @@ struct NodeArgs {
     mmpde_gnn_scales sc;
     const char *pk, *pkn;  // F16X3 images: this layer (U1, U2), next layer (W1)
     uint32_t *amax_out;
+    int parts;             // mean = sum of `parts` buffers part_stride floats apart
+    int64_t part_stride;
 };
 
 constexpr int NLD = 132;  // fp32 staging row stride (floats)
@@ -515,10 +524,13 @@ constexpr int NODE_WPE = MMPDE_NODE_WPE;  // node / embed launch bounds: waves p
 // prep(): rows of 128 fp32 values (src, row stride lds) -> image at k offset
 // kofs (multiple of 128) of an image KT wide; F16X3 scales each row by a power
 // of two (its max |x| -> [2^13, 2^14)) and records it in rs[row].  8 lanes per row.
+// nsum > 1: src is the first of nsum buffers sum_stride floats apart, added in
+// buffer order (the edge stage's per-part means).
 template <bool F16X3, int ROWS>
 __device__ __forceinline__ void prep(const float *src, int64_t lds, int64_t row0, int64_t nrows_valid,
                                      bool global, float4 *img, int KT, int kofs, float *rs,
-                                     float *copy = nullptr, int t0 = -1, int nthr = 512) {
+                                     float *copy = nullptr, int t0 = -1, int nthr = 512, int nsum = 1,
+                                     int64_t sum_stride = 0) {
     // threads t0 .. t0 + nthr (default: the whole workgroup) share the rows
     for (int idx = t0 < 0 ? (int)threadIdx.x : (int)threadIdx.x - t0; idx < ROWS * 8; idx += nthr) {
         // a wave takes 8 rows x 8 parts, lane = 8 part + row: the 8 lanes of one
@@ -529,6 +541,13 @@ __device__ __forceinline__ void prep(const float *src, int64_t lds, int64_t row0
         float4 x[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) x[q] = *(const float4 *)(sp + 4 * q);
+        for (int ps = 1; ps < nsum; ++ps) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 y = *(const float4 *)(sp + ps * sum_stride + 4 * q);
+                x[q] = make_float4(x[q].x + y.x, x[q].y + y.y, x[q].z + y.z, x[q].w + y.w);
+            }
+        }
         if (copy) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) *(float4 *)(copy + row * NLD + 16 * part + 4 * q) = x[q];
@@ -740,10 +759,12 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs p) {
     // ---- [h | mean] -> image (K = 256)
     if constexpr (ROWS * 8 <= 256) {  // h on waves 0-3, mean on waves 4-7 at once
         if (tid < 256) prep<F16X3, ROWS>(p.h, LH, row0, p.n, true, img, 256, 0, rs[0], hres, 0, 256);
-        else prep<F16X3, ROWS>(p.mean, LH, row0, p.n, true, img, 256, 128, rs[1], nullptr, 256, 256);
+        else prep<F16X3, ROWS>(p.mean, LH, row0, p.n, true, img, 256, 128, rs[1], nullptr, 256, 256, p.parts,
+                               p.part_stride);
     } else {
         prep<F16X3, ROWS>(p.h, LH, row0, p.n, true, img, 256, 0, rs[0], hres);
-        prep<F16X3, ROWS>(p.mean, LH, row0, p.n, true, img, 256, 128, rs[1]);
+        prep<F16X3, ROWS>(p.mean, LH, row0, p.n, true, img, 256, 128, rs[1], nullptr, -1, 512, p.parts,
+                          p.part_stride);
     }
     __syncthreads();
 
@@ -917,7 +938,9 @@ int device_cus() {
 
 int launch_edge_stage(const float *a, const float *b, const int32_t *nbr, const int32_t *deg,
                       int64_t n, int k, const mmpde_gnn_layer_params *p, const char *pk,
-                      const uint32_t *amax_in, float *mean, hipStream_t st) {
+                      const uint32_t *amax_in, float *mean, int64_t part_stride, int max_parts,
+                      int *parts_used, hipStream_t st) {
+    if (parts_used) *parts_used = 1;
     MMPDE_REQUIRE(a && b && nbr && p && mean && n > 0 && k > 0 && n <= (int64_t)INT32_MAX);
     MMPDE_REQUIRE(al16(a) && al16(b) && al16(p->msg2_w) && al16(mean));
     MMPDE_REQUIRE(!pk || (amax_in && al16(pk)));
@@ -925,6 +948,14 @@ int launch_edge_stage(const float *a, const float *b, const int32_t *nbr, const 
     MMPDE_REQUIRE(ntiles * ((k + ESL - 1) / ESL) < (int64_t)INT32_MAX);
     EdgeArgs e{a, b, nbr, n, k, (int)ntiles, p->msg2_w, p->msg2_b, pk, amax_in, mean, nullptr, deg};
     const int cus = device_cus();
+#ifndef MMPDE_EDGE_RING
+    // F16X3: one wave per SIMD with the operands in registers (edge_wave.hip)
+    if (pk) {
+        const int parts = edge_wave_parts(ntiles, cus, max_parts, k);
+        if (parts_used) *parts_used = parts;
+        return launch_edge_wave(a, b, nbr, deg, n, k, p->msg2_b, pk, amax_in, mean, parts, part_stride, cus, st);
+    }
+#endif
     const int grid = ntiles < cus ? (int)ntiles : cus;
     const dim3 block(64 * (4 * EDGE_NC + 4 * EDGE_NP));
     if (deg) {
@@ -938,18 +969,19 @@ int launch_edge_stage(const float *a, const float *b, const int32_t *nbr, const 
     return MMPDE_OK;
 }
 
-int launch_node_stage(const float *h, const float *mean, const float *u, const float *pos,
-                      int64_t n, mmpde_gnn_scales sc, const mmpde_gnn_layer_params *p,
-                      const mmpde_gnn_layer_params *next, const char *pk, const char *pkn,
-                      uint32_t *amax_out, float *h_out, float *a_out, float *b_out,
-                      hipStream_t st) {
+int launch_node_stage(const float *h, const float *mean, int parts, int64_t part_stride,
+                      const float *u, const float *pos, int64_t n, mmpde_gnn_scales sc,
+                      const mmpde_gnn_layer_params *p, const mmpde_gnn_layer_params *next,
+                      const char *pk, const char *pkn, uint32_t *amax_out, float *h_out, float *a_out,
+                      float *b_out, hipStream_t st) {
+    MMPDE_REQUIRE(parts >= 1 && parts <= 4 && (parts == 1 || part_stride >= n * LH));
     MMPDE_REQUIRE(h && mean && u && pos && p && h_out && n > 0);
     MMPDE_REQUIRE(al16(h) && al16(mean) && al16(h_out));
     MMPDE_REQUIRE(p->upd1_ld >= 257 && (p->upd1_ld & 3) == 0 && al16(p->upd1_w) && al16(p->upd2_w));
     MMPDE_REQUIRE(!pk || (al16(pk) && (!next || pkn)));
     NodeArgs a{h, mean, n, p->upd1_w, p->upd1_b, p->upd1_ld, p->upd2_w, p->upd2_b, p->bn_w, p->bn_b,
                p->bn_rm, p->bn_rv, p->eps, h_out, nullptr, nullptr, 0, a_out, b_out, u, pos, sc,
-               pk, pkn, amax_out};
+               pk, pkn, amax_out, parts, part_stride};
     if (next) {
         MMPDE_REQUIRE(a_out && b_out && next->msg1_ld >= 260 && (next->msg1_ld & 3) == 0 &&
                       al16(next->msg1_w));

@@ -11,6 +11,10 @@
 #include <random>
 #include <vector>
 
+int launch_edge_wave_diag(const float *a, const float *b, const int32_t *nbr, int64_t n, int k,
+                          const float *msg2_b, const char *pk, const uint32_t *amax_in, float *out,
+                          int cus, int diag, hipStream_t st);
+
 #define CK(x)                                                                     \
     do {                                                                          \
         hipError_t e_ = (x);                                                      \
@@ -111,7 +115,7 @@ int main(int argc, char **argv) {
         CK(hipMemcpy(amax, hs.data(), hs.size() * 4, hipMemcpyHostToDevice));
     }
     float *mean;
-    CK(hipMalloc(&mean, n * H * 4));
+    CK(hipMalloc(&mean, 2 * n * H * 4));
     const int it = 20;
     const int64_t ntiles = (n + ET - 1) / ET;
     int cus = device_cus();
@@ -122,28 +126,65 @@ int main(int argc, char **argv) {
     EdgeArgs e32{a, b, nbr, n, k, (int)ntiles, w2, b2, nullptr, nullptr, mean, stamps};
     EdgeArgs e16{a, b, nbr, n, k, (int)ntiles, w2, b2, pack, amax, mean, stamps};
     NodeArgs nd{h, mean, n, u1, c1, 260, u2, c2, bnw, bnb, bnm, bnv, 1e-5f, ho, w1, b1, 260, ao, bo,
-                u, pos, sc, pack, pack + kLayerPack, amax + 2 * kAmaxShards};
+                u, pos, sc, pack, pack + kLayerPack, amax + 2 * kAmaxShards, 1, 0};
     printf("n=%lld k=%d  (us per launch)\n", (long long)n, k);
     auto edge = [&](auto kern, int nw, const EdgeArgs &ea) {
         return time_it([&] { hipLaunchKernelGGL(kern, dim3(grid_e), dim3(64 * nw), 0, 0, ea); }, it);
     };
-    printf("edge f16x3 NC1NP2 %.1f  prio %.1f | NC1NP1 %.1f | NC2NP2 %.1f | NC2NP1 %.1f | f32 NC1NP2 %.1f\n",
-           edge(gnn_edge_kernel<true, 3, 1, 2>, 12, e16), edge(gnn_edge_kernel<true, 11, 1, 2>, 12, e16),
-           edge(gnn_edge_kernel<true, 3, 1, 1>, 8, e16), edge(gnn_edge_kernel<true, 3, 2, 2>, 16, e16),
-           edge(gnn_edge_kernel<true, 3, 2, 1>, 12, e16), edge(gnn_edge_kernel<false, 3, 1, 2>, 12, e32));
-    printf("edge f16x3 NC1NP2 no-gather %.1f\n", edge(gnn_edge_kernel<true, 7, 1, 2>, 12, e16));
-    printf("edge f16x3 slot-split NC2NP1 prio %.1f  noprio %.1f | NC2NP2 prio %.1f | column-split NC2NP1 prio %.1f\n",
-           edge(gnn_edge_kernel<true, 27, 2, 1>, 12, e16), edge(gnn_edge_kernel<true, 19, 2, 1>, 12, e16),
-           edge(gnn_edge_kernel<true, 27, 2, 2>, 16, e16), edge(gnn_edge_kernel<true, 11, 2, 1>, 12, e16));
-    printf("edge f16x3 slot-split NC2NP1: consume-only %.1f | no-gather %.1f | produce-only %.1f | "
-           "cvt-only producer %.1f (no gather %.1f)\n",
-           edge(gnn_edge_kernel<true, 26, 2, 1>, 12, e16), edge(gnn_edge_kernel<true, 31, 2, 1>, 12, e16),
-           edge(gnn_edge_kernel<true, 25, 2, 1>, 12, e16), edge(gnn_edge_kernel<true, 27 + 32, 2, 1>, 12, e16),
-           edge(gnn_edge_kernel<true, 31 + 32, 2, 1>, 12, e16));
-    printf("edge f16x3 slot-split NC2NP1: a rows re-read every round %.1f\n",
-           edge(gnn_edge_kernel<true, 27 + 128, 2, 1>, 12, e16));
-    printf("edge f16x3 slot-split NC2NP1: quarter ring stores %.1f (no gather %.1f)\n",
-           edge(gnn_edge_kernel<true, 27 + 64, 2, 1>, 12, e16), edge(gnn_edge_kernel<true, 31 + 64, 2, 1>, 12, e16));
+    {   // variants interleaved over several repetitions (the clock drifts between
+        // launches and devices differ): median per variant
+        struct V { const char *name; void (*k)(EdgeArgs); const EdgeArgs *a; };
+        V vs[] = {
+            {"ring kernel f16x3 (PH 27)", gnn_edge_kernel<true, 27, 2, 1>, &e16},
+            {"consume-only", gnn_edge_kernel<true, 26, 2, 1>, &e16},
+            {"produce-only", gnn_edge_kernel<true, 25, 2, 1>, &e16},
+            {"no-gather", gnn_edge_kernel<true, 31, 2, 1>, &e16},
+            {"cvt-only producer", gnn_edge_kernel<true, 27 + 32, 2, 1>, &e16},
+            {"quarter ring stores", gnn_edge_kernel<true, 27 + 64, 2, 1>, &e16},
+            {"prio: producers 2 > consumers 1", gnn_edge_kernel<true, 27 + 2048, 2, 1>, &e16},
+            {"prio: producers 2, consumers 0", gnn_edge_kernel<true, 19 + 2048, 2, 1>, &e16},
+            {"prio: none", gnn_edge_kernel<true, 19, 2, 1>, &e16},
+        };
+        const int nv = sizeof(vs) / sizeof(vs[0]), reps = 7;
+        std::vector<std::vector<float>> t(nv);
+        std::vector<float> tw1, tw2;
+        for (int r = 0; r < reps; ++r) {
+            for (int v = 0; v < nv; ++v) t[v].push_back(edge(vs[v].k, 12, *vs[v].a));
+            tw1.push_back(time_it([&] { launch_edge_wave(a, b, nbr, nullptr, n, k, b2, pack, amax, mean, 1, 0, cus, 0); }, it));
+            tw2.push_back(time_it([&] { launch_edge_wave(a, b, nbr, nullptr, n, k, b2, pack, amax, mean, 2, n * H, cus, 0); }, it));
+        }
+        for (int dgv : {1, 4, 8}) {
+            std::vector<float> td;
+            for (int r = 0; r < reps; ++r)
+                td.push_back(time_it([&] { launch_edge_wave_diag(a, b, nbr, n, k, b2, pack, amax, mean, cus, dgv, 0); }, it));
+            std::sort(td.begin(), td.end());
+            printf("edge wave parts=2 diag %d (%s%s%s%s) median %6.1f us\n", dgv, dgv & 1 ? "no-split " : "",
+                   dgv & 2 ? "no-relu-sum " : "", dgv & 4 ? "no-gather" : "", dgv & 8 ? "plain-VALU split" : "",
+                   td[reps / 2]);
+        }
+        std::sort(tw1.begin(), tw1.end());
+        std::sort(tw2.begin(), tw2.end());
+        printf("edge %-34s median %6.1f  min %6.1f  max %6.1f us\n", "wave kernel parts=1", tw1[reps / 2], tw1[0], tw1[reps - 1]);
+        printf("edge %-34s median %6.1f  min %6.1f  max %6.1f us\n", "wave kernel parts=2", tw2[reps / 2], tw2[0], tw2[reps - 1]);
+        {   // wave kernel (parts 1) vs ring kernel: same per-slot arithmetic
+            std::vector<float> m0(n * H), m1(n * H);
+            hipLaunchKernelGGL((gnn_edge_kernel<true, 27, 2, 1>), dim3(grid_e), dim3(768), 0, 0, e16);
+            CK(hipMemcpy(m0.data(), mean, n * H * 4, hipMemcpyDeviceToHost));
+            if (launch_edge_wave(a, b, nbr, nullptr, n, k, b2, pack, amax, mean, 1, 0, cus, 0)) return 1;
+            CK(hipMemcpy(m1.data(), mean, n * H * 4, hipMemcpyDeviceToHost));
+            double d = 0, mx = 0;
+            for (size_t i = 0; i < m0.size(); ++i) {
+                d = std::max(d, (double)std::fabs(m0[i] - m1[i]));
+                mx = std::max(mx, (double)std::fabs(m0[i]));
+            }
+            printf("wave vs ring kernel: max|diff| %.3e (max|mean| %.3e)\n", d, mx);
+        }
+        for (int v = 0; v < nv; ++v) {
+            std::sort(t[v].begin(), t[v].end());
+            printf("edge %-34s median %6.1f  min %6.1f  max %6.1f us\n", vs[v].name, t[v][reps / 2], t[v][0],
+                   t[v][reps - 1]);
+        }
+    }
     {   // slot-split vs column-split consumers: same sums, same order per target
         std::vector<float> m0(n * H), m1(n * H);
         hipLaunchKernelGGL((gnn_edge_kernel<true, 11, 2, 1>), dim3(grid_e), dim3(768), 0, 0, e16);
