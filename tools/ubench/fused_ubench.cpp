@@ -11,9 +11,6 @@
 #include <random>
 #include <vector>
 
-int launch_edge_wave_diag(const float *a, const float *b, const int32_t *nbr, int64_t n, int k,
-                          const float *msg2_b, const char *pk, const uint32_t *amax_in, float *out,
-                          int cus, int diag, hipStream_t st);
 
 #define CK(x)                                                                     \
     do {                                                                          \
@@ -152,15 +149,6 @@ int main(int argc, char **argv) {
             for (int v = 0; v < nv; ++v) t[v].push_back(edge(vs[v].k, 12, *vs[v].a));
             tw1.push_back(time_it([&] { launch_edge_wave(a, b, nbr, nullptr, n, k, b2, pack, amax, mean, 1, 0, cus, 0); }, it));
             tw2.push_back(time_it([&] { launch_edge_wave(a, b, nbr, nullptr, n, k, b2, pack, amax, mean, 2, n * H, cus, 0); }, it));
-        }
-        for (int dgv : {1, 4, 8}) {
-            std::vector<float> td;
-            for (int r = 0; r < reps; ++r)
-                td.push_back(time_it([&] { launch_edge_wave_diag(a, b, nbr, n, k, b2, pack, amax, mean, cus, dgv, 0); }, it));
-            std::sort(td.begin(), td.end());
-            printf("edge wave parts=2 diag %d (%s%s%s%s) median %6.1f us\n", dgv, dgv & 1 ? "no-split " : "",
-                   dgv & 2 ? "no-relu-sum " : "", dgv & 4 ? "no-gather" : "", dgv & 8 ? "plain-VALU split" : "",
-                   td[reps / 2]);
         }
         std::sort(tw1.begin(), tw1.end());
         std::sort(tw2.begin(), tw2.end());
