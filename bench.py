@@ -313,6 +313,25 @@ def main():
         "node_stage_ms": node_ms / nl,
         "finite": finite,
     }
+    if not moving:
+        # configs[2] is quoted against the scatter-add / HBM roofline: SURVEY.md
+        # §8(d)'s fused minimum of ~18.7 KB of HBM traffic per GNN node-update
+        # (per layer read + write h, the 2 KB of message_net_1 node halves, 35
+        # neighbour ids), against rocprofv3 FETCH/WRITE of the whole step
+        step_s = elapsed / args.steps
+        alg = n_local * 18.7e3
+        hbm = {"survey_fused_min_bytes_per_node_update": 18.7e3,
+               "algorithmic_bytes_per_step": alg, "achieved": alg / step_s / 1e9,
+               "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": alg / step_s / 1e9 / HBM_PEAK_GBS,
+               "measured_bytes_per_step": None}
+        rec_path = os.path.join(ROOT, "profiles", "r02_cy_gnn_step_hbm.json")
+        if os.path.exists(rec_path):
+            with open(rec_path) as f:
+                rec = json.load(f)
+            if rec.get("workload") == args.config and rec.get("nodes") == n_local:
+                hbm["measured_bytes_per_step"] = rec["hbm_bytes_per_step"]
+                hbm["measured_GBs"] = rec["hbm_bytes_per_step"] / step_s / 1e9
+        line["hbm"] = hbm
     if exact is not None:
         line["f32_exact"] = exact
     if world == 1 and not args.no_cpu_baseline:
