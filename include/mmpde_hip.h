@@ -182,6 +182,37 @@ int mmpde_gnn_edge_mean(const float *a, const float *b, const int32_t *nbr, int6
                         const float *msg2_w, const float *msg2_b, float *mean_out,
                         mmpde_stream_t stream);
 
+/* Edge stage with per-target in-degrees (deg may be NULL: every row has k
+ * live slots; slots e >= deg[i] are padding and ignored; mean over
+ * max(deg, 1)).  Exact fp32 arithmetic: the forward of the training path
+ * (train_helper_2d.py:114-126 -> gnn_2d.py:53-63 with aggr='mean'). */
+int mmpde_gnn_edge_mean_deg(const float *a, const float *b, const int32_t *nbr, const int32_t *deg,
+                            int64_t n, int k, const float *msg2_w, const float *msg2_b,
+                            float *mean_out, mmpde_stream_t stream);
+
+/* ---------------------------------------------------------------- training
+ * Backward of the edge stage (reference: loss.backward() at
+ * train_helper_2d.py:126 through GNN_Layer_FS_2D.message / aggr='mean',
+ * gnn_2d.py:53-63).  Given grad_mean = dL/dmean [n,128]:
+ *   grad_a [n,128]      = dL/da  (target half of message_net_1's output)
+ *   grad_edge [n*k,128] = dL/dz1 per edge slot (target-major as nbr; 0 for
+ *                         padding slots); dL/db = its per-source sum, see
+ *                         mmpde_gnn_edge_source_sum
+ *   grad_w2 [128,128], grad_b2 [128] = dL/d message_net_2.0 weight / bias.
+ * partials: device scratch of mmpde_gnn_edge_backward_partials() floats.
+ * z1/z2 are recomputed (nothing is kept by the forward); exact fp32 products;
+ * fixed reduction order (deterministic, no atomics). */
+int64_t mmpde_gnn_edge_backward_partials(int *grid);
+int mmpde_gnn_edge_backward(const float *a, const float *b, const int32_t *nbr, const int32_t *deg,
+                            int64_t n, int k, const float *msg2_w, const float *msg2_b,
+                            const float *grad_mean, float *grad_a, float *grad_edge,
+                            float *partials, float *grad_w2, float *grad_b2, mmpde_stream_t stream);
+/* grad_b[j] = sum over q in [rev_off[j], rev_off[j+1]) of grad_edge[rev_edge[q]]
+ * (rev_*: the reverse adjacency, slot ids i*k+e grouped by source j, in the
+ * order given: deterministic). */
+int mmpde_gnn_edge_source_sum(const float *grad_edge, const int64_t *rev_off, const int64_t *rev_edge,
+                              int64_t n, float *grad_b, mmpde_stream_t stream);
+
 /* out[n] = out_scale * output_mlp(h[:, None]) */
 int mmpde_gnn_head(const float *h, int64_t n, const mmpde_gnn_head_params *p, float *out,
                    mmpde_stream_t stream);

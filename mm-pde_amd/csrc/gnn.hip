@@ -381,6 +381,18 @@ extern "C" int mmpde_gnn_edge_mean(const float *a, const float *b, const int32_t
     return MMPDE_OK;
 }
 
+extern "C" int mmpde_gnn_edge_mean_deg(const float *a, const float *b, const int32_t *nbr, const int32_t *deg,
+                                       int64_t n, int k, const float *msg2_w, const float *msg2_b,
+                                       float *mean_out, mmpde_stream_t stream) {
+    MMPDE_REQUIRE(a && b && nbr && msg2_w && msg2_b && mean_out && n > 0 && k > 0);
+    mmpde_gnn_layer_params p{};
+    p.msg2_w = msg2_w;
+    p.msg2_b = msg2_b;
+    // exact fp32 ring kernel (no pack): the training forward of gnn_2d.py:53-63
+    return launch_edge_stage(a, b, nbr, deg, n, k, &p, nullptr, nullptr, mean_out, n * H, 1, nullptr,
+                             as_stream(stream));
+}
+
 static int gnn_layer_impl(const float *h_in, const float *u, const float *pos, int64_t n, int k,
                           const int32_t *nbr, mmpde_gnn_scales sc,
                           const mmpde_gnn_layer_params *p, float *workspace, float *h_out,

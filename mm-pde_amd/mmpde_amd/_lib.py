@@ -13,7 +13,7 @@ import os
 import torch
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libmmpde_hip.so")
-ABI_VERSION = 10700
+ABI_VERSION = 10800
 
 ACT_NONE, ACT_TANH, ACT_RELU = 0, 1, 2
 # message_net_2 edge GEMM arithmetic (include/mmpde_hip.h MMPDE_EDGE_GEMM_*)
@@ -102,6 +102,10 @@ _SIGS = {
     "mmpde_gnn_embed": (_I, [_P, _P, _I64, GnnScales, _P, _P, _P, _P]),
     "mmpde_gnn_layer": (_I, [_P, _P, _P, _I64, _I, _P, GnnScales, _P, _P, _P, _P]),
     "mmpde_gnn_edge_mean": (_I, [_P, _P, _P, _I64, _I, _P, _P, _P, _P]),
+    "mmpde_gnn_edge_mean_deg": (_I, [_P, _P, _P, _P, _I64, _I, _P, _P, _P, _P]),
+    "mmpde_gnn_edge_backward_partials": (_I64, [ctypes.POINTER(_I)]),
+    "mmpde_gnn_edge_backward": (_I, [_P, _P, _P, _P, _I64, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "mmpde_gnn_edge_source_sum": (_I, [_P, _P, _P, _I64, _P, _P]),
     "mmpde_gnn_head": (_I, [_P, _I64, _P, _P, _P]),
     "mmpde_gnn_forward": (_I, [_P, _P, _I64, _I, _P, GnnScales, _P, _P, _I, _P, _P, _P, _P]),
     "mmpde_gnn_pack_bytes": (_I64, [_I]),

@@ -130,7 +130,23 @@ class GraphCreator_FS_2D(nn.Module):  # noqa: N801 - reference name
         src = torch.cat((init_x, init_y), -1).reshape(-1, 2)
         qry = torch.cat((x, y), -1).reshape(-1, 2)
         idx = ops.knn_query(src, qry, nu, 30)
+        if itp_model.training:
+            return self._interpolate_autograd(itp_model, u, src, qry, idx, nu, mode)
         return ops.itp_interp(src, u.reshape(-1), qry, idx, nu, itp_model.packed(mode))
+
+    @staticmethod
+    def _interpolate_autograd(itp_model, u, src, qry, idx, nu, mode, addend=None):
+        """Training path of data_creator_2d.py:70-83: the HIP kNN-30 indices, then
+        the neighbour gather, ItpNet weights and weighted sum as device torch ops,
+        differentiable in the ItpNet parameters and in the values `u`."""
+        ns, nq = src.shape[0] // nu, qry.shape[0] // nu
+        gidx = idx.long().reshape(nu, nq * 30)
+        pts = src.reshape(nu, ns, 2)
+        nb = torch.gather(pts, 1, gidx[..., None].expand(nu, nq * 30, 2)).reshape(nu, nq, 30, 2)
+        lab = torch.gather(u.reshape(nu, ns), 1, gidx).reshape(nu, nq, 30)
+        w = itp_model.weights(nb, qry.reshape(nu, nq, 1, 2), mode)
+        out = torch.sum(w * lab, dim=-1).reshape(-1)
+        return out if addend is None else out + addend
 
     # ------------------------------------------------------------------ graph
     def _graph(self, u_nodes, mesh, t_nodes, labels_nodes, nbr, B, n, deg=None):
@@ -216,7 +232,11 @@ class GraphCreator_FS_2D(nn.Module):  # noqa: N801 - reference name
             n_src = n
         src = graph.pos[:, 1:3].contiguous()
         idx = ops.knn_query(src, qry, nu, 30)
-        out = ops.itp_interp(src, pred.reshape(-1), qry, idx, nu, itp_model.packed("2"),
-                             addend=res)
+        if itp_model.training:
+            out = self._interpolate_autograd(itp_model, pred, src, qry, idx, nu, "2",
+                                             addend=res)
+        else:
+            out = ops.itp_interp(src, pred.reshape(-1), qry, idx, nu, itp_model.packed("2"),
+                                 addend=res)
         assert src.shape[0] == nu * n_src
         return out.reshape(-1, 1)

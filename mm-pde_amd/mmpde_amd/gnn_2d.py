@@ -6,6 +6,15 @@ reference, so reference checkpoints load unchanged.  ``forward(data)`` runs the
 whole solver in one C-ABI call (mmpde_gnn_forward): embedding, 6 fused
 message-passing layers, Conv1d head -- eval-mode semantics (BatchNorm with
 running statistics), fp32 throughout.  There is no CPU / eager fallback.
+
+In ``train()`` mode (train_helper_2d.py:107-128) the forward is differentiable:
+the edge stage -- message_net_2 over every in-edge and the mean
+(gnn_2d.py:59-63, aggr='mean') -- runs as the ``EdgeMean`` autograd.Function on
+HIP kernels (mmpde_gnn_edge_mean_deg forward, mmpde_gnn_edge_backward +
+mmpde_gnn_edge_source_sum backward: no per-edge activation is stored); the
+per-node work (message_net_1 factored into its target and source halves,
+update MLPs, BatchNorm with batch statistics, embedding, Conv1d head) runs as
+device torch ops under autograd.
 """
 from __future__ import annotations
 
@@ -15,12 +24,13 @@ import torch
 from torch import nn
 
 from . import _lib as L
-from .ops import nbr_from_edge_index, nbr_table_from_edge_index
+from .ops import nbr_from_edge_index, nbr_table_from_edge_index, reverse_adjacency
 
 
 class BatchNorm(nn.Module):
     """Key-compatible stand-in for torch_geometric.nn.BatchNorm (PyG 2.0.3 wraps
-    nn.BatchNorm1d as ``.module``; reference gnn_2d.py:51)."""
+    nn.BatchNorm1d as ``.module``; reference gnn_2d.py:51).  The eval forward is
+    fused into the HIP layer kernels; this forward serves the training path."""
 
     def __init__(self, in_channels, eps=1e-5, momentum=0.1, affine=True,
                  track_running_stats=True):
@@ -28,7 +38,79 @@ class BatchNorm(nn.Module):
         self.module = nn.BatchNorm1d(in_channels, eps, momentum, affine, track_running_stats)
 
     def forward(self, x):
-        raise NotImplementedError("BatchNorm is fused into the HIP GNN layer kernels")
+        return self.module(x)
+
+
+class EdgeGraph:
+    """A message-passing graph as the HIP edge kernels take it: target-major
+    neighbour table nbr int32 [n, k], optional in-degrees int32 [n] (ragged
+    tables), and -- built on first use by a backward -- the reverse adjacency."""
+
+    def __init__(self, nbr: torch.Tensor, deg: torch.Tensor | None = None):
+        self.nbr = nbr.to(torch.int32).contiguous()
+        self.deg = deg.to(torch.int32).contiguous() if deg is not None else None
+        self._rev = None
+
+    @classmethod
+    def of(cls, data, n: int):
+        nbr = getattr(data, "nbr", None)
+        deg = getattr(data, "deg", None) if nbr is not None else None
+        if nbr is None:
+            nbr, deg = nbr_table_from_edge_index(data.edge_index, n)
+        return cls(nbr, deg)
+
+    def reverse(self):
+        if self._rev is None:
+            self._rev = reverse_adjacency(self.nbr, self.deg)
+        return self._rev
+
+
+class EdgeMean(torch.autograd.Function):
+    """mean_i = 1/max(deg_i, 1) sum_{e < deg_i} relu(W2 relu(a_i + b_{nbr[i,e]}) + b2):
+    message_net_2 over the in-edges and PyG's aggr='mean' (gnn_2d.py:36,59-63),
+    with a = the target half and b = the source half of message_net_1's
+    pre-activation.  Gradients for a, b, W2 and b2; exact fp32, deterministic."""
+
+    @staticmethod
+    def forward(ctx, a, b, w2, b2, graph: EdgeGraph):
+        n, k = graph.nbr.shape
+        if a.shape != (n, 128) or b.shape != (n, 128) or w2.shape != (128, 128):
+            raise ValueError("EdgeMean takes a, b [n, 128] and W2 [128, 128]")
+        L.require_device(a, b, w2, b2, graph.nbr, graph.deg)
+        a, b, w2, b2 = L.f32c(a), L.f32c(b), L.f32c(w2), L.f32c(b2)
+        mean = torch.empty((n, 128), dtype=torch.float32, device=a.device)
+        L.check(L.lib().mmpde_gnn_edge_mean_deg(L.ptr(a), L.ptr(b), L.ptr(graph.nbr),
+                                                L.ptr(graph.deg), n, k, L.ptr(w2), L.ptr(b2),
+                                                L.ptr(mean), L.stream(a.device)),
+                "mmpde_gnn_edge_mean_deg")
+        ctx.save_for_backward(a, b, w2, b2)
+        ctx.graph = graph
+        return mean
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b, w2, b2 = ctx.saved_tensors
+        graph = ctx.graph
+        n, k = graph.nbr.shape
+        dev = a.device
+        g = L.f32c(g)
+        lib = L.lib()
+        ga = torch.empty_like(a)
+        gb = torch.empty_like(b)
+        gedge = torch.empty((n * k, 128), dtype=torch.float32, device=dev)
+        part = torch.empty((lib.mmpde_gnn_edge_backward_partials(None),), dtype=torch.float32,
+                           device=dev)
+        gw2 = torch.empty((128, 128), dtype=torch.float32, device=dev)
+        gb2 = torch.empty((128,), dtype=torch.float32, device=dev)
+        st = L.stream(dev)
+        L.check(lib.mmpde_gnn_edge_backward(L.ptr(a), L.ptr(b), L.ptr(graph.nbr), L.ptr(graph.deg),
+                                            n, k, L.ptr(w2), L.ptr(b2), L.ptr(g), L.ptr(ga),
+                                            L.ptr(gedge), L.ptr(part), L.ptr(gw2), L.ptr(gb2), st),
+                "mmpde_gnn_edge_backward")
+        rev_off, rev_edge = graph.reverse()
+        L.check(lib.mmpde_gnn_edge_source_sum(L.ptr(gedge), L.ptr(rev_off), L.ptr(rev_edge), n,
+                                              L.ptr(gb), st), "mmpde_gnn_edge_source_sum")
+        return ga, gb, gw2, gb2, None
 
 
 class GNN_Layer_FS_2D(nn.Module):  # noqa: N801 - reference name
@@ -81,10 +163,32 @@ class GNN_Layer_FS_2D(nn.Module):  # noqa: N801 - reference name
             self._pack, self._pack_key = (p, keep), key
         return self._pack[0]
 
+    def train_forward(self, h, u, pos_x, pos_y, variables, graph: EdgeGraph):
+        """Differentiable layer (gnn_2d.py:53-69).  message_net_1 of the edge (i, j)
+        is W1 cat(h_i, h_j, u_i - u_j, dx, dy, t_i) + b1 = a_i + b_j with
+        a = [h u x y t] Wa^T + b1 and b = [h u x y] Wb^T (Wb holding -W1 on the
+        difference columns): two node GEMMs, then the EdgeMean kernels."""
+        if self.hidden_features != 128 or self.out_features != 128:
+            raise NotImplementedError("HIP edge kernels take hidden = out = 128")
+        f, tw = self.in_features, self.time_window
+        w1, b1 = self.message_net_1[0].weight, self.message_net_1[0].bias
+        wdu = w1[:, 2 * f:2 * f + tw]
+        wdxy = w1[:, 2 * f + tw:2 * f + tw + 2]
+        wt = w1[:, 2 * f + tw + 2:]
+        a = torch.addmm(b1, torch.cat((h, u, pos_x, pos_y, variables), -1),
+                        torch.cat((w1[:, :f], wdu, wdxy, wt), 1).t())
+        b = torch.cat((h, u, pos_x, pos_y), -1) @ torch.cat((w1[:, f:2 * f], -wdu, -wdxy), 1).t()
+        m2 = self.message_net_2[0]
+        mean = EdgeMean.apply(a, b, m2.weight, m2.bias, graph)
+        upd = self.update_net_2(self.update_net_1(torch.cat((h, mean, variables), -1)))
+        return self.norm(h + upd)
+
     def forward(self, x, u, pos_x, pos_y, variables, edge_index, batch):
         """Layer-level API of the reference (gnn_2d.py:53-57)."""
         if self.training:
-            raise NotImplementedError("training-mode forward is out of scope; call .eval()")
+            L.require_device(x, u, pos_x, pos_y, variables)
+            nbr, deg = nbr_table_from_edge_index(edge_index, x.shape[0])
+            return self.train_forward(x, u, pos_x, pos_y, variables, EdgeGraph(nbr, deg))
         if not self.supported():
             raise NotImplementedError("HIP layer supports hidden 128, time_window 1, 1 variable")
         L.require_device(x, u, pos_x, pos_y, variables)
@@ -189,8 +293,6 @@ class MP_PDE_Solver_2D(nn.Module):  # noqa: N801 - reference name
         return self._f16x3
 
     def check_supported(self):
-        if self.training:
-            raise NotImplementedError("training-mode forward is out of scope; call .eval()")
         if self.hidden_features != 128 or not 1 <= self.time_window <= 16 or \
                 len(self.eq_variables):
             raise NotImplementedError("HIP solver supports hidden 128, time_window 1..16, no "
@@ -203,6 +305,8 @@ class MP_PDE_Solver_2D(nn.Module):  # noqa: N801 - reference name
         radius graph's) or a PyG .edge_index (any in-degrees).  `trace`: optional
         _lib.GnnExec carrying hipEvents recorded around each layer's fused kernel
         (its edge_gemm field is set from self.edge_gemm)."""
+        if self.training:
+            return self.train_forward(data)
         self.check_supported()
         u, pos = data.x, data.pos
         L.require_device(u, pos)
@@ -234,3 +338,21 @@ class MP_PDE_Solver_2D(nn.Module):  # noqa: N801 - reference name
             ctypes.byref(trace), L.stream(u.device)),
             "mmpde_gnn_forward")
         return out
+
+    # ----------------------------------------------------------------- training
+    def train_forward(self, data):
+        """gnn_2d.py:119-141 in train() mode, differentiable (see module doc)."""
+        if self.hidden_features != 128:
+            raise NotImplementedError("HIP edge kernels take hidden_features = 128")
+        u, pos = data.x, data.pos
+        L.require_device(u, pos)
+        n = u.shape[0]
+        graph = EdgeGraph.of(data, n)
+        pos_x = pos[:, 1][:, None] / self.pde.Lx
+        pos_y = pos[:, 2][:, None] / self.pde.Ly
+        variables = pos[:, 0][:, None] / self.pde.tmax
+        h = self.embedding_mlp(torch.cat((u, pos_x, pos_y, variables), -1))
+        for layer in self.gnn_layers:
+            h = layer.train_forward(h, u, pos_x, pos_y, variables, graph)
+        diff = self.output_mlp(h[:, None]).squeeze(1)
+        return self.out_scales()[None].to(h.device) * diff

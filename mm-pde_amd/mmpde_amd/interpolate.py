@@ -6,6 +6,13 @@ Parameters and state_dict keys match the reference: ``layers`` (mode '1'),
 for Burgers).  Modes '1'/'2' run inside the fused kNN-30 + MLP + weighted-sum
 kernel driven by GraphCreator_FS_2D.interpolate; ``forward(..., 'res_cut')``
 runs the ``down`` network on the skinny-GEMM / conv kernels.
+
+In ``train()`` mode (mmpde.py:86, the ItpNet parameters are in the AdamW groups
+of mmpde.py:269-271) the forward follows interpolate.py:77-99 with device torch
+ops under autograd: the gradients reach ``layers``, ``layers2`` and ``down``
+through create_graph's mode-'1' interpolation and interpolate_pred's mode '2' +
+res_cut (train_helper_2d.py:108,116).  ``forward(neighbors, query, '1'|'2')``
+is that module-level MLP in either mode.
 """
 from __future__ import annotations
 
@@ -76,10 +83,25 @@ class ItpNet(nn.Module):
         self._packs[mode] = (key, buf, f)
         return buf
 
+    def weights(self, neighbors: torch.Tensor, query_points: torch.Tensor, mode: str):
+        """interpolate.py:79-93: the 30 weights of every query from its neighbours'
+        coordinates [..., 30, 2] and its own [..., 1, 2] (tanh MLP, linear last)."""
+        L.require_device(neighbors, query_points)
+        mods = self.layers if mode == "1" else self.layers2
+        x = torch.cat((neighbors, query_points), dim=-2).reshape(
+            neighbors.shape[0], neighbors.shape[1], -1)
+        for i, lin in enumerate(mods):
+            x = lin(x)
+            if i != len(mods) - 1:
+                x = torch.tanh(x)
+        return x
+
     def res_cut(self, data: torch.Tensor) -> torch.Tensor:
         """``down`` network (interpolate.py:95-97): data [B, N] (cylinder) or
         [B, 1, s, s] (Burgers)."""
         L.require_device(data)
+        if self.training:
+            return self.down(data)
         d = self.down
         if self.conv:
             x = data
@@ -92,10 +114,11 @@ class ItpNet(nn.Module):
         return x
 
     def forward(self, neighbors, query_points, mode, data=None):
-        if self.training:
-            raise NotImplementedError("training-mode forward is out of scope; call .eval()")
+        """interpolate.py:77-99.  Modes '1'/'2' return the [..., 30] weights;
+        the rollout path never calls this (GraphCreator_FS_2D.interpolate fuses
+        the kNN-30 search, these weights and the weighted sum in one kernel)."""
         if mode == "res_cut":
             return self.res_cut(data)
-        raise NotImplementedError(
-            "modes '1'/'2' are fused with the kNN-30 search and the weighted sum: call "
-            "GraphCreator_FS_2D.interpolate (mmpde_itp_interp)")
+        if mode in ("1", "2"):
+            return self.weights(neighbors, query_points, mode)
+        return data   # interpolate.py:77-99 returns `data` unchanged for other modes

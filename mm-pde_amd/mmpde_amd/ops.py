@@ -177,3 +177,23 @@ def itp_interp(src, vals, qry, idx, batches: int, packed: torch.Tensor, addend=N
                                      batches, ns, nq, L.ptr(packed), L.ptr(add), L.ptr(out),
                                      L.stream(src.device)), "mmpde_itp_interp")
     return out
+
+
+def reverse_adjacency(nbr: torch.Tensor, degree: torch.Tensor | None = None):
+    """Source-major view of a target-major table, for the source-side gradient of
+    the edge stage (mmpde_gnn_edge_source_sum): rev_edge int64 = the live slot
+    ids i*k+e grouped by source j (stable: target order within a source),
+    rev_off int64 [n+1] = the group offsets.  Index plumbing only."""
+    n, k = nbr.shape
+    src = nbr.reshape(-1).long()
+    slot = torch.arange(n * k, device=nbr.device)
+    if degree is not None:
+        live = (torch.arange(k, device=nbr.device)[None, :] < degree[:, None].long()).reshape(-1)
+        src, slot = src[live], slot[live]
+    if src.numel() and (int(src.min()) < 0 or int(src.max()) >= n):
+        raise ValueError("neighbour table holds sources outside [0, n)")
+    order = torch.argsort(src, stable=True)
+    rev_edge = slot[order].contiguous()
+    rev_off = torch.zeros((n + 1,), dtype=torch.int64, device=nbr.device)
+    rev_off[1:] = torch.cumsum(torch.bincount(src, minlength=n), 0)
+    return rev_off, rev_edge

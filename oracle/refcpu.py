@@ -143,10 +143,12 @@ def _lin(sd, p, x):
     return F.linear(x, sd[p + ".weight"], sd[p + ".bias"])
 
 
-def _bn(sd, p, x, eps=1e-5):
-    # nn.BatchNorm1d in eval() (model.eval(), mmpde.py:132-136 / 201)
+def _bn(sd, p, x, eps=1e-5, train=False, momentum=0.1):
+    # nn.BatchNorm1d in eval() (model.eval(), mmpde.py:132-136 / 201); with
+    # train=True the training-mode module (model.train(), mmpde.py:71-73): batch
+    # statistics, running buffers of `sd` updated in place (momentum 0.1)
     return F.batch_norm(x, sd[p + ".running_mean"], sd[p + ".running_var"],
-                        sd[p + ".weight"], sd[p + ".bias"], False, 0.0, eps)
+                        sd[p + ".weight"], sd[p + ".bias"], train, momentum if train else 0.0, eps)
 
 
 def propagate_mean(edge_index, n, message_fn):
@@ -165,7 +167,7 @@ def propagate_mean(edge_index, n, message_fn):
 # ----------------------------------------------------------------------------
 # MP_PDE_Solver_2D -- reference gnn_2d.py:19-141
 # ----------------------------------------------------------------------------
-def gnn_layer(sd, p, x, u, pos_x, pos_y, variables, edge_index):
+def gnn_layer(sd, p, x, u, pos_x, pos_y, variables, edge_index, train=False):
     """GNN_Layer_FS_2D.forward / message / update, gnn_2d.py:53-69."""
     n = x.shape[0]
 
@@ -181,12 +183,13 @@ def gnn_layer(sd, p, x, u, pos_x, pos_y, variables, edge_index):
     upd = torch.relu(_lin(sd, p + ".update_net_2.0", upd))
     x = x + upd
     # PyG BatchNorm wraps nn.BatchNorm1d as `.module` (gnn_2d.py:51,56)
-    return _bn(sd, p + ".norm.module", x)
+    return _bn(sd, p + ".norm.module", x, train=train)
 
 
 def mp_pde_solver(sd, pde: PDEConst, u, pos, edge_index, time_window=1, hidden_layer=6,
-                  return_hidden=False):
-    """MP_PDE_Solver_2D.forward, gnn_2d.py:119-141.  u=[n,tw], pos=[n,3]=(t,x,y)."""
+                  return_hidden=False, train=False):
+    """MP_PDE_Solver_2D.forward, gnn_2d.py:119-141.  u=[n,tw], pos=[n,3]=(t,x,y).
+    train=True: the model.train() forward (BatchNorm on batch statistics)."""
     pos_x = pos[:, 1][:, None] / pde.Lx
     pos_y = pos[:, 2][:, None] / pde.Ly
     pos_t = pos[:, 0][:, None] / pde.tmax
@@ -194,11 +197,12 @@ def mp_pde_solver(sd, pde: PDEConst, u, pos, edge_index, time_window=1, hidden_l
     node_input = torch.cat((u, pos_x, pos_y, variables), -1)
     # embedding_mlp, gnn_2d.py:99-106
     h = _lin(sd, "embedding_mlp.0", node_input)
-    h = torch.relu(_bn(sd, "embedding_mlp.1", h))
-    h = _bn(sd, "embedding_mlp.4", _lin(sd, "embedding_mlp.3", h))
+    h = torch.relu(_bn(sd, "embedding_mlp.1", h, train=train))
+    h = _bn(sd, "embedding_mlp.4", _lin(sd, "embedding_mlp.3", h), train=train)
     hs = [h]
     for i in range(hidden_layer):
-        h = gnn_layer(sd, f"gnn_layers.{i}", h, u, pos_x, pos_y, variables, edge_index)
+        h = gnn_layer(sd, f"gnn_layers.{i}", h, u, pos_x, pos_y, variables, edge_index,
+                      train=train)
         hs.append(h)
     # output_mlp Conv1d head, gnn_2d.py:108-114,136
     d = h[:, None]
@@ -539,6 +543,26 @@ def mmpde_step(pde: PDEConst, sds, data, labels, steps, moving_mesh=True, mesh_o
         ip = interpolate_pred(pde, sds["itp"], out_b, graph, data)
         return ip + out_u, {"graph": graph, "graph_uni": graph_uni, "out_b": out_b,
                             "out_u": out_u, "interp": ip}
+
+
+def mmpde_train_loss(pde: PDEConst, sds, data, labels, steps, mesh_override=None,
+                     moving_mesh=True):
+    """The loss of one training iteration, train_helper_2d.py:107-121
+    (training_loop_branch): graph / graph_uni built with grad enabled, model,
+    model_b in train() mode, pred = interpolate_pred(itp, model_b(graph), graph,
+    data) + model(graph_uni), MSELoss against the un-interpolated labels.  The
+    caller backpropagates (train_helper_2d.py:126).  `sds` tensors that require
+    grad receive their gradients; BatchNorm running buffers update in place."""
+    graph_uni = create_graph(pde, sds.get("itp"), data, labels, steps, dmm_sd=None)
+    out_u = mp_pde_solver(sds["model"], pde, graph_uni.x, graph_uni.pos, graph_uni.edge_index,
+                          train=True)
+    if not moving_mesh:
+        return mse(out_u, labels), {"graph_uni": graph_uni, "pred": out_u}
+    graph = create_graph(pde, sds["itp"], data, labels, steps, dmm_sd=sds.get("dmm"),
+                         mesh_override=mesh_override)
+    out_b = mp_pde_solver(sds["model_b"], pde, graph.x, graph.pos, graph.edge_index, train=True)
+    pred = interpolate_pred(pde, sds["itp"], out_b, graph, data) + out_u
+    return mse(pred, labels), {"graph": graph, "graph_uni": graph_uni, "pred": pred}
 
 
 def mse(pred, labels):

@@ -40,7 +40,7 @@ def test_version_and_status_strings_without_gpu():
     assert lib.mmpde_status_string(0) == b"ok"
     assert lib.mmpde_status_string(-1) == b"invalid argument"
     # sizing helpers are pure host arithmetic
-    assert lib.mmpde_gnn_workspace_bytes(1000) == 6 * 1000 * 128 * 4 + 32768 + 16 * 395776
+    assert lib.mmpde_gnn_workspace_bytes(1000) == 8 * 1000 * 128 * 4 + 32768 + 16 * 395776
     assert lib.mmpde_gnn_pack_bytes(6) == 6 * 395776
     assert lib.mmpde_itp_pack_bytes() > 0
 
@@ -52,3 +52,15 @@ def test_null_arguments_are_rejected_before_launch():
     assert lib.mmpde_knn_graph(None, 1, 100, 35, None, None, None) == -1
     assert lib.mmpde_gnn_edge_mean(None, None, None, 10, 35, None, None, None, None) == -1
     assert lib.mmpde_linear_skinny(None, 1, 1, 1, None, 1, None, 1, 0, None, 1, None) == -1
+    assert lib.mmpde_gnn_edge_mean_deg(None, None, None, None, 10, 35, None, None, None, None) == -1
+    assert lib.mmpde_gnn_edge_backward(None, None, None, None, 10, 35, None, None, None, None,
+                                       None, None, None, None, None) == -1
+    assert lib.mmpde_gnn_edge_source_sum(None, None, None, 10, None, None) == -1
+
+
+def test_edge_backward_partials_sizing_without_gpu():
+    from mmpde_amd import _lib
+
+    g = ctypes.c_int(0)
+    n = _lib.lib().mmpde_gnn_edge_backward_partials(ctypes.byref(g))
+    assert g.value > 0 and n == g.value * (128 * 128 + 128)

@@ -1,0 +1,208 @@
+"""Training backward: gradients of the HIP training path
+against torch.autograd through the float64 oracle.
+
+Reference iteration (train_helper_2d.py:107-128, models in train() mode,
+mmpde.py:71-73,86):
+
+    graph     = create_graph(itp, data, labels, steps, device, mesh_model)
+    graph_uni = create_graph(itp, data, labels, steps, device, None)
+    pred = interpolate_pred(itp, model_b(graph), graph, data, device) + model(graph_uni)
+    loss = MSELoss(pred, labels); loss.backward()
+
+The DMM mesh model is frozen (eval(), not in the AdamW groups of
+mmpde.py:269-271), so the mesh is a constant of the parameter gradients and
+both sides use the same moved mesh (the engine's, injected into the oracle).
+
+Bars, written per check: the edge-stage kernels 2e-5 of max|ref| (fp32
+arithmetic against float64, fixed seeds); every parameter gradient of model,
+model_b and ItpNet max(1e-4, 2 x torch-fp32's) relative L2 and 1e-3 of
+max|ref| element-wise (see _grad_close; a bias feeding a train-mode BatchNorm has an exactly-zero
+gradient: its absolute bar is 1e-4 of the sibling weight's max|ref|); the
+loss 1e-5 relative; BatchNorm running buffers after the step 1e-5 of
+max|ref|.  The same oracle run in float32 is printed beside each gradient as
+the fp32 floor of that quantity.
+"""
+import copy
+import math
+
+import pytest
+import torch
+
+from oracle import refcpu
+
+pytestmark = pytest.mark.gpu
+
+
+def _err(got, ref, what):
+    got = got.detach().double().cpu().reshape(-1)
+    ref = ref.detach().double().cpu().reshape(-1)
+    assert got.shape == ref.shape, (what, got.shape, ref.shape)
+    err = (got - ref).abs().max().item() if ref.numel() else 0.0
+    scale = ref.abs().max().item() if ref.numel() else 0.0
+    print(f"{what}: max|err| {err:.3e} max|ref| {scale:.3e} rel {err / max(scale, 1e-300):.2e}")
+    return err, scale
+
+
+def _close(got, ref, rtol, what, atol=0.0):
+    err, scale = _err(got, ref, what)
+    assert err <= rtol * scale + atol, (what, err, rtol * scale + atol)
+
+
+def _rel_norm(got, ref):
+    got = got.detach().double().cpu().reshape(-1)
+    ref = ref.detach().double().cpu().reshape(-1)
+    return ((got - ref).norm() / ref.norm().clamp(min=1e-300)).item()
+
+
+def _grad_close(got, ref, floor32, what, atol=0.0):
+    """Parameter gradients sum ~1e5 per-edge terms with heavy cancellation, and
+    a ReLU whose input rounds across 0 in one fp32 evaluation and not in another
+    moves single terms (torch's own fp32 autograd does the same, see the printed
+    floor): the bar is a relative L2 error of max(1e-4, 2 x the fp32 oracle's
+    own) -- model_b's inputs come through fp32 interpolation on both fp32
+    sides, which sets a floor near 1e-4 for burgers -- and 1e-3 of max|ref|
+    (+atol) element-wise."""
+    err, scale = _err(got, ref, what)
+    rn, floor = _rel_norm(got, ref), _rel_norm(floor32, ref)
+    print(f"    rel-L2 {rn:.2e} (fp32 oracle {floor:.2e})")
+    assert rn <= max(1e-4, 2 * floor) or (atol and err <= atol), (what, rn, floor)
+    assert err <= 1e-3 * scale + atol, (what, err, 1e-3 * scale + atol)
+
+
+# --------------------------------------------------------------------------- edge stage
+def _edge_mean_ref(a, b, w2, b2, nbr, deg):
+    """gnn_2d.py:59-63 message_net_2 + aggr='mean' over the factored first layer
+    (z1 = a_i + b_j), float64, padding slots (e >= deg) masked."""
+    n, k = nbr.shape
+    live = (torch.arange(k)[None, :] < deg[:, None]).to(a.dtype)
+    z1 = a[:, None, :] + b[nbr.clamp(min=0).long()]
+    m = torch.relu(torch.relu(z1) @ w2.t() + b2) * live[..., None]
+    return m.sum(1) / deg.clamp(min=1).to(a.dtype)[:, None]
+
+
+@pytest.mark.parametrize("ragged", [False, True])
+def test_edge_mean_forward_backward_vs_autograd(dev, ragged):
+    from mmpde_amd.gnn_2d import EdgeGraph, EdgeMean
+
+    g = torch.Generator().manual_seed(5 + ragged)
+    n, k = 203, 9                         # a partial last 16-row tile
+    a = 0.5 * torch.randn(n, 128, generator=g)
+    b = 0.5 * torch.randn(n, 128, generator=g)
+    w2 = torch.randn(128, 128, generator=g) / math.sqrt(128)
+    b2 = 0.1 * torch.randn(128, generator=g)
+    nbr = torch.randint(0, n, (n, k), generator=g, dtype=torch.int32)
+    if ragged:
+        deg = torch.randint(0, k + 1, (n,), generator=g, dtype=torch.int32)
+        deg[:3] = 0                       # isolated targets: mean 0, no gradient
+        nbr[torch.arange(k)[None, :] >= deg[:, None]] = -1
+    else:
+        deg = torch.full((n,), k, dtype=torch.int32)
+    gout = torch.randn(n, 128, generator=g)
+
+    ref_in = [t.double().requires_grad_() for t in (a, b, w2, b2)]
+    ref = _edge_mean_ref(*ref_in, nbr, deg)
+    (ref * gout.double()).sum().backward()
+
+    graph = EdgeGraph(nbr.to(dev), deg.to(dev) if ragged else None)
+    got_in = [t.to(dev).requires_grad_() for t in (a, b, w2, b2)]
+    out = EdgeMean.apply(*got_in, graph)
+    (out * gout.to(dev)).sum().backward()
+    torch.cuda.synchronize()
+    tag = "ragged" if ragged else "fixed"
+    _close(out, ref, 2e-5, f"{tag} mean")
+    for name, t, r in zip(("a", "b", "W2", "b2"), got_in, ref_in):
+        _close(t.grad, r.grad, 2e-5, f"{tag} d/d{name}")
+    # deterministic: a second backward gives the same bits
+    grads = [t.grad.clone() for t in got_in]
+    for t in got_in:
+        t.grad = None
+    EdgeMean.apply(*got_in, graph).mul(gout.to(dev)).sum().backward()
+    for t, g0 in zip(got_in, grads):
+        assert torch.equal(t.grad, g0)
+
+
+# --------------------------------------------------------------------------- whole step
+def _sds(dtype=torch.float64, **mods):
+    """State dicts in `dtype`; parameters are autograd leaves, buffers plain copies."""
+    out = {}
+    for key, m in mods.items():
+        params = {n for n, _ in m.named_parameters()}
+        d = {}
+        for n, t in m.state_dict().items():
+            t = t.detach().cpu().clone()
+            if t.is_floating_point():
+                t = t.to(dtype)
+                if n in params:
+                    t.requires_grad_(True)
+            d[n] = t
+        out[key] = d
+    return out
+
+
+def _setup(kind, B, seed=0):
+    from mmpde_amd.synth import build_models, burgers_grid_points, fields
+
+    pde, model, model_b, itp, dmm, gc = build_models(kind, seed=seed)
+    if kind == "cy":
+        u = fields(pde.ori_grid, B, 30, seed=seed + 1)
+        opde = refcpu.PDEConst("cy", pde.grid_size, ori_grid=pde.ori_grid.double())
+    else:
+        u = fields(burgers_grid_points(), B, 31, seed=seed + 1).reshape(B, 31, 48, 48)
+        opde = refcpu.PDEConst("burgers", pde.grid_size)
+    return pde, opde, model, model_b, itp, dmm, gc, u
+
+
+@pytest.mark.parametrize("kind", ["cy", "burgers"])
+def test_training_step_gradients_vs_oracle(dev, kind):
+    torch.set_num_threads(min(16, torch.get_num_threads()))
+    B = 2
+    pde, opde, model, model_b, itp, dmm, gc, u = _setup(kind, B)
+    steps = [4, 11]
+    sds = _sds(model=model, model_b=model_b, itp=itp)
+    sds32 = _sds(torch.float32, model=model, model_b=model_b, itp=itp)   # the fp32 floor
+    for m in (model, model_b, itp, dmm):
+        m.to(dev)
+    model.train()
+    model_b.train()
+    itp.train()
+    dmm.eval()                            # frozen mesh model (mmpde.py:201)
+
+    data, labels = gc.create_data(u, steps)
+    graph = gc.create_graph(itp, data, labels, steps, dev, dmm)
+    graph_uni = gc.create_graph(itp, data, labels, steps, dev, None)
+    pred = gc.interpolate_pred(itp, model_b(graph), graph, data, dev) + model(graph_uni)
+    loss = torch.nn.MSELoss()(pred, labels.to(dev).reshape(-1, 1))
+    loss.backward()
+    torch.cuda.synchronize()
+
+    mesh = graph.pos[:, 1:3].detach().cpu().double()
+    rloss, aux = refcpu.mmpde_train_loss(opde, sds, data.double(), labels.double(), steps,
+                                         mesh_override=mesh)
+    rloss.backward()
+    opde32 = copy.copy(opde)
+    if opde.ori_grid is not None:
+        opde32.ori_grid = opde.ori_grid.float()
+    loss32, _ = refcpu.mmpde_train_loss(opde32, sds32, data, labels, steps,
+                                        mesh_override=mesh.float())
+    loss32.backward()
+    assert torch.equal(graph.edge_index.cpu(), aux["graph"].edge_index)
+    _close(pred, aux["pred"], 2e-5, f"{kind} train-mode pred")
+    assert abs(loss.item() - rloss.item()) <= 1e-5 * rloss.item(), (loss.item(), rloss.item())
+
+    checked = 0
+    for key, mod in (("model", model), ("model_b", model_b), ("itp", itp)):
+        for name, p in mod.named_parameters():
+            r = sds[key][name].grad
+            if r is None:                 # layers3 (never used) / unused modes
+                assert p.grad is None or not p.grad.abs().max().item()
+                continue
+            assert p.grad is not None, f"{key}.{name} got no gradient"
+            atol = 0.0
+            if name.endswith(".bias"):
+                atol = 1e-4 * sds[key][name[:-5] + ".weight"].grad.abs().max().item()
+            _grad_close(p.grad, r, sds32[key][name].grad, f"{kind} grad {key}.{name}", atol=atol)
+            checked += 1
+        for name, buf in mod.named_buffers():
+            if name.endswith(("running_mean", "running_var")):
+                _close(buf, sds[key][name], 1e-5, f"{kind} {key}.{name} after step")
+    assert checked == 2 * 74 + (14 if kind == "cy" else 20)   # every trained parameter

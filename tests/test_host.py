@@ -65,11 +65,18 @@ def test_no_cpu_fallback():
         itp.res_cut(torch.zeros(1, 100))
 
 
-def test_training_mode_is_refused():
+def test_training_mode_needs_device_tensors():
+    """train() mode runs the differentiable HIP path (tests/test_gpu_train.py);
+    on host tensors it refuses instead of falling back to a CPU computation."""
+    from mmpde_amd.graph import Data
+
     _, model, _, _, _, _ = build_models("cy", grid=torch.rand(100, 2), moving_mesh=False)
     model.train()
-    with pytest.raises(NotImplementedError):
-        model.check_supported()
+    g = Data(x=torch.rand(100, 1), edge_index=None)
+    g.pos = torch.rand(100, 3)
+    g.nbr = torch.zeros((100, 4), dtype=torch.int32)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        model(g)
 
 
 def test_pde_constants():
