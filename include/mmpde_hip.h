@@ -212,6 +212,12 @@ int mmpde_gnn_edge_backward(const float *a, const float *b, const int32_t *nbr, 
  * order given: deterministic). */
 int mmpde_gnn_edge_source_sum(const float *grad_edge, const int64_t *rev_off, const int64_t *rev_edge,
                               int64_t n, float *grad_b, mmpde_stream_t stream);
+/* The same segmented sum for rows of any width: out[j, :] = sum over q in
+ * [rev_off[j], rev_off[j+1]) of rows[rev_edge[q], :] (n output rows), in list
+ * order.  The deterministic backward of a row gather (the kNN-30 neighbour
+ * values of the training-mode interpolation, data_creator_2d.py:77-83). */
+int mmpde_segment_sum(const float *rows, int64_t width, const int64_t *rev_off, const int64_t *rev_edge,
+                      int64_t n, float *out, mmpde_stream_t stream);
 
 /* out[n] = out_scale * output_mlp(h[:, None]) */
 int mmpde_gnn_head(const float *h, int64_t n, const mmpde_gnn_head_params *p, float *out,

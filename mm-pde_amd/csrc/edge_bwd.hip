@@ -215,6 +215,20 @@ __global__ __launch_bounds__(256) void edge_source_sum_kernel(const float *__res
     ((float2 *)(out + j * BH))[lane] = acc;
 }
 
+// out[j][c] = sum_{p in [off[j], off[j+1])} rows[edge[p]][c] for any row width:
+// one thread per (j, c), in list order.
+__global__ __launch_bounds__(256) void segment_sum_kernel(const float *__restrict__ rows, int64_t width,
+                                                          const int64_t *__restrict__ off,
+                                                          const int64_t *__restrict__ edge, int64_t n,
+                                                          float *__restrict__ out) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= n * width) return;
+    const int64_t j = t / width, c = t - j * width;
+    float acc = 0.0f;
+    for (int64_t q = off[j]; q < off[j + 1]; ++q) acc += rows[edge[q] * width + c];
+    out[t] = acc;
+}
+
 // out[i] = sum_{g < G} part[g * len + i], in g order.
 __global__ __launch_bounds__(256) void partial_sum_kernel(const float *__restrict__ part, int G, int64_t len,
                                                           float *__restrict__ out) {
@@ -266,6 +280,16 @@ extern "C" int mmpde_gnn_edge_source_sum(const float *grad_edge, const int64_t *
     MMPDE_REQUIRE(grad_edge && rev_off && rev_edge && grad_b && n > 0);
     hipLaunchKernelGGL(edge_source_sum_kernel, dim3((unsigned)ceil_div(n, 4)), dim3(256), 0, as_stream(stream),
                        grad_edge, rev_off, rev_edge, n, grad_b);
+    MMPDE_RET_LAUNCH();
+    return MMPDE_OK;
+}
+
+extern "C" int mmpde_segment_sum(const float *rows, int64_t width, const int64_t *rev_off,
+                                 const int64_t *rev_edge, int64_t n, float *out, mmpde_stream_t stream) {
+    MMPDE_REQUIRE(rows && rev_off && rev_edge && out && n > 0 && width > 0);
+    MMPDE_REQUIRE(n * width / 256 < (int64_t)INT32_MAX);
+    hipLaunchKernelGGL(segment_sum_kernel, dim3((unsigned)ceil_div(n * width, 256)), dim3(256), 0,
+                       as_stream(stream), rows, width, rev_off, rev_edge, n, out);
     MMPDE_RET_LAUNCH();
     return MMPDE_OK;
 }

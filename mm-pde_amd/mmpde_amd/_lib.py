@@ -106,6 +106,7 @@ _SIGS = {
     "mmpde_gnn_edge_backward_partials": (_I64, [ctypes.POINTER(_I)]),
     "mmpde_gnn_edge_backward": (_I, [_P, _P, _P, _P, _I64, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "mmpde_gnn_edge_source_sum": (_I, [_P, _P, _P, _I64, _P, _P]),
+    "mmpde_segment_sum": (_I, [_P, _I64, _P, _P, _I64, _P, _P]),
     "mmpde_gnn_head": (_I, [_P, _I64, _P, _P, _P]),
     "mmpde_gnn_forward": (_I, [_P, _P, _I64, _I, _P, GnnScales, _P, _P, _I, _P, _P, _P, _P]),
     "mmpde_gnn_pack_bytes": (_I64, [_I]),

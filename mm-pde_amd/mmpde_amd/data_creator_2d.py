@@ -143,7 +143,8 @@ class GraphCreator_FS_2D(nn.Module):  # noqa: N801 - reference name
         gidx = idx.long().reshape(nu, nq * 30)
         pts = src.reshape(nu, ns, 2)
         nb = torch.gather(pts, 1, gidx[..., None].expand(nu, nq * 30, 2)).reshape(nu, nq, 30, 2)
-        lab = torch.gather(u.reshape(nu, ns), 1, gidx).reshape(nu, nq, 30)
+        flat = (gidx + ns * torch.arange(nu, device=gidx.device)[:, None]).reshape(-1)
+        lab = ops.GatherRows.apply(u.reshape(nu * ns, 1).float(), flat).reshape(nu, nq, 30)
         w = itp_model.weights(nb, qry.reshape(nu, nq, 1, 2), mode)
         out = torch.sum(w * lab, dim=-1).reshape(-1)
         return out if addend is None else out + addend
@@ -201,7 +202,10 @@ class GraphCreator_FS_2D(nn.Module):  # noqa: N801 - reference name
         # node tensors (data_creator_2d.py:242-254): u [B*n, tw], labels, t[step]
         u_nodes = data.reshape(B, self.tw, n).permute(0, 2, 1).reshape(B * n, self.tw)
         y_nodes = labels.reshape(B, self.tw, n).permute(0, 2, 1).reshape(B * n, self.tw)
-        t_nodes = t[list(steps)].to(device).repeat_interleave(n)
+        # steps[b] for the B trajectories only: training_itp passes 128 x batch_size
+        # steps for a batch of batch_size (train_helper_2d.py:44,47; the reference
+        # loops b over the data, data_creator_2d.py:243-254)
+        t_nodes = t[list(steps)[:B]].to(device).repeat_interleave(n)
         deg = None
         if self.e == "radius":   # torch_cluster default max_num_neighbors = 32
             nbr, deg = ops.radius_graph_nbr(mesh.contiguous(), B, self.radius(), 32)

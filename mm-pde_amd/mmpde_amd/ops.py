@@ -179,14 +179,17 @@ def itp_interp(src, vals, qry, idx, batches: int, packed: torch.Tensor, addend=N
     return out
 
 
-def reverse_adjacency(nbr: torch.Tensor, degree: torch.Tensor | None = None):
+def reverse_adjacency(nbr: torch.Tensor, degree: torch.Tensor | None = None,
+                      n_src: int | None = None):
     """Source-major view of a target-major table, for the source-side gradient of
     the edge stage (mmpde_gnn_edge_source_sum): rev_edge int64 = the live slot
     ids i*k+e grouped by source j (stable: target order within a source),
-    rev_off int64 [n+1] = the group offsets.  Index plumbing only."""
-    n, k = nbr.shape
+    rev_off int64 [n_src+1] = the group offsets (n_src defaults to the number of
+    targets).  Index plumbing only."""
+    nt, k = nbr.shape
+    n = nt if n_src is None else n_src
     src = nbr.reshape(-1).long()
-    slot = torch.arange(n * k, device=nbr.device)
+    slot = torch.arange(nt * k, device=nbr.device)
     if degree is not None:
         live = (torch.arange(k, device=nbr.device)[None, :] < degree[:, None].long()).reshape(-1)
         src, slot = src[live], slot[live]
@@ -197,3 +200,27 @@ def reverse_adjacency(nbr: torch.Tensor, degree: torch.Tensor | None = None):
     rev_off = torch.zeros((n + 1,), dtype=torch.int64, device=nbr.device)
     rev_off[1:] = torch.cumsum(torch.bincount(src, minlength=n), 0)
     return rev_off, rev_edge
+
+
+class GatherRows(torch.autograd.Function):
+    """rows[idx] for a flat index list, whose backward is the fixed-order
+    segmented sum mmpde_segment_sum over the reverse index lists (torch's
+    scatter-add backward of a gather accumulates with atomics, in no fixed
+    order).  rows [n, w] fp32, idx int [m] -> [m, w]."""
+
+    @staticmethod
+    def forward(ctx, rows, idx):
+        L.require_device(rows, idx)
+        ctx.n = rows.shape[0]
+        ctx.idx = idx
+        return rows[idx.long()]
+
+    @staticmethod
+    def backward(ctx, g):
+        g = L.f32c(g)
+        n, w = ctx.n, g.shape[1]
+        rev_off, rev_edge = reverse_adjacency(ctx.idx.reshape(-1, 1), n_src=n)
+        out = torch.empty((n, w), dtype=torch.float32, device=g.device)
+        L.check(L.lib().mmpde_segment_sum(L.ptr(g), w, L.ptr(rev_off), L.ptr(rev_edge), n,
+                                          L.ptr(out), L.stream(g.device)), "mmpde_segment_sum")
+        return out, None

@@ -206,3 +206,56 @@ def test_training_step_gradients_vs_oracle(dev, kind):
             if name.endswith(("running_mean", "running_var")):
                 _close(buf, sds[key][name], 1e-5, f"{kind} {key}.{name} after step")
     assert checked == 2 * 74 + (14 if kind == "cy" else 20)   # every trained parameter
+
+
+# --------------------------------------------------------------------------- loops
+def _loop_run(dev, seed):
+    import random
+
+    from mmpde_amd.train import training_itp, training_loop_branch
+
+    pde, opde, model, model_b, itp, dmm, gc, u = _setup("cy", 4, seed=2)
+    for m in (model, model_b, itp, dmm):
+        m.to(dev)
+    model.train()
+    model_b.train()
+    itp.train()
+    dmm.eval()
+    opt = torch.optim.AdamW([{"params": model.parameters()}, {"params": model_b.parameters()},
+                             {"params": itp.parameters()}], lr=1e-4)   # mmpde.py:269-271
+    ds = torch.utils.data.TensorDataset(u, u)
+    loader = torch.utils.data.DataLoader(ds, batch_size=2, shuffle=False)
+    crit = torch.nn.MSELoss()
+    random.seed(seed)
+    li = training_itp(itp, dmm, [0], 128 * 2, opt, None, loader, gc, crit, dev)
+    lb = training_loop_branch(model, model_b, itp, dmm, [0, 1], 2, opt, None, loader, gc, crit,
+                              dev)
+    lb2 = training_loop_branch(model, model_b, itp, dmm, [0, 1], 2, opt, None, loader, gc, crit,
+                               dev)
+    params = {f"{k}.{n}": p.detach().cpu().clone()
+              for k, m in (("model", model), ("model_b", model_b), ("itp", itp))
+              for n, p in m.named_parameters()}
+    return li.cpu(), torch.cat((lb, lb2)).cpu(), params
+
+
+def test_training_loops_deterministic_and_learning(dev):
+    """training_itp + two epochs of training_loop_branch (train_helper_2d.py:9-134)
+    with AdamW: finite, the GNN loss falls, and a second run from the same seed
+    reproduces every loss and every parameter bit for bit.  The HIP kernels are
+    deterministic by construction (no atomics, fixed reduction orders); the
+    library ops around them (MIOpen / hipBLASLt backward) are made so with
+    torch.use_deterministic_algorithms -- without it the losses still repeat
+    but the parameters drift in the last bits."""
+    torch.use_deterministic_algorithms(True, warn_only=True)
+    try:
+        li, lb, p = _loop_run(dev, 0)
+        li2, lb2, p2 = _loop_run(dev, 0)
+    finally:
+        torch.use_deterministic_algorithms(False)
+    print("itp losses", li.tolist(), "branch losses", lb.tolist())
+    assert torch.isfinite(li).all() and torch.isfinite(lb).all()
+    assert all(torch.isfinite(t).all() for t in p.values())
+    assert lb[2:].mean() < lb[:2].mean()
+    differ = [n for n in p if not torch.equal(p[n], p2[n])]
+    print("parameters differing between the runs:", differ)
+    assert torch.equal(li, li2) and torch.equal(lb, lb2) and not differ
