@@ -1,0 +1,104 @@
+"""Training-iteration timing (not the headline metric).
+
+One iteration of train_helper_2d.py:95-131 (training_loop_branch's body) on
+synthetic cylinder data at BASELINE configs[3]'s shape (B trajectories of the
+2521-node mesh, k = 35, DMM frozen): create_graph x 2, model_b / model
+forward in train() mode, interpolate_pred, MSE, backward, AdamW step.  Prints
+one JSON line with ms per iteration and node-updates/s (B*N nodes of both
+GNNs' forward + backward per iteration).  The edge-stage backward kernel is
+timed with HIP events around a standalone EdgeMean backward of one layer.
+
+    python tools/train_bench.py [--batch 16] [--iters 10] [--warmup 3]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "mm-pde_amd")]
+
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    args = ap.parse_args()
+    from mmpde_amd.gnn_2d import EdgeGraph, EdgeMean
+    from mmpde_amd.synth import build_models, fields
+
+    dev = torch.device("cuda:0")
+    B = args.batch
+    pde, model, model_b, itp, dmm, gc = build_models("cy", seed=0)
+    u = fields(pde.ori_grid, B, 30, seed=1)
+    for m in (model, model_b, itp, dmm):
+        m.to(dev)
+    model.train()
+    model_b.train()
+    itp.train()
+    dmm.eval()
+    opt = torch.optim.AdamW([{"params": model.parameters()}, {"params": model_b.parameters()},
+                             {"params": itp.parameters()}], lr=1e-4)
+    crit = torch.nn.MSELoss()
+    steps = [(3 + 7 * b) % 27 + 1 for b in range(B)]
+    data, labels = gc.create_data(u, steps)
+    data, labels = data.to(dev), labels.to(dev)
+
+    def it():
+        opt.zero_grad()
+        graph = gc.create_graph(itp, data, labels, steps, dev, dmm)
+        graph_uni = gc.create_graph(itp, data, labels, steps, dev, None)
+        pred = gc.interpolate_pred(itp, model_b(graph), graph, data, dev) + model(graph_uni)
+        loss = crit(pred, labels.reshape(-1, 1))
+        loss.backward()
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        it()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.iters):
+        loss = it()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3 / args.iters
+
+    # one layer's edge backward alone (HIP events on the current stream)
+    n = B * 2521
+    g = torch.Generator(device="cpu").manual_seed(0)
+    a = torch.randn(n, 128, generator=g).to(dev).requires_grad_()
+    b = torch.randn(n, 128, generator=g).to(dev).requires_grad_()
+    lay = model.gnn_layers[0].message_net_2[0]
+    from mmpde_amd.ops import knn_graph_nbr
+    graph = EdgeGraph(knn_graph_nbr(gc.uniform_grid(dev).repeat(B, 1), B, 35))
+    gout = torch.randn(n, 128, device=dev)
+    for _ in range(3):
+        EdgeMean.apply(a, b, lay.weight, lay.bias, graph).backward(gout)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 10
+    out = EdgeMean.apply(a, b, lay.weight, lay.bias, graph)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(reps):
+        torch.autograd.grad(out, (a, b, lay.weight, lay.bias), gout, retain_graph=True)
+    e1.record()
+    torch.cuda.synchronize()
+    bwd_us = e0.elapsed_time(e1) * 1e3 / reps
+    edges = n * 35
+    flops = 3 * 2 * edges * 128 * 128          # z2, gm1 and the dW2 outer products
+    print(json.dumps({
+        "what": "MM-PDE training iteration (train_helper_2d.py:95-131), cy synthetic",
+        "batch": B, "nodes": n, "ms_per_iter": round(ms, 3),
+        "train_node_updates_per_s": round(2 * 6 * n / (ms * 1e-3)),
+        "loss": float(loss),
+        "edge_backward_layer_us": round(bwd_us, 1),
+        "edge_backward_tflops_fp32": round(flops / (bwd_us * 1e-6) / 1e12, 2),
+    }))
+
+
+if __name__ == "__main__":
+    main()
