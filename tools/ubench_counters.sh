@@ -9,7 +9,7 @@ i=0
 for grp in "$@"; do
   i=$((i+1))
   timeout -k 10 ${PMC_TIMEOUT:-300} rocprofv3 --pmc $grp --output-format csv -d "$OUT/g$i" -o run -- \
-      tools/ubench/fused_ubench 16 > "$OUT/g$i.log" 2>&1
+      ${UBENCH:-tools/ubench/fused_ubench 16} > "$OUT/g$i.log" 2>&1
   rc=$?
   echo "pmc group $i rc=$rc"
   if [ $rc -ne 0 ]; then tail -20 "$OUT/g$i.log"; exit $rc; fi
