@@ -99,6 +99,18 @@ int mmpde_edge_index_from_nbr(const int32_t *nbr, int64_t n, int k, int64_t *edg
 int mmpde_linear_skinny(const float *x, int64_t ldx, int64_t m, int64_t k, const float *w,
                         int64_t ldw, const float *b, int64_t n, int act, float *y,
                         int64_t ldy, mmpde_stream_t stream);
+/* The same with a device workspace of at least
+ * mmpde_linear_skinny_workspace_bytes(m, n, k) bytes (0: none needed), ZEROED
+ * before its first use and then reused (the call leaves its counters at zero
+ * again): K is split over several workgroups per output tile so that the
+ * weight stream fills the chip, and the partial tiles are added in a fixed
+ * order inside the launch (results identical run to run).  A NULL / short
+ * workspace falls back to no split.  Layout: 4096 ticket words (the only
+ * words that must start at zero), then the partial tiles. */
+int64_t mmpde_linear_skinny_workspace_bytes(int64_t m, int64_t n, int64_t k);
+int mmpde_linear_skinny_ws(const float *x, int64_t ldx, int64_t m, int64_t k, const float *w,
+                           int64_t ldw, const float *b, int64_t n, int act, float *y, int64_t ldy,
+                           float *workspace, int64_t workspace_bytes, mmpde_stream_t stream);
 
 /* out[b] = mean_i (pred[b, i] - labels[b, i])^2 per trajectory b (n_per values
  * each): the loss of mmpde.py:33-36 (MSELoss) kept per trajectory for the

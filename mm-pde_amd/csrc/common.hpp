@@ -111,3 +111,14 @@ struct BnAffine {
 };
 
 static inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+// library-internal entry points shared between translation units
+namespace mmpde_detail {
+// mmpde_conv2d (dense.hip) with a side job: threads [0, n_zero) also store 0
+// to zero[] (dmm.hip's split-K tickets, zeroed by its first kernel)
+__attribute__((visibility("hidden"))) int conv2d(const float *x, int64_t batches, int cin, int h,
+                                                 int w, const float *weight, const float *bias,
+                                                 int cout, int ks, int stride, int pad,
+                                                 const float *residual, int act, float *y,
+                                                 hipStream_t st, unsigned *zero, int n_zero);
+}  // namespace mmpde_detail

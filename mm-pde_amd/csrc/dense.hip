@@ -18,7 +18,15 @@ namespace {
 // products; lane (r, g) holds k = 16 q + 4 g + t of float4 number q).  The
 // per-wave partial tiles meet in LDS in a fixed order (deterministic).
 constexpr int kSkW = 8;               // waves per workgroup
+constexpr int kSkMaxZ = 16;           // K splits at most
 
+// Split K (part != nullptr): workgroup z of gridDim.z takes chunks
+// [z nchz, (z + 1) nchz) of K and stores its raw tile to part[z][m][n]; the
+// last of a tile's gridDim.z workgroups to finish (ticket counter, agent-scope
+// release / acquire) adds the partial tiles in z order (a fixed order:
+// deterministic) with the bias and activation.  Splitting K fills the chip
+// when n / 16 tiles alone are too few (res_cut: 128 - 158 tiles).  The
+// tickets (zero before the first launch) are reset by the reducing slice.
 template <int kSkW>
 __global__ __launch_bounds__(kSkW * 64) void linear_skinny_kernel(const float *__restrict__ x,
                                                                   int64_t ldx, int64_t m, int64_t k,
@@ -26,7 +34,9 @@ __global__ __launch_bounds__(kSkW * 64) void linear_skinny_kernel(const float *_
                                                                   int64_t ldw,
                                                                   const float *__restrict__ b,
                                                                   int64_t n, int act,
-                                                                  float *__restrict__ y, int64_t ldy) {
+                                                                  float *__restrict__ y, int64_t ldy,
+                                                                  int nchz, float *__restrict__ part,
+                                                                  unsigned *__restrict__ tickets) {
     constexpr int C = 64 * kSkW, LD = C + 4;
     __shared__ float sw[16 * LD], sx[16 * LD];
     const int tid = threadIdx.x;
@@ -35,7 +45,8 @@ __global__ __launch_bounds__(kSkW * 64) void linear_skinny_kernel(const float *_
     const int r = lane & 15, g = lane >> 4;
     const int64_t col0 = (int64_t)blockIdx.x * 16, row0 = (int64_t)blockIdx.y * 16;
     const int K = (int)k;
-    const int nch = (K + C - 1) / C;
+    const int c0 = (int)blockIdx.z * nchz;
+    const int nch = min((K + C - 1) / C - c0, nchz);
     // loader role: rows i = 0..15 of both tiles at k = kc + tid
     float lw[16], lx[16];
     auto load = [&](int kc) {
@@ -51,7 +62,7 @@ __global__ __launch_bounds__(kSkW * 64) void linear_skinny_kernel(const float *_
         }
     };
     f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-    load(0);
+    if (nch > 0) load(c0 * C);
     for (int c = 0; c < nch; ++c) {
         if (c) __syncthreads();  // chunk c - 1 consumed
 #pragma unroll
@@ -60,7 +71,7 @@ __global__ __launch_bounds__(kSkW * 64) void linear_skinny_kernel(const float *_
             sx[i * LD + tid] = lx[i];
         }
         __syncthreads();
-        if (c + 1 < nch) load((c + 1) * C);
+        if (c + 1 < nch) load((c0 + c + 1) * C);
         const float *aw = sw + r * LD + 64 * wave + 4 * g;
         const float *ax = sx + r * LD + 64 * wave + 4 * g;
 #pragma unroll
@@ -74,14 +85,74 @@ __global__ __launch_bounds__(kSkW * 64) void linear_skinny_kernel(const float *_
         }
     }
     __syncthreads();
-    f32x4 *part = (f32x4 *)sw;  // [wave][lane]
-    part[wave * 64 + lane] = acc;
+    f32x4 *wpart = (f32x4 *)sw;  // [wave][lane]
+    wpart[wave * 64 + lane] = acc;
     __syncthreads();
     if (wave != 0) return;
-    f32x4 s = part[lane];
+    f32x4 s = wpart[lane];
 #pragma unroll
-    for (int v = 1; v < kSkW; ++v) s += part[v * 64 + lane];
+    for (int v = 1; v < kSkW; ++v) s += wpart[v * 64 + lane];
     const int64_t col = col0 + r;
+    if (part) {
+        float *pz = part + (int64_t)blockIdx.z * m * n;
+        if (col < n) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int64_t row = row0 + 4 * g + q;
+                // write-through (sc1) store: visible chip-wide once drained,
+                // no release fence (no L2 write-back of the whole XCD)
+                if (row < m)
+                    __hip_atomic_store(pz + row * n + col, s[q], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        if (!tickets) return;
+        // in-launch reduction (cdna_hip_programming.md, split-K hand-off, sc1
+        // form): the slice that draws the last ticket of its tile adds the
+        // gridDim.z partial tiles in z order (deterministic), then resets the
+        // ticket.  The one storing wave drains its sc1 stores before the ticket.
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // the ticket's address goes through a VGPR the compiler cannot fold, so the
+        // atomic and the reset are vector-memory operations (never scalar-cache
+        // writes)
+        int vzero;
+        asm volatile("v_mov_b32 %0, 0" : "=v"(vzero));
+        unsigned *tk = tickets + blockIdx.y * gridDim.x + blockIdx.x + vzero;
+        unsigned ticket = 0u;
+        if (lane == 0) ticket = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // lane 0's ticket to the whole wave (register broadcast: an LDS flag
+        // would need a barrier the single remaining wave cannot order by itself)
+        ticket = __builtin_amdgcn_readfirstlane(ticket);
+        if (ticket != gridDim.z - 1) return;
+        // every slab load is an sc1 (agent-scope) load, so no acquire fence:
+        // the wavefront fence only keeps the loads below the ticket
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // every slab load issued before the first add (clamped addresses, no
+        // per-load branches), then the adds in z order
+        const int Z = (int)gridDim.z;
+        const int64_t cc = min(col, n - 1);
+        float v[kSkMaxZ][4];
+#pragma unroll
+        for (int zz = 0; zz < kSkMaxZ; ++zz) {
+            if (zz < Z) {
+                const float *pq = part + (int64_t)zz * m * n + cc;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    v[zz][q] = __hip_atomic_load(pq + min(row0 + 4 * g + q, m - 1) * n, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        f32x4 t = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int zz = 0; zz < kSkMaxZ; ++zz) {
+            if (zz < Z) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) t[q] += v[zz][q];
+            }
+        }
+        if (lane == 0) *tk = 0u;
+        s = t;
+    }
     if (col >= n) return;
     const float bb = b ? b[col] : 0.0f;
 #pragma unroll
@@ -91,6 +162,18 @@ __global__ __launch_bounds__(kSkW * 64) void linear_skinny_kernel(const float *_
     }
 }
 
+// K splits of a skinny linear: enough workgroups for ~4 per CU, chunks of
+// 64 kSkW k each, at most 16 splits
+inline int skinny_splits(int64_t m, int64_t n, int64_t k, int cus) {
+    const int64_t tiles = ((n + 15) / 16) * ((m + 15) / 16);
+    if (tiles > 4096) return 1;  // = kSkTickets
+    const int64_t chunks = (k + 64 * kSkW - 1) / (64 * kSkW);
+    int64_t z = (4 * (int64_t)cus + tiles - 1) / tiles;
+    z = z < chunks ? z : chunks;
+    z = z < kSkMaxZ ? z : kSkMaxZ;
+    return z > 1 ? (int)z : 1;
+}
+
 // one thread per output element; weight [cout][cin][ks][ks] (PyTorch layout)
 __global__ __launch_bounds__(256) void conv2d_kernel(const float *__restrict__ x, int64_t batches,
                                                      int cin, int h, int w,
@@ -98,9 +181,11 @@ __global__ __launch_bounds__(256) void conv2d_kernel(const float *__restrict__ x
                                                      const float *__restrict__ bias, int cout,
                                                      int ks, int stride, int pad, int oh, int ow,
                                                      const float *__restrict__ res, int act,
-                                                     float *__restrict__ y) {
+                                                     float *__restrict__ y,
+                                                     unsigned *__restrict__ zero, int n_zero) {
     const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const int64_t total = batches * cout * oh * ow;
+    if (e < n_zero) zero[e] = 0u;  // side job for the caller (dmm.hip's split-K tickets)
     if (e >= total) return;
     const int ox = (int)(e % ow);
     const int oy = (int)((e / ow) % oh);
@@ -150,7 +235,7 @@ __global__ __launch_bounds__(256) void traj_mse_kernel(const float *__restrict__
 
 }  // namespace
 
-extern "C" int mmpde_version(void) { return 10800; }
+extern "C" int mmpde_version(void) { return 10900; }
 
 extern "C" int mmpde_traj_mse(const float *pred, const float *labels, int64_t batches, int64_t n_per,
                               float *out, mmpde_stream_t stream) {
@@ -169,17 +254,52 @@ extern "C" const char *mmpde_status_string(int status) {
     return "unknown status";
 }
 
-extern "C" int mmpde_linear_skinny(const float *x, int64_t ldx, int64_t m, int64_t k,
-                                   const float *w, int64_t ldw, const float *b, int64_t n,
-                                   int act, float *y, int64_t ldy, mmpde_stream_t stream) {
+static int skinny_cus() {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+        return 256;
+    return cus;
+}
+
+// split-K scratch: a FIXED block of kSkTickets ticket words (one per output
+// tile; the same words for every shape, so one call's partial tiles never land
+// on another call's tickets when a workspace is reused), then z partial tiles.
+// A split only pays below ~4 workgroups per CU, i.e. far fewer tiles than this.
+constexpr int64_t kSkTickets = 4096;
+static int64_t skinny_ws_bytes(int64_t m, int64_t n, int z) {
+    return z > 1 ? (kSkTickets + (int64_t)z * m * n) * (int64_t)sizeof(float) : 0;
+}
+
+extern "C" int64_t mmpde_linear_skinny_workspace_bytes(int64_t m, int64_t n, int64_t k) {
+    if (m <= 0 || n <= 0 || k <= 0) return 0;
+    return skinny_ws_bytes(m, n, skinny_splits(m, n, k, skinny_cus()));
+}
+
+extern "C" int mmpde_linear_skinny_ws(const float *x, int64_t ldx, int64_t m, int64_t k, const float *w,
+                                      int64_t ldw, const float *b, int64_t n, int act, float *y, int64_t ldy,
+                                      float *workspace, int64_t workspace_bytes, mmpde_stream_t stream) {
     MMPDE_REQUIRE(x && w && y && m > 0 && k > 0 && n > 0 && m <= 4096);
     MMPDE_REQUIRE(ldx >= k && ldw >= k && ldy >= n && act >= 0 && act <= 2);
     hipStream_t st = as_stream(stream);
-    const dim3 grid((unsigned)ceil_div(n, 16), (unsigned)ceil_div(m, 16));
+    int z = skinny_splits(m, n, k, skinny_cus());
+    if (!workspace || workspace_bytes < skinny_ws_bytes(m, n, z)) z = 1;
+    const int chunks = ceil_div(k, 64 * kSkW);
+    const int nchz = z > 1 ? ceil_div(chunks, z) : chunks;
+    z = z > 1 ? ceil_div(chunks, nchz) : 1;  // no empty split
+    const dim3 grid((unsigned)ceil_div(n, 16), (unsigned)ceil_div(m, 16), (unsigned)z);
+    unsigned *tickets = z > 1 ? (unsigned *)workspace : nullptr;
+    float *part = z > 1 ? workspace + kSkTickets : nullptr;
     hipLaunchKernelGGL(linear_skinny_kernel<kSkW>, grid, dim3(kSkW * 64), 0, st, x, ldx, m, k, w, ldw, b,
-                       n, act, y, ldy);
+                       n, act, y, ldy, nchz, part, tickets);
     MMPDE_RET_LAUNCH();
     return MMPDE_OK;
+}
+
+extern "C" int mmpde_linear_skinny(const float *x, int64_t ldx, int64_t m, int64_t k,
+                                   const float *w, int64_t ldw, const float *b, int64_t n,
+                                   int act, float *y, int64_t ldy, mmpde_stream_t stream) {
+    return mmpde_linear_skinny_ws(x, ldx, m, k, w, ldw, b, n, act, y, ldy, nullptr, 0, stream);
 }
 
 extern "C" int mmpde_conv2d(const float *x, int64_t batches, int cin, int h, int w,
@@ -191,10 +311,21 @@ extern "C" int mmpde_conv2d(const float *x, int64_t batches, int cin, int h, int
     const int oh = (h + 2 * pad - ks) / stride + 1;
     const int ow = (w + 2 * pad - ks) / stride + 1;
     MMPDE_REQUIRE(oh > 0 && ow > 0);
+    return mmpde_detail::conv2d(x, batches, cin, h, w, weight, bias, cout, ks, stride, pad, residual, act,
+                                y, as_stream(stream), nullptr, 0);
+}
+
+namespace mmpde_detail {
+int conv2d(const float *x, int64_t batches, int cin, int h, int w, const float *weight, const float *bias,
+           int cout, int ks, int stride, int pad, const float *residual, int act, float *y, hipStream_t st,
+           unsigned *zero, int n_zero) {
+    const int oh = (h + 2 * pad - ks) / stride + 1;
+    const int ow = (w + 2 * pad - ks) / stride + 1;
     const int64_t total = batches * cout * oh * ow;
-    hipLaunchKernelGGL(conv2d_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, as_stream(stream),
-                       x, batches, cin, h, w, weight, bias, cout, ks, stride, pad, oh, ow,
-                       residual, act, y);
+    const int64_t threads = total > n_zero ? total : n_zero;
+    hipLaunchKernelGGL(conv2d_kernel, dim3(ceil_div(threads, 256)), dim3(256), 0, st, x, batches, cin, h, w,
+                       weight, bias, cout, ks, stride, pad, oh, ow, residual, act, y, zero, n_zero);
     MMPDE_RET_LAUNCH();
     return MMPDE_OK;
 }
+}  // namespace mmpde_detail

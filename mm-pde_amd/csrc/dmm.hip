@@ -31,8 +31,10 @@ __global__ __launch_bounds__(256) void dmm_embed_kernel(const float *__restrict_
                                                         const float2 *__restrict__ grid,
                                                         int64_t n_tot, int64_t n_per,
                                                         mmpde_dmm_graph_branch p,
-                                                        float4 *__restrict__ h) {
+                                                        float4 *__restrict__ h,
+                                                        unsigned *__restrict__ zero, int n_zero) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n_zero) zero[i] = 0u;  // the skinny linears' split-K tickets
     if (i >= n_tot) return;
     const float2 g = grid[i % n_per];
     const float in[3] = {u[i], g.x, g.y};  // cat(x, pos_x, pos_y), dmm_model.py:205
@@ -390,7 +392,7 @@ int64_t cache_floats(int64_t n_per, int hidden) { return 3 * n_per * hidden; }
 // branch [B, L] -> mesh [B*N, 2]; cache: a prepared grid side (or null: computed here)
 int dmm_head(const float *branch, const float *xi, int64_t batches, int64_t n_per,
              const mmpde_dmm_head *hd, float *ws, const float *cache, float *mesh_out,
-             hipStream_t st) {
+             hipStream_t st, float *sk, int64_t skf) {
     const int L = hd->latent, Lp = hd->hidden, th = hd->th;
     if (!head_ok(hd)) return MMPDE_ERR_UNSUPPORTED;
     HeadWs w = carve_head(ws, batches, n_per, L, Lp, th);
@@ -402,8 +404,8 @@ int dmm_head(const float *branch, const float *xi, int64_t batches, int64_t n_pe
         if (rc) return rc;
     }
     // P = Wb . branch + b_o1 (Wb = out_nn.layers.0.weight[:, :L], row stride 2L)
-    rc = mmpde_linear_skinny(branch, L, batches, L, hd->o0_w, 2 * L, hd->o0_b, Lp,
-                             MMPDE_ACT_NONE, w.p, Lp, st);
+    rc = mmpde_linear_skinny_ws(branch, L, batches, L, hd->o0_w, 2 * L, hd->o0_b, Lp, MMPDE_ACT_NONE, w.p, Lp,
+                                sk, skf * (int64_t)sizeof(float), st);
     if (rc) return rc;
     const size_t lds = (size_t)batches * Lp * sizeof(float);
     if (Lp == 512 && lds <= 65536) {
@@ -422,13 +424,36 @@ inline bool al16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
 
 }  // namespace
 
-extern "C" int64_t mmpde_dmm_workspace_bytes(int64_t batches, int64_t n_per, int latent,
-                                             int hidden) {
-    // branch-side scratch (graph: 2 h buffers + decode + MLP activations; array:
-    // conv activations), then the shared head region.
+namespace {
+// branch-side scratch (graph: 2 h buffers + decode + MLP activations; array:
+// conv activations), then the shared head region, then the split-K scratch of
+// the skinny linears (mmpde_linear_skinny_ws: its ticket counters first, then
+// at most 16 splits of an output of at most max(batches, 64) x 2048).  The
+// counters are zeroed by the branch's first kernel (dmm_embed_kernel /
+// conv0) on every mesh call; every skinny call leaves them zero.
+int64_t dmm_base_floats(int64_t batches, int64_t n_per, int latent, int hidden) {
     const int64_t branch_side = 2 * 4 * batches * n_per + batches * n_per + batches * 2048 +
                                 8 * batches * n_per + 256;
-    return (branch_side + head_floats(batches, n_per, latent, hidden, 64) + 256) *
+    return branch_side + head_floats(batches, n_per, latent, hidden, 64) + 256;
+}
+// dense.hip kSkTickets; zeroed by the branch's first kernel on every call
+int64_t dmm_skinny_ticket_floats(int64_t) { return 4096; }
+int64_t dmm_skinny_floats(int64_t batches) {
+    return dmm_skinny_ticket_floats(batches) + 16 * (batches > 64 ? batches : 64) * 2048;
+}
+
+// skinny linear with the workspace's split-K scratch
+int skinny(const float *x, int64_t ldx, int64_t m, int64_t k, const float *w, int64_t ldw, const float *b,
+           int64_t n, int act, float *y, int64_t ldy, float *scratch, int64_t scratch_floats,
+           mmpde_stream_t st) {
+    return mmpde_linear_skinny_ws(x, ldx, m, k, w, ldw, b, n, act, y, ldy, scratch,
+                                  scratch_floats * (int64_t)sizeof(float), st);
+}
+}  // namespace
+
+extern "C" int64_t mmpde_dmm_workspace_bytes(int64_t batches, int64_t n_per, int latent,
+                                             int hidden) {
+    return (dmm_base_floats(batches, n_per, latent, hidden) + dmm_skinny_floats(batches)) *
            (int64_t)sizeof(float);
 }
 
@@ -466,6 +491,8 @@ extern "C" int mmpde_dmm_mesh_graph_cached(const float *u, const float *grid, in
     hipStream_t st = as_stream(stream);
     const int64_t nt = batches * n_per;
     float *ws = (float *)workspace;
+    float *sk = ws + dmm_base_floats(batches, n_per, hd->latent, hd->hidden);
+    const int64_t skf = dmm_skinny_floats(batches);
     float4 *h0 = (float4 *)ws;
     float4 *h1 = h0 + nt;
     float *dec = (float *)(h1 + nt);
@@ -473,9 +500,10 @@ extern "C" int mmpde_dmm_mesh_graph_cached(const float *u, const float *grid, in
     float *om2 = om1 + batches * 512;
     float *branch = om2 + batches * 256;
     float *head_ws = branch + ((batches * hd->latent + 3) & ~int64_t(3));
-    const dim3 g1(ceil_div(nt, 256)), g4(ceil_div(4 * nt, 256));  // g4: four lanes per node
+    const int nz = (int)dmm_skinny_ticket_floats(batches);
+    const dim3 g1(ceil_div(nt > nz ? nt : nz, 256)), g4(ceil_div(4 * nt, 256));  // g4: four lanes per node
     hipLaunchKernelGGL(dmm_embed_kernel, g1, dim3(256), 0, st, u, (const float2 *)grid, nt, n_per,
-                       *br, h0);
+                       *br, h0, (unsigned *)sk, nz);
     MMPDE_RET_LAUNCH();
     for (int l = 0; l < br->n_gnn_layers; ++l) {
         hipLaunchKernelGGL(dmm_gnn_kernel, g4, dim3(256), 0, st, h0, u, (const float2 *)grid,
@@ -492,17 +520,17 @@ extern "C" int mmpde_dmm_mesh_graph_cached(const float *u, const float *grid, in
                        br->dec1_w, br->dec1_b, dec);
     MMPDE_RET_LAUNCH();
     // output_mlp: Linear(N,512) tanh Linear(512,256) tanh Linear(256,L) on [B, N]
-    int rc = mmpde_linear_skinny(dec, n_per, batches, n_per, br->om0_w, n_per, br->om0_b, 512,
-                                 MMPDE_ACT_TANH, om1, 512, stream);
+    int rc = skinny(dec, n_per, batches, n_per, br->om0_w, n_per, br->om0_b, 512, MMPDE_ACT_TANH, om1, 512,
+                    sk, skf, stream);
     if (rc) return rc;
-    rc = mmpde_linear_skinny(om1, 512, batches, 512, br->om2_w, 512, br->om2_b, 256,
-                             MMPDE_ACT_TANH, om2, 256, stream);
+    rc = skinny(om1, 512, batches, 512, br->om2_w, 512, br->om2_b, 256, MMPDE_ACT_TANH, om2, 256, sk, skf,
+                stream);
     if (rc) return rc;
-    rc = mmpde_linear_skinny(om2, 256, batches, 256, br->om4_w, 256, br->om4_b, hd->latent,
-                             MMPDE_ACT_NONE, branch, hd->latent, stream);
+    rc = skinny(om2, 256, batches, 256, br->om4_w, 256, br->om4_b, hd->latent, MMPDE_ACT_NONE, branch,
+                hd->latent, sk, skf, stream);
     if (rc) return rc;
     return dmm_head(branch, grid, batches, n_per, hd, head_ws, (const float *)head_cache, mesh_out,
-                    st);
+                    st, sk, skf);
 }
 
 extern "C" int mmpde_dmm_mesh_array(const float *u, const float *xi, int64_t batches,
@@ -525,6 +553,8 @@ extern "C" int mmpde_dmm_mesh_array_cached(const float *u, const float *xi, int6
     const int s1 = (s + 4 - 5) / 2 + 1;   // conv0, stride 2, pad 2
     const int s3 = (s1 + 4 - 5) / 2 + 1;  // conv3, stride 2, pad 2
     float *ws = (float *)workspace;
+    float *sk = ws + dmm_base_floats(batches, n_per, hd->latent, hd->hidden);
+    const int64_t skf = dmm_skinny_floats(batches);
     auto take = [&](int64_t nf) {
         float *p = ws;
         ws += (nf + 3) & ~int64_t(3);
@@ -538,8 +568,8 @@ extern "C" int mmpde_dmm_mesh_array_cached(const float *u, const float *xi, int6
     float *branch = take(batches * hd->latent);
     int rc;
     // ConvNet.forward, dmm_model.py:65-81
-    rc = mmpde_conv2d(u, batches, 1, s, s, br->c0_w, br->c0_b, 8, 5, 2, 2, nullptr, MMPDE_ACT_TANH,
-                      x1, stream);
+    rc = mmpde_detail::conv2d(u, batches, 1, s, s, br->c0_w, br->c0_b, 8, 5, 2, 2, nullptr, MMPDE_ACT_TANH,
+                              x1, st, (unsigned *)sk, (int)dmm_skinny_ticket_floats(batches));
     if (rc) return rc;
     rc = mmpde_conv2d(x1, batches, 8, s1, s1, br->c1_w, br->c1_b, 16, 5, 1, 2, nullptr,
                       MMPDE_ACT_TANH, x2, stream);
@@ -550,11 +580,11 @@ extern "C" int mmpde_dmm_mesh_array_cached(const float *u, const float *xi, int6
     rc = mmpde_conv2d(x3, batches, 8, s1, s1, br->c3_w, br->c3_b, 1, 5, 2, 2, nullptr,
                       MMPDE_ACT_TANH, x4, stream);
     if (rc) return rc;
-    rc = mmpde_linear_skinny(x4, s3 * s3, batches, s3 * s3, br->fc2_w, s3 * s3, br->fc2_b, 1024,
-                             MMPDE_ACT_TANH, f2, 1024, stream);
+    rc = skinny(x4, s3 * s3, batches, s3 * s3, br->fc2_w, s3 * s3, br->fc2_b, 1024, MMPDE_ACT_TANH, f2, 1024,
+                sk, skf, stream);
     if (rc) return rc;
-    rc = mmpde_linear_skinny(f2, 1024, batches, 1024, br->fc3_w, 1024, br->fc3_b, hd->latent,
-                             MMPDE_ACT_NONE, branch, hd->latent, stream);
+    rc = skinny(f2, 1024, batches, 1024, br->fc3_w, 1024, br->fc3_b, hd->latent, MMPDE_ACT_NONE, branch,
+                hd->latent, sk, skf, stream);
     if (rc) return rc;
-    return dmm_head(branch, xi, batches, n_per, hd, ws, (const float *)head_cache, mesh_out, st);
+    return dmm_head(branch, xi, batches, n_per, hd, ws, (const float *)head_cache, mesh_out, st, sk, skf);
 }

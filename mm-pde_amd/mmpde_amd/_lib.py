@@ -13,7 +13,7 @@ import os
 import torch
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libmmpde_hip.so")
-ABI_VERSION = 10800
+ABI_VERSION = 10900
 
 ACT_NONE, ACT_TANH, ACT_RELU = 0, 1, 2
 # message_net_2 edge GEMM arithmetic (include/mmpde_hip.h MMPDE_EDGE_GEMM_*)
@@ -96,6 +96,9 @@ _SIGS = {
     "mmpde_knn_query": (_I, [_P, _P, _I64, _I64, _I64, _I, _P, _P]),
     "mmpde_edge_index_from_nbr": (_I, [_P, _I64, _I, _P, _P]),
     "mmpde_linear_skinny": (_I, [_P, _I64, _I64, _I64, _P, _I64, _P, _I64, _I, _P, _I64, _P]),
+    "mmpde_linear_skinny_workspace_bytes": (_I64, [_I64, _I64, _I64]),
+    "mmpde_linear_skinny_ws": (_I, [_P, _I64, _I64, _I64, _P, _I64, _P, _I64, _I, _P, _I64, _P, _I64,
+                                    _P]),
     "mmpde_traj_mse": (_I, [_P, _P, _I64, _I64, _P, _P]),
     "mmpde_conv2d": (_I, [_P, _I64, _I, _I, _I, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P]),
     "mmpde_gnn_workspace_bytes": (_I64, [_I64]),

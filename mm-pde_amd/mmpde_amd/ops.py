@@ -131,6 +131,21 @@ def knn_query(src: torch.Tensor, qry: torch.Tensor, batches: int, k: int) -> tor
     return idx
 
 
+_SKINNY_WS = {}
+
+
+def _skinny_workspace(device, nbytes: int) -> torch.Tensor:
+    """Split-K scratch of mmpde_linear_skinny_ws: zeroed once, then reused (each
+    call leaves its ticket counters at zero).  One per device and stream: calls
+    on one stream are ordered, so they may share it."""
+    key = (str(device), torch.cuda.current_stream(device).cuda_stream)
+    ws = _SKINNY_WS.get(key)
+    if ws is None or ws.numel() * 4 < nbytes:
+        ws = torch.zeros((max(nbytes, 4) // 4 + 1024,), dtype=torch.float32, device=device)
+        _SKINNY_WS[key] = ws
+    return ws
+
+
 def linear_skinny(x: torch.Tensor, w: torch.Tensor, b=None, act: int = L.ACT_NONE,
                   out: torch.Tensor | None = None) -> torch.Tensor:
     """act(x @ w.T + b) for a few rows (M = trajectories)."""
@@ -140,9 +155,13 @@ def linear_skinny(x: torch.Tensor, w: torch.Tensor, b=None, act: int = L.ACT_NON
     m, k = x.shape
     n = w.shape[0]
     y = out if out is not None else torch.empty((m, n), dtype=torch.float32, device=x.device)
-    L.check(L.lib().mmpde_linear_skinny(L.ptr(x), k, m, k, L.ptr(w), k,
-                                        L.ptr(L.f32c(b)) if b is not None else None, n, act,
-                                        L.ptr(y), n, L.stream(x.device)), "mmpde_linear_skinny")
+    lib = L.lib()
+    wsb = lib.mmpde_linear_skinny_workspace_bytes(m, n, k)
+    ws = _skinny_workspace(x.device, wsb)
+    L.check(lib.mmpde_linear_skinny_ws(L.ptr(x), k, m, k, L.ptr(w), k,
+                                       L.ptr(L.f32c(b)) if b is not None else None, n, act,
+                                       L.ptr(y), n, L.ptr(ws), wsb, L.stream(x.device)),
+            "mmpde_linear_skinny")
     return y
 
 
