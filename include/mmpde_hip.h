@@ -119,6 +119,12 @@ int mmpde_linear_skinny_ws(const float *x, int64_t ldx, int64_t m, int64_t k, co
 int mmpde_traj_mse(const float *pred, const float *labels, int64_t batches, int64_t n_per,
                    float *out, mmpde_stream_t stream);
 
+/* F.interpolate(u, size=(oh, ow), mode='bilinear', align_corners=True) of
+ * `planes` contiguous h x w fp32 planes (data_creator_2d.py:102-103, moving_mesh's
+ * pre-resampling of u to the DMM grid size); y [planes, oh, ow]. */
+int mmpde_resample_bilinear(const float *x, int64_t planes, int h, int w, int oh, int ow, float *y,
+                            mmpde_stream_t stream);
+
 /* Direct 2-D convolution, NCHW fp32, square kernel ks, zero padding pad,
  * stride 1 or 2, fused act(conv + bias [+ residual]).  residual nullable,
  * same shape as the output.  ConvNet branch (mesh/dmm_model.py:53-57,65-81)
@@ -348,7 +354,10 @@ int mmpde_dmm_mesh_graph(const float *u, const float *grid, int64_t batches, int
                          mmpde_stream_t stream);
 
 /* Array mode (Burgers): u [B, s, s]; xi [N, 2] (np.meshgrid xy order,
- * data_creator_2d.py:94-100), N = s*s. */
+ * data_creator_2d.py:94-100).  N = s*s on the MM-PDE path; a coarser or finer
+ * xi is allowed (u bilinearly pre-resampled to s x s,
+ * data_creator_2d.py:102-103, mmpde_resample_bilinear), with the workspace
+ * sized by mmpde_dmm_workspace_bytes(B, max(N, s*s), ...). */
 int mmpde_dmm_mesh_array(const float *u, const float *xi, int64_t batches, int64_t n_per,
                          const mmpde_dmm_array_branch *br, const mmpde_dmm_head *hd,
                          void *workspace, float *mesh_out, mmpde_stream_t stream);
@@ -371,6 +380,30 @@ int mmpde_dmm_mesh_array_cached(const float *u, const float *xi, int64_t batches
                                 const mmpde_dmm_array_branch *br, const mmpde_dmm_head *hd,
                                 const void *head_cache, void *workspace, float *mesh_out,
                                 mmpde_stream_t stream);
+
+/* DMM.forward (dmm_model.py:185-219) in two calls, for callers that need phi
+ * itself (DMM evaluation, dmm_utils.py) rather than the moved mesh.
+ * The branch alone: branch_out [B, L] (L = hd->latent) from u on the fixed
+ * grid (graph: u [B, N], grid / grid_nbr as for mmpde_dmm_mesh_graph) or from
+ * u [B, s, s] (array: ConvNet.forward, dmm_model.py:65-81); workspace as for
+ * mmpde_dmm_mesh_* (array: N = s*s). */
+int mmpde_dmm_branch_graph(const float *u, const float *grid, int64_t batches, int64_t n_per,
+                           const int32_t *grid_nbr, int k, const mmpde_dmm_graph_branch *br,
+                           const mmpde_dmm_head *hd, void *workspace, float *branch_out,
+                           mmpde_stream_t stream);
+int mmpde_dmm_branch_array(const float *u, int64_t batches, const mmpde_dmm_array_branch *br,
+                           const mmpde_dmm_head *hd, void *workspace, float *branch_out,
+                           mmpde_stream_t stream);
+/* phi[i] = out_nn(cat(branch[b], trunk(grid[i])))  with b = i / (n_grid / B)
+ * (the reference's branch.repeat over grid rows, dmm_model.py:187-190,210-213);
+ * grid [n_grid, 2] (n_grid a multiple of B); o1_b = out_nn.layers.1.bias
+ * (nullable: 0); phi_out [n_grid]; second_out [n_grid, L'] = the tanh layer
+ * (the rf=True second output), nullable.  workspace >=
+ * mmpde_dmm_phi_workspace_bytes(B, n_grid, L, L', th) bytes, 16-B aligned. */
+int64_t mmpde_dmm_phi_workspace_bytes(int64_t batches, int64_t n_grid, int latent, int hidden, int th);
+int mmpde_dmm_phi(const float *branch, int64_t batches, const float *grid, int64_t n_grid,
+                  const mmpde_dmm_head *hd, const float *o1_b, void *workspace, float *phi_out,
+                  float *second_out, mmpde_stream_t stream);
 
 /* ------------------------------------------------------------------------
  * ItpNet interpolation (reference interpolate.py:77-93 + data_creator_2d.py:80-83)

@@ -174,6 +174,30 @@ inline int skinny_splits(int64_t m, int64_t n, int64_t k, int cus) {
     return z > 1 ? (int)z : 1;
 }
 
+// F.interpolate(mode='bilinear', align_corners=True) of `planes` h x w planes
+// to oh x ow (data_creator_2d.py:102-103): source coordinate = dst index x
+// (in - 1) / (out - 1) in fp32, the two neighbours (the upper one clamped) and
+// their linear weights, as PyTorch's upsample_bilinear2d computes them.  One
+// thread per output element.
+__global__ __launch_bounds__(256) void resample_bilinear_kernel(const float *__restrict__ x, int64_t planes,
+                                                                int h, int w, int oh, int ow, float sy,
+                                                                float sx, float *__restrict__ y) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= planes * oh * ow) return;
+    const int ox = (int)(e % ow);
+    const int oy = (int)((e / ow) % oh);
+    const int64_t pl = e / ((int64_t)ow * oh);
+    // rounded products (no fma contraction into the lambdas below): the source
+    // coordinate is an fp32 value first, as on PyTorch's side
+    const float fy = __fmul_rn(sy, (float)oy), fx = __fmul_rn(sx, (float)ox);
+    const int y0 = (int)fy, x0 = (int)fx;
+    const int y1 = y0 + (y0 < h - 1 ? 1 : 0), x1 = x0 + (x0 < w - 1 ? 1 : 0);
+    const float ly = fy - (float)y0, lx = fx - (float)x0;
+    const float hy = 1.0f - ly, hx = 1.0f - lx;
+    const float *p = x + pl * h * w;
+    y[e] = hy * (hx * p[y0 * w + x0] + lx * p[y0 * w + x1]) + ly * (hx * p[y1 * w + x0] + lx * p[y1 * w + x1]);
+}
+
 // one thread per output element; weight [cout][cin][ks][ks] (PyTorch layout)
 __global__ __launch_bounds__(256) void conv2d_kernel(const float *__restrict__ x, int64_t batches,
                                                      int cin, int h, int w,
@@ -235,7 +259,7 @@ __global__ __launch_bounds__(256) void traj_mse_kernel(const float *__restrict__
 
 }  // namespace
 
-extern "C" int mmpde_version(void) { return 10900; }
+extern "C" int mmpde_version(void) { return 11000; }
 
 extern "C" int mmpde_traj_mse(const float *pred, const float *labels, int64_t batches, int64_t n_per,
                               float *out, mmpde_stream_t stream) {
@@ -329,3 +353,14 @@ int conv2d(const float *x, int64_t batches, int cin, int h, int w, const float *
     return MMPDE_OK;
 }
 }  // namespace mmpde_detail
+
+extern "C" int mmpde_resample_bilinear(const float *x, int64_t planes, int h, int w, int oh, int ow, float *y,
+                                       mmpde_stream_t stream) {
+    MMPDE_REQUIRE(x && y && planes > 0 && h > 0 && w > 0 && oh > 0 && ow > 0);
+    const float sy = oh > 1 ? (float)(h - 1) / (float)(oh - 1) : 0.0f;
+    const float sx = ow > 1 ? (float)(w - 1) / (float)(ow - 1) : 0.0f;
+    hipLaunchKernelGGL(resample_bilinear_kernel, dim3(ceil_div(planes * oh * ow, 256)), dim3(256), 0,
+                       as_stream(stream), x, planes, h, w, oh, ow, sy, sx, y);
+    MMPDE_RET_LAUNCH();
+    return MMPDE_OK;
+}

@@ -325,6 +325,28 @@ __global__ __launch_bounds__(256) void mesh_vjp_wave_kernel(const float *__restr
     }
 }
 
+// phi[i] = w_o . tanh(P[b] + Q[i]) + b_o2, b = i / per (out_nn = DenseNet[2L, L', 1]
+// on cat(branch_b, trunk(grid_i)), dmm_model.py:190,213); second[i] = the tanh
+// row (rf=True's second_out).  One wave per grid row.
+__global__ __launch_bounds__(256) void phi_kernel(const float *__restrict__ P, const float *__restrict__ Q,
+                                                  const float *__restrict__ wo, const float *__restrict__ bo,
+                                                  int64_t n_grid, int64_t per, int hidden,
+                                                  float *__restrict__ phi, float *__restrict__ second) {
+    const int lane = threadIdx.x & 63;
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= n_grid) return;
+    const float *pb = P + (i / per) * hidden;
+    const float *q = Q + i * hidden;
+    float acc = 0.0f;
+    for (int kk = lane; kk < hidden; kk += 64) {
+        const float t = tanhf(pb[kk] + q[kk]);
+        if (second) second[i * hidden + kk] = t;
+        acc += wo[kk] * t;
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) phi[i] = acc + (bo ? bo[0] : 0.0f);
+}
+
 struct HeadWs {
     float *trunk, *s, *q, *t1t, *gt, *p;
     float2 *jac;
@@ -479,27 +501,20 @@ extern "C" int mmpde_dmm_mesh_graph(const float *u, const float *grid, int64_t b
                                        workspace, mesh_out, stream);
 }
 
-extern "C" int mmpde_dmm_mesh_graph_cached(const float *u, const float *grid, int64_t batches,
-                                           int64_t n_per, const int32_t *grid_nbr, int k,
-                                           const mmpde_dmm_graph_branch *br,
-                                           const mmpde_dmm_head *hd, const void *head_cache,
-                                           void *workspace, float *mesh_out,
-                                           mmpde_stream_t stream) {
-    MMPDE_REQUIRE(u && grid && grid_nbr && br && hd && workspace && mesh_out);
-    MMPDE_REQUIRE(batches > 0 && n_per > k && k > 0 && br->n_gnn_layers >= 0 &&
-                  br->n_gnn_layers <= 3 && al16(workspace));
-    hipStream_t st = as_stream(stream);
+namespace {
+// Graph-mode branch: u [B, N] on the fixed grid -> branch [B, L]
+// (dmm_model.py:197-210).  Scratch from ws (h ping-pong, decode, output_mlp
+// activations); *ws_end = the first float after it.
+int graph_branch(const float *u, const float *grid, int64_t batches, int64_t n_per,
+                 const int32_t *grid_nbr, int k, const mmpde_dmm_graph_branch *br, int latent, float *ws,
+                 float *sk, int64_t skf, float *branch, float **ws_end, hipStream_t st) {
     const int64_t nt = batches * n_per;
-    float *ws = (float *)workspace;
-    float *sk = ws + dmm_base_floats(batches, n_per, hd->latent, hd->hidden);
-    const int64_t skf = dmm_skinny_floats(batches);
     float4 *h0 = (float4 *)ws;
     float4 *h1 = h0 + nt;
     float *dec = (float *)(h1 + nt);
     float *om1 = dec + ((nt + 3) & ~int64_t(3));
     float *om2 = om1 + batches * 512;
-    float *branch = om2 + batches * 256;
-    float *head_ws = branch + ((batches * hd->latent + 3) & ~int64_t(3));
+    if (ws_end) *ws_end = om2 + batches * 256;
     const int nz = (int)dmm_skinny_ticket_floats(batches);
     const dim3 g1(ceil_div(nt > nz ? nt : nz, 256)), g4(ceil_div(4 * nt, 256));  // g4: four lanes per node
     hipLaunchKernelGGL(dmm_embed_kernel, g1, dim3(256), 0, st, u, (const float2 *)grid, nt, n_per,
@@ -521,14 +536,76 @@ extern "C" int mmpde_dmm_mesh_graph_cached(const float *u, const float *grid, in
     MMPDE_RET_LAUNCH();
     // output_mlp: Linear(N,512) tanh Linear(512,256) tanh Linear(256,L) on [B, N]
     int rc = skinny(dec, n_per, batches, n_per, br->om0_w, n_per, br->om0_b, 512, MMPDE_ACT_TANH, om1, 512,
-                    sk, skf, stream);
+                    sk, skf, st);
     if (rc) return rc;
     rc = skinny(om1, 512, batches, 512, br->om2_w, 512, br->om2_b, 256, MMPDE_ACT_TANH, om2, 256, sk, skf,
-                stream);
+                st);
     if (rc) return rc;
-    rc = skinny(om2, 256, batches, 256, br->om4_w, 256, br->om4_b, hd->latent, MMPDE_ACT_NONE, branch,
-                hd->latent, sk, skf, stream);
+    return skinny(om2, 256, batches, 256, br->om4_w, 256, br->om4_b, latent, MMPDE_ACT_NONE, branch, latent,
+                  sk, skf, st);
+}
+
+// Array-mode branch: ConvNet.forward (dmm_model.py:65-81), u [B, s, s] ->
+// branch [B, L].  conv0 also zeroes the skinny linears' tickets.
+int array_branch(const float *u, int64_t batches, const mmpde_dmm_array_branch *br, int latent, float *ws,
+                 float *sk, int64_t skf, float *branch, float **ws_end, hipStream_t st) {
+    const int s = br->s;
+    const int s1 = (s + 4 - 5) / 2 + 1;   // conv0, stride 2, pad 2
+    const int s3 = (s1 + 4 - 5) / 2 + 1;  // conv3, stride 2, pad 2
+    auto take = [&](int64_t nf) {
+        float *p = ws;
+        ws += (nf + 3) & ~int64_t(3);
+        return p;
+    };
+    float *x1 = take(batches * 8 * s1 * s1);
+    float *x2 = take(batches * 16 * s1 * s1);
+    float *x3 = take(batches * 8 * s1 * s1);
+    float *x4 = take(batches * s3 * s3);
+    float *f2 = take(batches * 1024);
+    if (ws_end) *ws_end = ws;
+    int rc = mmpde_detail::conv2d(u, batches, 1, s, s, br->c0_w, br->c0_b, 8, 5, 2, 2, nullptr, MMPDE_ACT_TANH,
+                                  x1, st, (unsigned *)sk, (int)dmm_skinny_ticket_floats(batches));
     if (rc) return rc;
+    rc = mmpde_conv2d(x1, batches, 8, s1, s1, br->c1_w, br->c1_b, 16, 5, 1, 2, nullptr, MMPDE_ACT_TANH, x2,
+                      st);
+    if (rc) return rc;
+    rc = mmpde_conv2d(x2, batches, 16, s1, s1, br->c2_w, br->c2_b, 8, 5, 1, 2, x1, MMPDE_ACT_TANH, x3, st);
+    if (rc) return rc;
+    rc = mmpde_conv2d(x3, batches, 8, s1, s1, br->c3_w, br->c3_b, 1, 5, 2, 2, nullptr, MMPDE_ACT_TANH, x4,
+                      st);
+    if (rc) return rc;
+    rc = skinny(x4, s3 * s3, batches, s3 * s3, br->fc2_w, s3 * s3, br->fc2_b, 1024, MMPDE_ACT_TANH, f2, 1024,
+                sk, skf, st);
+    if (rc) return rc;
+    return skinny(f2, 1024, batches, 1024, br->fc3_w, 1024, br->fc3_b, latent, MMPDE_ACT_NONE, branch, latent,
+                  sk, skf, st);
+}
+
+// array scratch is sized by max(N, s*s): xi may be coarser than u's grid
+// (moving_mesh's bilinear pre-resampling, data_creator_2d.py:102-103)
+int64_t array_n_eff(int64_t n_per, int s) { return n_per > (int64_t)s * s ? n_per : (int64_t)s * s; }
+}  // namespace
+
+extern "C" int mmpde_dmm_mesh_graph_cached(const float *u, const float *grid, int64_t batches,
+                                           int64_t n_per, const int32_t *grid_nbr, int k,
+                                           const mmpde_dmm_graph_branch *br,
+                                           const mmpde_dmm_head *hd, const void *head_cache,
+                                           void *workspace, float *mesh_out,
+                                           mmpde_stream_t stream) {
+    MMPDE_REQUIRE(u && grid && grid_nbr && br && hd && workspace && mesh_out);
+    MMPDE_REQUIRE(batches > 0 && n_per > k && k > 0 && br->n_gnn_layers >= 0 &&
+                  br->n_gnn_layers <= 3 && al16(workspace));
+    hipStream_t st = as_stream(stream);
+    float *ws = (float *)workspace;
+    float *sk = ws + dmm_base_floats(batches, n_per, hd->latent, hd->hidden);
+    const int64_t skf = dmm_skinny_floats(batches);
+    float *end = nullptr;
+    // branch [B, L] right after the branch scratch, then the head region
+    const int64_t nt = batches * n_per;
+    float *branch = ws + 8 * nt + ((nt + 3) & ~int64_t(3)) + batches * 768;
+    int rc = graph_branch(u, grid, batches, n_per, grid_nbr, k, br, hd->latent, ws, sk, skf, branch, &end, st);
+    if (rc) return rc;
+    float *head_ws = branch + ((batches * hd->latent + 3) & ~int64_t(3));
     return dmm_head(branch, grid, batches, n_per, hd, head_ws, (const float *)head_cache, mesh_out,
                     st, sk, skf);
 }
@@ -546,45 +623,74 @@ extern "C" int mmpde_dmm_mesh_array_cached(const float *u, const float *xi, int6
                                            const mmpde_dmm_head *hd, const void *head_cache,
                                            void *workspace, float *mesh_out,
                                            mmpde_stream_t stream) {
-    MMPDE_REQUIRE(u && xi && br && hd && workspace && mesh_out && batches > 0);
-    MMPDE_REQUIRE((int64_t)br->s * br->s == n_per && al16(workspace));
+    MMPDE_REQUIRE(u && xi && br && hd && workspace && mesh_out && batches > 0 && n_per > 0);
+    MMPDE_REQUIRE(br->s >= 5 && al16(workspace));
     hipStream_t st = as_stream(stream);
-    const int s = br->s;
-    const int s1 = (s + 4 - 5) / 2 + 1;   // conv0, stride 2, pad 2
-    const int s3 = (s1 + 4 - 5) / 2 + 1;  // conv3, stride 2, pad 2
+    float *ws = (float *)workspace;
+    float *sk = ws + dmm_base_floats(batches, array_n_eff(n_per, br->s), hd->latent, hd->hidden);
+    const int64_t skf = dmm_skinny_floats(batches);
+    float *end = nullptr;
+    // branch scratch, then branch [B, L], then the head region
+    const int s1 = (br->s + 4 - 5) / 2 + 1, s3 = (s1 + 4 - 5) / 2 + 1;
+    auto up4 = [](int64_t v) { return (v + 3) & ~int64_t(3); };
+    float *branch = ws + 2 * up4(batches * 8 * s1 * s1) + up4(batches * 16 * s1 * s1) + up4(batches * s3 * s3) +
+                    up4(batches * 1024);
+    int rc = array_branch(u, batches, br, hd->latent, ws, sk, skf, branch, &end, st);
+    if (rc) return rc;
+    float *head_ws = branch + up4(batches * hd->latent);
+    return dmm_head(branch, xi, batches, n_per, hd, head_ws, (const float *)head_cache, mesh_out, st, sk, skf);
+}
+
+// ---------------------------------------------------------------------------
+// DMM.forward pieces: the branch alone and phi itself (dmm_model.py:185-219)
+// ---------------------------------------------------------------------------
+extern "C" int mmpde_dmm_branch_graph(const float *u, const float *grid, int64_t batches, int64_t n_per,
+                                      const int32_t *grid_nbr, int k, const mmpde_dmm_graph_branch *br,
+                                      const mmpde_dmm_head *hd, void *workspace, float *branch_out,
+                                      mmpde_stream_t stream) {
+    MMPDE_REQUIRE(u && grid && grid_nbr && br && hd && workspace && branch_out && hd->latent > 0);
+    MMPDE_REQUIRE(batches > 0 && n_per > k && k > 0 && br->n_gnn_layers >= 0 &&
+                  br->n_gnn_layers <= 3 && al16(workspace));
     float *ws = (float *)workspace;
     float *sk = ws + dmm_base_floats(batches, n_per, hd->latent, hd->hidden);
-    const int64_t skf = dmm_skinny_floats(batches);
-    auto take = [&](int64_t nf) {
-        float *p = ws;
-        ws += (nf + 3) & ~int64_t(3);
-        return p;
-    };
-    float *x1 = take(batches * 8 * s1 * s1);
-    float *x2 = take(batches * 16 * s1 * s1);
-    float *x3 = take(batches * 8 * s1 * s1);
-    float *x4 = take(batches * s3 * s3);
-    float *f2 = take(batches * 1024);
-    float *branch = take(batches * hd->latent);
-    int rc;
-    // ConvNet.forward, dmm_model.py:65-81
-    rc = mmpde_detail::conv2d(u, batches, 1, s, s, br->c0_w, br->c0_b, 8, 5, 2, 2, nullptr, MMPDE_ACT_TANH,
-                              x1, st, (unsigned *)sk, (int)dmm_skinny_ticket_floats(batches));
+    return graph_branch(u, grid, batches, n_per, grid_nbr, k, br, hd->latent, ws, sk, dmm_skinny_floats(batches),
+                        branch_out, nullptr, as_stream(stream));
+}
+
+extern "C" int mmpde_dmm_branch_array(const float *u, int64_t batches, const mmpde_dmm_array_branch *br,
+                                      const mmpde_dmm_head *hd, void *workspace, float *branch_out,
+                                      mmpde_stream_t stream) {
+    MMPDE_REQUIRE(u && br && hd && workspace && branch_out && batches > 0 && hd->latent > 0 && br->s >= 5 &&
+                  al16(workspace));
+    float *ws = (float *)workspace;
+    float *sk = ws + dmm_base_floats(batches, (int64_t)br->s * br->s, hd->latent, hd->hidden);
+    return array_branch(u, batches, br, hd->latent, ws, sk, dmm_skinny_floats(batches), branch_out, nullptr,
+                        as_stream(stream));
+}
+
+extern "C" int64_t mmpde_dmm_phi_workspace_bytes(int64_t batches, int64_t n_grid, int latent, int hidden,
+                                                 int th) {
+    if (batches <= 0 || n_grid <= 0 || latent <= 0 || hidden <= 0 || th <= 0) return 0;
+    return (head_floats(batches, n_grid, latent, hidden, th) + 64) * (int64_t)sizeof(float);
+}
+
+extern "C" int mmpde_dmm_phi(const float *branch, int64_t batches, const float *grid, int64_t n_grid,
+                             const mmpde_dmm_head *hd, const float *o1_b, void *workspace, float *phi_out,
+                             float *second_out, mmpde_stream_t stream) {
+    MMPDE_REQUIRE(branch && grid && hd && workspace && phi_out && batches > 0 && n_grid > 0);
+    MMPDE_REQUIRE(n_grid % batches == 0 && al16(workspace) && ((uintptr_t)grid & 7u) == 0);
+    if (!head_ok(hd)) return MMPDE_ERR_UNSUPPORTED;
+    hipStream_t st = as_stream(stream);
+    const int L = hd->latent, Lp = hd->hidden;
+    HeadWs w = carve_head((float *)workspace, batches, n_grid, L, Lp, hd->th);
+    int rc = dmm_head_grid(grid, n_grid, hd, w, w.q, w.jac, st);  // trunk(grid), Q
     if (rc) return rc;
-    rc = mmpde_conv2d(x1, batches, 8, s1, s1, br->c1_w, br->c1_b, 16, 5, 1, 2, nullptr,
-                      MMPDE_ACT_TANH, x2, stream);
+    // P = Wb . branch + b_o1
+    rc = mmpde_linear_skinny(branch, L, batches, L, hd->o0_w, 2 * L, hd->o0_b, Lp, MMPDE_ACT_NONE, w.p, Lp,
+                             stream);
     if (rc) return rc;
-    rc = mmpde_conv2d(x2, batches, 16, s1, s1, br->c2_w, br->c2_b, 8, 5, 1, 2, x1, MMPDE_ACT_TANH,
-                      x3, stream);
-    if (rc) return rc;
-    rc = mmpde_conv2d(x3, batches, 8, s1, s1, br->c3_w, br->c3_b, 1, 5, 2, 2, nullptr,
-                      MMPDE_ACT_TANH, x4, stream);
-    if (rc) return rc;
-    rc = skinny(x4, s3 * s3, batches, s3 * s3, br->fc2_w, s3 * s3, br->fc2_b, 1024, MMPDE_ACT_TANH, f2, 1024,
-                sk, skf, stream);
-    if (rc) return rc;
-    rc = skinny(f2, 1024, batches, 1024, br->fc3_w, 1024, br->fc3_b, hd->latent, MMPDE_ACT_NONE, branch,
-                hd->latent, sk, skf, stream);
-    if (rc) return rc;
-    return dmm_head(branch, xi, batches, n_per, hd, ws, (const float *)head_cache, mesh_out, st, sk, skf);
+    hipLaunchKernelGGL(phi_kernel, dim3((unsigned)ceil_div(n_grid, 4)), dim3(256), 0, st, w.p, w.q, hd->o1_w,
+                       o1_b, n_grid, n_grid / batches, Lp, phi_out, second_out);
+    MMPDE_RET_LAUNCH();
+    return MMPDE_OK;
 }

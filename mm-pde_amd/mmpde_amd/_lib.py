@@ -13,7 +13,7 @@ import os
 import torch
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libmmpde_hip.so")
-ABI_VERSION = 10900
+ABI_VERSION = 11000
 
 ACT_NONE, ACT_TANH, ACT_RELU = 0, 1, 2
 # message_net_2 edge GEMM arithmetic (include/mmpde_hip.h MMPDE_EDGE_GEMM_*)
@@ -101,6 +101,7 @@ _SIGS = {
                                     _P]),
     "mmpde_traj_mse": (_I, [_P, _P, _I64, _I64, _P, _P]),
     "mmpde_conv2d": (_I, [_P, _I64, _I, _I, _I, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P]),
+    "mmpde_resample_bilinear": (_I, [_P, _I64, _I, _I, _I, _I, _P, _P]),
     "mmpde_gnn_workspace_bytes": (_I64, [_I64]),
     "mmpde_gnn_embed": (_I, [_P, _P, _I64, GnnScales, _P, _P, _P, _P]),
     "mmpde_gnn_layer": (_I, [_P, _P, _P, _I64, _I, _P, GnnScales, _P, _P, _P, _P]),
@@ -124,6 +125,10 @@ _SIGS = {
     "mmpde_dmm_head_prepare": (_I, [_P, _I64, _P, _P, _P, _P]),
     "mmpde_dmm_mesh_graph_cached": (_I, [_P, _P, _I64, _I64, _P, _I, _P, _P, _P, _P, _P, _P]),
     "mmpde_dmm_mesh_array_cached": (_I, [_P, _P, _I64, _I64, _P, _P, _P, _P, _P, _P]),
+    "mmpde_dmm_branch_graph": (_I, [_P, _P, _I64, _I64, _P, _I, _P, _P, _P, _P, _P]),
+    "mmpde_dmm_branch_array": (_I, [_P, _I64, _P, _P, _P, _P, _P]),
+    "mmpde_dmm_phi_workspace_bytes": (_I64, [_I64, _I64, _I, _I, _I]),
+    "mmpde_dmm_phi": (_I, [_P, _I64, _P, _I64, _P, _P, _P, _P, _P, _P]),
     "mmpde_itp_pack_bytes": (_I64, []),
     "mmpde_itp_pack": (_I, [_P, _P, _P]),
     "mmpde_itp_interp": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _P, _P, _P, _P]),

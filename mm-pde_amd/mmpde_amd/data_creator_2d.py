@@ -106,10 +106,9 @@ class GraphCreator_FS_2D(nn.Module):  # noqa: N801 - reference name
     def moving_mesh(self, u, mesh_model, n_grid_x, n_grid_y):
         """data_creator_2d.py:88-113 (Burgers, DMM array mode).  u [B, nx, ny].
         Returns (x1, x2), each [B*nx*ny, 1]."""
-        if (self.pde.movingmesh_grid_size[-2] != n_grid_x
-                or self.pde.movingmesh_grid_size[-1] != n_grid_y):
-            raise NotImplementedError("bilinear pre-resampling of u (data_creator_2d.py:102-103) "
-                                      "is not on the benchmarked path")
+        mx, my = self.pde.movingmesh_grid_size[-2], self.pde.movingmesh_grid_size[-1]
+        if mx != n_grid_x or my != n_grid_y:   # data_creator_2d.py:102-103
+            u = ops.resample_bilinear(u, mx, my)
         xi = self.xi_grid_xy(n_grid_x, n_grid_y, u.device)
         mesh = mesh_model.mesh(u, xi)
         return mesh[:, 0:1], mesh[:, 1:2]

@@ -11,6 +11,10 @@ x = xi + d(phi)/d(xi) that GraphCreator_FS_2D.moving_mesh[_tri] obtains with
 two autograd.grad calls (data_creator_2d.py:106-107,130-131).  ``DMM.mesh``
 returns exactly that through an analytic vector-Jacobian product
 (mmpde_dmm_mesh_graph / mmpde_dmm_mesh_array; derivation in dmm.hip).
+``DMM.forward`` (phi, and rf=True's second output) runs the branch and the
+head on the same kernels (mmpde_dmm_branch_*, mmpde_dmm_phi); ``DenseNet`` /
+``ConvNet`` forwards run on the skinny-linear and conv kernels.  All are
+eval-mode (DMM training is outside the hot path).
 """
 from __future__ import annotations
 
@@ -21,7 +25,14 @@ from torch import nn
 
 from . import _lib as L
 from .gnn_2d import BatchNorm
+from . import ops
 from .ops import knn_graph_nbr
+
+
+def _eval_only(m: nn.Module):
+    if m.training:
+        raise NotImplementedError("training-mode forward is out of scope (DMM training, "
+                                  "SURVEY.md §8(f) row 4); call .eval()")
 
 
 class DenseNet(nn.Module):
@@ -41,7 +52,15 @@ class DenseNet(nn.Module):
         self.fc0 = nn.Linear(4, width)
 
     def forward(self, x):
-        raise NotImplementedError("DenseNet runs inside the fused DMM mesh kernels")
+        """dmm_model.py:31-45 (normalize=False): (out, x) with x the last hidden
+        activation (the input of the last Linear)."""
+        _eval_only(self)
+        for i, l in enumerate(self.layers):
+            if i != self.n_layers - 1:
+                x = ops.linear_rows(x, l.weight, l.bias, L.ACT_TANH)
+            else:
+                out = ops.linear_rows(x, l.weight, l.bias, L.ACT_NONE)
+        return out, x
 
 
 class ConvNet(nn.Module):
@@ -60,7 +79,16 @@ class ConvNet(nn.Module):
         self.s = s
 
     def forward(self, x):
-        raise NotImplementedError("ConvNet runs inside mmpde_dmm_mesh_array")
+        """dmm_model.py:65-81: x [B, 1, s, s] -> [B, 512]."""
+        _eval_only(self)
+        c = self.layers
+        x1 = ops.conv2d(x, c[0].weight, c[0].bias, 2, 2, L.ACT_TANH)
+        x2 = ops.conv2d(x1, c[1].weight, c[1].bias, 1, 2, L.ACT_TANH)
+        x3 = ops.conv2d(x2, c[2].weight, c[2].bias, 1, 2, L.ACT_TANH, residual=x1)
+        x4 = ops.conv2d(x3, c[3].weight, c[3].bias, 2, 2, L.ACT_TANH)
+        f = torch.flatten(x4, 1)
+        f = ops.linear_rows(f, self.fc2.weight, self.fc2.bias, L.ACT_TANH)
+        return ops.linear_rows(f, self.fc3.weight, self.fc3.bias, L.ACT_NONE)
 
 
 class GNN_Layer_FS_2D(nn.Module):  # noqa: N801 - reference name
@@ -117,9 +145,48 @@ class DMM(nn.Module):
         self._grid_cache = {}
 
     def forward(self, u, grid, rf=False):
-        raise NotImplementedError(
-            "the MM-PDE step only needs the moved mesh: use DMM.mesh(u, xi) (analytic "
-            "d(phi)/d(xi)); phi values are used by DMM training, which is out of scope")
+        """dmm_model.py:185-219: phi = out_nn(cat(branch(u), trunk(grid))), the
+        branch of trajectory b repeated over its grid.shape[0] / B rows of grid.
+        u: graph [B, N] (values on self.ori_grid), array [B, s, s]; grid [B*m, 2].
+        Returns phi [B*m, 1], or (phi, second_out [B*m, L'], ones [B*m*L', 1])
+        with rf=True."""
+        L.require_device(u, grid)
+        bp, hd = self.device_params()
+        u = L.f32c(u)
+        grid = L.f32c(grid).reshape(-1, 2)
+        B, ng = u.shape[0], grid.shape[0]
+        if ng % B:
+            raise ValueError("grid rows must be a multiple of the batch size")
+        lib = L.lib()
+        st = L.stream(u.device)
+        branch = torch.empty((B, hd.latent), dtype=torch.float32, device=u.device)
+        if self.mode == "graph":
+            og = L.f32c(torch.as_tensor(self.ori_grid).to(u.device)).reshape(-1, 2)
+            N = og.shape[0]
+            nbr = self.grid_nbr(og)
+            ws = torch.empty((lib.mmpde_dmm_workspace_bytes(B, N, hd.latent, hd.hidden) // 4,),
+                             dtype=torch.float32, device=u.device)
+            L.check(lib.mmpde_dmm_branch_graph(L.ptr(u), L.ptr(og), B, N, L.ptr(nbr), nbr.shape[1],
+                                               ctypes.byref(bp), ctypes.byref(hd), L.ptr(ws),
+                                               L.ptr(branch), st), "mmpde_dmm_branch_graph")
+        else:
+            s = self.branch.s
+            ws = torch.empty((lib.mmpde_dmm_workspace_bytes(B, s * s, hd.latent, hd.hidden) // 4,),
+                             dtype=torch.float32, device=u.device)
+            L.check(lib.mmpde_dmm_branch_array(L.ptr(u), B, ctypes.byref(bp), ctypes.byref(hd),
+                                               L.ptr(ws), L.ptr(branch), st), "mmpde_dmm_branch_array")
+        nb = lib.mmpde_dmm_phi_workspace_bytes(B, ng, hd.latent, hd.hidden, hd.th)
+        ws2 = torch.empty((nb // 4,), dtype=torch.float32, device=u.device)
+        phi = torch.empty((ng, 1), dtype=torch.float32, device=u.device)
+        second = (torch.empty((ng, hd.hidden), dtype=torch.float32, device=u.device)
+                  if rf else None)
+        ob = self.out_nn.layers[1].bias
+        L.check(lib.mmpde_dmm_phi(L.ptr(branch), B, L.ptr(grid), ng, ctypes.byref(hd),
+                                  L.ptr(L.f32c(ob)) if ob is not None else None, L.ptr(ws2),
+                                  L.ptr(phi), L.ptr(second), st), "mmpde_dmm_phi")
+        if not rf:
+            return phi
+        return phi, second, torch.ones_like(second).reshape(-1, 1)
 
     # ----------------------------------------------------------------- packing
     def _check(self):
@@ -235,7 +302,8 @@ class DMM(nn.Module):
         xi = L.f32c(xi).reshape(-1, 2)
         B, N = u.shape[0], xi.shape[0]
         if workspace is None:
-            nb = L.lib().mmpde_dmm_workspace_bytes(B, N, hd.latent, hd.hidden)
+            ne = N if self.mode == "graph" else max(N, self.branch.s ** 2)  # array: xi may be coarser
+            nb = L.lib().mmpde_dmm_workspace_bytes(B, ne, hd.latent, hd.hidden)
             workspace = torch.empty((nb // 4,), dtype=torch.float32, device=u.device)
         if out is None:
             out = torch.empty((B * N, 2), dtype=torch.float32, device=u.device)

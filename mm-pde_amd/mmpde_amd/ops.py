@@ -165,6 +165,29 @@ def linear_skinny(x: torch.Tensor, w: torch.Tensor, b=None, act: int = L.ACT_NON
     return y
 
 
+def linear_rows(x: torch.Tensor, w: torch.Tensor, b=None, act: int = L.ACT_NONE) -> torch.Tensor:
+    """act(x @ w.T + b) for any number of rows (x [..., k]): linear_skinny on
+    blocks of at most 4096 rows (the skinny kernel's row limit)."""
+    lead = x.shape[:-1]
+    x2 = L.f32c(x).reshape(-1, x.shape[-1])
+    y = torch.empty((x2.shape[0], w.shape[0]), dtype=torch.float32, device=x2.device)
+    for r0 in range(0, x2.shape[0], 4096):
+        linear_skinny(x2[r0:r0 + 4096], w, b, act, out=y[r0:r0 + 4096])
+    return y.reshape(*lead, w.shape[0])
+
+
+def resample_bilinear(u: torch.Tensor, oh: int, ow: int) -> torch.Tensor:
+    """F.interpolate(u[:, None], size=(oh, ow), mode='bilinear',
+    align_corners=True)[:, 0] of u [..., h, w] (data_creator_2d.py:102-103)."""
+    L.require_device(u)
+    h, w = u.shape[-2:]
+    x = L.f32c(u).reshape(-1, h, w)
+    y = torch.empty((x.shape[0], oh, ow), dtype=torch.float32, device=x.device)
+    L.check(L.lib().mmpde_resample_bilinear(L.ptr(x), x.shape[0], h, w, oh, ow, L.ptr(y),
+                                            L.stream(x.device)), "mmpde_resample_bilinear")
+    return y.reshape(*u.shape[:-2], oh, ow)
+
+
 def conv2d(x: torch.Tensor, w: torch.Tensor, b, stride: int, pad: int, act: int,
            residual=None) -> torch.Tensor:
     """act(conv2d(x, w, b, stride, pad) [+ residual]), NCHW fp32."""
