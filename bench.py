@@ -272,7 +272,7 @@ def main():
     # fp32-equivalent peak is the dense fp16 MFMA peak / 3.
     peak = F32_MFMA_PEAK_TFLOPS if args.edge_gemm == "f32" else F16_MFMA_PEAK_TFLOPS / 3
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", "edge_pmc_r01.json")
+    pmc = os.path.join(ROOT, "profiles", "edge_pmc_r02.json")   # tools/gpu_pmc.sh, this round's kernels
     if os.path.exists(pmc):
         with open(pmc) as f:
             rec = json.load(f)
@@ -299,8 +299,9 @@ def main():
                    "parallelism": f"trajectory-shard x{world} (no data-path collective)",
                    "rollout": "autoregressive (pred -> next input)",
                    "launch": "hipGraph replay of the step" if args.graph else "eager, three HIP streams"},
-        "roofline": {"kernel": "gnn_edge_kernel (message_net_2 over every edge + mean "
-                               "aggregation, one launch per GNN layer, 12 per step)",
+        "roofline": {"kernel": ("gnn_edge_wave_kernel" if args.edge_gemm == "f16x3" else "gnn_edge_kernel")
+                               + " (message_net_2 over every edge + mean aggregation, one launch "
+                               "per GNN layer, 12 per step)",
                      "bound": "mfma", "achieved": achieved, "peak": peak,
                      "unit": "TFLOP/s", "frac": achieved / peak,
                      "traffic": traffic, "launch_ms": launch_ms, "launches": len(launches),

@@ -8,7 +8,7 @@
 set -u
 export TMPDIR=/tmp
 OUT=${PMC_OUT:-gpurun_out/pmc}
-REGEX=${PMC_REGEX:-gnn_edge_kernel}
+REGEX=${PMC_REGEX:-gnn_edge_kernel|gnn_edge_wave_kernel}
 mkdir -p "$OUT"
 for mode in f16x3 f32; do
   for c in FETCH_SIZE WRITE_SIZE; do
@@ -20,4 +20,4 @@ for mode in f16x3 f32; do
     if [ $rc -ne 0 ]; then tail -20 "$OUT/$mode.$c.log"; exit $rc; fi
   done
 done
-python3 tools/pmc_summary.py ${PMC_NAME:-edge_pmc_r01} cy-mmpde 40336 f16x3="$OUT/f16x3" f32="$OUT/f32"
+python3 tools/pmc_summary.py ${PMC_NAME:-edge_pmc_r02} cy-mmpde 40336 f16x3="$OUT/f16x3" f32="$OUT/f32"
