@@ -57,7 +57,8 @@ const char *mmpde_status_string(int status);
  *          [nbr_out.flatten(), repeat_interleave(arange(n), k)].
  * degenerate (nullable, device int32[1], accumulated): queries whose degree
  *          would be ragged in the reference (self not among the k+1 nearest).
- * Requires k+1 <= n_per <= 4096, k <= 63. */
+ * Requires k+1 <= n_per <= 16384, k <= 63 (more than 4096 points per
+ * trajectory: a slower path with the points in a 128 KB LDS block). */
 int mmpde_knn_graph(const float *pos, int64_t batches, int64_t n_per, int k,
                     int32_t *nbr_out, int32_t *degenerate, mmpde_stream_t stream);
 
@@ -66,7 +67,7 @@ int mmpde_knn_graph(const float *pos, int64_t batches, int64_t n_per, int k,
  * (dx*dx + dy*dy), ascending, ties by index.
  * src [batches*n_src, 2], qry [batches*n_qry, 2] fp32
  * idx_out [batches*n_qry, k] int32 LOCAL source index (0..n_src-1).
- * Requires k <= n_src <= 4096, k <= 63. */
+ * Requires k <= n_src <= 16384, k <= 63. */
 int mmpde_knn_query(const float *src, const float *qry, int64_t batches, int64_t n_src,
                     int64_t n_qry, int k, int32_t *idx_out, mmpde_stream_t stream);
 

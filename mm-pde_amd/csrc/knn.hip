@@ -4,7 +4,8 @@
 // mesh/dmm_model.py:228) and sklearn NearestNeighbors.kneighbors
 // (data_creator_2d.py:66-78).  One wave per query; the trajectory's point set
 // (<= 4096 points, <= 32 KB) is staged once per workgroup in LDS; every lane
-// keeps CPL fp32 squared distances in registers.  Selection: U = the kk-th
+// keeps CPL fp32 squared distances in registers (larger sets, up to 16384
+// points: knn_large_kernel below).  Selection: U = the kk-th
 // smallest of the 64 per-lane minima (a 64-wide bitonic sort across the wave)
 // bounds the kk-th smallest key from above; the points with key <= U (a few
 // dozen on a mesh; for the fp64 query key, fp32 key <= U plus a proven
@@ -199,6 +200,130 @@ __device__ __forceinline__ void wave_sort128(K &k0, int &i0, K &k1, int &i1, int
     }
 }
 
+// Selection and output of one query once the candidates C = {key <= thr} (m
+// of them, indices in sIdx) are compacted: sort / rank C by (key, index), or
+// the radix-select fallback over all cpl x 64 keys when C overflows kCap; then
+// the k answers in (key, index) order (the graph variant drops the self point).
+// sKey / sIdx / sSel: this wave's LDS lists.
+template <bool QUERY>
+__device__ __forceinline__ void knn_finish(const float2 *sP, typename KeyTraits<QUERY>::key_t *sKey,
+                                           int *sIdx, int *sSel, int m, float2 q, int kk, int k, int qi,
+                                           int b, int n_src, int n_q, int cpl, int lane, uint64_t below,
+                                           int32_t *__restrict__ out, int32_t *__restrict__ degenerate) {
+    typedef KeyTraits<QUERY> KT;
+    typedef typename KT::key_t key_t;
+    key_t mk = ~key_t(0);
+    int mi = 0x7fffffff;
+    int rank = lane;
+    if (m <= 64) {
+        // The common case (a mesh point's list holds ~1.5 kk): one pair per
+        // lane, one 64-wide bitonic sort.
+        wave_lds_sync();
+        key_t k0 = ~key_t(0);
+        int i0 = 0x7fffffff;
+        if (lane < m) {
+            i0 = sIdx[lane];
+            k0 = KT::key(sP[i0], q);
+        }
+        wave_sort64_ki(k0, i0, lane);
+        if (lane < kk) mi = i0;
+    } else if (m <= 128) {
+        // Two pairs per lane, one 128-wide bitonic sort.
+        wave_lds_sync();
+        key_t k0 = ~key_t(0), k1 = ~key_t(0);
+        int i0 = 0x7fffffff, i1 = 0x7fffffff;
+        if (lane < m) {
+            i0 = sIdx[lane];
+            k0 = KT::key(sP[i0], q);
+        }
+        if (lane + 64 < m) {
+            i1 = sIdx[lane + 64];
+            k1 = KT::key(sP[i1], q);
+        }
+        wave_sort128(k0, i0, k1, i1, lane);
+        if (lane < kk) mi = i0;
+    } else if (m <= kCap) {
+        wave_lds_sync();
+        for (int i = lane; i < m; i += 64) sKey[i] = KT::key(sP[sIdx[i]], q);
+        wave_lds_sync();
+        for (int i = lane; i < m; i += 64) {
+            const key_t ki = sKey[i];
+            const int ii = sIdx[i];
+            int rk = 0;
+            for (int f = 0; f < m; ++f) {
+                const key_t fk = sKey[f];
+                const int fi = sIdx[f];
+                rk += (fk < ki) || (fk == ki && fi < ii);
+            }
+            if (rk < kk) sSel[rk] = ii;
+        }
+        wave_lds_sync();
+        if (lane < kk) mi = sSel[lane];
+    } else {
+        // Fallback for adversarial point sets (hundreds of ties): full
+        // radix select on all exact keys, recomputed from LDS per use so
+        // that this rare path does not set the kernel's register budget.
+        auto key_at = [&](int c) -> key_t {
+            const int j = lane + 64 * c;
+            return (j < n_src) ? KT::key(sP[j], q) : ~key_t(0);
+        };
+        key_t T = 0;
+        for (int bit = KT::kTopBit; bit >= 0; --bit) {
+            const key_t Tc = T | (key_t(1) << bit);
+            int cnt = 0;
+#pragma unroll 4
+            for (int c = 0; c < cpl; ++c) cnt += __popcll(__ballot(key_at(c) < Tc));
+            if (cnt <= kk - 1) T = Tc;
+        }
+        int mlt = 0;
+#pragma unroll 4
+        for (int c = 0; c < cpl; ++c) mlt += __popcll(__ballot(key_at(c) < T));
+        const int need = kk - mlt;  // >= 1 candidates equal to T, taken in index order
+        int base = 0, eq_taken = 0;
+#pragma unroll 4
+        for (int c = 0; c < cpl; ++c) {
+            const key_t kc = key_at(c);
+            const bool lt = kc < T;
+            const bool eq = kc == T;
+            const uint64_t em = __ballot(eq);
+            const int eqrank = eq_taken + __popcll(em & below);
+            const bool sel = lt || (eq && eqrank < need);
+            eq_taken += __popcll(em);
+            const uint64_t sm = __ballot(sel);
+            if (sel) {
+                const int pidx = base + __popcll(sm & below);
+                sKey[pidx] = kc;
+                sIdx[pidx] = lane + 64 * c;
+            }
+            base += __popcll(sm);
+        }
+        wave_lds_sync();
+        if (lane < kk) {
+            mk = sKey[lane];
+            mi = sIdx[lane];
+        }
+        rank = 0;
+        for (int f = 0; f < kk; ++f) {
+            const key_t fk = sKey[f];
+            const int fi = sIdx[f];
+            rank += (fk < mk) || (fk == mk && fi < mi);
+        }
+    }
+    wave_lds_sync();  // the next query overwrites sKey / sIdx / sSel
+    const int64_t row = ((int64_t)b * n_q + qi) * k;
+    if (QUERY) {
+        if (lane < kk) out[row + rank] = mi;
+    } else {
+        const uint64_t smask = __ballot(lane < kk && mi == qi);
+        const bool has_self = smask != 0ull;
+        const int self_rank = has_self ? __shfl(rank, __ffsll((unsigned long long)smask) - 1, 64) : kk;
+        const int pos = rank - ((has_self && rank > self_rank) ? 1 : 0);
+        if (lane < kk && !(has_self && mi == qi) && pos < k)
+            out[row + pos] = b * n_src + mi;
+        if (!has_self && lane == 0 && degenerate) atomicAdd(degenerate, 1);
+    }
+}
+
 template <int CPL, bool QUERY>
 __global__ __launch_bounds__(256) void knn_kernel(const float2 *__restrict__ pts,
                                                   const float2 *__restrict__ qry, int n_src,
@@ -266,131 +391,109 @@ __global__ __launch_bounds__(256) void knn_kernel(const float2 *__restrict__ pts
             if (pidx < kCap) sIdx[wave][pidx] = lane + 64 * c;
             ++pidx;
         }
-        key_t mk = ~key_t(0);
-        int mi = 0x7fffffff;
-        int rank = lane;
-        if (m <= 64) {
-            // The common case (a mesh point's list holds ~1.5 kk): one pair per
-            // lane, one 64-wide bitonic sort.
-            wave_lds_sync();
-            key_t k0 = ~key_t(0);
-            int i0 = 0x7fffffff;
-            if (lane < m) {
-                i0 = sIdx[wave][lane];
-                k0 = KT::key(sP[i0], q);
-            }
-            wave_sort64_ki(k0, i0, lane);
-            if (lane < kk) mi = i0;
-        } else if (m <= 128) {
-            // Two pairs per lane, one 128-wide bitonic sort.
-            wave_lds_sync();
-            key_t k0 = ~key_t(0), k1 = ~key_t(0);
-            int i0 = 0x7fffffff, i1 = 0x7fffffff;
-            if (lane < m) {
-                i0 = sIdx[wave][lane];
-                k0 = KT::key(sP[i0], q);
-            }
-            if (lane + 64 < m) {
-                i1 = sIdx[wave][lane + 64];
-                k1 = KT::key(sP[i1], q);
-            }
-            wave_sort128(k0, i0, k1, i1, lane);
-            if (lane < kk) mi = i0;
-        } else if (m <= kCap) {
-            wave_lds_sync();
-            for (int i = lane; i < m; i += 64) sKey[wave][i] = KT::key(sP[sIdx[wave][i]], q);
-            wave_lds_sync();
-            for (int i = lane; i < m; i += 64) {
-                const key_t ki = sKey[wave][i];
-                const int ii = sIdx[wave][i];
-                int rk = 0;
-                for (int f = 0; f < m; ++f) {
-                    const key_t fk = sKey[wave][f];
-                    const int fi = sIdx[wave][f];
-                    rk += (fk < ki) || (fk == ki && fi < ii);
-                }
-                if (rk < kk) sSel[wave][rk] = ii;
-            }
-            wave_lds_sync();
-            if (lane < kk) mi = sSel[wave][lane];
-        } else {
-            // Fallback for adversarial point sets (hundreds of ties): full
-            // radix select on all exact keys, recomputed from LDS per use so
-            // that this rare path does not set the kernel's register budget.
-            auto key_at = [&](int c) -> key_t {
-                const int j = lane + 64 * c;
-                return (j < n_src) ? KT::key(sP[j], q) : ~key_t(0);
-            };
-            key_t T = 0;
-            for (int bit = KT::kTopBit; bit >= 0; --bit) {
-                const key_t Tc = T | (key_t(1) << bit);
-                int cnt = 0;
-#pragma unroll 4
-                for (int c = 0; c < CPL; ++c) cnt += __popcll(__ballot(key_at(c) < Tc));
-                if (cnt <= kk - 1) T = Tc;
-            }
-            int mlt = 0;
-#pragma unroll 4
-            for (int c = 0; c < CPL; ++c) mlt += __popcll(__ballot(key_at(c) < T));
-            const int need = kk - mlt;  // >= 1 candidates equal to T, taken in index order
-            int base = 0, eq_taken = 0;
-#pragma unroll 4
-            for (int c = 0; c < CPL; ++c) {
-                const key_t kc = key_at(c);
-                const bool lt = kc < T;
-                const bool eq = kc == T;
-                const uint64_t em = __ballot(eq);
-                const int eqrank = eq_taken + __popcll(em & below);
-                const bool sel = lt || (eq && eqrank < need);
-                eq_taken += __popcll(em);
-                const uint64_t sm = __ballot(sel);
-                if (sel) {
-                    const int pidx = base + __popcll(sm & below);
-                    sKey[wave][pidx] = kc;
-                    sIdx[wave][pidx] = lane + 64 * c;
-                }
-                base += __popcll(sm);
-            }
-            wave_lds_sync();
-            if (lane < kk) {
-                mk = sKey[wave][lane];
-                mi = sIdx[wave][lane];
-            }
-            rank = 0;
-            for (int f = 0; f < kk; ++f) {
-                const key_t fk = sKey[wave][f];
-                const int fi = sIdx[wave][f];
-                rank += (fk < mk) || (fk == mk && fi < mi);
-            }
-        }
-        wave_lds_sync();  // the next query overwrites sKey / sIdx / sSel
-        const int64_t row = ((int64_t)b * n_q + qi) * k;
-        if (QUERY) {
-            if (lane < kk) out[row + rank] = mi;
-        } else {
-            const uint64_t smask = __ballot(lane < kk && mi == qi);
-            const bool has_self = smask != 0ull;
-            const int self_rank = has_self ? __shfl(rank, __ffsll((unsigned long long)smask) - 1, 64) : kk;
-            const int pos = rank - ((has_self && rank > self_rank) ? 1 : 0);
-            if (lane < kk && !(has_self && mi == qi) && pos < k)
-                out[row + pos] = b * n_src + mi;
-            if (!has_self && lane == 0 && degenerate) atomicAdd(degenerate, 1);
-        }
+        knn_finish<QUERY>(sP, sKey[wave], sIdx[wave], sSel[wave], m, q, kk, k, qi, b, n_src, n_q, CPL, lane,
+                          below, out, degenerate);
     }
+}
+
+// Trajectories of more than 4096 points (up to kLargeMax): the same search
+// with the point set in dynamic LDS (one workgroup per CU) and the keys
+// recomputed from LDS instead of held in registers -- pass 1 the lane minima,
+// pass 2 the compaction of C in chunks of 64 columns -- so any size fits the
+// register budget.  64 queries per workgroup amortise the staging.  Same
+// selection (knn_finish), same results as knn_kernel.
+constexpr int kLargeMax = 16384;
+constexpr int kLargeQueries = 64;
+
+template <bool QUERY>
+__global__ __launch_bounds__(256) void knn_large_kernel(const float2 *__restrict__ pts,
+                                                        const float2 *__restrict__ qry, int n_src,
+                                                        int n_q, int k, int32_t *__restrict__ out,
+                                                        int32_t *__restrict__ degenerate) {
+    typedef KeyTraits<QUERY> KT;
+    typedef typename KT::key_t key_t;
+    extern __shared__ float2 sP[];
+    __shared__ key_t sKey[4][kCap];
+    __shared__ int sIdx[4][kCap];
+    __shared__ int sSel[4][64];
+
+    const int b = blockIdx.y;
+    const float2 *P = pts + (int64_t)b * n_src;
+    for (int i = threadIdx.x; i < n_src; i += 256) sP[i] = P[i];
+    __syncthreads();
+
+    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int kk = QUERY ? k : k + 1;
+    const int cpl = (n_src + 63) / 64;
+    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const int q_end = min((int)(blockIdx.x + 1) * kLargeQueries, n_q);
+    for (int qi = blockIdx.x * kLargeQueries + wave; qi < q_end; qi += 4) {
+        const float2 q = QUERY ? qry[(int64_t)b * n_q + qi] : sP[qi];
+        uint32_t lmin = ~0u;
+        for (int c = 0; c < cpl; ++c) {
+            const int j = lane + 64 * c;
+            const uint32_t f = (j < n_src) ? key_f32(sP[j], q) : ~0u;
+            lmin = f < lmin ? f : lmin;
+        }
+        const uint32_t thr = KT::filter_threshold(__shfl(wave_sort64(lmin, lane), kk - 1, 64));
+        int m = 0;
+        for (int c0 = 0; c0 < cpl; c0 += 64) {
+            const int cn = min(64, cpl - c0);
+            uint64_t cm = 0;
+            for (int c = 0; c < cn; ++c) {
+                const int j = lane + 64 * (c0 + c);
+                cm |= (uint64_t)(j < n_src && key_f32(sP[j], q) <= thr) << c;
+            }
+            const int cnt = __popcll(cm);
+            int tot = 0, pidx = 0;
+#pragma unroll
+            for (int bit = 0; bit < 7; ++bit) {  // cnt <= 64 < 2^7
+                const uint64_t plane = __ballot((cnt >> bit) & 1);
+                tot += __popcll(plane) << bit;
+                pidx += __popcll(plane & below) << bit;
+            }
+            pidx += m;
+            while (cm) {
+                const int c = __builtin_ctzll(cm);
+                cm &= cm - 1;
+                if (pidx < kCap) sIdx[wave][pidx] = lane + 64 * (c0 + c);
+                ++pidx;
+            }
+            m += tot;
+        }
+        knn_finish<QUERY>(sP, sKey[wave], sIdx[wave], sSel[wave], m, q, kk, k, qi, b, n_src, n_q, cpl, lane,
+                          below, out, degenerate);
+    }
+}
+
+template <bool QUERY>
+int launch_knn_large(const float2 *p, const float2 *q, int64_t batches, int ns, int nq, int k, int32_t *out,
+                     int32_t *degenerate, hipStream_t st) {
+    const size_t lds = (size_t)ns * sizeof(float2);
+    const hipError_t e =
+        hipFuncSetAttribute((const void *)knn_large_kernel<QUERY>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds);
+    if (e != hipSuccess) return MMPDE_ERR_HIP_BASE - (int)e;
+    dim3 grid(ceil_div(nq, kLargeQueries), (unsigned)batches);
+    hipLaunchKernelGGL(knn_large_kernel<QUERY>, grid, dim3(256), lds, st, p, q, ns, nq, k, out, degenerate);
+    MMPDE_RET_LAUNCH();
+    return MMPDE_OK;
 }
 
 template <bool QUERY>
 int launch_knn(const float *pts, const float *qry, int64_t batches, int64_t n_src, int64_t n_q,
                int k, int32_t *out, int32_t *degenerate, hipStream_t st) {
     const int kk = QUERY ? k : k + 1;
-    if (k < 1 || kk > 64 || n_src < kk || n_src > 4096 || n_q < 1 || batches < 1 ||
-        batches > 65535)
+    if (k < 1 || kk > 64 || n_src < kk || n_src > kLargeMax || n_q < 1 || batches < 1 ||
+        batches > 65535 || n_q > INT32_MAX / 64)
         return MMPDE_ERR_INVALID_ARG;
     dim3 grid(ceil_div(n_q, kQueriesPerBlock), (unsigned)batches);
     const int cpl = ceil_div(n_src, 64);
     const float2 *p = (const float2 *)pts;
     const float2 *q = (const float2 *)qry;
     const int ns = (int)n_src, nq = (int)n_q;
+    if (n_src > 4096) return launch_knn_large<QUERY>(p, q, batches, ns, nq, k, out, degenerate, st);
 #define MMPDE_KNN_CASE(C)                                                                     \
     if (cpl <= C) {                                                                           \
         hipLaunchKernelGGL((knn_kernel<C, QUERY>), grid, dim3(256), 0, st, p, q, ns, nq, k, out, \

@@ -14,13 +14,13 @@ from . import _lib as L
 # (include/mmpde_hip.h mmpde_knn_graph / mmpde_knn_query).  The reference's
 # benchmarked grids are 2521 (cy) and 48 x 48 = 2304 (burgers); burgers at the
 # PDE's own default 96 x 96 (PDEs.py:27) exceeds it.
-KNN_MAX_POINTS = 4096
+KNN_MAX_POINTS = 16384
 
 
 def _knn_points_check(n_per: int, k: int, what: str):
     if n_per > KNN_MAX_POINTS:
         raise ValueError(f"{what}: {n_per} points per trajectory; the HIP kNN kernels take at "
-                         f"most {KNN_MAX_POINTS} (run --base_resolution <= 64 x 64)")
+                         f"most {KNN_MAX_POINTS} (run --base_resolution <= 128 x 128)")
     if k > 63:
         raise ValueError(f"{what}: k = {k}; the HIP kNN kernels take k <= 63")
 

@@ -61,7 +61,8 @@ def test_knn_graph_integer_lattice_golden(dev):
     assert np.array_equal(nbr.cpu().numpy(), g["nbr"])
 
 
-@pytest.mark.parametrize("n,B", [(36, 3), (100, 5), (640, 2), (4096, 1), (3000, 2)])
+@pytest.mark.parametrize("n,B", [(36, 3), (100, 5), (640, 2), (4096, 1), (3000, 2),
+                                 (4097, 1), (9216, 2), (16384, 1)])   # > 4096: knn_large_kernel
 def test_knn_graph_sizes(dev, n, B):
     torch.manual_seed(n)
     _graph_case(torch.rand(n * B, 2), B, dev)
@@ -95,7 +96,8 @@ def test_knn_query_sklearn_golden(dev):
     assert np.array_equal(idx.cpu().numpy().reshape(g["idx"].shape), g["idx"])
 
 
-@pytest.mark.parametrize("ns,nq,B", [(2521, 2521, 2), (30, 7, 2), (2304, 2304, 1), (4096, 50, 1)])
+@pytest.mark.parametrize("ns,nq,B", [(2521, 2521, 2), (30, 7, 2), (2304, 2304, 1), (4096, 50, 1),
+                                     (9216, 2304, 2), (16384, 300, 1)])
 def test_knn_query_bit_exact(dev, ns, nq, B):
     from mmpde_amd import ops
 
@@ -104,6 +106,25 @@ def test_knn_query_bit_exact(dev, ns, nq, B):
     qry[:3] = src[:3]                                          # zero-distance hits
     idx = ops.knn_query(src.to(dev), qry.to(dev), B, 30)
     ref = refcpu.knn_query(src, qry, B, 30)
+    assert torch.equal(idx.cpu().long().reshape(ref.shape), ref)
+
+
+def test_knn_large_candidate_overflow_fallback(dev):
+    # > 4096 points per trajectory with hundreds of coincident points: the
+    # large-set kernel's chunked compaction overflows the LDS list and takes
+    # the radix-select path, for the graph and the query variant.
+    from mmpde_amd import ops
+
+    torch.manual_seed(13)
+    pos = torch.rand(2 * 6000, 2)
+    pos[100:900] = pos[5]                                      # 801 coincident points
+    pos[6000 + 4000:6000 + 5300] = 0.25                        # 1300 coincident points
+    _graph_case(pos, 2, dev)
+    qry = torch.rand(2 * 200, 2)
+    qry[:50] = pos[5]
+    qry[200:260] = 0.25
+    idx = ops.knn_query(pos.to(dev), qry.to(dev), 2, 30)
+    ref = refcpu.knn_query(pos, qry, 2, 30)
     assert torch.equal(idx.cpu().long().reshape(ref.shape), ref)
 
 
