@@ -41,12 +41,18 @@ F32_MFMA_PEAK_TFLOPS = 157.3          # MI355X_MICROARCH.md: dense fp32 matrix p
 F16_MFMA_PEAK_TFLOPS = 2516.6         # 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz (~2.5 PF dense)
 HBM_PEAK_GBS = 8000.0
 CONFIGS = {
-    # name: (kind, moving_mesh, default trajectories per GPU, BASELINE.json config)
-    "cy-mmpde": ("cy", True, 16, "configs[3]: Cylinder MM-PDE, batch=16"),
-    "cy-gnn": ("cy", False, 8, "configs[2]: Cylinder GNN, batch=8"),
-    "burgers-mmpde": ("burgers", True, 32, "configs[1]: Burgers' MM-PDE, batch=32"),
-    "burgers-gnn": ("burgers", False, 1, "configs[0]: Burgers' GNN, batch=1"),
+    # name: (kind, moving_mesh, default trajectories per GPU, BASELINE.json config,
+    #        Burgers grid side: 48 = the MM-PDE --base_resolution, 96 = PDEs.py's default)
+    "cy-mmpde": ("cy", True, 16, "configs[3]: Cylinder MM-PDE, batch=16", None),
+    "cy-gnn": ("cy", False, 8, "configs[2]: Cylinder GNN, batch=8", None),
+    "burgers-mmpde": ("burgers", True, 32, "configs[1]: Burgers' MM-PDE, batch=32", 48),
+    "burgers-gnn": ("burgers", False, 1, "configs[0]: Burgers' GNN, default resolution 96x96, batch=1", 96),
 }
+
+
+def set_burgers_side(pde, s):
+    """The Burgers grid (31, s, s) on a synth.build_models PDE (built at 48x48)."""
+    pde.grid_size = pde.movingmesh_grid_size = pde.ori_grid_size = [31, s, s]
 
 
 class HipEvents:
@@ -114,7 +120,7 @@ class EdgeTracer:
         return out
 
 
-def cpu_baseline(kind, moving_mesh, seconds):
+def cpu_baseline(kind, moving_mesh, seconds, side=48):
     """The CPU oracle (op-for-op restatement of the reference forward, unfused,
     brute-force kNN) on a bounded sample: 2 trajectories, repeated one-step
     forwards until `seconds` of work (>= 1 step)."""
@@ -132,9 +138,9 @@ def cpu_baseline(kind, moving_mesh, seconds):
         opde = refcpu.PDEConst("cy", [30, grid.shape[0]], ori_grid=grid)
         n_nodes = grid.shape[0]
     else:
-        u = fields(burgers_grid_points(), B, 31).reshape(B, 31, 48, 48)
-        opde = refcpu.PDEConst("burgers", [31, 48, 48])
-        n_nodes = 48 * 48
+        u = fields(burgers_grid_points(side), B, 31).reshape(B, 31, side, side)
+        opde = refcpu.PDEConst("burgers", [31, side, side])
+        n_nodes = side * side
     sds = {k: {n: t.detach() for n, t in m.state_dict().items()}
            for k, m in (("model", model), ("model_b", model_b), ("itp", itp), ("dmm", dmm))
            if m is not None}
@@ -185,12 +191,16 @@ def main():
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     device = torch.device(f"cuda:{local}")
     torch.cuda.set_device(device)
-    kind, moving, b_default, cfg_name = CONFIGS[args.config]
+    kind, moving, b_default, cfg_name, side = CONFIGS[args.config]
     B = args.batch or b_default
     total = B * world
     lo, hi = D.shard_range(total, rank, world)
 
     pde, model, model_b, itp, dmm, gc = build_models(kind, moving_mesh=moving)
+    if kind == "burgers" and side != 48:
+        if moving:
+            raise SystemExit("the synthetic MM-PDE models are built for the 48x48 grid")
+        set_burgers_side(pde, side)
     for m in (model, model_b, itp, dmm):
         if m is not None:
             m.to(device)
@@ -201,8 +211,8 @@ def main():
         pts, t_len = pde.ori_grid, 30
         u_all = fields(pts, total, t_len)[lo:hi]
     else:
-        pts, t_len = burgers_grid_points(), 31
-        u_all = fields(pts, total, t_len).reshape(total, t_len, 48, 48)[lo:hi]
+        pts, t_len = burgers_grid_points(side), 31
+        u_all = fields(pts, total, t_len).reshape(total, t_len, side, side)[lo:hi]
     n_nodes = pts.shape[0]
     eng = MMPDERollout(kind, model, model_b, itp, dmm, gc, hi - lo, device, moving_mesh=moving)
     n_gnn = 2 if moving else 1
@@ -280,7 +290,7 @@ def main():
             traffic = rec.get("modes", {}).get(args.edge_gemm, {}).get("hbm_bytes_per_launch")
     line = {
         "metric": METRIC if kind == "cy" else METRIC.replace("cylinder 2521-node mesh",
-                                                             "Burgers 48x48 grid"),
+                                                             f"Burgers {side}x{side} grid"),
         "value": total * n_nodes * args.steps / elapsed,
         "unit": "node-updates/s",
         "n_gpus": world,
@@ -336,7 +346,7 @@ def main():
     if exact is not None:
         line["f32_exact"] = exact
     if world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(kind, moving, args.cpu_seconds)
+        line["cpu_baseline"] = cpu_baseline(kind, moving, args.cpu_seconds, side or 48)
     print(json.dumps(line), flush=True)
 
 

@@ -363,6 +363,27 @@ def test_gnn_only_step_matches_oracle(dev):
     _close(eng.step(data[:, 0].to(dev), step), ref, 1e-5, 1e-9, "gnn-only step")
 
 
+def test_burgers_gnn_default_resolution_api_matches_oracle(dev):
+    """BASELINE configs[0]'s shape on the GPU: the Burgers GNN baseline
+    (moving_mesh=False) at the PDE's default resolution (31, 96, 96), 9216
+    nodes per trajectory (the large-set kNN kernel), through the drop-in API
+    (create_graph(..., None) -> model(graph), train_helper_2d.py:177-181)."""
+    from mmpde_amd.synth import build_models, burgers_grid_points, fields
+
+    pde, model, _, _, _, gc = build_models("burgers", moving_mesh=False, seed=4)
+    res = [31, 96, 96]
+    pde.grid_size = pde.movingmesh_grid_size = pde.ori_grid_size = res
+    B, step = 1, 7
+    u = fields(burgers_grid_points(96), B, 31, seed=5).reshape(B, 31, 96, 96)
+    data, labels = gc.create_data(u, [step] * B)
+    opde = refcpu.PDEConst("burgers", res)
+    ref, aux = refcpu.mmpde_step(opde, _sds(model=model), data, labels, [step] * B, moving_mesh=False)
+    model.to(dev)
+    graph = gc.create_graph(None, data, labels, [step] * B, dev, None)
+    assert torch.equal(graph.edge_index.cpu(), aux["graph_uni"].edge_index), "kNN-35 graph, 9216 nodes"
+    _close(model(graph), ref, 1e-5, 1e-9, "burgers GNN 96x96")
+
+
 def test_graph_creator_api_equals_engine(dev):
     """The drop-in GraphCreator path (create_graph / interpolate_pred) and the
     rollout engine compose the same kernels: identical bits.  (Oracle parity of
