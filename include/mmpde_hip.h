@@ -35,6 +35,9 @@ extern "C" {
 #define MMPDE_ACT_NONE 0
 #define MMPDE_ACT_TANH 1
 #define MMPDE_ACT_RELU 2
+#define MMPDE_ACT_ELU 3 /* x > 0 ? x : expm1(x) (F.elu, alpha 1) */
+#define MMPDE_PAD_ZEROS 0
+#define MMPDE_PAD_CIRCULAR 1
 
 typedef void *mmpde_stream_t; /* hipStream_t */
 
@@ -133,6 +136,14 @@ int mmpde_resample_bilinear(const float *x, int64_t planes, int h, int w, int oh
 int mmpde_conv2d(const float *x, int64_t batches, int cin, int h, int w, const float *weight,
                  const float *bias, int cout, int ks, int stride, int pad,
                  const float *residual, int act, float *y, mmpde_stream_t stream);
+/* The same with pad_mode MMPDE_PAD_ZEROS / MMPDE_PAD_CIRCULAR (nn.Conv2d
+ * padding_mode='circular': indices wrap) and res_after_act = 1 for
+ * residual + act(conv + bias) (BaseCNN's x + elu(conv(x)), models_cnn.py:70-76)
+ * instead of act(conv + bias + residual).  act: MMPDE_ACT_* incl. ELU. */
+int mmpde_conv2d_ex(const float *x, int64_t batches, int cin, int h, int w, const float *weight,
+                    const float *bias, int cout, int ks, int stride, int pad, int pad_mode,
+                    const float *residual, int res_after_act, int act, float *y,
+                    mmpde_stream_t stream);
 
 /* ------------------------------------------------------------------------
  * MP_PDE_Solver_2D (reference gnn_2d.py:19-141), hidden width 128.

@@ -88,6 +88,7 @@ __device__ __forceinline__ float amax_read(const uint32_t *slot) {
 __device__ __forceinline__ float act_apply(float v, int act) {
     if (act == MMPDE_ACT_TANH) return tanhf(v);
     if (act == MMPDE_ACT_RELU) return fmaxf(v, 0.0f);
+    if (act == MMPDE_ACT_ELU) return v > 0.0f ? v : expm1f(v);
     return v;
 }
 
@@ -120,5 +121,6 @@ __attribute__((visibility("hidden"))) int conv2d(const float *x, int64_t batches
                                                  int w, const float *weight, const float *bias,
                                                  int cout, int ks, int stride, int pad,
                                                  const float *residual, int act, float *y,
-                                                 hipStream_t st, unsigned *zero, int n_zero);
+                                                 hipStream_t st, unsigned *zero, int n_zero,
+                                                 int circular = 0, int res_after_act = 0);
 }  // namespace mmpde_detail

@@ -206,7 +206,8 @@ __global__ __launch_bounds__(256) void conv2d_kernel(const float *__restrict__ x
                                                      int ks, int stride, int pad, int oh, int ow,
                                                      const float *__restrict__ res, int act,
                                                      float *__restrict__ y,
-                                                     unsigned *__restrict__ zero, int n_zero) {
+                                                     unsigned *__restrict__ zero, int n_zero,
+                                                     int circular, int res_after_act) {
     const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const int64_t total = batches * cout * oh * ow;
     if (e < n_zero) zero[e] = 0u;  // side job for the caller (dmm.hip's split-K tickets)
@@ -220,14 +221,20 @@ __global__ __launch_bounds__(256) void conv2d_kernel(const float *__restrict__ x
         const float *xp = x + (bb * cin + ci) * (int64_t)h * w;
         const float *wp = wt + ((int64_t)co * cin + ci) * ks * ks;
         for (int ky = 0; ky < ks; ++ky) {
-            const int iy = oy * stride - pad + ky;
-            if (iy < 0 || iy >= h) continue;
+            int iy = oy * stride - pad + ky;
+            if (circular) iy = ((iy % h) + h) % h;
+            else if (iy < 0 || iy >= h) continue;
             for (int kx = 0; kx < ks; ++kx) {
-                const int ix = ox * stride - pad + kx;
-                if (ix < 0 || ix >= w) continue;
+                int ix = ox * stride - pad + kx;
+                if (circular) ix = ((ix % w) + w) % w;
+                else if (ix < 0 || ix >= w) continue;
                 acc += wp[ky * ks + kx] * xp[iy * w + ix];
             }
         }
+    }
+    if (res_after_act) {
+        y[e] = res[e] + act_apply(acc, act);
+        return;
     }
     if (res) acc = res[e] + acc;
     y[e] = act_apply(acc, act);
@@ -259,7 +266,7 @@ __global__ __launch_bounds__(256) void traj_mse_kernel(const float *__restrict__
 
 }  // namespace
 
-extern "C" int mmpde_version(void) { return 11000; }
+extern "C" int mmpde_version(void) { return 11100; }
 
 extern "C" int mmpde_traj_mse(const float *pred, const float *labels, int64_t batches, int64_t n_per,
                               float *out, mmpde_stream_t stream) {
@@ -339,16 +346,32 @@ extern "C" int mmpde_conv2d(const float *x, int64_t batches, int cin, int h, int
                                 y, as_stream(stream), nullptr, 0);
 }
 
+extern "C" int mmpde_conv2d_ex(const float *x, int64_t batches, int cin, int h, int w, const float *weight,
+                               const float *bias, int cout, int ks, int stride, int pad, int pad_mode,
+                               const float *residual, int res_after_act, int act, float *y,
+                               mmpde_stream_t stream) {
+    MMPDE_REQUIRE(x && weight && y && batches > 0 && cin > 0 && cout > 0 && ks > 0);
+    MMPDE_REQUIRE((stride == 1 || stride == 2) && pad >= 0 && act >= 0 && act <= 3);
+    MMPDE_REQUIRE(pad_mode == MMPDE_PAD_ZEROS || pad_mode == MMPDE_PAD_CIRCULAR);
+    MMPDE_REQUIRE(!res_after_act || residual);
+    const int oh = (h + 2 * pad - ks) / stride + 1;
+    const int ow = (w + 2 * pad - ks) / stride + 1;
+    MMPDE_REQUIRE(oh > 0 && ow > 0 && (pad_mode == MMPDE_PAD_ZEROS || (pad <= h && pad <= w)));
+    return mmpde_detail::conv2d(x, batches, cin, h, w, weight, bias, cout, ks, stride, pad, residual, act,
+                                y, as_stream(stream), nullptr, 0, pad_mode == MMPDE_PAD_CIRCULAR, res_after_act);
+}
+
 namespace mmpde_detail {
 int conv2d(const float *x, int64_t batches, int cin, int h, int w, const float *weight, const float *bias,
            int cout, int ks, int stride, int pad, const float *residual, int act, float *y, hipStream_t st,
-           unsigned *zero, int n_zero) {
+           unsigned *zero, int n_zero, int circular, int res_after_act) {
     const int oh = (h + 2 * pad - ks) / stride + 1;
     const int ow = (w + 2 * pad - ks) / stride + 1;
     const int64_t total = batches * cout * oh * ow;
     const int64_t threads = total > n_zero ? total : n_zero;
     hipLaunchKernelGGL(conv2d_kernel, dim3(ceil_div(threads, 256)), dim3(256), 0, st, x, batches, cin, h, w,
-                       weight, bias, cout, ks, stride, pad, oh, ow, residual, act, y, zero, n_zero);
+                       weight, bias, cout, ks, stride, pad, oh, ow, residual, act, y, zero, n_zero, circular,
+                       res_after_act);
     MMPDE_RET_LAUNCH();
     return MMPDE_OK;
 }

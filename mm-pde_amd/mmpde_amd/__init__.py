@@ -11,8 +11,9 @@ from .dmm_model import DMM, ConvNet, DenseNet
 from .gnn_2d import GNN_Layer_FS_2D, MP_PDE_Solver_2D
 from .graph import Data
 from .interpolate import ItpNet
+from .models_cnn import BaseCNN
 from .pdes import PDE, burgers, cy
 from .rollout import MMPDERollout
 
-__all__ = ["GraphCreator_FS_2D", "DMM", "ConvNet", "DenseNet", "GNN_Layer_FS_2D",
+__all__ = ["BaseCNN", "GraphCreator_FS_2D", "DMM", "ConvNet", "DenseNet", "GNN_Layer_FS_2D",
            "MP_PDE_Solver_2D", "Data", "ItpNet", "PDE", "burgers", "cy", "MMPDERollout"]

@@ -13,9 +13,10 @@ import os
 import torch
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libmmpde_hip.so")
-ABI_VERSION = 11000
+ABI_VERSION = 11100
 
-ACT_NONE, ACT_TANH, ACT_RELU = 0, 1, 2
+ACT_NONE, ACT_TANH, ACT_RELU, ACT_ELU = 0, 1, 2, 3
+PAD_ZEROS, PAD_CIRCULAR = 0, 1
 # message_net_2 edge GEMM arithmetic (include/mmpde_hip.h MMPDE_EDGE_GEMM_*)
 EDGE_GEMM = {"f32": 0, "f16x3": 1}
 
@@ -102,6 +103,7 @@ _SIGS = {
     "mmpde_traj_mse": (_I, [_P, _P, _I64, _I64, _P, _P]),
     "mmpde_conv2d": (_I, [_P, _I64, _I, _I, _I, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P]),
     "mmpde_resample_bilinear": (_I, [_P, _I64, _I, _I, _I, _I, _P, _P]),
+    "mmpde_conv2d_ex": (_I, [_P, _I64, _I, _I, _I, _P, _P, _I, _I, _I, _I, _I, _P, _I, _I, _P, _P]),
     "mmpde_gnn_workspace_bytes": (_I64, [_I64]),
     "mmpde_gnn_embed": (_I, [_P, _P, _I64, GnnScales, _P, _P, _P, _P]),
     "mmpde_gnn_layer": (_I, [_P, _P, _P, _I64, _I, _P, GnnScales, _P, _P, _P, _P]),

@@ -189,8 +189,9 @@ def resample_bilinear(u: torch.Tensor, oh: int, ow: int) -> torch.Tensor:
 
 
 def conv2d(x: torch.Tensor, w: torch.Tensor, b, stride: int, pad: int, act: int,
-           residual=None) -> torch.Tensor:
-    """act(conv2d(x, w, b, stride, pad) [+ residual]), NCHW fp32."""
+           residual=None, circular: bool = False, res_after_act: bool = False) -> torch.Tensor:
+    """act(conv2d(x, w, b, stride, pad) [+ residual]), NCHW fp32; circular:
+    padding_mode='circular'; res_after_act: residual + act(conv2d(...))."""
     L.require_device(x, w)
     x = L.f32c(x)
     bt, cin, h, wd = x.shape
@@ -198,10 +199,12 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, b, stride: int, pad: int, act: int,
     oh = (h + 2 * pad - ks) // stride + 1
     ow = (wd + 2 * pad - ks) // stride + 1
     y = torch.empty((bt, cout, oh, ow), dtype=torch.float32, device=x.device)
-    L.check(L.lib().mmpde_conv2d(L.ptr(x), bt, cin, h, wd, L.ptr(L.f32c(w)),
-                                 L.ptr(L.f32c(b)) if b is not None else None, cout, ks, stride,
-                                 pad, L.ptr(residual), act, L.ptr(y), L.stream(x.device)),
-            "mmpde_conv2d")
+    res = L.f32c(residual) if residual is not None else None
+    L.check(L.lib().mmpde_conv2d_ex(L.ptr(x), bt, cin, h, wd, L.ptr(L.f32c(w)),
+                                    L.ptr(L.f32c(b)) if b is not None else None, cout, ks, stride,
+                                    pad, L.PAD_CIRCULAR if circular else L.PAD_ZEROS, L.ptr(res),
+                                    int(res_after_act), act, L.ptr(y), L.stream(x.device)),
+            "mmpde_conv2d_ex")
     return y
 
 

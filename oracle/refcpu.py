@@ -251,6 +251,24 @@ def convnet(sd, p, x):
     return _lin(sd, f"{p}.fc3", x)
 
 
+def basecnn(sd, dt, u, tw):
+    """BaseCNN.forward, models_cnn.py:66-83: circular-padded Conv2d stack with ELU
+    and residuals (padding_mode='circular' = F.pad(mode='circular') + valid conv),
+    then u[:, -1] + cumsum(dt) * x, squeezed.  u [B, tw, X, Y]."""
+    def conv(i, x):
+        w, b = sd[f"conv{i}.weight"], sd[f"conv{i}.bias"]
+        p = w.shape[-1] // 2
+        return F.conv2d(F.pad(x, (p, p, p, p), mode="circular"), w, b)
+
+    x = F.elu(conv(1, u))
+    for i in range(2, 8):
+        x = x + F.elu(conv(i, x))
+    x = conv(8, x)
+    dtc = torch.cumsum(torch.ones(1, tw) * dt, dim=1)[None, :, :, None, None]
+    out = u[:, -1, :, :][:, None, None, :, :].repeat(1, 1, tw, 1, 1) + dtc * x[:, None, :, :, :]
+    return out.squeeze()
+
+
 def dmm_gnn_layer(sd, p, x, u, pos_x, pos_y, edge_index):
     """DMM GNN_Layer_FS_2D (tanh), dmm_model.py:126-142."""
     n = x.shape[0]
