@@ -1,12 +1,14 @@
 #!/bin/bash
-# A/B of two builds of libmmpde_hip.so (mm-pde_amd/mmpde_amd/lib/ab/{a,b}.so, built
+# A/B of builds of libmmpde_hip.so (mm-pde_amd/mmpde_amd/lib/ab/*.so, built
 # beforehand on the CPU side): each is copied over the in-tree library in turn
 # and timed with a short serial rocprofv3 kernel-trace run of bench.py.
 set -u
 export TMPDIR=/tmp
 L=mm-pde_amd/mmpde_amd/lib
-for v in a b; do
-  cp $L/ab/$v.so $L/libmmpde_hip.so
+cp $L/libmmpde_hip.so /tmp/libmmpde_hip.orig.so
+for so in $L/ab/*.so; do
+  v=$(basename $so .so)
+  cp $so $L/libmmpde_hip.so
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/ab/$v -o run -- \
       python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-f32-exact --serial \
       > gpurun_out/ab/$v.log 2>&1 || { tail -20 gpurun_out/ab/$v.log; exit 1; }
@@ -14,7 +16,8 @@ for v in a b; do
   echo "== $v: $(grep -o '"value": [0-9.e+]*' gpurun_out/ab/$v.log | head -1)"
   python3 - "$f" <<'PY'
 import csv, sys
-for r in list(csv.DictReader(open(sys.argv[1])))[:6]:
+for r in list(csv.DictReader(open(sys.argv[1])))[:1]:
     print("%-60s %5s calls avg %8.1f us" % (r["Name"][:60], r["Calls"], float(r["AverageNs"]) / 1e3))
 PY
 done
+cp /tmp/libmmpde_hip.orig.so $L/libmmpde_hip.so
