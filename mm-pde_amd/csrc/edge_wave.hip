@@ -19,9 +19,9 @@
 // Work unit = (16-target tile, part): part p of `parts` covers slots
 // [p k / parts, (p + 1) k / parts) of the tile (parts > 1 balances the grid
 // when tiles per wave are few).  Each wave walks a contiguous, XCD-local range
-// of units as one slot stream.  Part q writes its slots' sum divided by the
-// degree to out + q * part_stride; launch_node_stage adds the parts in part
-// order.  Deterministic: fixed summation order, no atomics.
+// of units as one slot stream.  Part q writes its slots' sum to out + q *
+// part_stride; launch_node_stage adds the parts in part order and divides by
+// the degree.  Deterministic: fixed summation order, no atomics.
 #include "common.hpp"
 #include "f16x3.hpp"
 #include "layer.hpp"
@@ -97,9 +97,10 @@ __device__ __forceinline__ half8 pin_agpr(half8 v) {
 }
 
 // DIAG (profiling builds only, tools/ubench; production = 0): bit 0 skips the
-// split VALU, bit 1 the relu-sums, bit 2 the b gathers, bit 3 replaces the
-// split's packed / mixed-precision instructions by plain VOP2 ones of the same
-// count (all wrong values).
+// split VALU, bit 1 the relu-sums, bit 2 the b gathers (all wrong values; without
+// the relu-sums the compiler drops the MFMAs they would read), bit 5 replaces the relu-sums by empty register sinks
+// (MFMAs kept), bit 6 the unit stores likewise, bit 7 skips the a-row reload
+// at tile switches (wrong values).
 template <bool RAGGED, int PARTS, int DIAG = 0>
 __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
     const int lane = threadIdx.x, r = lane & 15, g = lane >> 4;
@@ -182,16 +183,7 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
         const float4 &bb = X[a_piece(j)];
         const float x0 = (j & 1) ? fmaf(bb.z, sc, ap.z) : fmaf(bb.x, sc, ap.x);
         const float x1 = (j & 1) ? fmaf(bb.w, sc, ap.w) : fmaf(bb.y, sc, ap.y);
-        if (DIAG & 8) {
-            uint32_t hh, ll;
-            asm("v_cvt_pkrtz_f16_f32 %0, %2, %3\n\tv_add_f32_e32 %1, %2, %0\n\t"
-                "v_add_f32_e32 %1, %3, %1\n\tv_max_f32_e32 %0, 0, %0"
-                : "=&v"(hh), "=&v"(ll) : "v"(x0), "v"(x1));
-            nh[j >> 2][j & 3] = hh;
-            nl[j >> 2][j & 3] = ll;
-        } else {
-            split2_relu_rtz(x0, x1, nh[j >> 2][j & 3], nl[j >> 2][j & 3]);
-        }
+        split2_relu_rtz(x0, x1, nh[j >> 2][j & 3], nl[j >> 2][j & 3]);
     };
     f32x4 S[8];
     int dg[4] = {k, k, k, k}, dg_prev[4] = {k, k, k, k};
@@ -217,19 +209,28 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
         if (RAGGED) v = e < d[t] ? v : 0.0f;
         Sc[t] += v;
     };
-    // the finished unit's sums (unscaled): mean = sum / degree, or the part's partial sum
-    auto write_unit = [&](int64_t row0, int part, const int *d) {
+    // the finished unit's sums, unscaled (a power-of-two multiply: exact).  The
+    // node stage adds the parts and divides by the degree (PyG mean = sum / count).
+    // Stores are unconditional unless the tile runs past n (wave-uniform test),
+    // at immediate offsets from one base per lane.
+    auto write_unit = [&](int64_t row0, int part) {
+        if (DIAG & 64) {  // no stores: keep the sums alive only
 #pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            const int col = 16 * c + r;
+            for (int c = 0; c < 8; ++c) asm volatile("" ::"v"(S[c]));
+            return;
+        }
+        float *o = p.out + part * p.part_stride + (row0 + 4 * g) * LH + r;
+        if (row0 + ET <= p.n) {
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const int64_t row = row0 + 4 * g + t;
-                if (row < p.n) {
-                    const float div = RAGGED ? (float)max(d[t], 1) : (float)k;
-                    p.out[part * p.part_stride + row * LH + col] = S[c][t] * inv[c] / div;
-                }
-            }
+            for (int c = 0; c < 8; ++c)
+#pragma unroll
+                for (int t = 0; t < 4; ++t) o[t * LH + 16 * c] = S[c][t] * inv[c];
+        } else {
+#pragma unroll
+            for (int c = 0; c < 8; ++c)
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    if (row0 + 4 * g + t < p.n) o[t * LH + 16 * c] = S[c][t] * inv[c];
         }
     };
     auto body = [&](float4 *X, uint32_t (*h)[4], uint32_t (*l)[4], uint32_t (*nh)[4], uint32_t (*nl)[4]) {
@@ -243,48 +244,58 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
         {   // a rows of the split slot's tile
             const int st = unit_tile(cS);
             if (st != atile) {
-                load_a(st);
+                if (!(DIAG & 128)) load_a(st);
                 atile = st;
             }
         }
+        // Per-MFMA placement: every MFMA gap carries at most one 2-instruction
+        // VALU unit (8 issue cycles beside the MFMA's 8 of 16), pinned by
+        // sched_barriers.  Group G = 4 c + s (the 3 MFMAs of column tile c, K
+        // step s): gap 0 the relu-sum of value G, gaps 1 / 2 split pair G >> 1
+        // (G even: its two fmas, then cvt_pkrtz + mixlo; G odd: mixhi + pk_max,
+        // then at G = 4 p + 3 the refill of piece p, whose last pair (4 p + 2)
+        // has read it).  The relu-sums trail their tile's MFMAs by six groups
+        // (groups 0-5: the previous slot's tiles 6 and 7).
         f32x4 acc[8];
+        float xs0 = 0.0f, xs1 = 0.0f;
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
             acc[c] = (f32x4){bias[c], bias[c], bias[c], bias[c]};
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
                 const half8 ah = __builtin_bit_cast(half8, h[s]), al = __builtin_bit_cast(half8, l[s]);
+                const int G = 4 * c + s, j = G >> 1;
                 acc[c] = mfma_f16(ah, wh[c][s], acc[c]);
+                {
+                    f32x4 &Sc = G >= 6 ? S[(G - 6) >> 2] : (G < 2 ? S[6] : S[7]);
+                    const int t = G >= 6 ? (G - 6) & 3 : (G < 2 ? G + 2 : G - 2);
+                    const float x = G >= 6 ? acc[(G - 6) >> 2][t] : (G < 2 ? acc6[t] : acc7[t]);
+                    if (RAGGED) relu_add(Sc, x, t, G >= 6 ? e : e_prev, G >= 6 ? dg : dg_prev);
+                    else if (DIAG & 32) asm volatile("" ::"v"(x));  // MFMAs kept, no VALU
+                    else if (!(DIAG & 2)) Sc[t] = relu_acc(Sc[t], x);
+                }
+                __builtin_amdgcn_sched_barrier(0);
                 acc[c] = mfma_f16(ah, wl[c][s], acc[c]);
-                acc[c] = mfma_f16(al, wh[c][s], acc[c]);
-                // VALU of this group: a split pair of slot q+1 every other
-                // group, one relu-sum value trailing the MFMAs by six groups
-                // (groups 0-5: the previous slot's tiles 6 and 7)
-                const int G = 4 * c + s;
-                if ((G & 1) == 0 && !(DIAG & 1)) split_pair(G >> 1, X, nh, nl);
-                if ((G & 3) == 2 && !(DIAG & 4)) X[G >> 2] = *(const float4 *)(brow + piece(G >> 2));  // piece consumed: refill
-                if (RAGGED) {
-                    if (G >= 6) {
-                        const int cc = (G - 6) >> 2, t = (G - 6) & 3;
-                        relu_add(S[cc], acc[cc][t], t, e, dg);
-                    } else if (G < 2) {
-                        relu_add(S[6], acc6[G + 2], G + 2, e_prev, dg_prev);
+                if (!(DIAG & 1)) {
+                    if ((G & 1) == 0) {
+                        const float4 &ap = av[a_piece(j)];
+                        const float4 &bb = X[a_piece(j)];
+                        xs0 = (j & 1) ? fmaf(bb.z, sc, ap.z) : fmaf(bb.x, sc, ap.x);
+                        xs1 = (j & 1) ? fmaf(bb.w, sc, ap.w) : fmaf(bb.y, sc, ap.y);
                     } else {
-                        relu_add(S[7], acc7[G - 2], G - 2, e_prev, dg_prev);
-                    }
-                } else if (!(DIAG & 2)) {
-                    if (G >= 6) {
-                        const int cc = (G - 6) >> 2, t = (G - 6) & 3;
-                        S[cc][t] = relu_acc(S[cc][t], acc[cc][t]);
-                    } else if (G < 2) {
-                        S[6][G + 2] = relu_acc(S[6][G + 2], acc6[G + 2]);
-                    } else {
-                        S[7][G - 2] = relu_acc(S[7][G - 2], acc7[G - 2]);
+                        split2_relu_rtz_b(xs1, nh[j >> 2][j & 3], nl[j >> 2][j & 3]);
                     }
                 }
                 __builtin_amdgcn_sched_barrier(0);
+                acc[c] = mfma_f16(al, wh[c][s], acc[c]);
+                if ((G & 1) == 0) {
+                    if (!(DIAG & 1)) split2_relu_rtz_a(xs0, xs1, nh[j >> 2][j & 3], nl[j >> 2][j & 3]);
+                } else if ((G & 3) == 3 && !(DIAG & 4)) {
+                    X[G >> 2] = *(const float4 *)(brow + piece(G >> 2));
+                }
+                __builtin_amdgcn_sched_barrier(0);
                 if (G == 5 && close_prev) {  // the previous unit is complete: write, restart
-                    write_unit(row0_prev, part_prev, dg_prev);
+                    write_unit(row0_prev, part_prev);
 #pragma unroll
                     for (int c2 = 0; c2 < 8; ++c2) S[c2] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
                 }
@@ -318,7 +329,7 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
     for (int t = 2; t < 4; ++t) relu_add(S[6], acc6[t], t, e_prev, dg_prev);
 #pragma unroll
     for (int t = 0; t < 4; ++t) relu_add(S[7], acc7[t], t, e_prev, dg_prev);
-    write_unit(row0_prev, part_prev, dg_prev);
+    write_unit(row0_prev, part_prev);
 }
 
 }  // namespace
@@ -357,7 +368,12 @@ int launch_edge_wave_diag(const float *a, const float *b, const int32_t *nbr, in
     case 3: hipLaunchKernelGGL((gnn_edge_wave_kernel<false, 2, 3>), dim3(grid), dim3(64), 0, st, w); break;
     case 4: hipLaunchKernelGGL((gnn_edge_wave_kernel<false, 2, 4>), dim3(grid), dim3(64), 0, st, w); break;
     case 7: hipLaunchKernelGGL((gnn_edge_wave_kernel<false, 2, 7>), dim3(grid), dim3(64), 0, st, w); break;
-    case 8: hipLaunchKernelGGL((gnn_edge_wave_kernel<false, 2, 8>), dim3(grid), dim3(64), 0, st, w); break;
+    case 33: hipLaunchKernelGGL((gnn_edge_wave_kernel<false, 2, 33>), dim3(grid), dim3(64), 0, st, w); break;
+    case 97: hipLaunchKernelGGL((gnn_edge_wave_kernel<false, 2, 97>), dim3(grid), dim3(64), 0, st, w); break;
+    case 32: hipLaunchKernelGGL((gnn_edge_wave_kernel<false, 2, 32>), dim3(grid), dim3(64), 0, st, w); break;
+    case 64: hipLaunchKernelGGL((gnn_edge_wave_kernel<false, 2, 64>), dim3(grid), dim3(64), 0, st, w); break;
+    case 128: hipLaunchKernelGGL((gnn_edge_wave_kernel<false, 2, 128>), dim3(grid), dim3(64), 0, st, w); break;
+    case 36: hipLaunchKernelGGL((gnn_edge_wave_kernel<false, 2, 36>), dim3(grid), dim3(64), 0, st, w); break;
     default: hipLaunchKernelGGL((gnn_edge_wave_kernel<false, 2, 0>), dim3(grid), dim3(64), 0, st, w); break;
     }
     MMPDE_RET_LAUNCH();

@@ -169,6 +169,22 @@ __device__ __forceinline__ void split2_relu_rtz(float x0, float x1, uint32_t &hi
         : "v"(x0), "v"(x1));
 }
 
+// split2_relu_rtz in two halves of two instructions, for schedules that place
+// each half in its own MFMA gap: _a = hi (RTZ, before the relu) and the low
+// word of lo, _b = the high word of lo and the relu of hi.
+__device__ __forceinline__ void split2_relu_rtz_a(float x0, float x1, uint32_t &hi, uint32_t &lo) {
+    asm("v_cvt_pkrtz_f16_f32 %0, %2, %3\n\t"
+        "v_fma_mixlo_f16 %1, %2, 1.0, -%0 op_sel_hi:[0,0,1] clamp"
+        : "=&v"(hi), "=&v"(lo)
+        : "v"(x0), "v"(x1));
+}
+__device__ __forceinline__ void split2_relu_rtz_b(float x1, uint32_t &hi, uint32_t &lo) {
+    asm("v_fma_mixhi_f16 %1, %2, 1.0, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1] clamp\n\t"
+        "v_pk_max_f16 %0, %0, 0"
+        : "+v"(hi), "+v"(lo)
+        : "v"(x1));
+}
+
 __device__ __forceinline__ float absmax4(float m, const float4 &v) {
     return fmaxf(fmaxf(fmaxf(m, fabsf(v.x)), fmaxf(fabsf(v.y), fabsf(v.z))), fabsf(v.w));
 }

@@ -545,13 +545,15 @@ extern "C" int mmpde_gnn_forward_ex(const float *u, const float *pos, int64_t n,
         uint32_t *aout = pack && next ? amax + 2 * kAmaxShards * (l + 1) : nullptr;
         if (eb && hipEventRecord(eb, st) != hipSuccess) return MMPDE_ERR_INVALID_ARG;
         int parts = 1;
-        rc = launch_edge_stage(wa, wb, nbr, exec ? exec->degree : nullptr, n, k, &layers[l], pk,
-                               ain, wmean, n * H, kGnnBufs - 4, &parts, st);
+        bool sums = false;
+        const int32_t *deg = exec ? exec->degree : nullptr;
+        rc = launch_edge_stage(wa, wb, nbr, deg, n, k, &layers[l], pk, ain, wmean, n * H, kGnnBufs - 4,
+                               &parts, st, &sums);
         if (rc) return rc;
         if (ee && hipEventRecord(ee, st) != hipSuccess) return MMPDE_ERR_INVALID_ARG;
         // a, b are rewritten in place: this layer's edge stage has consumed them
         rc = launch_node_stage(hb[cur], wmean, parts, n * H, u, pos, n, sc, &layers[l], next, pk, pkn, aout,
-                               hb[cur ^ 1], wa, wb, st);
+                               hb[cur ^ 1], wa, wb, st, sums ? deg : nullptr, sums ? k : 0);
         if (rc) return rc;
         if (ne && hipEventRecord(ne, st) != hipSuccess) return MMPDE_ERR_INVALID_ARG;
         cur ^= 1;

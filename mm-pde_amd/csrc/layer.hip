@@ -510,6 +510,10 @@ struct NodeArgs {
     uint32_t *amax_out;
     int parts;             // mean = sum of `parts` buffers part_stride floats apart
     int64_t part_stride;
+    // div_k > 0: the buffers hold neighbour sums (F16X3 wave edge kernel); the
+    // mean is their total / max(div_deg[row], 1), or / div_k without degrees
+    const int32_t *div_deg = nullptr;
+    int div_k = 0;
 };
 
 constexpr int NLD = 132;  // fp32 staging row stride (floats)
@@ -525,12 +529,15 @@ constexpr int NODE_WPE = MMPDE_NODE_WPE;  // node / embed launch bounds: waves p
 // kofs (multiple of 128) of an image KT wide; F16X3 scales each row by a power
 // of two (its max |x| -> [2^13, 2^14)) and records it in rs[row].  8 lanes per row.
 // nsum > 1: src is the first of nsum buffers sum_stride floats apart, added in
-// buffer order (the edge stage's per-part means).
+// buffer order (the edge stage's per-part sums); div_k > 0: the total is then
+// divided by the row's degree max(div_deg[row], 1), or by div_k (IEEE division:
+// torch_scatter's mean = sum / count).
 template <bool F16X3, int ROWS>
 __device__ __forceinline__ void prep(const float *src, int64_t lds, int64_t row0, int64_t nrows_valid,
                                      bool global, float4 *img, int KT, int kofs, float *rs,
                                      float *copy = nullptr, int t0 = -1, int nthr = 512, int nsum = 1,
-                                     int64_t sum_stride = 0) {
+                                     int64_t sum_stride = 0, const int32_t *div_deg = nullptr,
+                                     int div_k = 0) {
     // threads t0 .. t0 + nthr (default: the whole workgroup) share the rows
     for (int idx = t0 < 0 ? (int)threadIdx.x : (int)threadIdx.x - t0; idx < ROWS * 8; idx += nthr) {
         // a wave takes 8 rows x 8 parts, lane = 8 part + row: the 8 lanes of one
@@ -547,6 +554,11 @@ __device__ __forceinline__ void prep(const float *src, int64_t lds, int64_t row0
                 const float4 y = *(const float4 *)(sp + ps * sum_stride + 4 * q);
                 x[q] = make_float4(x[q].x + y.x, x[q].y + y.y, x[q].z + y.z, x[q].w + y.w);
             }
+        }
+        if (div_k > 0) {
+            const float d = div_deg ? (float)max(div_deg[srow], 1) : (float)div_k;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) x[q] = make_float4(x[q].x / d, x[q].y / d, x[q].z / d, x[q].w / d);
         }
         if (copy) {
 #pragma unroll
@@ -760,11 +772,11 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs p) {
     if constexpr (ROWS * 8 <= 256) {  // h on waves 0-3, mean on waves 4-7 at once
         if (tid < 256) prep<F16X3, ROWS>(p.h, LH, row0, p.n, true, img, 256, 0, rs[0], hres, 0, 256);
         else prep<F16X3, ROWS>(p.mean, LH, row0, p.n, true, img, 256, 128, rs[1], nullptr, 256, 256, p.parts,
-                               p.part_stride);
+                               p.part_stride, p.div_deg, p.div_k);
     } else {
         prep<F16X3, ROWS>(p.h, LH, row0, p.n, true, img, 256, 0, rs[0], hres);
         prep<F16X3, ROWS>(p.mean, LH, row0, p.n, true, img, 256, 128, rs[1], nullptr, -1, 512, p.parts,
-                          p.part_stride);
+                          p.part_stride, p.div_deg, p.div_k);
     }
     __syncthreads();
 
@@ -939,8 +951,9 @@ int device_cus() {
 int launch_edge_stage(const float *a, const float *b, const int32_t *nbr, const int32_t *deg,
                       int64_t n, int k, const mmpde_gnn_layer_params *p, const char *pk,
                       const uint32_t *amax_in, float *mean, int64_t part_stride, int max_parts,
-                      int *parts_used, hipStream_t st) {
+                      int *parts_used, hipStream_t st, bool *sums) {
     if (parts_used) *parts_used = 1;
+    if (sums) *sums = false;
     MMPDE_REQUIRE(a && b && nbr && p && mean && n > 0 && k > 0 && n <= (int64_t)INT32_MAX);
     MMPDE_REQUIRE(al16(a) && al16(b) && al16(p->msg2_w) && al16(mean));
     MMPDE_REQUIRE(!pk || (amax_in && al16(pk)));
@@ -951,6 +964,9 @@ int launch_edge_stage(const float *a, const float *b, const int32_t *nbr, const 
 #ifndef MMPDE_EDGE_RING
     // F16X3: one wave per SIMD with the operands in registers (edge_wave.hip)
     if (pk) {
+        // the wave kernel leaves the division to the node stage
+        MMPDE_REQUIRE(sums);
+        *sums = true;
         const int parts = edge_wave_parts(ntiles, cus, max_parts, k);
         if (parts_used) *parts_used = parts;
         return launch_edge_wave(a, b, nbr, deg, n, k, p->msg2_b, pk, amax_in, mean, parts, part_stride, cus, st);
@@ -973,15 +989,15 @@ int launch_node_stage(const float *h, const float *mean, int parts, int64_t part
                       const float *u, const float *pos, int64_t n, mmpde_gnn_scales sc,
                       const mmpde_gnn_layer_params *p, const mmpde_gnn_layer_params *next,
                       const char *pk, const char *pkn, uint32_t *amax_out, float *h_out, float *a_out,
-                      float *b_out, hipStream_t st) {
-    MMPDE_REQUIRE(parts >= 1 && parts <= 4 && (parts == 1 || part_stride >= n * LH));
+                      float *b_out, hipStream_t st, const int32_t *div_deg, int div_k) {
+    MMPDE_REQUIRE(parts >= 1 && parts <= 4 && (parts == 1 || part_stride >= n * LH) && div_k >= 0);
     MMPDE_REQUIRE(h && mean && u && pos && p && h_out && n > 0);
     MMPDE_REQUIRE(al16(h) && al16(mean) && al16(h_out));
     MMPDE_REQUIRE(p->upd1_ld >= 257 && (p->upd1_ld & 3) == 0 && al16(p->upd1_w) && al16(p->upd2_w));
     MMPDE_REQUIRE(!pk || (al16(pk) && (!next || pkn)));
     NodeArgs a{h, mean, n, p->upd1_w, p->upd1_b, p->upd1_ld, p->upd2_w, p->upd2_b, p->bn_w, p->bn_b,
                p->bn_rm, p->bn_rv, p->eps, h_out, nullptr, nullptr, 0, a_out, b_out, u, pos, sc,
-               pk, pkn, amax_out, parts, part_stride};
+               pk, pkn, amax_out, parts, part_stride, div_deg, div_k};
     if (next) {
         MMPDE_REQUIRE(a_out && b_out && next->msg1_ld >= 260 && (next->msg1_ld & 3) == 0 &&
                       al16(next->msg1_w));

@@ -161,8 +161,8 @@ int main(int argc, char **argv) {
             if (launch_edge_wave(a, b, nbr, nullptr, n, k, b2, pack, amax, mean, 1, 0, cus, 0)) return 1;
             CK(hipMemcpy(m1.data(), mean, n * H * 4, hipMemcpyDeviceToHost));
             double d = 0, mx = 0;
-            for (size_t i = 0; i < m0.size(); ++i) {
-                d = std::max(d, (double)std::fabs(m0[i] - m1[i]));
+            for (size_t i = 0; i < m0.size(); ++i) {  // the wave kernel stores sums
+                d = std::max(d, (double)std::fabs(m0[i] - m1[i] / k));
                 mx = std::max(mx, (double)std::fabs(m0[i]));
             }
             printf("wave vs ring kernel: max|diff| %.3e (max|mean| %.3e)\n", d, mx);
