@@ -691,13 +691,16 @@ __device__ __forceinline__ void proj_phase(const BOps<F16X3, F16X3 ? 4 : 8> &bA,
         gemm_tile<F16X3, RB, S1>(aB, img, 128, 0, bB, lane);
     }
     float amx = 0.0f, bmx = 0.0f;
+    // stores at immediate offsets from one base per lane; the row test only
+    // for a tile that runs past n (wave-uniform)
+    const bool full = row0 + ROWS <= n;
+    float *ap = a_out + (row0 + 4 * g) * LH + col, *bp = b_out + (row0 + 4 * g) * LH + col;
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int lr = 16 * rb + 4 * g + q;
-            const int64_t row = row0 + lr;
-            if (row < n) {
+            if (full || row0 + lr < n) {
                 float za = aA[rb][q], zb = aB[rb][q];
                 if (F16X3) {
                     const float ir = pow2_inv(rs[lr]);
@@ -709,8 +712,8 @@ __device__ __forceinline__ void proj_phase(const BOps<F16X3, F16X3 ? 4 : 8> &bA,
                 node = node + w.dx * rowv[ROWS + lr] + w.dy * rowv[2 * ROWS + lr];
                 const float va = za + node + w.t * rowv[lr] + w.b;
                 const float vb = zb - node;
-                a_out[row * LH + col] = va;
-                b_out[row * LH + col] = vb;
+                ap[(16 * rb + q) * LH] = va;
+                bp[(16 * rb + q) * LH] = vb;
                 amx = fmaxf(amx, fabsf(va));
                 bmx = fmaxf(bmx, fabsf(vb));
             }
@@ -813,17 +816,18 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs p) {
         gemm_tile<F16X3, RB, S1>(acc, img, 128, 0, bU2, lane);
         // next layer's message_net_1 operands of a' (column tile wave)
         if (NEXT) bA.load(p.pkn + kPkW1, 4, wave, 0, w1r, 0, lane);
+        const bool full = row0 + ROWS <= p.n;
+        float *hp = p.h_out + (row0 + 4 * g) * LH + col;
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int lr = 16 * rb + 4 * g + q;
-                const int64_t row = row0 + lr;
                 float z = acc[rb][q];
                 if (F16X3) z = z * pow2_inv(rs[2][lr]) * u2_is;
                 const float x = hres[lr * NLD + col] + fmaxf(z + u2_b, 0.0f);
                 const float y = bn(x);
-                if (row < p.n) p.h_out[row * LH + col] = y;
+                if (full || row0 + lr < p.n) hp[(16 * rb + q) * LH] = y;
                 if (NEXT) stage[lr * NLD + col] = y;
             }
         }
@@ -912,14 +916,15 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_embed_kernel(EmbedArgs p) {
         for (int rb = 0; rb < RB; ++rb) acc[rb] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
         gemm_tile<false, RB, 8>(acc, img, 128, 0, b3, lane);
         bA.load(p.pk + kPkW1, 4, wave, 0, w1r, 0, lane);
+        const bool full = row0 + ROWS <= p.n;
+        float *hp = p.h_out + (row0 + 4 * g) * LH + col;
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int lr = 16 * rb + 4 * g + q;
-                const int64_t row = row0 + lr;
                 const float y = bn4(acc[rb][q] + h_b);
-                if (row < p.n) p.h_out[row * LH + col] = y;
+                if (full || row0 + lr < p.n) hp[(16 * rb + q) * LH] = y;
                 stage[lr * NLD + col] = y;
             }
         }

@@ -81,6 +81,7 @@ int main(int argc, char **argv) {
     printf("n=%lld parts=%d cus=%d (us per launch, median of 7)\n", (long long)n, parts, cus);
     NodeArgs nd{h, mean, n, u1, c1, 260, u2, c2, bnw, bnb, bnm, bnv, 1e-5f, ho[1], w1, b1, 260, ao[1], bo[1],
                 u, pos, sc, pack, pack + kLayerPack, amax + 2 * kAmaxShards, parts, n * H};
+    nd.div_k = 35;  // the wave edge kernel's buffers hold sums (production)
     NodeArgs nt = nd;
     nt.h_out = ho[0];
     nt.a_out = ao[0];
