@@ -16,12 +16,14 @@
 // registers; the slot's split VALU (relu(a + b) -> scaled fp16 hi / lo) and its
 // relu-sums are the MFMA-gap fillers of the same instruction stream.
 //
-// Work unit = (16-target tile, part): part p of `parts` covers slots
-// [p k / parts, (p + 1) k / parts) of the tile (parts > 1 balances the grid
-// when tiles per wave are few).  Each wave walks a contiguous, XCD-local range
-// of units as one slot stream.  Part q writes its slots' sum to out + q *
-// part_stride; launch_node_stage adds the parts in part order and divides by
-// the degree.  Deterministic: fixed summation order, no atomics.
+// Work split: the S = ntiles * k neighbour slots (slot = one neighbour of one
+// 16-target tile) form one stream; wave rank w (XCD-contiguous ranks) walks
+// slots [w S / G, (w + 1) S / G), so every wave gets the same work to one slot.
+// A unit is the wave's run of slots inside one tile.  The unit that starts at
+// its tile's first slot stores its sums to out; a wave that starts inside a
+// tile stores that first unit to side[w] (16 x 128), and the node stage adds
+// those side buffers in rank (= slot) order before dividing by the degree.
+// Deterministic: fixed summation order, no atomics.
 #include "common.hpp"
 #include "f16x3.hpp"
 #include "layer.hpp"
@@ -38,41 +40,38 @@ struct WaveArgs {
     const int32_t *nbr;
     const int32_t *deg;  // RAGGED: in-degree per target (nullable otherwise)
     int64_t n;
-    int k, ntiles, parts;
-    int64_t part_stride;
+    int k, ntiles;
+    int64_t S;                // slots = ntiles * k
     const float *b2;          // message_net_2.0 bias
     const char *pk;           // this layer's packed images (W2 at kPkW2)
     const uint32_t *amax_in;  // range slots of a, b
-    float *out;               // mean, or the partial sums
+    float *out;               // neighbour sums of the units that start a tile
+    float *side;              // [G][16][128]: the unit a wave starts inside a tile
 };
 
-// Contiguous unit range [u0, u0 + cnt) of wave-workgroup bid: blocks b and b + 8
-// share an XCD, which owns a contiguous share of the units (speed only).
-__device__ __forceinline__ void unit_range(int bid, int G, int nunits, int &u0, int &cnt) {
+// Rank of wave-workgroup bid: blocks b and b + 8 share an XCD; ranks number the
+// blocks XCD by XCD, so each XCD walks a contiguous share of the slots (speed only).
+__device__ __forceinline__ int wave_rank(int bid, int G) {
     const int x = bid & 7, i = bid >> 3;
     const int q = G >> 3, rem = G & 7;
-    const int nW = q + (x < rem ? 1 : 0);
-    const int cum = x * q + min(x, rem);
-    const int lo = (int)((int64_t)nunits * cum / G);
-    const int hi = (int)((int64_t)nunits * (cum + nW) / G);
-    const int len = hi - lo;
-    u0 = lo + (int)((int64_t)len * i / nW);
-    cnt = lo + (int)((int64_t)len * (i + 1) / nW) - u0;
+    return x * q + min(x, rem) + i;
 }
 
-// Position in the slot stream: unit u (relative to u0) and slot e of that
-// unit's range [e0, e1).
-template <int PARTS>
+// Position in the slot stream: tile, neighbour slot e < k, global slot index.
 struct SlotCtr {
-    int u, e, e1;
-    __device__ void start(int u0, int uu, int k) {
-        u = uu;
-        const int part = (u0 + uu) % PARTS;
-        e = part * k / PARTS;
-        e1 = (part + 1) * k / PARTS;
+    int tile, e;
+    int64_t pos;
+    __device__ void start(int64_t s, int k) {
+        pos = s;
+        tile = (int)(s / k);
+        e = (int)(s - (int64_t)tile * k);
     }
-    __device__ void next(int u0, int k) {
-        if (++e == e1) start(u0, u + 1, k);
+    __device__ void next(int k) {
+        ++pos;
+        if (++e == k) {
+            e = 0;
+            ++tile;
+        }
     }
 };
 
@@ -101,14 +100,16 @@ __device__ __forceinline__ half8 pin_agpr(half8 v) {
 // the relu-sums the compiler drops the MFMAs they would read), bit 5 replaces the relu-sums by empty register sinks
 // (MFMAs kept), bit 6 the unit stores likewise, bit 7 skips the a-row reload
 // at tile switches (wrong values).
-template <bool RAGGED, int PARTS, int DIAG = 0>
+template <bool RAGGED, int DIAG = 0>
 __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
     const int lane = threadIdx.x, r = lane & 15, g = lane >> 4;
     const int k = p.k;
     const int64_t nmax = p.n - 1;
-    int u0, nu;
-    unit_range(blockIdx.x, gridDim.x, p.ntiles * PARTS, u0, nu);
-    if (nu <= 0) return;
+    const int rank = wave_rank(blockIdx.x, gridDim.x);
+    const int64_t s0 = (int64_t)rank * p.S / gridDim.x, s1 = (int64_t)(rank + 1) * p.S / gridDim.x;
+    if (s0 >= s1) return;
+    // the first unit goes to side[rank] when the wave starts inside a tile
+    const int t_side = s0 % k ? (int)(s0 / k) : -1;
     // |a + b| <= max|a| + max|b|, scaled below 2^11 (split8_relu_rtz)
     const float sc = 0.125f * split_scale(amax_read(p.amax_in) + amax_read(p.amax_in + kAmaxShards));
     // message_net_2: B operands (AGPRs), accumulator start (bias, scaled), unscale
@@ -130,11 +131,11 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
     }
     // F16X3 operand piece i of this lane: k = 32 (i >> 1) + 8 g + 4 (i & 1) .. + 3
     auto piece = [&](int i) { return 32 * (i >> 1) + 8 * g + 4 * (i & 1); };
-    auto unit_tile = [&](const SlotCtr<PARTS> &c) { return min((u0 + c.u) / PARTS, p.ntiles - 1); };
+    auto unit_tile = [&](const SlotCtr &c) { return min(c.tile, p.ntiles - 1); };
     // every prefetch issues the same loads (clamped past the end)
-    auto src_of = [&](const SlotCtr<PARTS> &c) -> uint32_t {
+    auto src_of = [&](const SlotCtr &c) -> uint32_t {
         const int64_t row = min((int64_t)unit_tile(c) * ET + r, nmax);
-        return (uint32_t)p.nbr[row * k + min(c.e, k - 1)];
+        return (uint32_t)p.nbr[row * k + c.e];
     };
     auto gather = [&](float4 *dst, uint32_t src) {
         const float *br = p.b + (int64_t)min(src, (uint32_t)nmax) * LH;  // clamped: a malformed table must not fault
@@ -150,14 +151,13 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
     // and the relu-sums of slot q's column tiles trail its MFMAs by six groups
     // (tiles 6 and 7 finish in body q+1), so the VALU work of three slots is
     // spread across one slot's MFMA stream.
-    SlotCtr<PARTS> cC, cS, cG, cI;
-    cC.start(u0, 0, k);
+    SlotCtr cC, cS, cI;
+    cC.start(s0, k);
     cS = cC;
-    cS.next(u0, k);
-    cG = cS;
-    cG.next(u0, k);
-    cI = cG;
-    cI.next(u0, k);
+    cS.next(k);
+    cI = cS;
+    cI.next(k);
+    cI.next(k);
     float4 av[8];  // a rows of the split slot's tile (scaled), this lane's pieces
     auto load_a = [&](int tile) {
         const float *ar = p.a + min((int64_t)tile * ET + r, nmax) * LH;
@@ -167,7 +167,7 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) av[i] = make_float4(v[i].x * sc, v[i].y * sc, v[i].z * sc, v[i].w * sc);
     };
-    auto load_deg = [&](int *d, const SlotCtr<PARTS> &c) {
+    auto load_deg = [&](int *d, const SlotCtr &c) {
         const int64_t row0 = (int64_t)unit_tile(c) * ET;
 #pragma unroll
         for (int t = 0; t < 4; ++t) d[t] = p.deg[min(row0 + 4 * g + t, nmax)];
@@ -196,31 +196,38 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
 #pragma unroll
     for (int j = 0; j < 16; ++j) split_pair(j, bx, hA, lA);
     gather(bx, src_of(cS));
-    uint32_t i_next = src_of(cG);  // neighbour index of the slot gathered next
+    uint32_t i_next;  // neighbour index of the slot gathered next (slot 2)
+    {
+        SlotCtr c2 = cS;
+        c2.next(k);
+        i_next = src_of(c2);
+    }
 #pragma unroll
     for (int c = 0; c < 8; ++c) S[c] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
     // column tiles 6, 7 of the previous slot, summed at the start of the next
     // body (before the first slot: relu(-big) = 0 adds nothing)
     f32x4 acc6 = (f32x4){-3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f}, acc7 = acc6;
-    int e_prev = 0, row0_prev = 0, part_prev = 0;
+    int e_prev = 0, row0_prev = 0;
+    bool side_prev = false;
     bool close_prev = false;  // the previous slot was its unit's last: write after its deferred sums
     auto relu_add = [&](f32x4 &Sc, float x, int t, int e, const int *d) {
         float v = __builtin_amdgcn_fmed3f(x, 0.0f, 3.402823466e38f);  // relu
         if (RAGGED) v = e < d[t] ? v : 0.0f;
         Sc[t] += v;
     };
-    // the finished unit's sums, unscaled (a power-of-two multiply: exact).  The
-    // node stage adds the parts and divides by the degree (PyG mean = sum / count).
-    // Stores are unconditional unless the tile runs past n (wave-uniform test),
-    // at immediate offsets from one base per lane.
-    auto write_unit = [&](int64_t row0, int part) {
+    // the finished unit's sums, unscaled (a power-of-two multiply: exact), to out
+    // (rows of the tile) or to side[rank].  The node stage adds the side buffers
+    // and divides by the degree (PyG mean = sum / count).  Stores are
+    // unconditional unless the tile runs past n (wave-uniform test), at
+    // immediate offsets from one base per lane.
+    auto write_unit = [&](int64_t row0, bool to_side) {
         if (DIAG & 64) {  // no stores: keep the sums alive only
 #pragma unroll
             for (int c = 0; c < 8; ++c) asm volatile("" ::"v"(S[c]));
             return;
         }
-        float *o = p.out + part * p.part_stride + (row0 + 4 * g) * LH + r;
-        if (row0 + ET <= p.n) {
+        float *o = (to_side ? p.side + (int64_t)rank * ET * LH : p.out + row0 * LH) + 4 * g * LH + r;
+        if (to_side || row0 + ET <= p.n) {
 #pragma unroll
             for (int c = 0; c < 8; ++c)
 #pragma unroll
@@ -236,9 +243,8 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
     auto body = [&](float4 *X, uint32_t (*h)[4], uint32_t (*l)[4], uint32_t (*nh)[4], uint32_t (*nl)[4]) {
         // memory: index of slot q+3 now, b rows of slot q+2 piece by piece below
         const uint32_t i_after = src_of(cI);
-        cI.next(u0, k);
+        cI.next(k);
         const float *brow = p.b + (int64_t)min(i_next, (uint32_t)nmax) * LH;  // clamped: a malformed table must not fault
-        cG.next(u0, k);
         i_next = i_after;
         const int e = cC.e;
         {   // a rows of the split slot's tile
@@ -295,7 +301,7 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 if (G == 5 && close_prev) {  // the previous unit is complete: write, restart
-                    write_unit(row0_prev, part_prev);
+                    write_unit(row0_prev, side_prev);
 #pragma unroll
                     for (int c2 = 0; c2 < 8; ++c2) S[c2] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
                 }
@@ -304,15 +310,15 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
         acc6 = acc[6];
         acc7 = acc[7];
         e_prev = e;
-        close_prev = cC.e + 1 == cC.e1;
+        close_prev = cC.e + 1 == k || cC.pos + 1 == s1;
         row0_prev = unit_tile(cC) * ET;
-        part_prev = (u0 + cC.u) % PARTS;
+        side_prev = cC.tile == t_side;
         if (RAGGED) {
 #pragma unroll
             for (int t = 0; t < 4; ++t) dg_prev[t] = dg[t];
         }
-        cC.next(u0, k);
-        cS.next(u0, k);
+        cC.next(k);
+        cS.next(k);
         if (RAGGED && close_prev) load_deg(dg, cC);
     };
     // (the S reset of a unit's first slot happens at group 5 of its body, after
@@ -320,93 +326,69 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
     // at group 6.  The first slot starts from S = 0.)
     for (;;) {
         body(bx, hA, lA, hB, lB);
-        if (cC.u >= nu) break;
+        if (cC.pos >= s1) break;
         body(bx, hB, lB, hA, lA);
-        if (cC.u >= nu) break;
+        if (cC.pos >= s1) break;
     }
     // the last slot's deferred sums, then its unit (always the last slot of one)
 #pragma unroll
     for (int t = 2; t < 4; ++t) relu_add(S[6], acc6[t], t, e_prev, dg_prev);
 #pragma unroll
     for (int t = 0; t < 4; ++t) relu_add(S[7], acc7[t], t, e_prev, dg_prev);
-    write_unit(row0_prev, part_prev);
+    write_unit(row0_prev, side_prev);
 }
 
 }  // namespace
 
-// Parts per tile: the smallest count (<= max_parts, <= k) whose grid keeps the
-// busiest wave within 3 % of the mean work per wave (4 waves per CU), else the
-// best balanced one.  Extra parts cost one more partial buffer in the node stage.
-int edge_wave_parts(int64_t ntiles, int cus, int max_parts, int k) {
-    const double waves = 4.0 * cus;
-    int best = 1;
-    double best_eff = 0.0;
-    for (int q = 1; q <= max_parts && q <= k && q <= 4; ++q) {
-        const double units = (double)ntiles * q;
-        const double per = units / waves;
-        const double eff = units <= waves ? units / waves : per / std::ceil(per);
-        if (eff >= 0.97) return q;
-        if (eff > best_eff + 1e-9) {
-            best_eff = eff;
-            best = q;
-        }
-    }
-    return best;
+// Waves of the slot-range split: one per SIMD, at most one per slot, at most
+// side_cap (the side buffer's capacity in 16 x 128 blocks).
+int edge_wave_grid(int64_t S, int cus, int64_t side_cap) {
+    int64_t g = 4 * (int64_t)cus;
+    if (g > S) g = S;
+    if (g > side_cap) g = side_cap;
+    return (int)(g < 1 ? 1 : g);
 }
 
-// Profiling aid (tools/ubench): the non-ragged parts = 2 kernel with DIAG bits.
+// Profiling aid (tools/ubench): the non-ragged kernel with DIAG bits, one wave
+// per SIMD; side = a [4 cus][16][128] buffer.
 int launch_edge_wave_diag(const float *a, const float *b, const int32_t *nbr, int64_t n, int k,
                           const float *msg2_b, const char *pk, const uint32_t *amax_in, float *out,
-                          int cus, int diag, hipStream_t st) {
-    const int64_t ntiles = (n + ET - 1) / ET;
-    WaveArgs w{a, b, nbr, nullptr, n, k, (int)ntiles, 2, n * LH, msg2_b, pk, amax_in, out};
-    const int64_t units = ntiles * 2, waves = 4 * (int64_t)cus;
-    const int grid = (int)(units < waves ? units : waves);
+                          float *side, int cus, int diag, hipStream_t st) {
+    const int64_t ntiles = (n + ET - 1) / ET, S = ntiles * k;
+    WaveArgs w{a, b, nbr, nullptr, n, k, (int)ntiles, S, msg2_b, pk, amax_in, out, side};
+    const int grid = edge_wave_grid(S, cus, 4 * (int64_t)cus);
+#define MMPDE_DIAG(D) \
+    case D: hipLaunchKernelGGL((gnn_edge_wave_kernel<false, D>), dim3(grid), dim3(64), 0, st, w); break
     switch (diag) {
-    case 1: hipLaunchKernelGGL((gnn_edge_wave_kernel<false, 2, 1>), dim3(grid), dim3(64), 0, st, w); break;
-    case 2: hipLaunchKernelGGL((gnn_edge_wave_kernel<false, 2, 2>), dim3(grid), dim3(64), 0, st, w); break;
-    case 3: hipLaunchKernelGGL((gnn_edge_wave_kernel<false, 2, 3>), dim3(grid), dim3(64), 0, st, w); break;
-    case 4: hipLaunchKernelGGL((gnn_edge_wave_kernel<false, 2, 4>), dim3(grid), dim3(64), 0, st, w); break;
-    case 7: hipLaunchKernelGGL((gnn_edge_wave_kernel<false, 2, 7>), dim3(grid), dim3(64), 0, st, w); break;
-    case 33: hipLaunchKernelGGL((gnn_edge_wave_kernel<false, 2, 33>), dim3(grid), dim3(64), 0, st, w); break;
-    case 97: hipLaunchKernelGGL((gnn_edge_wave_kernel<false, 2, 97>), dim3(grid), dim3(64), 0, st, w); break;
-    case 32: hipLaunchKernelGGL((gnn_edge_wave_kernel<false, 2, 32>), dim3(grid), dim3(64), 0, st, w); break;
-    case 64: hipLaunchKernelGGL((gnn_edge_wave_kernel<false, 2, 64>), dim3(grid), dim3(64), 0, st, w); break;
-    case 128: hipLaunchKernelGGL((gnn_edge_wave_kernel<false, 2, 128>), dim3(grid), dim3(64), 0, st, w); break;
-    case 36: hipLaunchKernelGGL((gnn_edge_wave_kernel<false, 2, 36>), dim3(grid), dim3(64), 0, st, w); break;
-    default: hipLaunchKernelGGL((gnn_edge_wave_kernel<false, 2, 0>), dim3(grid), dim3(64), 0, st, w); break;
+        MMPDE_DIAG(1);
+        MMPDE_DIAG(2);
+        MMPDE_DIAG(3);
+        MMPDE_DIAG(4);
+        MMPDE_DIAG(7);
+        MMPDE_DIAG(32);
+        MMPDE_DIAG(33);
+        MMPDE_DIAG(36);
+        MMPDE_DIAG(64);
+        MMPDE_DIAG(97);
+        MMPDE_DIAG(128);
+    default: hipLaunchKernelGGL((gnn_edge_wave_kernel<false, 0>), dim3(grid), dim3(64), 0, st, w); break;
     }
+#undef MMPDE_DIAG
     MMPDE_RET_LAUNCH();
     return MMPDE_OK;
 }
 
 int launch_edge_wave(const float *a, const float *b, const int32_t *nbr, const int32_t *deg, int64_t n,
                      int k, const float *msg2_b, const char *pk, const uint32_t *amax_in, float *out,
-                     int parts, int64_t part_stride, int cus, hipStream_t st) {
-    MMPDE_REQUIRE(a && b && nbr && msg2_b && pk && amax_in && out && n > 0 && k > 0);
-    MMPDE_REQUIRE(parts >= 1 && parts <= 4 && parts <= k);
-    MMPDE_REQUIRE(parts == 1 || part_stride >= n * LH);
-    const int64_t ntiles = (n + ET - 1) / ET;
-    MMPDE_REQUIRE(ntiles * parts < (int64_t)INT32_MAX && n * (int64_t)k < ((int64_t)1 << 40));
-    WaveArgs w{a, b, nbr, deg, n, k, (int)ntiles, parts, part_stride, msg2_b, pk, amax_in, out};
-    const int64_t waves = 4 * (int64_t)cus;   // one 64-thread workgroup per SIMD
-    const int64_t units = ntiles * parts;
-    const int grid = (int)(units < waves ? units : waves);
-#define MMPDE_WAVE(RG, P) hipLaunchKernelGGL((gnn_edge_wave_kernel<RG, P>), dim3(grid), dim3(64), 0, st, w)
-#define MMPDE_WAVE_P(RG)              \
-    switch (parts) {                  \
-    case 1: MMPDE_WAVE(RG, 1); break; \
-    case 2: MMPDE_WAVE(RG, 2); break; \
-    case 3: MMPDE_WAVE(RG, 3); break; \
-    default: MMPDE_WAVE(RG, 4); break; \
-    }
-    if (deg) {
-        MMPDE_WAVE_P(true);
-    } else {
-        MMPDE_WAVE_P(false);
-    }
-#undef MMPDE_WAVE_P
-#undef MMPDE_WAVE
+                     float *side, int64_t side_cap, int cus, EdgeSplit *split, hipStream_t st) {
+    MMPDE_REQUIRE(a && b && nbr && msg2_b && pk && amax_in && out && side && split && n > 0 && k > 0);
+    const int64_t ntiles = (n + ET - 1) / ET, S = ntiles * k;
+    MMPDE_REQUIRE(ntiles < (int64_t)INT32_MAX && S < ((int64_t)1 << 40) && side_cap >= 1);
+    const int grid = edge_wave_grid(S, cus, side_cap);
+    WaveArgs w{a, b, nbr, deg, n, k, (int)ntiles, S, msg2_b, pk, amax_in, out, side};
+    *split = EdgeSplit{side, S, grid, k};
+    if (deg) hipLaunchKernelGGL((gnn_edge_wave_kernel<true>), dim3(grid), dim3(64), 0, st, w);
+    else hipLaunchKernelGGL((gnn_edge_wave_kernel<false>), dim3(grid), dim3(64), 0, st, w);
     MMPDE_RET_LAUNCH();
     return MMPDE_OK;
 }

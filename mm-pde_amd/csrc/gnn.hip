@@ -389,7 +389,7 @@ extern "C" int mmpde_gnn_edge_mean_deg(const float *a, const float *b, const int
     p.msg2_w = msg2_w;
     p.msg2_b = msg2_b;
     // exact fp32 ring kernel (no pack): the training forward of gnn_2d.py:53-63
-    return launch_edge_stage(a, b, nbr, deg, n, k, &p, nullptr, nullptr, mean_out, n * H, 1, nullptr,
+    return launch_edge_stage(a, b, nbr, deg, n, k, &p, nullptr, nullptr, mean_out, nullptr, 0, nullptr,
                              as_stream(stream));
 }
 
@@ -544,16 +544,16 @@ extern "C" int mmpde_gnn_forward_ex(const float *u, const float *pos, int64_t n,
         const uint32_t *ain = pack ? amax + 2 * kAmaxShards * l : nullptr;
         uint32_t *aout = pack && next ? amax + 2 * kAmaxShards * (l + 1) : nullptr;
         if (eb && hipEventRecord(eb, st) != hipSuccess) return MMPDE_ERR_INVALID_ARG;
-        int parts = 1;
-        bool sums = false;
+        EdgeSplit split;
         const int32_t *deg = exec ? exec->degree : nullptr;
-        rc = launch_edge_stage(wa, wb, nbr, deg, n, k, &layers[l], pk, ain, wmean, n * H, kGnnBufs - 4,
-                               &parts, st, &sums);
+        // side blocks of the wave edge kernel: the workspace after the mean
+        rc = launch_edge_stage(wa, wb, nbr, deg, n, k, &layers[l], pk, ain, wmean, wmean + n * H,
+                               (kGnnBufs - 5) * n * H / (16 * H), &split, st);
         if (rc) return rc;
         if (ee && hipEventRecord(ee, st) != hipSuccess) return MMPDE_ERR_INVALID_ARG;
         // a, b are rewritten in place: this layer's edge stage has consumed them
-        rc = launch_node_stage(hb[cur], wmean, parts, n * H, u, pos, n, sc, &layers[l], next, pk, pkn, aout,
-                               hb[cur ^ 1], wa, wb, st, sums ? deg : nullptr, sums ? k : 0);
+        rc = launch_node_stage(hb[cur], wmean, &split, deg, u, pos, n, sc, &layers[l], next, pk, pkn, aout,
+                               hb[cur ^ 1], wa, wb, st);
         if (rc) return rc;
         if (ne && hipEventRecord(ne, st) != hipSuccess) return MMPDE_ERR_INVALID_ARG;
         cur ^= 1;

@@ -514,6 +514,7 @@ struct NodeArgs {
     // mean is their total / max(div_deg[row], 1), or / div_k without degrees
     const int32_t *div_deg = nullptr;
     int div_k = 0;
+    EdgeSplit split;       // G > 0: add the wave kernel's side blocks first
 };
 
 constexpr int NLD = 132;  // fp32 staging row stride (floats)
@@ -537,7 +538,7 @@ __device__ __forceinline__ void prep(const float *src, int64_t lds, int64_t row0
                                      bool global, float4 *img, int KT, int kofs, float *rs,
                                      float *copy = nullptr, int t0 = -1, int nthr = 512, int nsum = 1,
                                      int64_t sum_stride = 0, const int32_t *div_deg = nullptr,
-                                     int div_k = 0) {
+                                     int div_k = 0, const EdgeSplit *split = nullptr) {
     // threads t0 .. t0 + nthr (default: the whole workgroup) share the rows
     for (int idx = t0 < 0 ? (int)threadIdx.x : (int)threadIdx.x - t0; idx < ROWS * 8; idx += nthr) {
         // a wave takes 8 rows x 8 parts, lane = 8 part + row: the 8 lanes of one
@@ -553,6 +554,21 @@ __device__ __forceinline__ void prep(const float *src, int64_t lds, int64_t row0
             for (int q = 0; q < 4; ++q) {
                 const float4 y = *(const float4 *)(sp + ps * sum_stride + 4 * q);
                 x[q] = make_float4(x[q].x + y.x, x[q].y + y.y, x[q].z + y.z, x[q].w + y.w);
+            }
+        }
+        if (split && split->G > 0) {
+            // side blocks of the waves whose first slot s0(w) = floor(w S / G) lies
+            // strictly inside this row's 16-row tile t: t k < s0(w) < (t + 1) k
+            const int64_t t = srow / 16, S = split->S, G = split->G, kk = split->k;
+            const int64_t lo = max(((t * kk + 1) * G + S - 1) / S, (int64_t)1);
+            const int64_t hi = min(((t + 1) * kk * G + S - 1) / S - 1, G - 1);
+            for (int64_t w = lo; w <= hi; ++w) {
+                const float *q4 = split->side + (w * 16 + (srow & 15)) * 128 + 16 * part;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4 y = *(const float4 *)(q4 + 4 * q);
+                    x[q] = make_float4(x[q].x + y.x, x[q].y + y.y, x[q].z + y.z, x[q].w + y.w);
+                }
             }
         }
         if (div_k > 0) {
@@ -775,11 +791,11 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs p) {
     if constexpr (ROWS * 8 <= 256) {  // h on waves 0-3, mean on waves 4-7 at once
         if (tid < 256) prep<F16X3, ROWS>(p.h, LH, row0, p.n, true, img, 256, 0, rs[0], hres, 0, 256);
         else prep<F16X3, ROWS>(p.mean, LH, row0, p.n, true, img, 256, 128, rs[1], nullptr, 256, 256, p.parts,
-                               p.part_stride, p.div_deg, p.div_k);
+                               p.part_stride, p.div_deg, p.div_k, &p.split);
     } else {
         prep<F16X3, ROWS>(p.h, LH, row0, p.n, true, img, 256, 0, rs[0], hres);
         prep<F16X3, ROWS>(p.mean, LH, row0, p.n, true, img, 256, 128, rs[1], nullptr, -1, 512, p.parts,
-                          p.part_stride, p.div_deg, p.div_k);
+                          p.part_stride, p.div_deg, p.div_k, &p.split);
     }
     __syncthreads();
 
@@ -955,10 +971,9 @@ int device_cus() {
 
 int launch_edge_stage(const float *a, const float *b, const int32_t *nbr, const int32_t *deg,
                       int64_t n, int k, const mmpde_gnn_layer_params *p, const char *pk,
-                      const uint32_t *amax_in, float *mean, int64_t part_stride, int max_parts,
-                      int *parts_used, hipStream_t st, bool *sums) {
-    if (parts_used) *parts_used = 1;
-    if (sums) *sums = false;
+                      const uint32_t *amax_in, float *mean, float *side, int64_t side_cap,
+                      EdgeSplit *split, hipStream_t st) {
+    if (split) *split = EdgeSplit{};
     MMPDE_REQUIRE(a && b && nbr && p && mean && n > 0 && k > 0 && n <= (int64_t)INT32_MAX);
     MMPDE_REQUIRE(al16(a) && al16(b) && al16(p->msg2_w) && al16(mean));
     MMPDE_REQUIRE(!pk || (amax_in && al16(pk)));
@@ -969,12 +984,9 @@ int launch_edge_stage(const float *a, const float *b, const int32_t *nbr, const 
 #ifndef MMPDE_EDGE_RING
     // F16X3: one wave per SIMD with the operands in registers (edge_wave.hip)
     if (pk) {
-        // the wave kernel leaves the division to the node stage
-        MMPDE_REQUIRE(sums);
-        *sums = true;
-        const int parts = edge_wave_parts(ntiles, cus, max_parts, k);
-        if (parts_used) *parts_used = parts;
-        return launch_edge_wave(a, b, nbr, deg, n, k, p->msg2_b, pk, amax_in, mean, parts, part_stride, cus, st);
+        // the wave kernel leaves the side blocks and the division to the node stage
+        return launch_edge_wave(a, b, nbr, deg, n, k, p->msg2_b, pk, amax_in, mean, side, side_cap, cus,
+                                split, st);
     }
 #endif
     const int grid = ntiles < cus ? (int)ntiles : cus;
@@ -990,19 +1002,21 @@ int launch_edge_stage(const float *a, const float *b, const int32_t *nbr, const 
     return MMPDE_OK;
 }
 
-int launch_node_stage(const float *h, const float *mean, int parts, int64_t part_stride,
+int launch_node_stage(const float *h, const float *mean, const EdgeSplit *split, const int32_t *deg,
                       const float *u, const float *pos, int64_t n, mmpde_gnn_scales sc,
                       const mmpde_gnn_layer_params *p, const mmpde_gnn_layer_params *next,
                       const char *pk, const char *pkn, uint32_t *amax_out, float *h_out, float *a_out,
-                      float *b_out, hipStream_t st, const int32_t *div_deg, int div_k) {
-    MMPDE_REQUIRE(parts >= 1 && parts <= 4 && (parts == 1 || part_stride >= n * LH) && div_k >= 0);
+                      float *b_out, hipStream_t st) {
+    const bool sums = split && split->G > 0;
+    MMPDE_REQUIRE(!sums || (split->side && split->S > 0 && split->k > 0));
     MMPDE_REQUIRE(h && mean && u && pos && p && h_out && n > 0);
     MMPDE_REQUIRE(al16(h) && al16(mean) && al16(h_out));
     MMPDE_REQUIRE(p->upd1_ld >= 257 && (p->upd1_ld & 3) == 0 && al16(p->upd1_w) && al16(p->upd2_w));
     MMPDE_REQUIRE(!pk || (al16(pk) && (!next || pkn)));
     NodeArgs a{h, mean, n, p->upd1_w, p->upd1_b, p->upd1_ld, p->upd2_w, p->upd2_b, p->bn_w, p->bn_b,
                p->bn_rm, p->bn_rv, p->eps, h_out, nullptr, nullptr, 0, a_out, b_out, u, pos, sc,
-               pk, pkn, amax_out, parts, part_stride, div_deg, div_k};
+               pk, pkn, amax_out, 1, 0, sums ? deg : nullptr, sums ? split->k : 0};
+    if (sums) a.split = *split;
     if (next) {
         MMPDE_REQUIRE(a_out && b_out && next->msg1_ld >= 260 && (next->msg1_ld & 3) == 0 &&
                       al16(next->msg1_w));

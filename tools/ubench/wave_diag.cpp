@@ -19,7 +19,7 @@
 
 int launch_edge_wave_diag(const float *a, const float *b, const int32_t *nbr, int64_t n, int k,
                           const float *msg2_b, const char *pk, const uint32_t *amax_in, float *out,
-                          int cus, int diag, hipStream_t st);
+                          float *side, int cus, int diag, hipStream_t st);
 
 #define CK(x)                                                                          \
     do {                                                                               \
@@ -103,11 +103,12 @@ int main(int argc, char **argv) {
         std::vector<uint32_t> hs(2 * kAmaxShards, 0x3f800000u);
         CK(hipMemcpy(amax, hs.data(), hs.size() * 4, hipMemcpyHostToDevice));
     }
-    float *out;
+    float *out, *side;
     CK(hipMalloc(&out, 2 * n * H * 4));
     int dev = 0, cus = 256;
     hipGetDevice(&dev);
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    CK(hipMalloc(&side, (size_t)4 * cus * 16 * H * 4));
     const int64_t ntiles = (n + 15) / 16;
     const double mfmas = (double)ntiles * k * 96;
     printf("n=%lld k=%d cus=%d  MFMAs per launch %.3e (%.0f per SIMD)\n", (long long)n, k, cus, mfmas,
@@ -128,20 +129,23 @@ int main(int argc, char **argv) {
     const int iters = (int)(mfmas / (4.0 * cus) / 24.0 + 0.5);
     for (int r = 0; r < reps; ++r) {
         for (int v = 0; v < nv; ++v)
-            t[v].push_back(time_it([&] { launch_edge_wave_diag(a, b, nbr, n, k, b2, pack, amax, out, cus, vs[v].diag, 0); }, it));
+            t[v].push_back(time_it([&] { launch_edge_wave_diag(a, b, nbr, n, k, b2, pack, amax, out, side, cus, vs[v].diag, 0); }, it));
         t[nv].push_back(time_it([&] { hipLaunchKernelGGL(mfma_only_wave, dim3(4 * cus), dim3(64), 0, 0, seed, iters, mo); }, it));
     }
     CK(hipGetLastError());
     {   // production and the placement variant against fp64 sums on sampled rows
-        std::vector<float> ha(n * H), hb(n * H), hw(128 * 128), hbias(128), m(2 * n * H);
+        std::vector<float> ha(n * H), hb(n * H), hw(128 * 128), hbias(128), m(2 * n * H), sd(4 * cus * 16 * H);
         CK(hipMemcpy(ha.data(), a, ha.size() * 4, hipMemcpyDeviceToHost));
         CK(hipMemcpy(hb.data(), b, hb.size() * 4, hipMemcpyDeviceToHost));
         CK(hipMemcpy(hw.data(), w2, hw.size() * 4, hipMemcpyDeviceToHost));
         CK(hipMemcpy(hbias.data(), b2, hbias.size() * 4, hipMemcpyDeviceToHost));
         for (int d : {0}) {
             CK(hipMemset(out, 0, 2 * n * H * 4));
-            launch_edge_wave_diag(a, b, nbr, n, k, b2, pack, amax, out, cus, d, 0);
+            launch_edge_wave_diag(a, b, nbr, n, k, b2, pack, amax, out, side, cus, d, 0);
             CK(hipMemcpy(m.data(), out, m.size() * 4, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(sd.data(), side, sd.size() * 4, hipMemcpyDeviceToHost));
+            // the node stage's combine: side blocks of the waves starting inside the tile
+            const int64_t S = ((n + 15) / 16) * k, G = std::min<int64_t>(4 * cus, S);
             double worst = 0;
             for (int64_t i = 0; i < n; i += 997) {
                 for (int o = 0; o < H; ++o) {
@@ -156,7 +160,11 @@ int main(int argc, char **argv) {
                         ref += y > 0 ? y : 0;
                         mx = std::max(mx, std::fabs(y));
                     }
-                    const double got = (double)m[i * H + o] + (double)m[n * H + i * H + o];
+                    double got = (double)m[i * H + o];
+                    const int64_t t = i / 16;
+                    const int64_t lo = std::max<int64_t>(((t * k + 1) * G + S - 1) / S, 1);
+                    const int64_t hi = std::min<int64_t>(((t + 1) * k * G + S - 1) / S - 1, G - 1);
+                    for (int64_t w = lo; w <= hi; ++w) got += sd[(w * 16 + (i & 15)) * H + o];
                     worst = std::max(worst, std::fabs(got - ref) / (k * mx));
                 }
             }
@@ -165,12 +173,12 @@ int main(int argc, char **argv) {
     }
     {   // the schedule variants must reproduce the production sums bit for bit
         std::vector<float> m0(2 * n * H), m1(2 * n * H);
-        launch_edge_wave_diag(a, b, nbr, n, k, b2, pack, amax, out, cus, 0, 0);
+        launch_edge_wave_diag(a, b, nbr, n, k, b2, pack, amax, out, side, cus, 0, 0);
         CK(hipMemcpy(m0.data(), out, m0.size() * 4, hipMemcpyDeviceToHost));
         for (int v = 0; v < nv; ++v) {
             if (vs[v].diag != 16) continue;
             CK(hipMemset(out, 0, m1.size() * 4));
-            launch_edge_wave_diag(a, b, nbr, n, k, b2, pack, amax, out, cus, vs[v].diag, 0);
+            launch_edge_wave_diag(a, b, nbr, n, k, b2, pack, amax, out, side, cus, vs[v].diag, 0);
             CK(hipMemcpy(m1.data(), out, m1.size() * 4, hipMemcpyDeviceToHost));
             size_t bad = 0;
             for (size_t i = 0; i < m0.size(); ++i) bad += memcmp(&m0[i], &m1[i], 4) != 0;
