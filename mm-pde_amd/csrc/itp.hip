@@ -5,43 +5,50 @@
 //   X[q]  = [n0x, n0y, ..., n29x, n29y, qx, qy]                   (62)
 //   W[q]  = L2(tanh(L1(tanh(L0(X[q])))))                         (62 -> 128 -> 64 -> 30)
 //   out   = sum_e W[q, e] * vals[b, idx[q, e]]  (+ addend)
-// One wave owns 32 queries and runs the three layers transposed (features on
-// accumulator rows, queries on lanes) with v_mfma_f32_32x32x2_f32, so each
-// layer's accumulator is directly the next layer's B operand -- no LDS or lane
-// shuffles between layers.  The weights are re-laid once (mmpde_itp_pack) into
-// the exact per-lane A-operand image; L0 and L1 images (64 KB) are staged in
-// LDS per workgroup, the L2 image (8 KB) and biases are read from L2.
+// One wave owns 16 queries and runs the three layers transposed (features on
+// accumulator rows, queries on lanes) with exact-fp32 v_mfma_f32_16x16x4_f32.
+// Lane (g, q) = (l >> 4, l & 15) holds rows 4 g + i (i < 4) of each 16-row
+// accumulator tile, which is exactly the B operand of the next layer's K step
+// (tile t, i) when that layer's K order is permuted to k = 16 t + 4 g + i: the
+// weight images are packed in that order (mmpde_itp_pack), so no LDS or lane
+// shuffles between layers.  16 queries per wave (not 32) halve each wave's
+// serial MFMA chain.  Grid: two 512-thread workgroups per CU, all resident (the
+// L0 and L1 images, 64 KB, are staged in LDS per workgroup; the L2 image, 8 KB,
+// and the biases are read from L2); query tile t runs on workgroup t mod G, so
+// every CU gets the same number of tiles (a 256-thread grid of one tile per wave
+// ran the tail workgroups in a second round: 38 us at cy B=16).
 #include "common.hpp"
 
 namespace {
 
 constexpr int kNb = 30;                     // ItpNet.n (interpolate.py:8)
-constexpr int kImg0 = 4 * 32 * 64;          // [rt][s][lane]
-constexpr int kImg1 = 2 * 64 * 64;          // [gt][ks][lane]
-constexpr int kImg2 = 32 * 64;              // [ks][lane]
+constexpr int kImg0 = 8 * 16 * 64;          // [rt 16-feature tile][s K step][lane]
+constexpr int kImg1 = 4 * 32 * 64;          // [rt][t * 4 + i][lane]
+constexpr int kImg2 = 2 * 16 * 64;          // [rt][t * 4 + i][lane]
 constexpr int kBias = 128 + 64 + 32;
 constexpr int kPackFloats = kImg0 + kImg1 + kImg2 + kBias;
 
+// lane l of a 16x16x4 A operand: row l & 15, k-index l >> 4 of the K step.
+// Layer 0's K order is the input order (62 padded to 64); layers 1 and 2 take
+// step (t, i) as inputs 16 t + 4 g + i, g = k-index.
 __global__ void itp_pack_kernel(mmpde_itp_mlp m, float *__restrict__ pk) {
     const int e = blockIdx.x * 256 + threadIdx.x;
     if (e >= kPackFloats) return;
     float v = 0.0f;
     if (e < kImg0) {
-        const int lane = e & 63, s = (e >> 6) & 31, rt = e >> 11;
-        const int in = 2 * s + (lane >> 5);
-        if (in < 62) v = m.w0[(32 * rt + (lane & 31)) * 62 + in];
+        const int lane = e & 63, s = (e >> 6) & 15, rt = e >> 10;
+        const int in = 4 * s + (lane >> 4);
+        if (in < 62) v = m.w0[(16 * rt + (lane & 15)) * 62 + in];
     } else if (e < kImg0 + kImg1) {
         const int f = e - kImg0;
-        const int lane = f & 63, ks = (f >> 6) & 63, gt = f >> 12;
-        const int rt = ks >> 4, p = ks & 15;
-        const int feat = 32 * rt + acc_row(p, lane);
-        v = m.w1[(32 * gt + (lane & 31)) * 128 + feat];
+        const int lane = f & 63, ks = (f >> 6) & 31, rt = f >> 11;
+        const int feat = 16 * (ks >> 2) + 4 * (lane >> 4) + (ks & 3);
+        v = m.w1[(16 * rt + (lane & 15)) * 128 + feat];
     } else if (e < kImg0 + kImg1 + kImg2) {
         const int f = e - kImg0 - kImg1;
-        const int lane = f & 63, ks = f >> 6;
-        const int gt = ks >> 4, p = ks & 15;
-        const int feat = 32 * gt + acc_row(p, lane);
-        const int o = lane & 31;
+        const int lane = f & 63, ks = (f >> 6) & 15, rt = f >> 10;
+        const int feat = 16 * (ks >> 2) + 4 * (lane >> 4) + (ks & 3);
+        const int o = 16 * rt + (lane & 15);
         if (o < kNb) v = m.w2[o * 64 + feat];
     } else {
         const int f = e - kImg0 - kImg1 - kImg2;
@@ -52,14 +59,16 @@ __global__ void itp_pack_kernel(mmpde_itp_mlp m, float *__restrict__ pk) {
     pk[e] = v;
 }
 
-__global__ __launch_bounds__(256, 2) void itp_interp_kernel(
+constexpr int kItpThreads = 512;
+
+__global__ __launch_bounds__(kItpThreads, 4) void itp_interp_kernel(
     const float *__restrict__ src, const float *__restrict__ vals, const float *__restrict__ qry,
     const int32_t *__restrict__ idx, int64_t batches, int64_t n_src, int64_t n_qry,
     const float *__restrict__ pk, const float *__restrict__ addend, float *__restrict__ out) {
     __shared__ float4 img[(kImg0 + kImg1) / 4];  // 64 KB
     {
-        const float4 *g = (const float4 *)pk;
-        for (int e = threadIdx.x; e < (kImg0 + kImg1) / 4; e += 256) img[e] = g[e];
+        const float4 *gsrc = (const float4 *)pk;
+        for (int e = threadIdx.x; e < (kImg0 + kImg1) / 4; e += kItpThreads) img[e] = gsrc[e];
     }
     __syncthreads();
     const float *img0 = (const float *)img;
@@ -69,79 +78,88 @@ __global__ __launch_bounds__(256, 2) void itp_interp_kernel(
 
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
-    const int half = lane >> 5;
-    const int64_t tiles_per_b = (n_qry + 31) / 32;
+    const int g = lane >> 4;
+    const int64_t tiles_per_b = (n_qry + 15) / 16;
     const int64_t n_tiles = tiles_per_b * batches;
 
-    for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile < n_tiles;
-         tile += (int64_t)gridDim.x * 4) {
+    // waves w and w + 4 share a SIMD: odd workgroups start on the other SIMD pair
+    const int slot = (blockIdx.x & 1) ? (wave + 2) & 7 : wave;
+    for (int64_t tile = (int64_t)slot * gridDim.x + blockIdx.x; tile < n_tiles;
+         tile += (int64_t)gridDim.x * (kItpThreads / 64)) {
         const int64_t b = tile / tiles_per_b;
-        const int64_t q0 = (tile - b * tiles_per_b) * 32;
-        int64_t q = q0 + (lane & 31);
+        const int64_t q0 = (tile - b * tiles_per_b) * 16;
+        int64_t q = q0 + (lane & 15);
         const bool valid = q < n_qry;
         if (!valid) q = n_qry - 1;
         const int64_t qrow = b * n_qry + q;
         const int32_t *ir = idx + qrow * kNb;
         const float2 *sp = (const float2 *)src + b * n_src;
 
-        // layer-0 B operand: coordinate `half` of point s (neighbours 0..29, query, 0)
-        float xin[32];
+        // layer-0 B operand of K step s: input 4 s + g (neighbour 2 s + g / 2,
+        // coordinate g & 1; step 15: the query's coordinates, then 0)
+        float xin[16];
 #pragma unroll
-        for (int s = 0; s < kNb; ++s) {
-            const float2 p = sp[min((uint32_t)ir[s], (uint32_t)(n_src - 1))];
-            xin[s] = half ? p.y : p.x;
+        for (int s = 0; s < 15; ++s) {
+            const float2 p = sp[min((uint32_t)ir[2 * s + (g >> 1)], (uint32_t)(n_src - 1))];
+            xin[s] = (g & 1) ? p.y : p.x;
         }
         {
             const float2 p = ((const float2 *)qry)[qrow];
-            xin[30] = half ? p.y : p.x;
-            xin[31] = 0.0f;
+            xin[15] = g == 0 ? p.x : g == 1 ? p.y : 0.0f;
         }
-        // L0 row tile rt (32 of the 128 hidden units, H1^T[32 x 32q]) is computed,
-        // tanh'd and immediately consumed by L1 as its k-steps (rt, p), p = register:
-        // only one L0 tile is ever live.
-        f32x16 a1[2];
+        // L0 row tile rt (16 of the 128 hidden units) is computed, tanh'd and
+        // immediately consumed by L1 as its K steps (rt, i): one L0 tile live.
+        f32x4 a1[4];
 #pragma unroll
-        for (int gt = 0; gt < 2; ++gt)
+        for (int rt = 0; rt < 4; ++rt)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) a1[gt][r] = bias[128 + 32 * gt + acc_row(r, lane)];
+            for (int i = 0; i < 4; ++i) a1[rt][i] = bias[128 + 16 * rt + 4 * g + i];
 #pragma unroll 1
-        for (int rt = 0; rt < 4; ++rt) {
-            f32x16 a0;
+        for (int rt = 0; rt < 8; ++rt) {
+            f32x4 a0;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) a0[r] = bias[32 * rt + acc_row(r, lane)];
+            for (int i = 0; i < 4; ++i) a0[i] = bias[16 * rt + 4 * g + i];
 #pragma unroll
-            for (int s = 0; s < 32; ++s) a0 = mfma32(img0[(rt * 32 + s) * 64 + lane], xin[s], a0);
+            for (int s = 0; s < 16; ++s) a0 = mfma16(img0[(rt * 16 + s) * 64 + lane], xin[s], a0);
 #pragma unroll
-            for (int r = 0; r < 16; ++r) a0[r] = tanhf(a0[r]);
+            for (int i = 0; i < 4; ++i) a0[i] = tanhf(a0[i]);
 #pragma unroll
-            for (int p = 0; p < 16; ++p)
+            for (int i = 0; i < 4; ++i)
 #pragma unroll
-                for (int gt = 0; gt < 2; ++gt)
-                    a1[gt] = mfma32(img1[(gt * 64 + rt * 16 + p) * 64 + lane], a0[p], a1[gt]);
+                for (int r1 = 0; r1 < 4; ++r1)
+                    a1[r1] = mfma16(img1[(r1 * 32 + rt * 4 + i) * 64 + lane], a0[i], a1[r1]);
         }
 #pragma unroll
-        for (int gt = 0; gt < 2; ++gt)
+        for (int r1 = 0; r1 < 4; ++r1)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) a1[gt][r] = tanhf(a1[gt][r]);
-        // L2: weights^T [30(32) x 32q]
-        f32x16 a2;
+            for (int i = 0; i < 4; ++i) a1[r1][i] = tanhf(a1[r1][i]);
+        // L2: weights^T [30 (32) x 16 q]
+        f32x4 a2[2];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) a2[r] = bias[192 + acc_row(r, lane)];
+        for (int r2 = 0; r2 < 2; ++r2)
 #pragma unroll
-        for (int gt = 0; gt < 2; ++gt)
+            for (int i = 0; i < 4; ++i) a2[r2][i] = bias[192 + 16 * r2 + 4 * g + i];
 #pragma unroll
-            for (int p = 0; p < 16; ++p)
-                a2 = mfma32(img2[(gt * 16 + p) * 64 + lane], a1[gt][p], a2);
-        // weighted sum of the neighbour values (data_creator_2d.py:83)
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int r2 = 0; r2 < 2; ++r2)
+                    a2[r2] = mfma16(img2[(r2 * 16 + t * 4 + i) * 64 + lane], a1[t][i], a2[r2]);
+        // weighted sum of the neighbour values (data_creator_2d.py:83): this lane's
+        // outputs o = 16 r2 + 4 g + i, then the 4 lanes of the query
         const float *vb = vals + b * n_src;
         float sum = 0.0f;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int o = acc_row(r, lane);
-            if (o < kNb) sum += a2[r] * vb[min((uint32_t)ir[o], (uint32_t)(n_src - 1))];
-        }
+        for (int r2 = 0; r2 < 2; ++r2)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int o = 16 * r2 + 4 * g + i;
+                if (o < kNb) sum += a2[r2][i] * vb[min((uint32_t)ir[o], (uint32_t)(n_src - 1))];
+            }
+        sum += __shfl_xor(sum, 16, 64);
         sum += __shfl_xor(sum, 32, 64);
-        if (half == 0 && valid) out[qrow] = addend ? addend[qrow] + sum : sum;
+        if (g == 0 && valid) out[qrow] = addend ? addend[qrow] + sum : sum;
     }
 }
 
@@ -163,10 +181,14 @@ extern "C" int mmpde_itp_interp(const float *src, const float *vals, const float
                                 float *out, mmpde_stream_t stream) {
     MMPDE_REQUIRE(src && vals && qry && idx && packed && out);
     MMPDE_REQUIRE(batches > 0 && n_src >= kNb && n_qry > 0);
-    const int64_t tiles = ((n_qry + 31) / 32) * batches;
-    int blocks = ceil_div(tiles, 4);
-    if (blocks > 1024) blocks = 1024;
-    hipLaunchKernelGGL(itp_interp_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), src, vals,
+    const int64_t tiles = ((n_qry + 15) / 16) * batches;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+        cus = 256;
+    int64_t blocks = 2 * (int64_t)cus;               // two resident workgroups per CU
+    if (blocks > tiles) blocks = tiles;
+    hipLaunchKernelGGL(itp_interp_kernel, dim3((unsigned)blocks), dim3(kItpThreads), 0, as_stream(stream), src, vals,
                        qry, idx, batches, n_src, n_qry, (const float *)packed, addend, out);
     MMPDE_RET_LAUNCH();
     return MMPDE_OK;
