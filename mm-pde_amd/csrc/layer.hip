@@ -862,7 +862,7 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs p) {
 // Embedding + layer 0's message_net_1 halves in one launch (gnn_2d.py:99-106,
 // 122-131, then the first GNN layer's projections): per 64-row tile
 //   z  = relu(BN1(W0 [u, x/Lx, y/Ly, t/tmax] + b0))        (VALU, K = 4)
-//   h0 = BN4(W3 z + b3)                                     (exact fp32 MFMA)
+//   h0 = BN4(W3 z + b3)            (F16X3: fp16x3 MFMA, W3 split in-kernel; F32: exact fp32)
 //   a0, b0 = layer 0's message_net_1 node halves of h0      (F16X3 or fp32)
 // ---------------------------------------------------------------------------
 struct EmbedArgs {
@@ -885,6 +885,7 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_embed_kernel(EmbedArgs p) {
     __shared__ float4 img[RB * 8 * 64];   // K = 128 operand image
     __shared__ float stage[ROWS * NLD];   // fp32 z, then h0
     __shared__ float rs[ROWS];            // h0 row scales
+    __shared__ float rsz[ROWS];           // z row scales (F16X3 embedding GEMM)
     __shared__ float rowv[3 + MAX_TW][ROWS];  // per row: t / tmax, x / Lx, y / Ly, u_0 .. u_{tw-1}
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int g = lane >> 4;
@@ -899,8 +900,34 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_embed_kernel(EmbedArgs p) {
         for (int c = 0; c < tw; ++c) rowv[3 + c][tid] = p.u[row * tw + c];
     }
     const mmpde_gnn_embed_params &e = p.e;
-    BOps<false, 8> b3;  // embedding_mlp.3 weight row of this lane's column
-    b3.load(nullptr, 0, 0, 0, e.w3 + (int64_t)col * LH, 0, lane);
+    // embedding_mlp.3 weight row of this lane's column: F32 as the exact fp32
+    // B operand; F16X3 split here into the fp16 hi / lo operand with a
+    // power-of-two column scale (one 128 x 128 weight: no packed image needed)
+    BOps<false, 8> b3;
+    BOps<true, 4> b3h;
+    float w3_is = 1.0f;
+    if (F16X3) {
+        const float *wr = e.w3 + (int64_t)col * LH;
+        float4 w[8];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            w[2 * s] = *(const float4 *)(wr + 32 * s + 8 * g);
+            w[2 * s + 1] = *(const float4 *)(wr + 32 * s + 8 * g + 4);
+        }
+        float m = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) m = absmax4(m, w[i]);
+        m = fmaxf(m, __shfl_xor(m, 16, 64));
+        m = fmaxf(m, __shfl_xor(m, 32, 64));
+        const float sw = split_scale(m);
+        w3_is = pow2_inv(sw);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) w[i] = make_float4(w[i].x * sw, w[i].y * sw, w[i].z * sw, w[i].w * sw);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) split8_rn(w[2 * s], w[2 * s + 1], b3h.h[s], b3h.l[s]);
+    } else {
+        b3.load(nullptr, 0, 0, 0, e.w3 + (int64_t)col * LH, 0, lane);
+    }
     const float h_b = e.b3[col];
     BnAffine bn4;
     bn4.set(e.bn4_rm[col], e.bn4_rv[col], e.bn4_w[col], e.bn4_b[col], e.eps);
@@ -923,14 +950,22 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_embed_kernel(EmbedArgs p) {
         stage[row * NLD + c] = fmaxf(bn1(v), 0.0f);
     }
     __syncthreads();
-    prep<false, ROWS>(stage, NLD, 0, ROWS, false, img, 128, 0, rs);
+    prep<F16X3, ROWS>(stage, NLD, 0, ROWS, false, img, 128, 0, rsz);
     __syncthreads();
     BOps<F16X3, S1> bA;
     {
         f32x4 acc[RB];
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) acc[rb] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
-        gemm_tile<false, RB, 8>(acc, img, 128, 0, b3, lane);
+        if (F16X3) {
+            gemm_tile<true, RB, 4>(acc, img, 128, 0, b3h, lane);
+#pragma unroll
+            for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) acc[rb][q] *= pow2_inv(rsz[16 * rb + 4 * g + q]) * w3_is;
+        } else {
+            gemm_tile<false, RB, 8>(acc, img, 128, 0, b3, lane);
+        }
         bA.load(p.pk + kPkW1, 4, wave, 0, w1r, 0, lane);
         const bool full = row0 + ROWS <= p.n;
         float *hp = p.h_out + (row0 + 4 * g) * LH + col;
