@@ -349,9 +349,10 @@ inline bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
 // C-ABI
 // ===========================================================================
 extern "C" int64_t mmpde_gnn_workspace_bytes(int64_t n) {
-    // h ping-pong, a, b and up to 4 edge-stage mean parts = 8 x [n,128] fp32
-    // (the unfused per-layer API uses 4 of them as a, b, mean, v), then the
-    // F16X3 range slots and room for per-call weight images
+    // h ping-pong, a, b, the edge stage's sums and 3 x [n,128] for the wave edge
+    // kernel's side blocks = 8 x [n,128] fp32 (the unfused per-layer API uses 4
+    // of them as a, b, mean, v), then the F16X3 range slots and room for
+    // per-call weight images
     return kGnnBufs * n * H * (int64_t)sizeof(float) + kAmaxBytes +
            (int64_t)MMPDE_GNN_MAX_LAYERS * kLayerPack;
 }
