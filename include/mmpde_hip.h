@@ -65,6 +65,24 @@ const char *mmpde_status_string(int status);
 int mmpde_knn_graph(const float *pos, int64_t batches, int64_t n_per, int k,
                     int32_t *nbr_out, int32_t *degenerate, mmpde_stream_t stream);
 
+/* Static candidate table of mmpde_knn_graph_cand for fixed points xi [n_per, 2]
+ * (128 <= n_per <= 4096): cand_out [n_per, 128] int32 LOCAL = the 128 nearest of
+ * xi_p in xi, (d2, index) order (xi_p first).  Built once per fixed mesh. */
+int mmpde_knn_candidates(const float *xi, int64_t n_per, int32_t *cand_out, mmpde_stream_t stream);
+
+/* mmpde_knn_graph of moved points pos = xi + displacement (the DMM's moved mesh,
+ * reference data_creator_2d.py:88-137 then :260), the same output bit for bit,
+ * answered from the candidate table where a distance bound proves it complete
+ * (|x_j - x_p| >= R128(xi_p) - |d_p| - max |d| for every non-candidate j), by
+ * the full search elsewhere.  xi [n_per, 2] the fixed points every trajectory
+ * moves from; cand from mmpde_knn_candidates(xi); scratch: device bytes from
+ * mmpde_knn_graph_cand_scratch_bytes.  k <= 63 and 128 <= n_per <= 4096, else it
+ * is mmpde_knn_graph. */
+int64_t mmpde_knn_graph_cand_scratch_bytes(int64_t batches, int64_t n_per);
+int mmpde_knn_graph_cand(const float *pos, const float *xi, int64_t batches, int64_t n_per, int k,
+                         const int32_t *cand, int32_t *nbr_out, int32_t *degenerate, void *scratch,
+                         mmpde_stream_t stream);
+
 /* sklearn NearestNeighbors(n_neighbors=k).fit(src_b).kneighbors(qry_b) per
  * trajectory b (reference data_creator_2d.py:66-78).  Distances in fp64
  * (dx*dx + dy*dy), ascending, ties by index.
@@ -73,6 +91,18 @@ int mmpde_knn_graph(const float *pos, int64_t batches, int64_t n_per, int k,
  * Requires k <= n_src <= 16384, k <= 63. */
 int mmpde_knn_query(const float *src, const float *qry, int64_t batches, int64_t n_src,
                     int64_t n_qry, int k, int32_t *idx_out, mmpde_stream_t stream);
+
+/* mmpde_knn_query of qry [batches * n_per, 2] onto moved points src = xi +
+ * displacement [batches * n_per, 2] (reference data_creator_2d.py:66-78, the
+ * kNN-30 query of the fixed grid onto the DMM's moved mesh), the same output
+ * bit for bit, answered from mmpde_knn_candidates(xi) where the bound of
+ * mmpde_knn_graph_cand (less |qry_p - xi_p|) proves it complete, by the full
+ * search elsewhere.  n_src = n_qry = n_per; scratch as for
+ * mmpde_knn_graph_cand.  k <= 64 and 128 <= n_per <= 4096, else it is
+ * mmpde_knn_query. */
+int mmpde_knn_query_cand(const float *src, const float *qry, const float *xi, int64_t batches,
+                         int64_t n_per, int k, const int32_t *cand, int32_t *idx_out, void *scratch,
+                         mmpde_stream_t stream);
 
 /* torch_cluster.radius_graph(pos, r, batch, loop=False, max_num_neighbors)
  * (data_creator_2d.py:257-258, connect_edge='radius'; r at :195 / :226) for

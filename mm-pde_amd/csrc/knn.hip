@@ -328,7 +328,8 @@ template <int CPL, bool QUERY>
 __global__ __launch_bounds__(256) void knn_kernel(const float2 *__restrict__ pts,
                                                   const float2 *__restrict__ qry, int n_src,
                                                   int n_q, int k, int32_t *__restrict__ out,
-                                                  int32_t *__restrict__ degenerate) {
+                                                  int32_t *__restrict__ degenerate,
+                                                  const uint8_t *__restrict__ done = nullptr) {
     typedef KeyTraits<QUERY> KT;
     typedef typename KT::key_t key_t;
     __shared__ float2 sP[CPL * 64];
@@ -337,6 +338,11 @@ __global__ __launch_bounds__(256) void knn_kernel(const float2 *__restrict__ pts
     __shared__ int sSel[4][64];
 
     const int b = blockIdx.y;
+    if (done) {  // queries answered by knn_cand_kernel are skipped; so is an all-done block
+        const int qi = blockIdx.x * kQueriesPerBlock + (int)threadIdx.x;
+        const int need = threadIdx.x < kQueriesPerBlock && qi < n_q && !done[(int64_t)b * n_q + qi];
+        if (!__syncthreads_or(need)) return;
+    }
     const float2 *P = pts + (int64_t)b * n_src;
     for (int i = threadIdx.x; i < n_src; i += 256) sP[i] = P[i];
     __syncthreads();
@@ -348,6 +354,7 @@ __global__ __launch_bounds__(256) void knn_kernel(const float2 *__restrict__ pts
     const int q_end = min((int)(blockIdx.x + 1) * kQueriesPerBlock, n_q);
 
     for (int qi = blockIdx.x * kQueriesPerBlock + wave; qi < q_end; qi += 4) {
+        if (done && done[(int64_t)b * n_q + qi]) continue;  // wave-uniform
         const float2 q = QUERY ? qry[(int64_t)b * n_q + qi] : sP[qi];
         uint32_t fkey[CPL];
         uint32_t lmin = ~0u;
@@ -514,6 +521,142 @@ int launch_knn(const float *pts, const float *qry, int64_t batches, int64_t n_sr
     return MMPDE_ERR_UNSUPPORTED;
 }
 
+// ---------------------------------------------------------------------------
+// Moving-mesh graph from a static candidate list (exact, with a fallback).
+// The DMM moves every node x_i = xi_i + d_i only a little, so the answer for
+// x_p is almost always among cand[p] = the 128 nearest of xi_p in the fixed
+// mesh xi ((key, index) order, xi_p itself first).  A point j outside cand[p]
+// has |xi_j - xi_p| >= R = sqrt(key of cand[p][127]) (up to rounding), hence
+// |x_j - x_p| >= R - |d_p| - max_i |d_i| = L.  If the kk-th candidate distance
+// is below L (every bound with a 2^-20 relative margin, which covers the fp32
+// key's rounding), no non-candidate can enter the first kk in (key, index)
+// order, so the candidates sorted by (key, index) ARE the answer, ties
+// included.  Otherwise knn_kernel answers the query (done[q] = 0).
+// ---------------------------------------------------------------------------
+constexpr int kCandN = 128;
+constexpr float kUp = 1.0f + 1.0f / 1048576.0f, kDown = 1.0f - 1.0f / 1048576.0f;
+
+// cand[p] = the kCandN nearest of xi_p in xi, (key, index) order: one
+// workgroup per point, (key << 32 | index) pairs bitonic-sorted in LDS.  Built
+// once per fixed mesh.
+__global__ __launch_bounds__(256) void knn_table_kernel(const float2 *__restrict__ xi, int n_per,
+                                                        int32_t *__restrict__ cand) {
+    __shared__ uint64_t sk[4096];
+    const int p = blockIdx.x;
+    const float2 q = xi[p];
+    for (int j = threadIdx.x; j < 4096; j += 256)
+        sk[j] = j < n_per ? (((uint64_t)key_f32(xi[j], q) << 32) | (uint32_t)j) : ~0ull;
+    __syncthreads();
+    for (int size = 2; size <= 4096; size <<= 1)
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int t = threadIdx.x; t < 2048; t += 256) {
+                const int i = 2 * t - (t & (stride - 1)), l = i + stride;
+                const uint64_t a = sk[i], c = sk[l];
+                if ((a > c) == ((i & size) == 0)) {
+                    sk[i] = c;
+                    sk[l] = a;
+                }
+            }
+            __syncthreads();
+        }
+    if (threadIdx.x < kCandN) cand[(int64_t)p * kCandN + threadIdx.x] = (int32_t)(uint32_t)sk[threadIdx.x];
+}
+
+// dmax[b] >= max_i |x_bi - xi_i| (one workgroup per trajectory)
+__global__ __launch_bounds__(256) void knn_dmax_kernel(const float2 *__restrict__ x,
+                                                       const float2 *__restrict__ xi, int n_per,
+                                                       float *__restrict__ dmax) {
+    __shared__ float red[4];
+    const int b = blockIdx.x;
+    float m = 0.0f;
+    for (int i = threadIdx.x; i < n_per; i += 256) {
+        const float2 a = x[(int64_t)b * n_per + i], c = xi[i];
+        const float dx = a.x - c.x, dy = a.y - c.y;
+        m = fmaxf(m, sqrtf(dx * dx + dy * dy));
+    }
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) dmax[b] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])) * kUp;
+}
+
+// L = a lower bound on |x_j - q| over every j outside cand[p]: R = the 128th
+// candidate's distance in xi (every non-candidate of xi_p is at least that far
+// from xi_p), less the query's offset from xi_p and the largest displacement
+// |x_j - xi_j|.  Subtrahends grouped so the one cancelling subtraction errs
+// relative to L itself; <= 0 when the bound proves nothing.
+__device__ __forceinline__ float cand_bound(const float2 *__restrict__ xi, int n_per,
+                                            const int32_t *__restrict__ cr, int pl, float2 q,
+                                            float dmax) {
+    const float2 xp = xi[pl];
+    const int jl = min(max(cr[kCandN - 1], 0), n_per - 1);
+    const float R = sqrtf(__uint_as_float(key_f32(xi[jl], xp))) * kDown;
+    const float ddx = q.x - xp.x, ddy = q.y - xp.y;
+    const float dq = sqrtf(ddx * ddx + ddy * ddy) * kUp;
+    return (R - (dq + dmax) * kUp) * kDown;
+}
+
+// One wave per query point: the 128 candidates' keys (two per lane), one
+// 128-wide (key, index) sort; the first kk are the answer when the kk-th
+// candidate is closer than the bound.  QUERY = false: the moved-mesh graph
+// (fp32 keys, self dropped, global indices, as knn_finish's graph branch);
+// true: the kNN query of qry onto the moved mesh (fp64 keys, local indices).
+template <bool QUERY>
+__global__ __launch_bounds__(256) void knn_cand_kernel(const float2 *__restrict__ x,
+                                                       const float2 *__restrict__ qry,
+                                                       const float2 *__restrict__ xi, int n_per,
+                                                       int64_t n_tot, int k,
+                                                       const int32_t *__restrict__ cand,
+                                                       const float *__restrict__ dmax,
+                                                       int32_t *__restrict__ out,
+                                                       int32_t *__restrict__ degenerate,
+                                                       uint8_t *__restrict__ done) {
+    typedef KeyTraits<QUERY> KT;
+    typedef typename KT::key_t key_t;
+    const int lane = threadIdx.x & 63;
+    const int64_t p = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (p >= n_tot) return;  // wave-uniform
+    const int b = (int)(p / n_per);
+    const int pl = (int)(p - (int64_t)b * n_per);
+    const float2 *X = x + (int64_t)b * n_per;
+    const float2 q = QUERY ? qry[p] : X[pl];
+    const int32_t *cr = cand + (int64_t)pl * kCandN;
+    const float L = cand_bound(xi, n_per, cr, pl, q, dmax[b]);
+    const int kk = QUERY ? k : k + 1;
+    // Skipped (the fallback answers; wave-uniform) when the bound proves
+    // nothing, or when already the unmoved kk-th candidate lies beyond it: the
+    // moved one then almost never passes, and the sort would be wasted.  A
+    // heuristic only -- the test below decides.
+    const int jk = min(max(cr[kk - 1], 0), n_per - 1);
+    if (!(L > 0.0f) || sqrtf(__uint_as_float(key_f32(xi[jk], xi[pl]))) >= L) {
+        if (lane == 0) done[p] = 0;
+        return;
+    }
+    int i0 = min(max(cr[lane], 0), n_per - 1), i1 = min(max(cr[64 + lane], 0), n_per - 1);
+    key_t k0 = KT::key(X[i0], q), k1 = KT::key(X[i1], q);
+    wave_sort128(k0, i0, k1, i1, lane);
+    const key_t key_kk = __shfl(k0, kk - 1, 64);
+    float d_kk;
+    if constexpr (QUERY)
+        d_kk = (float)sqrt(__longlong_as_double((long long)key_kk)) * kUp;
+    else
+        d_kk = sqrtf(__uint_as_float(key_kk)) * kUp;
+    const bool ok = d_kk < L;  // same on every lane
+    if (lane == 0) done[p] = ok ? 1 : 0;
+    if (!ok) return;
+    const int mi = i0, rank = lane;
+    if (QUERY) {
+        if (lane < kk) out[p * k + rank] = mi;
+    } else {
+        const uint64_t smask = __ballot(lane < kk && mi == pl);
+        const bool has_self = smask != 0ull;
+        const int self_rank = has_self ? __shfl(rank, __ffsll((unsigned long long)smask) - 1, 64) : kk;
+        const int pos = rank - ((has_self && rank > self_rank) ? 1 : 0);
+        if (lane < kk && !(has_self && mi == pl) && pos < k) out[p * k + pos] = b * n_per + mi;
+        if (!has_self && lane == 0 && degenerate) atomicAdd(degenerate, 1);
+    }
+}
+
 // torch_cluster radius_graph(x, r, batch, loop=False, max_num_neighbors)
 // (reference data_creator_2d.py:257-258): radius(x, x, ..., max_num_neighbors
 // + 1) scans the query's segment in index order and keeps the first w = max_nn
@@ -565,6 +708,81 @@ extern "C" int mmpde_knn_graph(const float *pos, int64_t batches, int64_t n_per,
     MMPDE_REQUIRE(pos && nbr_out);
     return launch_knn<false>(pos, nullptr, batches, n_per, n_per, k, nbr_out, degenerate,
                              as_stream(stream));
+}
+
+extern "C" int mmpde_knn_candidates(const float *xi, int64_t n_per, int32_t *cand_out,
+                                    mmpde_stream_t stream) {
+    MMPDE_REQUIRE(xi && cand_out && n_per >= kCandN && n_per <= 4096);
+    hipLaunchKernelGGL(knn_table_kernel, dim3((unsigned)n_per), dim3(256), 0, as_stream(stream),
+                       (const float2 *)xi, (int)n_per, cand_out);
+    MMPDE_RET_LAUNCH();
+    return MMPDE_OK;
+}
+
+extern "C" int64_t mmpde_knn_graph_cand_scratch_bytes(int64_t batches, int64_t n_per) {
+    return (batches * 4 + 15) / 16 * 16 + batches * n_per;  // dmax, answered flags
+}
+
+// The candidate path: dmax, the candidate kernel, the full search for the
+// queries it could not answer (done[q] = 0).
+template <bool QUERY>
+static int knn_cand_launch(const float *pos, const float *qry, const float *xi, int64_t batches,
+                           int64_t n_per, int k, const int32_t *cand, int32_t *out, int32_t *degenerate,
+                           void *scratch, hipStream_t st) {
+    float *dmax = (float *)scratch;
+    uint8_t *done = (uint8_t *)scratch + (batches * 4 + 15) / 16 * 16;
+    const int64_t n_tot = batches * n_per;
+    const float2 *x = (const float2 *)pos, *q = (const float2 *)qry, *x0 = (const float2 *)xi;
+    hipLaunchKernelGGL(knn_dmax_kernel, dim3((unsigned)batches), dim3(256), 0, st, x, x0, (int)n_per, dmax);
+    hipLaunchKernelGGL(knn_cand_kernel<QUERY>, dim3((unsigned)ceil_div(n_tot, 4)), dim3(256), 0, st, x, q, x0,
+                       (int)n_per, n_tot, k, cand, dmax, out, degenerate, done);
+    MMPDE_RET_LAUNCH();
+    dim3 grid(ceil_div(n_per, kQueriesPerBlock), (unsigned)batches);
+    const int ns = (int)n_per, cpl = ceil_div(n_per, 64);
+#define MMPDE_KNN_FALLBACK(C)                                                                         \
+    if (cpl <= C) {                                                                                   \
+        hipLaunchKernelGGL((knn_kernel<C, QUERY>), grid, dim3(256), 0, st, x, QUERY ? q : x, ns, ns, k, \
+                           out, degenerate, (const uint8_t *)done);                                   \
+        MMPDE_RET_LAUNCH();                                                                           \
+        return MMPDE_OK;                                                                              \
+    }
+    MMPDE_KNN_FALLBACK(4)
+    MMPDE_KNN_FALLBACK(8)
+    MMPDE_KNN_FALLBACK(16)
+    MMPDE_KNN_FALLBACK(24)
+    MMPDE_KNN_FALLBACK(32)
+    MMPDE_KNN_FALLBACK(40)
+    MMPDE_KNN_FALLBACK(48)
+    MMPDE_KNN_FALLBACK(56)
+    MMPDE_KNN_FALLBACK(64)
+#undef MMPDE_KNN_FALLBACK
+    return MMPDE_ERR_UNSUPPORTED;
+}
+
+static bool cand_path_applies(int64_t batches, int64_t n_per, int kk) {
+    // the answer inside the first 64 sorted candidates; the register kernels' sizes
+    return kk >= 1 && kk <= 64 && n_per >= kCandN && n_per <= 4096 && batches >= 1 && batches <= 65535 &&
+           batches * n_per <= INT32_MAX;
+}
+
+extern "C" int mmpde_knn_graph_cand(const float *pos, const float *xi, int64_t batches, int64_t n_per,
+                                    int k, const int32_t *cand, int32_t *nbr_out, int32_t *degenerate,
+                                    void *scratch, mmpde_stream_t stream) {
+    MMPDE_REQUIRE(pos && xi && cand && nbr_out && scratch);
+    hipStream_t st = as_stream(stream);
+    if (k < 1 || !cand_path_applies(batches, n_per, k + 1))
+        return launch_knn<false>(pos, nullptr, batches, n_per, n_per, k, nbr_out, degenerate, st);
+    return knn_cand_launch<false>(pos, nullptr, xi, batches, n_per, k, cand, nbr_out, degenerate, scratch, st);
+}
+
+extern "C" int mmpde_knn_query_cand(const float *src, const float *qry, const float *xi, int64_t batches,
+                                    int64_t n_per, int k, const int32_t *cand, int32_t *idx_out,
+                                    void *scratch, mmpde_stream_t stream) {
+    MMPDE_REQUIRE(src && qry && xi && cand && idx_out && scratch);
+    hipStream_t st = as_stream(stream);
+    if (!cand_path_applies(batches, n_per, k))
+        return launch_knn<true>(src, qry, batches, n_per, n_per, k, idx_out, nullptr, st);
+    return knn_cand_launch<true>(src, qry, xi, batches, n_per, k, cand, idx_out, nullptr, scratch, st);
 }
 
 extern "C" int mmpde_knn_query(const float *src, const float *qry, int64_t batches,

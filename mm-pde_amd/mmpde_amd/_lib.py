@@ -94,6 +94,10 @@ _SIGS = {
     "mmpde_version": (_I, []),
     "mmpde_status_string": (ctypes.c_char_p, [_I]),
     "mmpde_knn_graph": (_I, [_P, _I64, _I64, _I, _P, _P, _P]),
+    "mmpde_knn_candidates": (_I, [_P, _I64, _P, _P]),
+    "mmpde_knn_graph_cand_scratch_bytes": (_I64, [_I64, _I64]),
+    "mmpde_knn_graph_cand": (_I, [_P, _P, _I64, _I64, _I, _P, _P, _P, _P, _P]),
+    "mmpde_knn_query_cand": (_I, [_P, _P, _P, _I64, _I64, _I, _P, _P, _P, _P]),
     "mmpde_knn_query": (_I, [_P, _P, _I64, _I64, _I64, _I, _P, _P]),
     "mmpde_edge_index_from_nbr": (_I, [_P, _I64, _I, _P, _P]),
     "mmpde_linear_skinny": (_I, [_P, _I64, _I64, _I64, _P, _I64, _P, _I64, _I, _P, _I64, _P]),

@@ -43,6 +43,52 @@ def knn_graph_nbr(pos: torch.Tensor, batches: int, k: int, count_degenerate: boo
     return (nbr, deg) if count_degenerate else nbr
 
 
+KNN_CAND = 128  # candidates per point in mmpde_knn_candidates' table
+
+
+def knn_candidates(xi: torch.Tensor):
+    """Static candidate table of knn_graph_moved for fixed points xi [N, 2]:
+    [N, 128] int32, the 128 nearest of each point in (d2, index) order, or None
+    where the candidate path does not apply (N outside [128, 4096])."""
+    L.require_device(xi)
+    xi = L.f32c(xi).reshape(-1, 2)
+    N = xi.shape[0]
+    if N < KNN_CAND or N > 4096:
+        return None
+    cand = torch.empty((N, KNN_CAND), dtype=torch.int32, device=xi.device)
+    L.check(L.lib().mmpde_knn_candidates(L.ptr(xi), N, L.ptr(cand), L.stream(xi.device)),
+            "mmpde_knn_candidates")
+    return cand
+
+
+def knn_graph_moved(pos: torch.Tensor, xi: torch.Tensor, cand, batches: int, k: int,
+                    scratch: torch.Tensor | None = None, count_degenerate: bool = False):
+    """knn_graph_nbr of moved points pos [batches * N, 2] (every trajectory's
+    mesh moved from the same xi [N, 2]), bit for bit, answered from the
+    candidate table `cand` (knn_candidates(xi)) where a distance bound proves
+    it complete and by the full search elsewhere (reference
+    data_creator_2d.py:260 on the DMM's moved mesh)."""
+    if cand is None:
+        return knn_graph_nbr(pos, batches, k, count_degenerate)
+    L.require_device(pos)
+    pos = L.f32c(pos).reshape(-1, 2)
+    xi = L.f32c(xi).reshape(-1, 2)
+    n = pos.shape[0]
+    N = xi.shape[0]
+    if n != batches * N or cand.shape != (N, KNN_CAND):
+        raise ValueError("pos must hold `batches` meshes of xi's size; cand from knn_candidates(xi)")
+    _knn_points_check(N, k, "knn_graph")
+    need = L.lib().mmpde_knn_graph_cand_scratch_bytes(batches, N)
+    if scratch is None or scratch.numel() * scratch.element_size() < need:
+        scratch = torch.empty((need,), dtype=torch.uint8, device=pos.device)
+    nbr = torch.empty((n, k), dtype=torch.int32, device=pos.device)
+    deg = torch.zeros((1,), dtype=torch.int32, device=pos.device) if count_degenerate else None
+    L.check(L.lib().mmpde_knn_graph_cand(L.ptr(pos), L.ptr(xi), batches, N, k, L.ptr(cand),
+                                         L.ptr(nbr), L.ptr(deg), L.ptr(scratch),
+                                         L.stream(pos.device)), "mmpde_knn_graph_cand")
+    return (nbr, deg) if count_degenerate else nbr
+
+
 def radius_graph_nbr(pos: torch.Tensor, batches: int, r: float, max_num_neighbors: int = 32):
     """torch_cluster.radius_graph(pos, r, batch, loop=False, max_num_neighbors) for
     `batches` equal contiguous segments (reference data_creator_2d.py:257-258),
@@ -128,6 +174,34 @@ def knn_query(src: torch.Tensor, qry: torch.Tensor, batches: int, k: int) -> tor
     idx = torch.empty((batches * nq, k), dtype=torch.int32, device=src.device)
     L.check(L.lib().mmpde_knn_query(L.ptr(src), L.ptr(qry), batches, ns, nq, k, L.ptr(idx),
                                     L.stream(src.device)), "mmpde_knn_query")
+    return idx
+
+
+def knn_query_moved(src: torch.Tensor, qry: torch.Tensor, xi: torch.Tensor, cand, batches: int,
+                    k: int, scratch: torch.Tensor | None = None) -> torch.Tensor:
+    """knn_query of qry onto moved points src (every trajectory's mesh moved
+    from the same xi [N, 2]; n_src = n_qry = N), bit for bit, answered from the
+    candidate table `cand` (knn_candidates(xi)) where a distance bound proves
+    it complete and by the full search elsewhere (reference
+    data_creator_2d.py:66-78 onto the DMM's moved mesh)."""
+    if cand is None:
+        return knn_query(src, qry, batches, k)
+    L.require_device(src, qry)
+    src = L.f32c(src).reshape(-1, 2)
+    qry = L.f32c(qry).reshape(-1, 2)
+    xi = L.f32c(xi).reshape(-1, 2)
+    N = xi.shape[0]
+    if src.shape[0] != batches * N or qry.shape[0] != batches * N or cand.shape != (N, KNN_CAND):
+        raise ValueError("src and qry must hold `batches` point sets of xi's size; "
+                         "cand from knn_candidates(xi)")
+    _knn_points_check(N, k, "knn_query")
+    need = L.lib().mmpde_knn_graph_cand_scratch_bytes(batches, N)
+    if scratch is None or scratch.numel() * scratch.element_size() < need:
+        scratch = torch.empty((need,), dtype=torch.uint8, device=src.device)
+    idx = torch.empty((batches * N, k), dtype=torch.int32, device=src.device)
+    L.check(L.lib().mmpde_knn_query_cand(L.ptr(src), L.ptr(qry), L.ptr(xi), batches, N, k,
+                                         L.ptr(cand), L.ptr(idx), L.ptr(scratch),
+                                         L.stream(src.device)), "mmpde_knn_query_cand")
     return idx
 
 

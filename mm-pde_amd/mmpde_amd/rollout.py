@@ -73,6 +73,13 @@ class MMPDERollout:
                 itp.packed(mode)
             # the DMM head's grid side depends on xi and the weights only
             self.dmm_cache = dmm.head_cache(self.xi, workspace=self.ws_dmm)
+            # the moved-mesh graph from the 128 nearest of each xi point (exact:
+            # csrc/knn.hip knn_cand_kernel, full search where its bound fails)
+            self.knn_cand = ops.knn_candidates(self.xi)
+            nb = L.lib().mmpde_knn_graph_cand_scratch_bytes(batches, N)
+            self.knn_scratch = torch.empty((nb,), dtype=torch.uint8, device=self.device)
+            # the kNN-30 query runs on side2 beside the graph: its own scratch
+            self.knn_scratch_q = torch.empty((nb,), dtype=torch.uint8, device=self.device)
             # the fixed-grid model depends on u only: it runs on a side stream,
             # with its own workspace, beside the moving-mesh chain
             self.side = torch.cuda.Stream(self.device)
@@ -149,7 +156,8 @@ class MMPDERollout:
         side2.wait_stream(cur)
         with torch.cuda.stream(side2):
             u.record_stream(side2)
-            idx2 = ops.knn_query(mesh, self.grid_rep, B, 30)
+            idx2 = ops.knn_query_moved(mesh, self.grid_rep, self.xi, self.knn_cand, B, 30,
+                                       self.knn_scratch_q)
             if self.kind == "burgers":
                 res = self.itp.res_cut(u.reshape(B, 1, self.s, self.s)).reshape(-1)
             else:
@@ -158,7 +166,7 @@ class MMPDERollout:
             res.record_stream(cur)
         self.pos_m[:, 1:3] = mesh
         self._set_t(self.pos_m, step_idx)
-        nbr_m = ops.knn_graph_nbr(mesh, B, self.gc.n)
+        nbr_m = ops.knn_graph_moved(mesh, self.xi, self.knn_cand, B, self.gc.n, self.knn_scratch)
         if self.kind == "burgers":
             idx1 = ops.knn_query(self.grid_rep, mesh, B, 30)
             u_m = ops.itp_interp(self.grid_rep, u_flat, mesh, idx1, B, self.itp.packed("1"))

@@ -53,6 +53,38 @@ def test_knn_graph_burgers_grid_ties_bit_exact(dev):
     _graph_case(burgers_grid_points().repeat(2, 1), 2, dev)   # linspace grid: ties at the cut
 
 
+@pytest.mark.parametrize("kind", ["cy", "burgers"])
+def test_knn_graph_moved_candidates_bit_exact(dev, kind):
+    """The candidate-table graph (mmpde_knn_graph_cand) against the oracle and
+    the full search: small displacements (the table answers), one trajectory
+    moved far (the bound fails, the full search answers), and the unmoved grid
+    (ties at the cut on the burgers lattice)."""
+    from mmpde_amd import ops
+    from mmpde_amd.synth import burgers_grid_points, cy_synth_mesh
+
+    xi = cy_synth_mesh() if kind == "cy" else burgers_grid_points()
+    gen = torch.Generator().manual_seed(5)
+    moved = [xi, xi + 0.004 * torch.sin(9 * xi.flip(1)),
+             xi + 0.002 * torch.randn(xi.shape, generator=gen),
+             xi + 0.3 * torch.sin(3 * xi.flip(1))]
+    B = len(moved)
+    pos = torch.cat(moved)
+    cand = ops.knn_candidates(xi.to(dev))
+    assert cand is not None and cand.shape == (xi.shape[0], ops.KNN_CAND)
+    nbr, deg = ops.knn_graph_moved(pos.to(dev), xi.to(dev), cand, B, 35, count_degenerate=True)
+    _, ref, rdeg = refcpu.knn_graph(pos, 35, B)
+    assert int(deg.item()) == rdeg
+    assert torch.equal(nbr.cpu().long(), ref)
+    assert torch.equal(nbr, ops.knn_graph_nbr(pos.to(dev), B, 35))
+    # the kNN-30 query of the grid onto the moved meshes (queries = xi; and
+    # queries moved off xi, which the bound must account for)
+    for qry in (xi.repeat(B, 1), xi.repeat(B, 1) + 0.003 * torch.cos(5 * xi.repeat(B, 1))):
+        idx = ops.knn_query_moved(pos.to(dev), qry.to(dev), xi.to(dev), cand, B, 30)
+        assert torch.equal(idx, ops.knn_query(pos.to(dev), qry.to(dev), B, 30))
+        ref_q = refcpu.knn_query(pos, qry, B, 30)
+        assert torch.equal(idx.cpu().long().reshape(ref_q.shape), ref_q)
+
+
 def test_knn_graph_integer_lattice_golden(dev):
     from mmpde_amd import ops
 
