@@ -65,23 +65,56 @@ const char *mmpde_status_string(int status);
 int mmpde_knn_graph(const float *pos, int64_t batches, int64_t n_per, int k,
                     int32_t *nbr_out, int32_t *degenerate, mmpde_stream_t stream);
 
-/* Static candidate table of mmpde_knn_graph_cand for fixed points xi [n_per, 2]
- * (128 <= n_per <= 4096): cand_out [n_per, 128] int32 LOCAL = the 128 nearest of
- * xi_p in xi, (d2, index) order (xi_p first).  Built once per fixed mesh. */
-int mmpde_knn_candidates(const float *xi, int64_t n_per, int32_t *cand_out, mmpde_stream_t stream);
+/* Static candidate table of the moved-mesh kNN entry points below, for fixed
+ * points xi [n_per, 2] (128 <= n_per <= 4096) and reference points ref
+ * [n_per, 2] (NULL: xi): cand_out [n_per, 128] int32 LOCAL = the 128 nearest
+ * of ref_p in xi, (d2, index) order.  Built once per fixed mesh: ref = xi for
+ * mmpde_knn_graph_cand; for mmpde_knn_query_cand ref = the fixed query points
+ * (e.g. the uniform grid, in its own order). */
+int mmpde_knn_candidates(const float *xi, const float *ref, int64_t n_per, int32_t *cand_out,
+                         mmpde_stream_t stream);
+
+/* Displacement record of moved points pos = xi + d [batches * n_per, 2]: per
+ * trajectory, the box of xi cut into 16 x 16 cells and, per cell, the largest
+ * |d_j| of the points whose xi_j lies in it, the largest |d_j| overall, and
+ * per role (graph, query) the number of queries the candidate table could not
+ * answer in the last call of that role (mmpde_knn_table_misses; calls of one
+ * role on one record must not overlap).
+ * cells_out: device memory of mmpde_knn_moved_cells_bytes(batches).  One
+ * launch per moved mesh, shared by mmpde_knn_graph_cand and
+ * mmpde_knn_query_cand. */
+int64_t mmpde_knn_moved_cells_bytes(int64_t batches);
+int mmpde_knn_moved_cells(const float *pos, const float *xi, int64_t batches, int64_t n_per,
+                          float *cells_out, mmpde_stream_t stream);
+/* out[0] (device float) = half the median over the reference points p of
+ * R128(p) - R_kk(p), the 128th and the kk-th nearest distance of ref_p in xi
+ * (cand from mmpde_knn_candidates(xi, ref)): the skip_above of the calls below
+ * (past that displacement about half the lookups cannot pass).  Once per
+ * table. */
+int mmpde_knn_skip_threshold(const float *xi, const float *ref, int64_t n_per, const int32_t *cand,
+                             int kk, float *out, mmpde_stream_t stream);
+/* misses_out [batches, 2] int32 (device): per trajectory, the graph and the
+ * query misses counted in the record (diagnostics; stream-ordered copy). */
+int mmpde_knn_table_misses(const float *cells, int64_t batches, int32_t *misses_out,
+                           mmpde_stream_t stream);
 
 /* mmpde_knn_graph of moved points pos = xi + displacement (the DMM's moved mesh,
  * reference data_creator_2d.py:88-137 then :260), the same output bit for bit,
  * answered from the candidate table where a distance bound proves it complete
- * (|x_j - x_p| >= R128(xi_p) - |d_p| - max |d| for every non-candidate j), by
- * the full search elsewhere.  xi [n_per, 2] the fixed points every trajectory
- * moves from; cand from mmpde_knn_candidates(xi); scratch: device bytes from
- * mmpde_knn_graph_cand_scratch_bytes.  k <= 63 and 128 <= n_per <= 4096, else it
+ * (|x_j - x_p| >= max(R128(xi_p) - |d_p|, dist(x_p, cell of xi_j)) - max |d|
+ * over that cell, for every non-candidate j), by the full search elsewhere.
+ * xi [n_per, 2] the fixed points every trajectory moves from; cand from
+ * mmpde_knn_candidates(xi, NULL); cells from mmpde_knn_moved_cells(pos, xi);
+ * scratch: device bytes from mmpde_knn_graph_cand_scratch_bytes (a flag per
+ * query: the ones the full search answers).  skip_above > 0: a trajectory
+ * whose largest displacement exceeds it goes straight to the full search
+ * (mmpde_knn_skip_threshold gives the displacement beyond which half the
+ * table's lookups must fail); <= 0: the table is always tried.  k <= 63 and 128 <= n_per <= 4096, else it
  * is mmpde_knn_graph. */
 int64_t mmpde_knn_graph_cand_scratch_bytes(int64_t batches, int64_t n_per);
-int mmpde_knn_graph_cand(const float *pos, const float *xi, int64_t batches, int64_t n_per, int k,
-                         const int32_t *cand, int32_t *nbr_out, int32_t *degenerate, void *scratch,
-                         mmpde_stream_t stream);
+int mmpde_knn_graph_cand(const float *pos, const float *xi, const float *cells, float skip_above,
+                         int64_t batches, int64_t n_per, int k, const int32_t *cand, int32_t *nbr_out,
+                         int32_t *degenerate, void *scratch, mmpde_stream_t stream);
 
 /* sklearn NearestNeighbors(n_neighbors=k).fit(src_b).kneighbors(qry_b) per
  * trajectory b (reference data_creator_2d.py:66-78).  Distances in fp64
@@ -95,13 +128,16 @@ int mmpde_knn_query(const float *src, const float *qry, int64_t batches, int64_t
 /* mmpde_knn_query of qry [batches * n_per, 2] onto moved points src = xi +
  * displacement [batches * n_per, 2] (reference data_creator_2d.py:66-78, the
  * kNN-30 query of the fixed grid onto the DMM's moved mesh), the same output
- * bit for bit, answered from mmpde_knn_candidates(xi) where the bound of
- * mmpde_knn_graph_cand (less |qry_p - xi_p|) proves it complete, by the full
- * search elsewhere.  n_src = n_qry = n_per; scratch as for
+ * bit for bit, answered from mmpde_knn_candidates(xi, ref) where the bound of
+ * mmpde_knn_graph_cand (with |qry_p - ref_p| in place of |d_p|) proves it
+ * complete, by the full search elsewhere.  ref [n_per, 2]: the reference
+ * points the table was built for (NULL: xi); cells from
+ * mmpde_knn_moved_cells(src, xi).  n_src = n_qry = n_per; scratch as for
  * mmpde_knn_graph_cand.  k <= 64 and 128 <= n_per <= 4096, else it is
  * mmpde_knn_query. */
-int mmpde_knn_query_cand(const float *src, const float *qry, const float *xi, int64_t batches,
-                         int64_t n_per, int k, const int32_t *cand, int32_t *idx_out, void *scratch,
+int mmpde_knn_query_cand(const float *src, const float *qry, const float *xi, const float *ref,
+                         const float *cells, float skip_above, int64_t batches, int64_t n_per, int k,
+                         const int32_t *cand, int32_t *idx_out, void *scratch,
                          mmpde_stream_t stream);
 
 /* torch_cluster.radius_graph(pos, r, batch, loop=False, max_num_neighbors)
@@ -327,6 +363,11 @@ typedef struct {
                                 holds degree[i] sources, the rest of its k entries are
                                 ignored; PyG mean = sum / max(degree, 1)), e.g. from
                                 mmpde_radius_graph; NULL: every row holds k */
+    int64_t seg_n;           /* rows per trajectory segment (the graph's batch segments:
+                                no edge crosses one); F16X3 takes the activation split
+                                scale per segment, so a trajectory's output does not
+                                depend on the others in the launch.  0 (or a value
+                                that does not divide n, or < 32): one segment */
 } mmpde_gnn_exec;
 
 /* Most layers mmpde_gnn_forward_ex accepts (sizes the workspace's packed

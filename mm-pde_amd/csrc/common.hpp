@@ -64,27 +64,6 @@ __device__ __forceinline__ float wave_max(float v) {
     return v;
 }
 
-// Range slots: kAmaxShards shards of a non-negative float maximum kept as uint
-// bits (IEEE order = integer order for v >= 0).  Producers publish one wave
-// max per wave into the shard of their global wave index (spreads the
-// memory-side atomics); consumers take the max over all shards.  Zeroed per
-// forward.
-constexpr int kAmaxShards = 256;
-
-__device__ __forceinline__ void amax_publish(float lane_max, uint32_t *slot) {
-    const float m = wave_max(lane_max);
-    const uint32_t shard = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (kAmaxShards - 1);
-    if ((threadIdx.x & 63) == 0) atomicMax(slot + shard, __float_as_uint(m));
-}
-
-__device__ __forceinline__ float amax_read(const uint32_t *slot) {
-    const int l = threadIdx.x & 63;
-    float m = 0.0f;
-#pragma unroll
-    for (int i = 0; i < kAmaxShards / 64; ++i) m = fmaxf(m, __uint_as_float(slot[l + 64 * i]));
-    return wave_max(m);
-}
-
 __device__ __forceinline__ float act_apply(float v, int act) {
     if (act == MMPDE_ACT_TANH) return tanhf(v);
     if (act == MMPDE_ACT_RELU) return fmaxf(v, 0.0f);

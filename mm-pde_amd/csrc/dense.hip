@@ -162,13 +162,15 @@ __global__ __launch_bounds__(kSkW * 64) void linear_skinny_kernel(const float *_
     }
 }
 
-// K splits of a skinny linear: enough workgroups for ~4 per CU, chunks of
-// 64 kSkW k each, at most 16 splits
+// K splits of a skinny linear: enough workgroups for ~4 per CU over the
+// output column tiles, chunks of 64 kSkW k each, at most 16 splits.  The split
+// (hence every output row's summation order) depends on n and k only, not on
+// the row count m, so a row's result does not depend on the rows beside it.
 inline int skinny_splits(int64_t m, int64_t n, int64_t k, int cus) {
-    const int64_t tiles = ((n + 15) / 16) * ((m + 15) / 16);
-    if (tiles > 4096) return 1;  // = kSkTickets
+    const int64_t ctiles = (n + 15) / 16;
+    if (ctiles * ((m + 15) / 16) > 4096) return 1;  // = kSkTickets
     const int64_t chunks = (k + 64 * kSkW - 1) / (64 * kSkW);
-    int64_t z = (4 * (int64_t)cus + tiles - 1) / tiles;
+    int64_t z = (4 * (int64_t)cus + ctiles - 1) / ctiles;
     z = z < chunks ? z : chunks;
     z = z < kSkMaxZ ? z : kSkMaxZ;
     return z > 1 ? (int)z : 1;
@@ -266,7 +268,7 @@ __global__ __launch_bounds__(256) void traj_mse_kernel(const float *__restrict__
 
 }  // namespace
 
-extern "C" int mmpde_version(void) { return 11100; }
+extern "C" int mmpde_version(void) { return 11200; }
 
 extern "C" int mmpde_traj_mse(const float *pred, const float *labels, int64_t batches, int64_t n_per,
                               float *out, mmpde_stream_t stream) {

@@ -16,14 +16,24 @@
 // registers; the slot's split VALU (relu(a + b) -> scaled fp16 hi / lo) and its
 // relu-sums are the MFMA-gap fillers of the same instruction stream.
 //
-// Work split: the S = ntiles * k neighbour slots (slot = one neighbour of one
-// 16-target tile) form one stream; wave rank w (XCD-contiguous ranks) walks
-// slots [w S / G, (w + 1) S / G), so every wave gets the same work to one slot.
-// A unit is the wave's run of slots inside one tile.  The unit that starts at
-// its tile's first slot stores its sums to out; a wave that starts inside a
-// tile stores that first unit to side[w] (16 x 128), and the node stage adds
-// those side buffers in rank (= slot) order before dividing by the degree.
-// Deterministic: fixed summation order, no atomics.
+// Work split: rows form trajectory segments of seg_n rows (layer.hpp
+// EdgeSplit), each cut into 16-row tiles; a segment's S = tiles * k neighbour
+// slots (slot = one neighbour of one 16-target tile) form one stream, cut into
+// U summation units, unit u = slots [u S / U, (u + 1) S / U).  A run is the part
+// of a unit inside one tile: its relu-sums accumulate in slot order; the run
+// that starts at its tile's first slot stores them to out, a run that starts
+// at a unit boundary inside a tile to side[s U + u] (16 x 128), and the node
+// stage adds those side blocks in unit order before dividing by the degree.
+// So a row's sum is a fixed function of (k, U) and the row's tile position.
+// Physical waves: wave j of segment s (XCD-contiguous ranks s * wpsp + j) takes
+// the m = U / wpsp units [j m, (j + 1) m), so every wave of a segment gets the
+// same work to one slot when m = 1.  A wave never leaves its segment, so its
+// split scale comes from its segment's range records alone.  U depends on the
+// segment size and, below 16 segments, on the segment count (layer.hpp
+// edge_wave_plan); a trajectory's result therefore does not depend on the
+// trajectories launched beside it whenever the launches have the same U (every
+// launch of >= 16 cylinder trajectories).  Deterministic: fixed summation
+// order, no atomics.
 #include "common.hpp"
 #include "f16x3.hpp"
 #include "layer.hpp"
@@ -40,14 +50,19 @@ struct WaveArgs {
     const int32_t *nbr;
     const int32_t *deg;  // RAGGED: in-degree per target (nullable otherwise)
     int64_t n;
-    int k, ntiles;
-    int64_t S;                // slots = ntiles * k
+    int k;
+    int64_t seg_n;            // rows per segment
+    int tps;                  // 16-row tiles per segment
+    int64_t S;                // slots per segment = tps * k
+    int U;                    // summation units per segment
+    int m;                    // units per wave (wpsp = U / m waves per segment)
     const float *b2;          // message_net_2.0 bias
     const char *pk;           // this layer's packed images (W2 at kPkW2)
-    const uint32_t *amax_in;  // range slots of a, b
+    const float *rng;         // range records of a, b (layer.hpp)
     float *out;               // neighbour sums of the units that start a tile
     float *side;              // [G][16][128]: the unit a wave starts inside a tile
 };
+
 
 // Rank of wave-workgroup bid: blocks b and b + 8 share an XCD; ranks number the
 // blocks XCD by XCD, so each XCD walks a contiguous share of the slots (speed only).
@@ -106,12 +121,22 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
     const int k = p.k;
     const int64_t nmax = p.n - 1;
     const int rank = wave_rank(blockIdx.x, gridDim.x);
-    const int64_t s0 = (int64_t)rank * p.S / gridDim.x, s1 = (int64_t)(rank + 1) * p.S / gridDim.x;
+    const int wpsp = p.U / p.m;
+    const int seg = rank / wpsp, jw = rank - seg * wpsp;
+    const int u_end = min((jw + 1) * p.m, p.U);
+    int u_next = jw * p.m + 1;  // the next unit to start
+    const int64_t s0 = (int64_t)jw * p.m * p.S / p.U, s1 = (int64_t)u_end * p.S / p.U;
     if (s0 >= s1) return;
-    // the first unit goes to side[rank] when the wave starts inside a tile
-    const int t_side = s0 % k ? (int)(s0 / k) : -1;
-    // |a + b| <= max|a| + max|b|, scaled below 2^11 (split8_relu_rtz)
-    const float sc = 0.125f * split_scale(amax_read(p.amax_in) + amax_read(p.amax_in + kAmaxShards));
+    // slot where unit u_next starts (s1 past the wave's last unit)
+    int64_t ub = u_next < u_end ? (int64_t)u_next * p.S / p.U : s1;
+    // rows of this wave's segment: base + local row, local rows <= last
+    const int64_t base = (int64_t)seg * p.seg_n;
+    const int last = (int)p.seg_n - 1;
+    // destination of the run being computed: -1 = out (it starts its tile),
+    // else the side block of the unit it starts
+    int run_side = s0 % k ? seg * p.U + jw * p.m : -1;
+    // |a + b| <= max|a| + max|b| over the segment, scaled below 2^11 (split8_relu_rtz)
+    const float sc = 0.125f * split_scale(segment_range(p.rng, p.seg_n, seg));
     // message_net_2: B operands (AGPRs), accumulator start (bias, scaled), unscale
     half8 wh[8][4], wl[8][4];
     float bias[8], inv[8];
@@ -131,10 +156,12 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
     }
     // F16X3 operand piece i of this lane: k = 32 (i >> 1) + 8 g + 4 (i & 1) .. + 3
     auto piece = [&](int i) { return 32 * (i >> 1) + 8 * g + 4 * (i & 1); };
-    auto unit_tile = [&](const SlotCtr &c) { return min(c.tile, p.ntiles - 1); };
+    auto unit_tile = [&](const SlotCtr &c) { return min(c.tile, p.tps - 1); };
+    // global row of local row q of this segment (clamped to the segment)
+    auto grow = [&](int q) { return base + min(q, last); };
     // every prefetch issues the same loads (clamped past the end)
     auto src_of = [&](const SlotCtr &c) -> uint32_t {
-        const int64_t row = min((int64_t)unit_tile(c) * ET + r, nmax);
+        const int64_t row = grow(unit_tile(c) * ET + r);
         return (uint32_t)p.nbr[row * k + c.e];
     };
     auto gather = [&](float4 *dst, uint32_t src) {
@@ -160,7 +187,7 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
     cI.next(k);
     float4 av[8];  // a rows of the split slot's tile (scaled), this lane's pieces
     auto load_a = [&](int tile) {
-        const float *ar = p.a + min((int64_t)tile * ET + r, nmax) * LH;
+        const float *ar = p.a + grow(tile * ET + r) * LH;
         float4 v[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) v[i] = *(const float4 *)(ar + piece(i));
@@ -168,9 +195,9 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
         for (int i = 0; i < 8; ++i) av[i] = make_float4(v[i].x * sc, v[i].y * sc, v[i].z * sc, v[i].w * sc);
     };
     auto load_deg = [&](int *d, const SlotCtr &c) {
-        const int64_t row0 = (int64_t)unit_tile(c) * ET;
+        const int row0 = unit_tile(c) * ET;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) d[t] = p.deg[min(row0 + 4 * g + t, nmax)];
+        for (int t = 0; t < 4; ++t) d[t] = p.deg[grow(row0 + 4 * g + t)];
     };
     // pair j (0..15) of a slot's A operand: K step j >> 2, values 2 (j & 3), +1
     // of that step (x of piece 2 (j >> 2) + ((j >> 1) & 1), components
@@ -208,7 +235,7 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
     // body (before the first slot: relu(-big) = 0 adds nothing)
     f32x4 acc6 = (f32x4){-3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f}, acc7 = acc6;
     int e_prev = 0, row0_prev = 0;
-    bool side_prev = false;
+    int side_prev = -1;
     bool close_prev = false;  // the previous slot was its unit's last: write after its deferred sums
     auto relu_add = [&](f32x4 &Sc, float x, int t, int e, const int *d) {
         float v = __builtin_amdgcn_fmed3f(x, 0.0f, 3.402823466e38f);  // relu
@@ -218,16 +245,17 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
     // the finished unit's sums, unscaled (a power-of-two multiply: exact), to out
     // (rows of the tile) or to side[rank].  The node stage adds the side buffers
     // and divides by the degree (PyG mean = sum / count).  Stores are
-    // unconditional unless the tile runs past n (wave-uniform test), at
-    // immediate offsets from one base per lane.
-    auto write_unit = [&](int64_t row0, bool to_side) {
+    // unconditional unless the tile runs past the segment (wave-uniform test),
+    // at immediate offsets from one base per lane.  row0: local row.
+    auto write_unit = [&](int row0, int side_idx) {
+        const bool to_side = side_idx >= 0;
         if (DIAG & 64) {  // no stores: keep the sums alive only
 #pragma unroll
             for (int c = 0; c < 8; ++c) asm volatile("" ::"v"(S[c]));
             return;
         }
-        float *o = (to_side ? p.side + (int64_t)rank * ET * LH : p.out + row0 * LH) + 4 * g * LH + r;
-        if (to_side || row0 + ET <= p.n) {
+        float *o = (to_side ? p.side + (int64_t)side_idx * ET * LH : p.out + (base + row0) * LH) + 4 * g * LH + r;
+        if (to_side || row0 + ET <= last + 1) {
 #pragma unroll
             for (int c = 0; c < 8; ++c)
 #pragma unroll
@@ -237,7 +265,7 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
             for (int c = 0; c < 8; ++c)
 #pragma unroll
                 for (int t = 0; t < 4; ++t)
-                    if (row0 + 4 * g + t < p.n) o[t * LH + 16 * c] = S[c][t] * inv[c];
+                    if (row0 + 4 * g + t <= last) o[t * LH + 16 * c] = S[c][t] * inv[c];
         }
     };
     auto body = [&](float4 *X, uint32_t (*h)[4], uint32_t (*l)[4], uint32_t (*nh)[4], uint32_t (*nl)[4]) {
@@ -310,15 +338,24 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
         acc6 = acc[6];
         acc7 = acc[7];
         e_prev = e;
-        close_prev = cC.e + 1 == k || cC.pos + 1 == s1;
+        // the run closes at its tile's end, at a unit boundary and at the end
+        const bool new_unit = cC.pos + 1 == ub;
+        close_prev = cC.e + 1 == k || cC.pos + 1 == s1 || new_unit;
         row0_prev = unit_tile(cC) * ET;
-        side_prev = cC.tile == t_side;
+        side_prev = run_side;
         if (RAGGED) {
 #pragma unroll
             for (int t = 0; t < 4; ++t) dg_prev[t] = dg[t];
         }
         cC.next(k);
         cS.next(k);
+        if (close_prev) {  // the next run starts at cC
+            run_side = new_unit && cC.e != 0 ? seg * p.U + u_next : -1;
+            if (new_unit) {
+                ++u_next;
+                ub = u_next < u_end ? (int64_t)u_next * p.S / p.U : s1;
+            }
+        }
         if (RAGGED && close_prev) load_deg(dg, cC);
     };
     // (the S reset of a unit's first slot happens at group 5 of its body, after
@@ -340,23 +377,56 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
 
 }  // namespace
 
-// Waves of the slot-range split: one per SIMD, at most one per slot, at most
-// side_cap (the side buffer's capacity in 16 x 128 blocks).
-int edge_wave_grid(int64_t S, int cus, int64_t side_cap) {
-    int64_t g = 4 * (int64_t)cus;
-    if (g > S) g = S;
-    if (g > side_cap) g = side_cap;
-    return (int)(g < 1 ? 1 : g);
+// Summation units and waves of one launch (layer.hpp edge_wave_plan).
+EdgePlan edge_wave_plan(int64_t nseg, int64_t S_seg, int cus, int64_t side_cap) {
+    EdgePlan pl;
+    // U0: a power of two depending on the segment only, units of 44..88 slots
+    int64_t u0 = 1;
+    while (u0 * 2 * 44 <= S_seg) u0 *= 2;
+    // U1: the waves per segment that fill one wave per SIMD
+    int64_t u1 = 4 * (int64_t)cus / nseg;
+    if (u1 < 1) u1 = 1;
+    const int64_t m = (u0 + u1 - 1) / u1;   // units per wave
+    int64_t U = u1 * m;                      // = u0 when u1 is a power of two <= u0
+    const int64_t cap = S_seg < side_cap / nseg ? S_seg : side_cap / nseg;  // >= 1 slot per unit
+    if (U > cap) {                           // tiny segments: one unit per wave
+        U = cap < 1 ? 1 : cap;
+        pl.m = 1;
+    } else {
+        pl.m = (int)m;
+    }
+    pl.U = (int)U;
+    pl.waves = nseg * (U / pl.m);
+    return pl;
 }
 
+namespace {
+// Kernel arguments and grid of one launch (slot split of layer.hpp EdgeSplit).
+int edge_wave_setup(const float *a, const float *b, const int32_t *nbr, const int32_t *deg, int64_t n,
+                    int k, int64_t seg_n, const float *msg2_b, const char *pk, const float *rng,
+                    float *out, float *side, int64_t side_cap, int cus, WaveArgs *w, EdgeSplit *split) {
+    seg_n = effective_seg(n, seg_n);
+    const int64_t nseg = n / seg_n, tps = (seg_n + ET - 1) / ET, S = tps * k;
+    if (!(tps < (int64_t)INT32_MAX && S < ((int64_t)1 << 40) && side_cap >= nseg)) return 0;
+    const EdgePlan pl = edge_wave_plan(nseg, S, cus, side_cap);
+    // every wave takes m whole units: U must be a multiple of m
+    if (pl.U % pl.m || pl.waves > (int64_t)INT32_MAX || nseg * pl.U > (int64_t)INT32_MAX) return 0;
+    *w = WaveArgs{a, b, nbr, deg, n, k, seg_n, (int)tps, S, pl.U, pl.m, msg2_b, pk, rng, out, side};
+    *split = EdgeSplit{side, S, pl.U, k, seg_n};
+    return (int)pl.waves;
+}
+}  // namespace
+
 // Profiling aid (tools/ubench): the non-ragged kernel with DIAG bits, one wave
-// per SIMD; side = a [4 cus][16][128] buffer.
+// per SIMD, one segment of n rows; side = a [4 cus][16][128] buffer.
 int launch_edge_wave_diag(const float *a, const float *b, const int32_t *nbr, int64_t n, int k,
-                          const float *msg2_b, const char *pk, const uint32_t *amax_in, float *out,
+                          const float *msg2_b, const char *pk, const float *rng, float *out,
                           float *side, int cus, int diag, hipStream_t st) {
-    const int64_t ntiles = (n + ET - 1) / ET, S = ntiles * k;
-    WaveArgs w{a, b, nbr, nullptr, n, k, (int)ntiles, S, msg2_b, pk, amax_in, out, side};
-    const int grid = edge_wave_grid(S, cus, 4 * (int64_t)cus);
+    WaveArgs w;
+    EdgeSplit split;
+    const int grid = edge_wave_setup(a, b, nbr, nullptr, n, k, n, msg2_b, pk, rng, out, side,
+                                     4 * (int64_t)cus, cus, &w, &split);
+    MMPDE_REQUIRE(grid > 0);
 #define MMPDE_DIAG(D) \
     case D: hipLaunchKernelGGL((gnn_edge_wave_kernel<false, D>), dim3(grid), dim3(64), 0, st, w); break
     switch (diag) {
@@ -379,14 +449,13 @@ int launch_edge_wave_diag(const float *a, const float *b, const int32_t *nbr, in
 }
 
 int launch_edge_wave(const float *a, const float *b, const int32_t *nbr, const int32_t *deg, int64_t n,
-                     int k, const float *msg2_b, const char *pk, const uint32_t *amax_in, float *out,
-                     float *side, int64_t side_cap, int cus, EdgeSplit *split, hipStream_t st) {
-    MMPDE_REQUIRE(a && b && nbr && msg2_b && pk && amax_in && out && side && split && n > 0 && k > 0);
-    const int64_t ntiles = (n + ET - 1) / ET, S = ntiles * k;
-    MMPDE_REQUIRE(ntiles < (int64_t)INT32_MAX && S < ((int64_t)1 << 40) && side_cap >= 1);
-    const int grid = edge_wave_grid(S, cus, side_cap);
-    WaveArgs w{a, b, nbr, deg, n, k, (int)ntiles, S, msg2_b, pk, amax_in, out, side};
-    *split = EdgeSplit{side, S, grid, k};
+                     int k, int64_t seg_n, const float *msg2_b, const char *pk, const float *rng,
+                     float *out, float *side, int64_t side_cap, int cus, EdgeSplit *split, hipStream_t st) {
+    MMPDE_REQUIRE(a && b && nbr && msg2_b && pk && rng && out && side && split && n > 0 && k > 0);
+    WaveArgs w;
+    const int grid = edge_wave_setup(a, b, nbr, deg, n, k, seg_n, msg2_b, pk, rng, out, side, side_cap,
+                                     cus, &w, split);
+    MMPDE_REQUIRE(grid > 0);
     if (deg) hipLaunchKernelGGL((gnn_edge_wave_kernel<true>), dim3(grid), dim3(64), 0, st, w);
     else hipLaunchKernelGGL((gnn_edge_wave_kernel<false>), dim3(grid), dim3(64), 0, st, w);
     MMPDE_RET_LAUNCH();

@@ -41,8 +41,6 @@ constexpr int64_t kPkU2 = kPkU1 + 131072 + 512;           // 128 x 128
 constexpr int64_t kPkW1 = kPkU2 + 65536 + 512;            // 256 x 128
 constexpr int64_t kLayerPack = kPkW1 + 131072 + 1024;     // bytes per layer (16-B multiple)
 static_assert(kLayerPack % 16 == 0, "pack alignment");
-// per layer: |a| and |b| range slots of kAmaxShards uint32 each
-constexpr int64_t kAmaxBytes = (int64_t)MMPDE_GNN_MAX_LAYERS * 2 * kAmaxShards * 4;
 
 struct PackSrc {
     const float *w[MMPDE_GNN_MAX_LAYERS];

@@ -55,14 +55,12 @@ struct EpiProj {  // message_net_1 split (see header comment)
     int64_t ldw1;
     const float *u, *pos;
     mmpde_gnn_scales sc;
-    uint32_t *amax;  // nullable: range slot of the consumer layer ([0,64): |a|, [64,128): |b|)
     __device__ void operator()(const f32x16 &acc, int64_t row0, int col0, int lane, int64_t m,
                                int part) const {
         const int c = col0 + (lane & 31);
         const float wdu = w_du[c * ldw1], wdx = w_dx[c * ldw1], wdy = w_dy[c * ldw1];
         const float wt = w_t[c * ldw1], bb = b1[c];
         float *dst = part == 0 ? out_a : out_b;
-        float vmax = 0.0f;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int64_t row = row0 + acc_row(r, lane);
@@ -79,10 +77,8 @@ struct EpiProj {  // message_net_1 split (see header comment)
                     v = acc[r] - node;
                 }
                 dst[row * H + c] = v;
-                vmax = fmaxf(vmax, fabsf(v));
             }
         }
-        if (amax) amax_publish(vmax, amax + kAmaxShards * part);
     }
 };
 
@@ -351,9 +347,9 @@ inline bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
 extern "C" int64_t mmpde_gnn_workspace_bytes(int64_t n) {
     // h ping-pong, a, b, the edge stage's sums and 3 x [n,128] for the wave edge
     // kernel's side blocks = 8 x [n,128] fp32 (the unfused per-layer API uses 4
-    // of them as a, b, mean, v), then the F16X3 range slots and room for
-    // per-call weight images
-    return kGnnBufs * n * H * (int64_t)sizeof(float) + kAmaxBytes +
+    // of them as a, b, mean, v), then the F16X3 range records (layer.hpp) and
+    // room for per-call weight images
+    return kGnnBufs * n * H * (int64_t)sizeof(float) + range_tiles(n) * 16 +
            (int64_t)MMPDE_GNN_MAX_LAYERS * kLayerPack;
 }
 
@@ -390,7 +386,7 @@ extern "C" int mmpde_gnn_edge_mean_deg(const float *a, const float *b, const int
     p.msg2_w = msg2_w;
     p.msg2_b = msg2_b;
     // exact fp32 ring kernel (no pack): the training forward of gnn_2d.py:53-63
-    return launch_edge_stage(a, b, nbr, deg, n, k, &p, nullptr, nullptr, mean_out, nullptr, 0, nullptr,
+    return launch_edge_stage(a, b, nbr, deg, n, k, n, &p, nullptr, nullptr, mean_out, nullptr, 0, nullptr,
                              as_stream(stream));
 }
 
@@ -510,16 +506,18 @@ extern "C" int mmpde_gnn_forward_ex(const float *u, const float *pos, int64_t n,
     float *hb[2] = {ws, ws + n * H};
     float *wa = ws + 2 * n * H, *wb = ws + 3 * n * H, *wmean = ws + 4 * n * H;
     const char *pack = nullptr;
-    // range slots of every layer's message inputs (F16X3 split scale)
-    uint32_t *amax = (uint32_t *)(ws + kGnnBufs * n * H);
+    // range records of the current layer's message inputs (F16X3 split scale):
+    // written by the embed / node stage, read by the next edge stage
+    float *rng = ws + kGnnBufs * n * H;
+    // rows per trajectory segment: the split scale is taken per segment
+    const int64_t seg_n = exec ? exec->seg_n : 0;
     int rc;
     if (mode == MMPDE_EDGE_GEMM_F16X3 && n_layers > 0) {
-        if (hipMemsetAsync(amax, 0, kAmaxBytes, st) != hipSuccess) return MMPDE_ERR_INVALID_ARG;
         if (exec->packed) {
             MMPDE_REQUIRE(aligned16(exec->packed));
             pack = (const char *)exec->packed;
         } else {
-            char *wpk = (char *)(ws + kGnnBufs * n * H) + kAmaxBytes;
+            char *wpk = (char *)(ws + kGnnBufs * n * H) + range_tiles(n) * 16;
             rc = mmpde_gnn_pack_f16x3(layers, n_layers, wpk, stream);
             if (rc) return rc;
             pack = wpk;
@@ -528,7 +526,7 @@ extern "C" int mmpde_gnn_forward_ex(const float *u, const float *pos, int64_t n,
     if (n_layers > 0) {
         // embedding + layer 0's message_net_1 halves (later layers get theirs
         // from the previous layer's node stage)
-        rc = launch_embed_stage(u, pos, n, sc, emb, &layers[0], pack, pack ? amax : nullptr, hb[0],
+        rc = launch_embed_stage(u, pos, n, seg_n, sc, emb, &layers[0], pack, pack ? rng : nullptr, hb[0],
                                 wa, wb, st);
     } else {
         rc = mmpde_gnn_embed(u, pos, n, sc, emb, wmean, hb[0], stream);  // wmean: scratch
@@ -542,19 +540,20 @@ extern "C" int mmpde_gnn_forward_ex(const float *u, const float *pos, int64_t n,
         const mmpde_gnn_layer_params *next = l + 1 < n_layers ? &layers[l + 1] : nullptr;
         const char *pk = pack ? pack + (int64_t)l * kLayerPack : nullptr;
         const char *pkn = pack && next ? pack + (int64_t)(l + 1) * kLayerPack : nullptr;
-        const uint32_t *ain = pack ? amax + 2 * kAmaxShards * l : nullptr;
-        uint32_t *aout = pack && next ? amax + 2 * kAmaxShards * (l + 1) : nullptr;
+        // one record buffer serves every layer: edge stage l reads it before
+        // node stage l (stream order) writes layer l + 1's
+        float *rout = pack && next ? rng : nullptr;
         if (eb && hipEventRecord(eb, st) != hipSuccess) return MMPDE_ERR_INVALID_ARG;
         EdgeSplit split;
         const int32_t *deg = exec ? exec->degree : nullptr;
         // side blocks of the wave edge kernel: the workspace after the mean
-        rc = launch_edge_stage(wa, wb, nbr, deg, n, k, &layers[l], pk, ain, wmean, wmean + n * H,
-                               (kGnnBufs - 5) * n * H / (16 * H), &split, st);
+        rc = launch_edge_stage(wa, wb, nbr, deg, n, k, seg_n, &layers[l], pk, pack ? rng : nullptr, wmean,
+                               wmean + n * H, (kGnnBufs - 5) * n * H / (16 * H), &split, st);
         if (rc) return rc;
         if (ee && hipEventRecord(ee, st) != hipSuccess) return MMPDE_ERR_INVALID_ARG;
         // a, b are rewritten in place: this layer's edge stage has consumed them
-        rc = launch_node_stage(hb[cur], wmean, &split, deg, u, pos, n, sc, &layers[l], next, pk, pkn, aout,
-                               hb[cur ^ 1], wa, wb, st);
+        rc = launch_node_stage(hb[cur], wmean, &split, deg, u, pos, n, seg_n, sc, &layers[l], next, pk, pkn,
+                               rout, hb[cur ^ 1], wa, wb, st);
         if (rc) return rc;
         if (ne && hipEventRecord(ne, st) != hipSuccess) return MMPDE_ERR_INVALID_ARG;
         cur ^= 1;

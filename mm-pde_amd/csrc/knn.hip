@@ -31,6 +31,24 @@ namespace {
 constexpr int kQueriesPerBlock = 16;  // 4 per wave
 constexpr int kCap = 256;             // LDS list of candidates with key <= U, per wave
 
+// Moved-mesh displacement record (mmpde_knn_moved_cells), per trajectory:
+// dcell[kCells] (-1: empty cell), box (x0, y0, hx, hy, eps), the largest
+// displacement, then per role (0: graph, 1: query) the count of queries the
+// candidate table could not answer in the last call (written by the
+// fallback; diagnostics).
+constexpr int kCellG = 16;                           // cells per axis
+constexpr int kCells = kCellG * kCellG;
+constexpr int kCellRec = kCells + 16;                // floats per trajectory record
+__device__ __forceinline__ int32_t *cell_last_miss(const float *cells, int b) {
+    return (int32_t *)(cells + (int64_t)b * kCellRec + kCells + 8);  // [role]
+}
+// set (plain stores of 1) by knn_cand_kernel when any query of the trajectory
+// missed, zeroed with the record: a fallback workgroup of a trajectory without
+// misses returns at once
+__device__ __forceinline__ int32_t *cell_any_miss(const float *cells, int b) {
+    return (int32_t *)(cells + (int64_t)b * kCellRec + kCells + 10);  // [role]
+}
+
 // fp32 squared distance as raw bits: the graph key, and the query's filter key.
 __device__ __forceinline__ uint32_t key_f32(float2 p, float2 q) {
 #pragma clang fp contract(off)
@@ -324,12 +342,22 @@ __device__ __forceinline__ void knn_finish(const float2 *sP, typename KeyTraits<
     }
 }
 
-template <int CPL, bool QUERY>
+// miss != nullptr (the candidate path's fallback, grid.x = ceil(n_q / QPB)):
+// miss[b n_q + i] != 0 marks the queries of trajectory b the table could not
+// answer.  Every workgroup counts the trajectory's flags and ranks them in
+// index order (wave ballots, no atomics).  With more than half missed it
+// answers its own QPB queries as the plain search does (re-answering a few is
+// harmless: same result); otherwise the missed queries of ranks x, x + grid.x,
+// ... (at most QPB), so a few misses spread over many workgroups; with none it
+// returns before staging the points.  Workgroup 0 records the count.
+template <int CPL, bool QUERY, int QPB = kQueriesPerBlock>
 __global__ __launch_bounds__(256) void knn_kernel(const float2 *__restrict__ pts,
                                                   const float2 *__restrict__ qry, int n_src,
                                                   int n_q, int k, int32_t *__restrict__ out,
                                                   int32_t *__restrict__ degenerate,
-                                                  const uint8_t *__restrict__ done = nullptr) {
+                                                  const uint8_t *__restrict__ miss = nullptr,
+                                                  float *__restrict__ cells = nullptr,
+                                                  int role = 0) {
     typedef KeyTraits<QUERY> KT;
     typedef typename KT::key_t key_t;
     __shared__ float2 sP[CPL * 64];
@@ -338,10 +366,38 @@ __global__ __launch_bounds__(256) void knn_kernel(const float2 *__restrict__ pts
     __shared__ int sSel[4][64];
 
     const int b = blockIdx.y;
-    if (done) {  // queries answered by knn_cand_kernel are skipped; so is an all-done block
-        const int qi = blockIdx.x * kQueriesPerBlock + (int)threadIdx.x;
-        const int need = threadIdx.x < kQueriesPerBlock && qi < n_q && !done[(int64_t)b * n_q + qi];
-        if (!__syncthreads_or(need)) return;
+    int q_count = n_q;  // queries of this trajectory to answer
+    __shared__ int sList[QPB];
+    if (miss) {
+        if (!cell_any_miss(cells, b)[role]) {  // workgroup-uniform
+            if (blockIdx.x == 0 && threadIdx.x == 0) cell_last_miss(cells, b)[role] = 0;
+            return;
+        }
+        __shared__ int sWave[4];
+        const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+        const int gx = (int)gridDim.x, x = (int)blockIdx.x;
+        const uint64_t below_l = l == 0 ? 0ull : (~0ull >> (64 - l));
+        int total = 0;  // misses before the current chunk
+        for (int c0 = 0; c0 < n_q; c0 += 256) {
+            const int i = c0 + tid;
+            const bool f = i < n_q && miss[(int64_t)b * n_q + i];
+            const uint64_t bal = __ballot(f);
+            if (l == 0) sWave[w] = __popcll(bal);
+            __syncthreads();
+            int before = total;
+            for (int v = 0; v < w; ++v) before += sWave[v];
+            const int r = before + __popcll(bal & below_l);  // rank of this miss
+            if (f && r % gx == x && r / gx < QPB) sList[r / gx] = i;
+            total += sWave[0] + sWave[1] + sWave[2] + sWave[3];
+            __syncthreads();  // sWave is rewritten by the next chunk
+        }
+        if (x == 0 && tid == 0) cell_last_miss(cells, b)[role] = total;
+        if (2 * total > n_q) {
+            miss = nullptr;  // most missed: the plain search's own queries
+        } else {
+            q_count = total > x ? min((total - x + gx - 1) / gx, QPB) : 0;  // entries of this workgroup
+            if (q_count == 0) return;  // workgroup-uniform: nothing to answer
+        }
     }
     const float2 *P = pts + (int64_t)b * n_src;
     for (int i = threadIdx.x; i < n_src; i += 256) sP[i] = P[i];
@@ -351,10 +407,11 @@ __global__ __launch_bounds__(256) void knn_kernel(const float2 *__restrict__ pts
     const int lane = threadIdx.x & 63;
     const int kk = QUERY ? k : k + 1;
     const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    const int q_end = min((int)(blockIdx.x + 1) * kQueriesPerBlock, n_q);
+    const int q_beg = miss ? 0 : (int)blockIdx.x * QPB;
+    const int q_end = miss ? q_count : min((int)(blockIdx.x + 1) * QPB, n_q);
 
-    for (int qi = blockIdx.x * kQueriesPerBlock + wave; qi < q_end; qi += 4) {
-        if (done && done[(int64_t)b * n_q + qi]) continue;  // wave-uniform
+    for (int qe = q_beg + wave; qe < q_end; qe += 4) {
+        const int qi = miss ? sList[qe] : qe;
         const float2 q = QUERY ? qry[(int64_t)b * n_q + qi] : sP[qi];
         uint32_t fkey[CPL];
         uint32_t lmin = ~0u;
@@ -522,28 +579,35 @@ int launch_knn(const float *pts, const float *qry, int64_t batches, int64_t n_sr
 }
 
 // ---------------------------------------------------------------------------
-// Moving-mesh graph from a static candidate list (exact, with a fallback).
-// The DMM moves every node x_i = xi_i + d_i only a little, so the answer for
-// x_p is almost always among cand[p] = the 128 nearest of xi_p in the fixed
-// mesh xi ((key, index) order, xi_p itself first).  A point j outside cand[p]
-// has |xi_j - xi_p| >= R = sqrt(key of cand[p][127]) (up to rounding), hence
-// |x_j - x_p| >= R - |d_p| - max_i |d_i| = L.  If the kk-th candidate distance
-// is below L (every bound with a 2^-20 relative margin, which covers the fp32
-// key's rounding), no non-candidate can enter the first kk in (key, index)
-// order, so the candidates sorted by (key, index) ARE the answer, ties
-// included.  Otherwise knn_kernel answers the query (done[q] = 0).
+// Moving-mesh kNN from a static candidate list (exact, with a fallback).
+// The DMM moves every node x_i = xi_i + d_i only a little, so the answer for a
+// query q near a fixed reference point r_p (graph: r_p = xi_p, q = x_p; query:
+// r_p = the fixed query point, q = qry_p) is almost always among cand[p] = the
+// 128 nearest of r_p in the fixed mesh xi ((key, index) order).  A point j
+// outside cand[p] has |xi_j - r_p| >= R = sqrt(key of cand[p][127]) (up to
+// rounding), hence |x_j - q| >= max(R - |q - r_p|, dist(q, cell(xi_j))) -
+// |d_j|, where cell(xi_j) is the point's cell in a 16 x 16 grid over the box of
+// xi and |d_j| <= dcell[cell] = the largest displacement of that cell's points
+// (mmpde_knn_moved_cells, per trajectory and step).  L = the minimum of that
+// bound over the cells.  If the kk-th candidate distance is below L (every
+// bound with a 2^-20 relative margin, which covers the fp32 rounding), no
+// non-candidate can enter the first kk in (key, index) order, so the
+// candidates sorted by (key, index) ARE the answer, ties included.  Otherwise
+// the query joins its trajectory's fallback list, which knn_kernel answers.  A
+// far-moved node only weakens the bound of the queries near its cell.
 // ---------------------------------------------------------------------------
 constexpr int kCandN = 128;
 constexpr float kUp = 1.0f + 1.0f / 1048576.0f, kDown = 1.0f - 1.0f / 1048576.0f;
 
-// cand[p] = the kCandN nearest of xi_p in xi, (key, index) order: one
+// cand[p] = the kCandN nearest of r_p in xi, (key, index) order: one
 // workgroup per point, (key << 32 | index) pairs bitonic-sorted in LDS.  Built
-// once per fixed mesh.
-__global__ __launch_bounds__(256) void knn_table_kernel(const float2 *__restrict__ xi, int n_per,
+// once per fixed mesh (and query set).
+__global__ __launch_bounds__(256) void knn_table_kernel(const float2 *__restrict__ xi,
+                                                        const float2 *__restrict__ ref, int n_per,
                                                         int32_t *__restrict__ cand) {
     __shared__ uint64_t sk[4096];
     const int p = blockIdx.x;
-    const float2 q = xi[p];
+    const float2 q = ref[p];
     for (int j = threadIdx.x; j < 4096; j += 256)
         sk[j] = j < n_per ? (((uint64_t)key_f32(xi[j], q) << 32) | (uint32_t)j) : ~0ull;
     __syncthreads();
@@ -562,55 +626,132 @@ __global__ __launch_bounds__(256) void knn_table_kernel(const float2 *__restrict
     if (threadIdx.x < kCandN) cand[(int64_t)p * kCandN + threadIdx.x] = (int32_t)(uint32_t)sk[threadIdx.x];
 }
 
-// dmax[b] >= max_i |x_bi - xi_i| (one workgroup per trajectory)
-__global__ __launch_bounds__(256) void knn_dmax_kernel(const float2 *__restrict__ x,
-                                                       const float2 *__restrict__ xi, int n_per,
-                                                       float *__restrict__ dmax) {
-    __shared__ float red[4];
-    const int b = blockIdx.x;
-    float m = 0.0f;
-    for (int i = threadIdx.x; i < n_per; i += 256) {
+// Per trajectory b (one workgroup each): the box of xi (x0, y0, cell sizes
+// hx, hy, their inverses, a margin eps that covers the rounding of the cell
+// assignment) and dcell[c] >= max |x_bj - xi_j| over the points j with xi_j in
+// cell c (-1: empty cell).  rec[b] = {dcell[256], box[8]}.
+__global__ __launch_bounds__(256) void knn_cells_kernel(const float2 *__restrict__ x,
+                                                        const float2 *__restrict__ xi, int n_per,
+                                                        float *__restrict__ rec) {
+    __shared__ float red[4][4];
+    __shared__ uint32_t cell[kCells];
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    float mnx = 3.0e38f, mny = 3.0e38f, mxx = -3.0e38f, mxy = -3.0e38f;
+    for (int i = tid; i < n_per; i += 256) {
+        const float2 c = xi[i];
+        mnx = fminf(mnx, c.x);
+        mny = fminf(mny, c.y);
+        mxx = fmaxf(mxx, c.x);
+        mxy = fmaxf(mxy, c.y);
+    }
+    mnx = -wave_max(-mnx);
+    mny = -wave_max(-mny);
+    mxx = wave_max(mxx);
+    mxy = wave_max(mxy);
+    if (lane == 0) {
+        red[wave][0] = mnx;
+        red[wave][1] = mny;
+        red[wave][2] = mxx;
+        red[wave][3] = mxy;
+    }
+    cell[tid] = 0u;  // empty (kCells == 256 threads)
+    __syncthreads();
+    const float x0 = fminf(fminf(red[0][0], red[1][0]), fminf(red[2][0], red[3][0]));
+    const float y0 = fminf(fminf(red[0][1], red[1][1]), fminf(red[2][1], red[3][1]));
+    const float x1 = fmaxf(fmaxf(red[0][2], red[1][2]), fmaxf(red[2][2], red[3][2]));
+    const float y1 = fmaxf(fmaxf(red[0][3], red[1][3]), fmaxf(red[2][3], red[3][3]));
+    const float hx = (x1 - x0) / kCellG, hy = (y1 - y0) / kCellG;
+    const float ihx = hx > 0.0f ? 1.0f / hx : 0.0f, ihy = hy > 0.0f ? 1.0f / hy : 0.0f;
+    for (int i = tid; i < n_per; i += 256) {
         const float2 a = x[(int64_t)b * n_per + i], c = xi[i];
         const float dx = a.x - c.x, dy = a.y - c.y;
-        m = fmaxf(m, sqrtf(dx * dx + dy * dy));
+        const float d = sqrtf(dx * dx + dy * dy) * kUp;
+        const int cx = min(max((int)((c.x - x0) * ihx), 0), kCellG - 1);
+        const int cy = min(max((int)((c.y - y0) * ihy), 0), kCellG - 1);
+        // non-negative floats order like their bits; stored as bits + 1 so
+        // that 0 marks an empty cell
+        atomicMax(&cell[cy * kCellG + cx], __float_as_uint(d) + 1u);
     }
-    m = wave_max(m);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
     __syncthreads();
-    if (threadIdx.x == 0) dmax[b] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])) * kUp;
+    float *r = rec + (int64_t)b * kCellRec;
+    const uint32_t v = cell[tid];
+    r[tid] = v == 0u ? -1.0f : __uint_as_float(v - 1u);
+    const float dall = wave_max(v == 0u ? 0.0f : __uint_as_float(v - 1u));
+    __syncthreads();
+    if (lane == 0) red[wave][0] = dall;
+    __syncthreads();
+    if (tid == 0) {
+        const float eps = 1.0e-5f * fmaxf(x1 - x0, y1 - y0);
+        r[kCells + 0] = x0;
+        r[kCells + 1] = y0;
+        r[kCells + 2] = hx;
+        r[kCells + 3] = hy;
+        r[kCells + 4] = eps;
+        r[kCells + 5] = fmaxf(fmaxf(red[0][0], red[1][0]), fmaxf(red[2][0], red[3][0]));
+        for (int i = 0; i < 2; ++i) {
+            cell_last_miss(rec, b)[i] = 0;
+            cell_any_miss(rec, b)[i] = 0;
+        }
+    }
 }
 
-// L = a lower bound on |x_j - q| over every j outside cand[p]: R = the 128th
-// candidate's distance in xi (every non-candidate of xi_p is at least that far
-// from xi_p), less the query's offset from xi_p and the largest displacement
-// |x_j - xi_j|.  Subtrahends grouped so the one cancelling subtraction errs
-// relative to L itself; <= 0 when the bound proves nothing.
-__device__ __forceinline__ float cand_bound(const float2 *__restrict__ xi, int n_per,
-                                            const int32_t *__restrict__ cr, int pl, float2 q,
-                                            float dmax) {
-    const float2 xp = xi[pl];
+// Lower bounds on |x_j - q| over every j outside cand[p] (see above), <= 0 when
+// they prove nothing; every rounding step errs downward.  R = the 128th
+// candidate's distance from r_p, rq = R - |q - r_p|.  The global bound takes
+// the trajectory's largest displacement; the per-cell bound, per cell, the
+// distance from q to the cell's box (widened by eps) less the cell's largest
+// displacement (never below the global one, costlier: only when that fails).
+__device__ __forceinline__ float cand_rq(const float2 *__restrict__ xi, float2 rp, int n_per,
+                                         const int32_t *__restrict__ cr, float2 q) {
     const int jl = min(max(cr[kCandN - 1], 0), n_per - 1);
-    const float R = sqrtf(__uint_as_float(key_f32(xi[jl], xp))) * kDown;
-    const float ddx = q.x - xp.x, ddy = q.y - xp.y;
+    const float R = sqrtf(__uint_as_float(key_f32(xi[jl], rp))) * kDown;
+    const float ddx = q.x - rp.x, ddy = q.y - rp.y;
     const float dq = sqrtf(ddx * ddx + ddy * ddy) * kUp;
-    return (R - (dq + dmax) * kUp) * kDown;
+    return (R - dq * kUp) * kDown;
+}
+
+__device__ __forceinline__ float cand_bound_global(float rq, const float *__restrict__ rec) {
+    return (rq - rec[kCells + 5] * kUp) * kDown;
+}
+
+__device__ __forceinline__ float cand_bound_cells(float rq, float2 q, const float *__restrict__ rec, int lane) {
+    const float x0 = rec[kCells], y0 = rec[kCells + 1], hx = rec[kCells + 2], hy = rec[kCells + 3];
+    const float eps = rec[kCells + 4];
+    float L = 3.0e38f;
+#pragma unroll
+    for (int t = 0; t < kCells / 64; ++t) {
+        const int c = lane + 64 * t;
+        const float dc = rec[c];
+        if (dc >= 0.0f) {
+            const int cx = c % kCellG, cy = c / kCellG;
+            const float lx = x0 + cx * hx - eps, ux = x0 + (cx + 1) * hx + eps;
+            const float ly = y0 + cy * hy - eps, uy = y0 + (cy + 1) * hy + eps;
+            const float ex = fmaxf(fmaxf(lx - q.x, q.x - ux), 0.0f);
+            const float ey = fmaxf(fmaxf(ly - q.y, q.y - uy), 0.0f);
+            const float dist = sqrtf(ex * ex + ey * ey) * kDown;
+            L = fminf(L, (fmaxf(dist, rq) - dc * kUp) * kDown);
+        }
+    }
+    return -wave_max(-L);
 }
 
 // One wave per query point: the 128 candidates' keys (two per lane), one
 // 128-wide (key, index) sort; the first kk are the answer when the kk-th
 // candidate is closer than the bound.  QUERY = false: the moved-mesh graph
-// (fp32 keys, self dropped, global indices, as knn_finish's graph branch);
-// true: the kNN query of qry onto the moved mesh (fp64 keys, local indices).
+// (fp32 keys, self dropped, global indices, as knn_finish's graph branch; ref =
+// xi); true: the kNN query of qry onto the moved mesh (fp64 keys, local
+// indices; ref = the fixed query points the table was built for).
 template <bool QUERY>
 __global__ __launch_bounds__(256) void knn_cand_kernel(const float2 *__restrict__ x,
                                                        const float2 *__restrict__ qry,
-                                                       const float2 *__restrict__ xi, int n_per,
+                                                       const float2 *__restrict__ xi,
+                                                       const float2 *__restrict__ ref, int n_per,
                                                        int64_t n_tot, int k,
                                                        const int32_t *__restrict__ cand,
-                                                       const float *__restrict__ dmax,
+                                                       const float *__restrict__ cells,
                                                        int32_t *__restrict__ out,
                                                        int32_t *__restrict__ degenerate,
-                                                       uint8_t *__restrict__ done) {
+                                                       uint8_t *__restrict__ miss, float skip_above) {
     typedef KeyTraits<QUERY> KT;
     typedef typename KT::key_t key_t;
     const int lane = threadIdx.x & 63;
@@ -621,16 +762,38 @@ __global__ __launch_bounds__(256) void knn_cand_kernel(const float2 *__restrict_
     const float2 *X = x + (int64_t)b * n_per;
     const float2 q = QUERY ? qry[p] : X[pl];
     const int32_t *cr = cand + (int64_t)pl * kCandN;
-    const float L = cand_bound(xi, n_per, cr, pl, q, dmax[b]);
+    const float *rec = cells + (int64_t)b * kCellRec;
+    const float2 rp = ref[pl];
+    const float rq = cand_rq(xi, rp, n_per, cr, q);
     const int kk = QUERY ? k : k + 1;
-    // Skipped (the fallback answers; wave-uniform) when the bound proves
-    // nothing, or when already the unmoved kk-th candidate lies beyond it: the
-    // moved one then almost never passes, and the sort would be wasted.  A
-    // heuristic only -- the test below decides.
-    const int jk = min(max(cr[kk - 1], 0), n_per - 1);
-    if (!(L > 0.0f) || sqrtf(__uint_as_float(key_f32(xi[jk], xi[pl]))) >= L) {
-        if (lane == 0) done[p] = 0;
+    // a query the table cannot answer is flagged for the fallback
+    auto give_up = [&]() {
+        if (lane == 0) {
+            miss[p] = 1;
+            cell_any_miss(cells, b)[QUERY ? 1 : 0] = 1;
+        }
+    };
+    // a trajectory moved by more than skip_above: the table is not tried
+    if (skip_above > 0.0f && rec[kCells + 5] > skip_above) {
+        give_up();
         return;
+    }
+    // Given up (wave-uniform) when the bound proves nothing, or when already
+    // the unmoved kk-th candidate lies beyond it: the moved one then almost
+    // never passes, and the sort would be wasted.  A heuristic only -- the
+    // test after the sort decides.  The per-cell bound only when the global
+    // one fails.
+    const int jk = min(max(cr[kk - 1], 0), n_per - 1);
+    const float dk0 = sqrtf(__uint_as_float(key_f32(xi[jk], rp)));
+    float L = cand_bound_global(rq, rec);
+    bool cells_done = false;
+    if (!(L > 0.0f) || dk0 >= L) {
+        L = cand_bound_cells(rq, q, rec, lane);
+        cells_done = true;
+        if (!(L > 0.0f) || dk0 >= L) {
+            give_up();
+            return;
+        }
     }
     int i0 = min(max(cr[lane], 0), n_per - 1), i1 = min(max(cr[64 + lane], 0), n_per - 1);
     key_t k0 = KT::key(X[i0], q), k1 = KT::key(X[i1], q);
@@ -641,9 +804,12 @@ __global__ __launch_bounds__(256) void knn_cand_kernel(const float2 *__restrict_
         d_kk = (float)sqrt(__longlong_as_double((long long)key_kk)) * kUp;
     else
         d_kk = sqrtf(__uint_as_float(key_kk)) * kUp;
-    const bool ok = d_kk < L;  // same on every lane
-    if (lane == 0) done[p] = ok ? 1 : 0;
-    if (!ok) return;
+    if (!(d_kk < L) && !cells_done) L = cand_bound_cells(rq, q, rec, lane);
+    if (!(d_kk < L)) {  // same on every lane
+        give_up();
+        return;
+    }
+    if (lane == 0) miss[p] = 0;
     const int mi = i0, rank = lane;
     if (QUERY) {
         if (lane < kk) out[p * k + rank] = mi;
@@ -710,39 +876,111 @@ extern "C" int mmpde_knn_graph(const float *pos, int64_t batches, int64_t n_per,
                              as_stream(stream));
 }
 
-extern "C" int mmpde_knn_candidates(const float *xi, int64_t n_per, int32_t *cand_out,
+extern "C" int mmpde_knn_candidates(const float *xi, const float *ref, int64_t n_per, int32_t *cand_out,
                                     mmpde_stream_t stream) {
     MMPDE_REQUIRE(xi && cand_out && n_per >= kCandN && n_per <= 4096);
     hipLaunchKernelGGL(knn_table_kernel, dim3((unsigned)n_per), dim3(256), 0, as_stream(stream),
-                       (const float2 *)xi, (int)n_per, cand_out);
+                       (const float2 *)xi, (const float2 *)(ref ? ref : xi), (int)n_per, cand_out);
+    MMPDE_RET_LAUNCH();
+    return MMPDE_OK;
+}
+
+extern "C" int64_t mmpde_knn_moved_cells_bytes(int64_t batches) {
+    return batches < 0 ? 0 : batches * kCellRec * (int64_t)sizeof(float);
+}
+
+extern "C" int mmpde_knn_moved_cells(const float *pos, const float *xi, int64_t batches, int64_t n_per,
+                                     float *cells_out, mmpde_stream_t stream) {
+    MMPDE_REQUIRE(pos && xi && cells_out && batches >= 1 && batches <= 65535 && n_per >= 1 &&
+                  n_per <= INT32_MAX);
+    hipLaunchKernelGGL(knn_cells_kernel, dim3((unsigned)batches), dim3(256), 0, as_stream(stream),
+                       (const float2 *)pos, (const float2 *)xi, (int)n_per, cells_out);
+    MMPDE_RET_LAUNCH();
+    return MMPDE_OK;
+}
+
+// Half the median over reference points p of R128(p) - R_kk(p) (the 128th and
+// the kk-th candidate distance of r_p in xi): past that displacement about
+// half the table's lookups cannot pass.  One workgroup, bitonic sort in LDS.
+__global__ __launch_bounds__(256) void knn_margin_kernel(const float2 *__restrict__ xi,
+                                                         const float2 *__restrict__ ref, int n_per,
+                                                         const int32_t *__restrict__ cand, int kk,
+                                                         float *__restrict__ out) {
+    __shared__ float sm[4096];
+    for (int p = threadIdx.x; p < 4096; p += 256) {
+        float m = 3.0e38f;
+        if (p < n_per) {
+            const float2 r = ref[p];
+            const int32_t *cr = cand + (int64_t)p * kCandN;
+            const int j1 = min(max(cr[kCandN - 1], 0), n_per - 1), jk = min(max(cr[kk - 1], 0), n_per - 1);
+            m = sqrtf(__uint_as_float(key_f32(xi[j1], r))) - sqrtf(__uint_as_float(key_f32(xi[jk], r)));
+        }
+        sm[p] = m;
+    }
+    __syncthreads();
+    for (int size = 2; size <= 4096; size <<= 1)
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int t = threadIdx.x; t < 2048; t += 256) {
+                const int i = 2 * t - (t & (stride - 1)), l = i + stride;
+                const float a = sm[i], c = sm[l];
+                if ((a > c) == ((i & size) == 0)) {
+                    sm[i] = c;
+                    sm[l] = a;
+                }
+            }
+            __syncthreads();
+        }
+    if (threadIdx.x == 0) out[0] = 0.5f * sm[n_per / 2];
+}
+
+__global__ void knn_misses_kernel(const float *__restrict__ cells, int batches, int32_t *__restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < 2 * batches) out[i] = cell_last_miss(cells, i >> 1)[i & 1];
+}
+
+extern "C" int mmpde_knn_table_misses(const float *cells, int64_t batches, int32_t *misses_out,
+                                      mmpde_stream_t stream) {
+    MMPDE_REQUIRE(cells && misses_out && batches >= 1 && batches <= 65535);
+    hipLaunchKernelGGL(knn_misses_kernel, dim3(ceil_div(2 * batches, 256)), dim3(256), 0, as_stream(stream),
+                       cells, (int)batches, misses_out);
+    MMPDE_RET_LAUNCH();
+    return MMPDE_OK;
+}
+
+extern "C" int mmpde_knn_skip_threshold(const float *xi, const float *ref, int64_t n_per, const int32_t *cand,
+                                        int kk, float *out, mmpde_stream_t stream) {
+    MMPDE_REQUIRE(xi && cand && out && n_per >= kCandN && n_per <= 4096 && kk >= 1 && kk <= kCandN);
+    hipLaunchKernelGGL(knn_margin_kernel, dim3(1), dim3(256), 0, as_stream(stream), (const float2 *)xi,
+                       (const float2 *)(ref ? ref : xi), (int)n_per, cand, kk, out);
     MMPDE_RET_LAUNCH();
     return MMPDE_OK;
 }
 
 extern "C" int64_t mmpde_knn_graph_cand_scratch_bytes(int64_t batches, int64_t n_per) {
-    return (batches * 4 + 15) / 16 * 16 + batches * n_per;  // dmax, answered flags
+    return batches * n_per;  // the miss flags
 }
 
-// The candidate path: dmax, the candidate kernel, the full search for the
-// queries it could not answer (done[q] = 0).
+// The candidate path: the candidate kernel, then the full search for the
+// queries it could not answer (knn_kernel's miss mode: its cost follows the
+// number of such queries, and is the plain search's when most missed).
 template <bool QUERY>
-static int knn_cand_launch(const float *pos, const float *qry, const float *xi, int64_t batches,
-                           int64_t n_per, int k, const int32_t *cand, int32_t *out, int32_t *degenerate,
-                           void *scratch, hipStream_t st) {
-    float *dmax = (float *)scratch;
-    uint8_t *done = (uint8_t *)scratch + (batches * 4 + 15) / 16 * 16;
+static int knn_cand_launch(const float *pos, const float *qry, const float *xi, const float *ref,
+                           const float *cells, float skip_above, int64_t batches, int64_t n_per, int k,
+                           const int32_t *cand, int32_t *out, int32_t *degenerate, void *scratch,
+                           hipStream_t st) {
+    uint8_t *miss = (uint8_t *)scratch;
     const int64_t n_tot = batches * n_per;
     const float2 *x = (const float2 *)pos, *q = (const float2 *)qry, *x0 = (const float2 *)xi;
-    hipLaunchKernelGGL(knn_dmax_kernel, dim3((unsigned)batches), dim3(256), 0, st, x, x0, (int)n_per, dmax);
     hipLaunchKernelGGL(knn_cand_kernel<QUERY>, dim3((unsigned)ceil_div(n_tot, 4)), dim3(256), 0, st, x, q, x0,
-                       (int)n_per, n_tot, k, cand, dmax, out, degenerate, done);
+                       (const float2 *)ref, (int)n_per, n_tot, k, cand, cells, out, degenerate, miss,
+                       skip_above);
     MMPDE_RET_LAUNCH();
     dim3 grid(ceil_div(n_per, kQueriesPerBlock), (unsigned)batches);
     const int ns = (int)n_per, cpl = ceil_div(n_per, 64);
 #define MMPDE_KNN_FALLBACK(C)                                                                         \
     if (cpl <= C) {                                                                                   \
-        hipLaunchKernelGGL((knn_kernel<C, QUERY>), grid, dim3(256), 0, st, x, QUERY ? q : x, ns, ns, k, \
-                           out, degenerate, (const uint8_t *)done);                                   \
+        hipLaunchKernelGGL((knn_kernel<C, QUERY, kQueriesPerBlock>), grid, dim3(256), 0, st, x, QUERY ? q : x, ns, \
+                           ns, k, out, degenerate, (const uint8_t *)miss, (float *)cells, QUERY ? 1 : 0); \
         MMPDE_RET_LAUNCH();                                                                           \
         return MMPDE_OK;                                                                              \
     }
@@ -765,24 +1003,27 @@ static bool cand_path_applies(int64_t batches, int64_t n_per, int kk) {
            batches * n_per <= INT32_MAX;
 }
 
-extern "C" int mmpde_knn_graph_cand(const float *pos, const float *xi, int64_t batches, int64_t n_per,
-                                    int k, const int32_t *cand, int32_t *nbr_out, int32_t *degenerate,
-                                    void *scratch, mmpde_stream_t stream) {
-    MMPDE_REQUIRE(pos && xi && cand && nbr_out && scratch);
+extern "C" int mmpde_knn_graph_cand(const float *pos, const float *xi, const float *cells, float skip_above,
+                                    int64_t batches, int64_t n_per, int k, const int32_t *cand, int32_t *nbr_out,
+                                    int32_t *degenerate, void *scratch, mmpde_stream_t stream) {
+    MMPDE_REQUIRE(pos && xi && cells && cand && nbr_out && scratch);
     hipStream_t st = as_stream(stream);
     if (k < 1 || !cand_path_applies(batches, n_per, k + 1))
         return launch_knn<false>(pos, nullptr, batches, n_per, n_per, k, nbr_out, degenerate, st);
-    return knn_cand_launch<false>(pos, nullptr, xi, batches, n_per, k, cand, nbr_out, degenerate, scratch, st);
+    return knn_cand_launch<false>(pos, nullptr, xi, xi, cells, skip_above, batches, n_per, k, cand, nbr_out,
+                                  degenerate, scratch, st);
 }
 
-extern "C" int mmpde_knn_query_cand(const float *src, const float *qry, const float *xi, int64_t batches,
-                                    int64_t n_per, int k, const int32_t *cand, int32_t *idx_out,
-                                    void *scratch, mmpde_stream_t stream) {
-    MMPDE_REQUIRE(src && qry && xi && cand && idx_out && scratch);
+extern "C" int mmpde_knn_query_cand(const float *src, const float *qry, const float *xi, const float *ref,
+                                    const float *cells, float skip_above, int64_t batches, int64_t n_per, int k,
+                                    const int32_t *cand, int32_t *idx_out, void *scratch,
+                                    mmpde_stream_t stream) {
+    MMPDE_REQUIRE(src && qry && xi && cells && cand && idx_out && scratch);
     hipStream_t st = as_stream(stream);
     if (!cand_path_applies(batches, n_per, k))
         return launch_knn<true>(src, qry, batches, n_per, n_per, k, idx_out, nullptr, st);
-    return knn_cand_launch<true>(src, qry, xi, batches, n_per, k, cand, idx_out, nullptr, scratch, st);
+    return knn_cand_launch<true>(src, qry, xi, ref ? ref : xi, cells, skip_above, batches, n_per, k, cand,
+                                 idx_out, nullptr, scratch, st);
 }
 
 extern "C" int mmpde_knn_query(const float *src, const float *qry, int64_t batches,

@@ -32,9 +32,9 @@
 // Node stage: 64 (or 32) rows per workgroup, 8 waves; every GEMM reads its
 // weight operand once per workgroup (wave w owns output column tile w for all
 // row blocks); activations are staged in LDS as MFMA operand images with
-// per-row power-of-two scales (F16X3).  The only atomics are the F16X3 range
-// slots (amax_publish: atomicMax of non-negative floats), whose result does
-// not depend on order, so every output is deterministic.
+// per-row power-of-two scales (F16X3), and (F16X3) each workgroup stores the
+// range record of its rows (layer.hpp).  No atomics: every output is
+// deterministic.
 #include "common.hpp"
 #include "f16x3.hpp"
 #include "layer.hpp"
@@ -72,7 +72,7 @@ struct EdgeArgs {
     int k, ntiles;
     const float *w2, *b2;      // message_net_2.0 weight [128,128], bias
     const char *pk;            // F16X3: this layer's packed images (column scales of W2)
-    const uint32_t *amax_in;   // F16X3: range slots of a, b
+    const float *rng;          // F16X3: range records of a, b (layer.hpp; one segment)
     float *mean;               // [n, 128]
     uint64_t *stamps;          // profiling builds (PH bit 10): per-round s_memtime of block 0
     const int32_t *deg;        // RAGGED: in-degree of every target (nbr row entries past it are ignored)
@@ -154,7 +154,7 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
     const int64_t nmax = p.n - 1;
     // F16X3: |a + b| <= max|a| + max|b|, scaled below 2^11 (split8_relu_rtz)
     float sc = 1.0f;
-    if (F16X3) sc = 0.125f * split_scale(amax_read(p.amax_in) + amax_read(p.amax_in + kAmaxShards));
+    if (F16X3) sc = 0.125f * split_scale(segment_range(p.rng, p.n, 0));
     auto tile_row = [&](int j, int row) { return min((int64_t)(first + j * stride) * ET + row, nmax); };
 
     // a tiles (scaled by sc for F16X3): the consumer waves stage tile j + 1 while
@@ -507,14 +507,15 @@ struct NodeArgs {
     const float *u, *pos;
     mmpde_gnn_scales sc;
     const char *pk, *pkn;  // F16X3 images: this layer (U1, U2), next layer (W1)
-    uint32_t *amax_out;
+    float *rng_out;        // F16X3: range records of a', b' (layer.hpp)
+    int64_t seg_n;         // rows per trajectory segment (range records)
     int parts;             // mean = sum of `parts` buffers part_stride floats apart
     int64_t part_stride;
     // div_k > 0: the buffers hold neighbour sums (F16X3 wave edge kernel); the
     // mean is their total / max(div_deg[row], 1), or / div_k without degrees
     const int32_t *div_deg = nullptr;
     int div_k = 0;
-    EdgeSplit split;       // G > 0: add the wave kernel's side blocks first
+    EdgeSplit split;       // units > 0: add the wave kernel's side blocks first
 };
 
 constexpr int NLD = 132;  // fp32 staging row stride (floats)
@@ -556,14 +557,16 @@ __device__ __forceinline__ void prep(const float *src, int64_t lds, int64_t row0
                 x[q] = make_float4(x[q].x + y.x, x[q].y + y.y, x[q].z + y.z, x[q].w + y.w);
             }
         }
-        if (split && split->G > 0) {
-            // side blocks of the waves whose first slot s0(w) = floor(w S / G) lies
-            // strictly inside this row's 16-row tile t: t k < s0(w) < (t + 1) k
-            const int64_t t = srow / 16, S = split->S, G = split->G, kk = split->k;
+        if (split && split->units > 0) {
+            // side blocks of the units u of this row's segment whose first slot
+            // s0(u) = floor(u S / U) lies strictly inside the row's 16-row tile
+            // t (local): t k < s0(u) < (t + 1) k
+            const int64_t sg = srow / split->seg_n, q = srow - sg * split->seg_n, t = q / 16;
+            const int64_t S = split->S, G = split->units, kk = split->k;
             const int64_t lo = max(((t * kk + 1) * G + S - 1) / S, (int64_t)1);
             const int64_t hi = min(((t + 1) * kk * G + S - 1) / S - 1, G - 1);
             for (int64_t w = lo; w <= hi; ++w) {
-                const float *q4 = split->side + (w * 16 + (srow & 15)) * 128 + 16 * part;
+                const float *q4 = split->side + ((sg * G + w) * 16 + (q & 15)) * 128 + 16 * part;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const float4 y = *(const float4 *)(q4 + 4 * q);
@@ -693,8 +696,8 @@ template <bool F16X3, int RB>
 __device__ __forceinline__ void proj_phase(const BOps<F16X3, F16X3 ? 4 : 8> &bA, const float4 *img,
                                            const float *rs, const float *rowv, const W1C &w,
                                            const char *pk, const float *w1r, int tw, int64_t row0,
-                                           int64_t n, float *a_out, float *b_out,
-                                           uint32_t *amax_out, int wave, int lane) {
+                                           int64_t n, int64_t seg_n, float *a_out, float *b_out,
+                                           float *rng_out, int wave, int lane) {
     constexpr int ROWS = 16 * RB, S1 = F16X3 ? 4 : 8;
     const int col = 16 * wave + (lane & 15), g = lane >> 4;
     f32x4 aA[RB], aB[RB];
@@ -706,7 +709,10 @@ __device__ __forceinline__ void proj_phase(const BOps<F16X3, F16X3 ? 4 : 8> &bA,
         bB.load(pk + kPkW1, 4, 8 + wave, 0, w1r, 128, lane);
         gemm_tile<F16X3, RB, S1>(aB, img, 128, 0, bB, lane);
     }
-    float amx = 0.0f, bmx = 0.0f;
+    // |a|, |b| maxima of the rows in the tile's first segment (0) and in the
+    // next one (1) for the range record (seg_n >= ROWS: at most two segments)
+    float amx[2] = {0.0f, 0.0f}, bmx[2] = {0.0f, 0.0f};
+    const int64_t seg1 = (row0 / seg_n + 1) * seg_n;  // first row of the next segment
     // stores at immediate offsets from one base per lane; the row test only
     // for a tile that runs past n (wave-uniform)
     const bool full = row0 + ROWS <= n;
@@ -730,14 +736,29 @@ __device__ __forceinline__ void proj_phase(const BOps<F16X3, F16X3 ? 4 : 8> &bA,
                 const float vb = zb - node;
                 ap[(16 * rb + q) * LH] = va;
                 bp[(16 * rb + q) * LH] = vb;
-                amx = fmaxf(amx, fabsf(va));
-                bmx = fmaxf(bmx, fabsf(vb));
+                const int sx = row0 + lr >= seg1;
+                amx[sx] = fmaxf(amx[sx], fabsf(va));
+                bmx[sx] = fmaxf(bmx[sx], fabsf(vb));
             }
         }
     }
-    if (amax_out) {
-        amax_publish(amx, amax_out);
-        amax_publish(bmx, amax_out + kAmaxShards);
+    if (rng_out) {
+        // wave maxima, then the workgroup's through LDS: one float4 record
+        __shared__ float red[8][4];
+        const float m0 = wave_max(amx[0]), m1 = wave_max(bmx[0]), m2 = wave_max(amx[1]), m3 = wave_max(bmx[1]);
+        if (lane == 0) {
+            red[wave][0] = m0;
+            red[wave][1] = m1;
+            red[wave][2] = m2;
+            red[wave][3] = m3;
+        }
+        __syncthreads();
+        if (wave == 0 && lane < 4) {
+            float m = red[0][lane];
+#pragma unroll
+            for (int w = 1; w < 8; ++w) m = fmaxf(m, red[w][lane]);
+            rng_out[4 * (row0 / ROWS) + lane] = m;
+        }
     }
 }
 
@@ -853,8 +874,8 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs p) {
         prep<F16X3, ROWS>(stage, NLD, 0, ROWS, false, img, 128, 0, rs[3]);
         __syncthreads();
         // ---- next layer's message_net_1 node halves
-        proj_phase<F16X3, RB>(bA, img, rs[3], &rowv[0][0], w1c, p.pkn, w1r, tw, row0, p.n, p.a_out,
-                              p.b_out, p.amax_out, wave, lane);
+        proj_phase<F16X3, RB>(bA, img, rs[3], &rowv[0][0], w1c, p.pkn, w1r, tw, row0, p.n, p.seg_n,
+                              p.a_out, p.b_out, p.rng_out, wave, lane);
     }
 }
 
@@ -875,7 +896,8 @@ struct EmbedArgs {
     int64_t ld_w1;
     float *a_out, *b_out;
     const char *pk;        // F16X3: layer 0's packed images
-    uint32_t *amax_out;    // F16X3: layer 0's range slots
+    float *rng_out;        // F16X3: layer 0's range records
+    int64_t seg_n;         // rows per trajectory segment (range records)
 };
 
 template <bool F16X3, int RB>
@@ -983,8 +1005,8 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_embed_kernel(EmbedArgs p) {
     __syncthreads();
     prep<F16X3, ROWS>(stage, NLD, 0, ROWS, false, img, 128, 0, rs);
     __syncthreads();
-    proj_phase<F16X3, RB>(bA, img, rs, &rowv[0][0], w1c, p.pk, w1r, tw, row0, p.n, p.a_out,
-                          p.b_out, p.amax_out, wave, lane);
+    proj_phase<F16X3, RB>(bA, img, rs, &rowv[0][0], w1c, p.pk, w1r, tw, row0, p.n, p.seg_n,
+                          p.a_out, p.b_out, p.rng_out, wave, lane);
 }
 
 inline bool al16(const void *q) { return ((uintptr_t)q & 15u) == 0; }
@@ -1004,24 +1026,26 @@ int device_cus() {
 #define MMPDE_NODE_RB 2
 #endif
 
+static_assert(16 * MMPDE_NODE_RB == kRangeRows, "range records are per node tile");
+
 int launch_edge_stage(const float *a, const float *b, const int32_t *nbr, const int32_t *deg,
-                      int64_t n, int k, const mmpde_gnn_layer_params *p, const char *pk,
-                      const uint32_t *amax_in, float *mean, float *side, int64_t side_cap,
+                      int64_t n, int k, int64_t seg_n, const mmpde_gnn_layer_params *p, const char *pk,
+                      const float *rng, float *mean, float *side, int64_t side_cap,
                       EdgeSplit *split, hipStream_t st) {
     if (split) *split = EdgeSplit{};
     MMPDE_REQUIRE(a && b && nbr && p && mean && n > 0 && k > 0 && n <= (int64_t)INT32_MAX);
     MMPDE_REQUIRE(al16(a) && al16(b) && al16(p->msg2_w) && al16(mean));
-    MMPDE_REQUIRE(!pk || (amax_in && al16(pk)));
+    MMPDE_REQUIRE(!pk || (rng && al16(pk) && al16(rng)));
     const int64_t ntiles = (n + ET - 1) / ET;
     MMPDE_REQUIRE(ntiles * ((k + ESL - 1) / ESL) < (int64_t)INT32_MAX);
-    EdgeArgs e{a, b, nbr, n, k, (int)ntiles, p->msg2_w, p->msg2_b, pk, amax_in, mean, nullptr, deg};
+    EdgeArgs e{a, b, nbr, n, k, (int)ntiles, p->msg2_w, p->msg2_b, pk, rng, mean, nullptr, deg};
     const int cus = device_cus();
 #ifndef MMPDE_EDGE_RING
     // F16X3: one wave per SIMD with the operands in registers (edge_wave.hip)
     if (pk) {
         // the wave kernel leaves the side blocks and the division to the node stage
-        return launch_edge_wave(a, b, nbr, deg, n, k, p->msg2_b, pk, amax_in, mean, side, side_cap, cus,
-                                split, st);
+        return launch_edge_wave(a, b, nbr, deg, n, k, seg_n, p->msg2_b, pk, rng, mean, side, side_cap,
+                                cus, split, st);
     }
 #endif
     const int grid = ntiles < cus ? (int)ntiles : cus;
@@ -1038,19 +1062,21 @@ int launch_edge_stage(const float *a, const float *b, const int32_t *nbr, const 
 }
 
 int launch_node_stage(const float *h, const float *mean, const EdgeSplit *split, const int32_t *deg,
-                      const float *u, const float *pos, int64_t n, mmpde_gnn_scales sc,
+                      const float *u, const float *pos, int64_t n, int64_t seg_n, mmpde_gnn_scales sc,
                       const mmpde_gnn_layer_params *p, const mmpde_gnn_layer_params *next,
-                      const char *pk, const char *pkn, uint32_t *amax_out, float *h_out, float *a_out,
+                      const char *pk, const char *pkn, float *rng_out, float *h_out, float *a_out,
                       float *b_out, hipStream_t st) {
-    const bool sums = split && split->G > 0;
-    MMPDE_REQUIRE(!sums || (split->side && split->S > 0 && split->k > 0));
+    const bool sums = split && split->units > 0;
+    MMPDE_REQUIRE(!sums || (split->side && split->S > 0 && split->k > 0 && split->seg_n > 0 &&
+                            n % split->seg_n == 0));
+    MMPDE_REQUIRE(!rng_out || al16(rng_out));
     MMPDE_REQUIRE(h && mean && u && pos && p && h_out && n > 0);
     MMPDE_REQUIRE(al16(h) && al16(mean) && al16(h_out));
     MMPDE_REQUIRE(p->upd1_ld >= 257 && (p->upd1_ld & 3) == 0 && al16(p->upd1_w) && al16(p->upd2_w));
     MMPDE_REQUIRE(!pk || (al16(pk) && (!next || pkn)));
     NodeArgs a{h, mean, n, p->upd1_w, p->upd1_b, p->upd1_ld, p->upd2_w, p->upd2_b, p->bn_w, p->bn_b,
                p->bn_rm, p->bn_rv, p->eps, h_out, nullptr, nullptr, 0, a_out, b_out, u, pos, sc,
-               pk, pkn, amax_out, 1, 0, sums ? deg : nullptr, sums ? split->k : 0};
+               pk, pkn, rng_out, effective_seg(n, seg_n), 1, 0, sums ? deg : nullptr, sums ? split->k : 0};
     if (sums) a.split = *split;
     if (next) {
         MMPDE_REQUIRE(a_out && b_out && next->msg1_ld >= 260 && (next->msg1_ld & 3) == 0 &&
@@ -1072,16 +1098,16 @@ int launch_node_stage(const float *h, const float *mean, const EdgeSplit *split,
     return MMPDE_OK;
 }
 
-int launch_embed_stage(const float *u, const float *pos, int64_t n, mmpde_gnn_scales sc,
+int launch_embed_stage(const float *u, const float *pos, int64_t n, int64_t seg_n, mmpde_gnn_scales sc,
                        const mmpde_gnn_embed_params *e, const mmpde_gnn_layer_params *l0,
-                       const char *pk0, uint32_t *amax_out, float *h_out, float *a_out,
+                       const char *pk0, float *rng_out, float *h_out, float *a_out,
                        float *b_out, hipStream_t st) {
     MMPDE_REQUIRE(u && pos && e && l0 && h_out && a_out && b_out && n > 0);
     MMPDE_REQUIRE(al16(e->w3) && al16(h_out) && al16(a_out) && al16(b_out));
     MMPDE_REQUIRE(l0->msg1_ld >= 260 && (l0->msg1_ld & 3) == 0 && al16(l0->msg1_w));
-    MMPDE_REQUIRE(!pk0 || (al16(pk0) && amax_out));
+    MMPDE_REQUIRE(!pk0 || (al16(pk0) && rng_out && al16(rng_out)));
     EmbedArgs a{u, pos, n, sc, *e, h_out, l0->msg1_w, l0->msg1_b, l0->msg1_ld, a_out, b_out, pk0,
-                amax_out};
+                rng_out, effective_seg(n, seg_n)};
     constexpr int RB = MMPDE_NODE_RB;
     const dim3 grid((unsigned)ceil_div(n, 16 * RB));
     if (pk0) hipLaunchKernelGGL((gnn_embed_kernel<true, RB>), grid, dim3(512), 0, st, a);

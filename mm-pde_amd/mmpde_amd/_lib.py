@@ -13,7 +13,7 @@ import os
 import torch
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libmmpde_hip.so")
-ABI_VERSION = 11100
+ABI_VERSION = 11200
 
 ACT_NONE, ACT_TANH, ACT_RELU, ACT_ELU = 0, 1, 2, 3
 PAD_ZEROS, PAD_CIRCULAR = 0, 1
@@ -62,7 +62,7 @@ class GnnExec(ctypes.Structure):
     """mmpde_gnn_exec: optional per-layer hipEvents + the edge-GEMM arithmetic."""
     _fields_ = [("edge_begin", ctypes.POINTER(_P)), ("edge_end", ctypes.POINTER(_P)),
                 ("edge_gemm", _I), ("packed", _P), ("node_end", ctypes.POINTER(_P)),
-                ("degree", _P)]
+                ("degree", _P), ("seg_n", _I64)]
 
 
 class DmmGraphBranch(ctypes.Structure):
@@ -94,10 +94,14 @@ _SIGS = {
     "mmpde_version": (_I, []),
     "mmpde_status_string": (ctypes.c_char_p, [_I]),
     "mmpde_knn_graph": (_I, [_P, _I64, _I64, _I, _P, _P, _P]),
-    "mmpde_knn_candidates": (_I, [_P, _I64, _P, _P]),
+    "mmpde_knn_candidates": (_I, [_P, _P, _I64, _P, _P]),
+    "mmpde_knn_moved_cells_bytes": (_I64, [_I64]),
+    "mmpde_knn_moved_cells": (_I, [_P, _P, _I64, _I64, _P, _P]),
+    "mmpde_knn_table_misses": (_I, [_P, _I64, _P, _P]),
     "mmpde_knn_graph_cand_scratch_bytes": (_I64, [_I64, _I64]),
-    "mmpde_knn_graph_cand": (_I, [_P, _P, _I64, _I64, _I, _P, _P, _P, _P, _P]),
-    "mmpde_knn_query_cand": (_I, [_P, _P, _P, _I64, _I64, _I, _P, _P, _P, _P]),
+    "mmpde_knn_skip_threshold": (_I, [_P, _P, _I64, _P, _I, _P, _P]),
+    "mmpde_knn_graph_cand": (_I, [_P, _P, _P, _F, _I64, _I64, _I, _P, _P, _P, _P, _P]),
+    "mmpde_knn_query_cand": (_I, [_P, _P, _P, _P, _P, _F, _I64, _I64, _I, _P, _P, _P, _P]),
     "mmpde_knn_query": (_I, [_P, _P, _I64, _I64, _I64, _I, _P, _P]),
     "mmpde_edge_index_from_nbr": (_I, [_P, _I64, _I, _P, _P]),
     "mmpde_linear_skinny": (_I, [_P, _I64, _I64, _I64, _P, _I64, _P, _I64, _I, _P, _I64, _P]),

@@ -50,15 +50,32 @@ class GraphCreator_FS_2D(nn.Module):  # noqa: N801 - reference name
 
     def uniform_grid(self, device, nx=None, ny=None):
         """Array mode: meshgrid(linspace, linspace) 'ij' flattened (data_creator_2d.py:187-194);
-        cylinder: pde.ori_grid.  Returns [N, 2] fp32 on `device`."""
+        cylinder: pde.ori_grid.  Returns [N, 2] fp32 on `device` -- the same tensor
+        for the same grid parameters (cached), so that the fixed-grid graph cache
+        below hits by identity without comparing contents on the host."""
         if self._is_array():
             nx = self.pde.grid_size[1] if nx is None else nx
             ny = self.pde.grid_size[2] if ny is None else ny
+            key = ("ij", str(device), nx, ny, float(self.pde.Lx), float(self.pde.Ly))
+        else:
+            og = self.pde.ori_grid
+            key = ("ori", str(device), id(og), og._version, tuple(og.shape))
+        cache = self.__dict__.setdefault("_uniform_grid_cache", {})
+        hit = cache.get(key)
+        if hit is not None and (key[0] == "ij" or hit[0] is self.pde.ori_grid):
+            return hit[1]
+        if self._is_array():
             x = torch.linspace(0, self.pde.Lx, nx)
             y = torch.linspace(0, self.pde.Ly, ny)
             gx, gy = torch.meshgrid(x, y, indexing="ij")
-            return torch.stack((gx, gy), 2).float().reshape(-1, 2).to(device)
-        return self.pde.ori_grid.float().reshape(-1, 2).to(device)
+            g = torch.stack((gx, gy), 2).float().reshape(-1, 2).to(device)
+        else:
+            g = self.pde.ori_grid.float().reshape(-1, 2).to(device)
+            if g.data_ptr() == self.pde.ori_grid.data_ptr():
+                g = g.clone()   # own storage: a caller's in-place edit of ori_grid misses the cache
+        # the pde's grid object is kept with the entry, so its id cannot be reused
+        cache[key] = (self.pde.ori_grid if key[0] == "ori" else None, g)
+        return g
 
     def xi_grid_xy(self, n_grid_x, n_grid_y, device):
         """The DMM xi grid of moving_mesh (data_creator_2d.py:94-96): numpy
@@ -82,15 +99,15 @@ class GraphCreator_FS_2D(nn.Module):  # noqa: N801 - reference name
         return float(self.n * torch.sqrt(dx ** 2 + dy ** 2) + 0.0001)
 
     def fixed_graph_nbr(self, grid: torch.Tensor, batches: int) -> torch.Tensor:
-        """kNN-k table of `batches` copies of the fixed grid (cached)."""
-        # keyed on the grid's content (create_graph builds a fresh grid tensor
-        # every call, so an address key could match a different grid allocated
-        # at a freed address): the host copy of the grid is compared exactly
-        host = grid.detach().to("cpu", torch.float32).contiguous()
-        key = (tuple(host.shape), str(grid.device), batches, self.n)
+        """kNN-k table of `batches` copies of the fixed grid (cached).  Keyed on
+        the grid tensor's identity and version: the cache holds the tensor, so
+        its storage cannot be freed and reused by another grid while the entry
+        lives, and an in-place change bumps the version (no host copy, no
+        device sync per call; create_graph passes the cached uniform_grid)."""
+        key = (grid.data_ptr(), grid._version, tuple(grid.shape), str(grid.device), batches, self.n)
         hit = self._fixed_graph_cache.get(key)
-        if hit is None or not torch.equal(hit[0], host):
-            hit = (host, ops.knn_graph_nbr(grid.repeat(batches, 1), batches, self.n))
+        if hit is None or hit[0] is not grid:
+            hit = (grid, ops.knn_graph_nbr(grid.repeat(batches, 1), batches, self.n))
             self._fixed_graph_cache = {key: hit}
         return hit[1]
 
@@ -158,6 +175,7 @@ class GraphCreator_FS_2D(nn.Module):  # noqa: N801 - reference name
         g.batch = batch
         g.nbr = nbr
         g.deg = deg
+        g.seg_n = n
         return g
 
     def create_graph(self, itp_model, data, labels, steps, device, mesh_model=None):

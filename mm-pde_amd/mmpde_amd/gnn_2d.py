@@ -330,6 +330,10 @@ class MP_PDE_Solver_2D(nn.Module):  # noqa: N801 - reference name
             trace = L.GnnExec(None, None, 0, None)
         trace.edge_gemm = L.EDGE_GEMM[self.edge_gemm]
         trace.degree = L.ptr(deg)
+        # nodes per trajectory: the f16x3 split scale is then taken per trajectory
+        # (a trajectory's output does not depend on the others in the batch)
+        seg = getattr(data, "seg_n", None)
+        trace.seg_n = int(seg) if seg else 0
         trace.packed = (L.ptr(self.packed_f16x3(u.device)) if self.edge_gemm == "f16x3"
                         else None)
         L.check(L.lib().mmpde_gnn_forward_ex(

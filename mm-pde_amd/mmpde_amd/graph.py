@@ -4,7 +4,9 @@ data_creator_2d.py:262-267 (PyG is not a dependency of this engine).
 Fields the reference sets and the models read: ``x`` [n, tw], ``pos`` [n, 3] =
 (t, x, y), ``edge_index`` int64 [2, n*k] (row 0 source, row 1 target), ``batch``
 int64 [n] and ``y`` [n, tw].  The engine adds ``nbr`` -- the same graph as an
-int32 target-major [n, k] table, which is what the HIP kernels consume.  Any
+int32 target-major [n, k] table, which is what the HIP kernels consume, and
+``seg_n`` -- the nodes per trajectory (every batch segment has that many; no
+edge leaves its segment).  Any
 object with the PyG fields (including a real ``torch_geometric.data.Data``) is
 accepted by the models; ``nbr`` is then derived from ``edge_index``.
 """
@@ -22,6 +24,7 @@ class Data:
         self.batch = None
         self.nbr = None
         self.deg = None   # ragged graphs (radius): in-degree per target, nbr rows padded
+        self.seg_n = None  # nodes per trajectory (batch segment), when all are equal
         for k, v in kwargs.items():
             setattr(self, k, v)
 

@@ -46,28 +46,91 @@ def knn_graph_nbr(pos: torch.Tensor, batches: int, k: int, count_degenerate: boo
 KNN_CAND = 128  # candidates per point in mmpde_knn_candidates' table
 
 
-def knn_candidates(xi: torch.Tensor):
-    """Static candidate table of knn_graph_moved for fixed points xi [N, 2]:
-    [N, 128] int32, the 128 nearest of each point in (d2, index) order, or None
-    where the candidate path does not apply (N outside [128, 4096])."""
-    L.require_device(xi)
+def knn_candidates(xi: torch.Tensor, ref: torch.Tensor | None = None):
+    """Static candidate table of knn_graph_moved / knn_query_moved for fixed
+    points xi [N, 2] and reference points ref [N, 2] (default xi; for a query,
+    the fixed query points): [N, 128] int32, the 128 nearest of ref_p in xi in
+    (d2, index) order, or None where the candidate path does not apply (N
+    outside [128, 4096])."""
+    L.require_device(xi, ref)
     xi = L.f32c(xi).reshape(-1, 2)
     N = xi.shape[0]
     if N < KNN_CAND or N > 4096:
         return None
+    if ref is not None:
+        ref = L.f32c(ref).reshape(-1, 2)
+        if ref.shape[0] != N:
+            raise ValueError("ref must hold one reference point per xi point")
     cand = torch.empty((N, KNN_CAND), dtype=torch.int32, device=xi.device)
-    L.check(L.lib().mmpde_knn_candidates(L.ptr(xi), N, L.ptr(cand), L.stream(xi.device)),
+    L.check(L.lib().mmpde_knn_candidates(L.ptr(xi), L.ptr(ref), N, L.ptr(cand), L.stream(xi.device)),
             "mmpde_knn_candidates")
     return cand
 
 
+def knn_skip_threshold(xi: torch.Tensor, cand, kk: int, ref: torch.Tensor | None = None) -> float:
+    """The skip_above of knn_graph_moved / knn_query_moved for a table cand =
+    knn_candidates(xi, ref) and kk = k + 1 (graph) or k (query): half the median
+    of R128 - R_kk over the reference points (mmpde_knn_skip_threshold).  Reads
+    one float back to the host: call once per table, not per step."""
+    if cand is None:
+        return 0.0
+    L.require_device(xi, cand, ref)
+    xi = L.f32c(xi).reshape(-1, 2)
+    ref = None if ref is None else L.f32c(ref).reshape(-1, 2)
+    out = torch.empty((1,), dtype=torch.float32, device=xi.device)
+    L.check(L.lib().mmpde_knn_skip_threshold(L.ptr(xi), L.ptr(ref), xi.shape[0], L.ptr(cand), kk,
+                                             L.ptr(out), L.stream(xi.device)), "mmpde_knn_skip_threshold")
+    return float(out.item())
+
+
+def knn_moved_cells(pos: torch.Tensor, xi: torch.Tensor, batches: int,
+                    out: torch.Tensor | None = None) -> torch.Tensor:
+    """Per-trajectory displacement record of moved points pos [batches * N, 2]
+    (every trajectory moved from xi [N, 2]): the largest |pos_j - xi_j| per cell
+    of a 16 x 16 grid over xi's box (mmpde_knn_moved_cells).  One per moved mesh,
+    shared by knn_graph_moved and knn_query_moved."""
+    L.require_device(pos, xi)
+    pos = L.f32c(pos).reshape(-1, 2)
+    xi = L.f32c(xi).reshape(-1, 2)
+    N = xi.shape[0]
+    if pos.shape[0] != batches * N:
+        raise ValueError("pos must hold `batches` meshes of xi's size")
+    nf = L.lib().mmpde_knn_moved_cells_bytes(batches) // 4
+    if out is None or out.numel() < nf:
+        out = torch.empty((nf,), dtype=torch.float32, device=pos.device)
+    L.check(L.lib().mmpde_knn_moved_cells(L.ptr(pos), L.ptr(xi), batches, N, L.ptr(out),
+                                          L.stream(pos.device)), "mmpde_knn_moved_cells")
+    return out
+
+
+def knn_table_share(cells: torch.Tensor, batches: int, n_per: int) -> torch.Tensor:
+    """[batches, 2] float: per trajectory, the share of the graph (column 0) and
+    query (column 1) lookups the candidate tables answered since `cells` was
+    computed (knn_moved_cells), from the record's miss counters (diagnostics)."""
+    L.require_device(cells)
+    miss = torch.empty((batches, 2), dtype=torch.int32, device=cells.device)
+    L.check(L.lib().mmpde_knn_table_misses(L.ptr(cells), batches, L.ptr(miss),
+                                           L.stream(cells.device)), "mmpde_knn_table_misses")
+    return 1.0 - miss.float() / n_per
+
+
+def _cand_scratch(scratch, batches, N, device):
+    need = L.lib().mmpde_knn_graph_cand_scratch_bytes(batches, N)
+    if scratch is None or scratch.numel() * scratch.element_size() < need:
+        scratch = torch.empty((max(need, 1),), dtype=torch.uint8, device=device)
+    return scratch
+
+
 def knn_graph_moved(pos: torch.Tensor, xi: torch.Tensor, cand, batches: int, k: int,
-                    scratch: torch.Tensor | None = None, count_degenerate: bool = False):
+                    scratch: torch.Tensor | None = None, count_degenerate: bool = False,
+                    cells: torch.Tensor | None = None, skip_above: float = 0.0):
     """knn_graph_nbr of moved points pos [batches * N, 2] (every trajectory's
     mesh moved from the same xi [N, 2]), bit for bit, answered from the
     candidate table `cand` (knn_candidates(xi)) where a distance bound proves
     it complete and by the full search elsewhere (reference
-    data_creator_2d.py:260 on the DMM's moved mesh)."""
+    data_creator_2d.py:260 on the DMM's moved mesh).  cells: knn_moved_cells(pos,
+    xi, batches) if already computed; skip_above > 0: trajectories moved
+    further go straight to the full search (knn_skip_threshold)."""
     if cand is None:
         return knn_graph_nbr(pos, batches, k, count_degenerate)
     L.require_device(pos)
@@ -78,13 +141,14 @@ def knn_graph_moved(pos: torch.Tensor, xi: torch.Tensor, cand, batches: int, k: 
     if n != batches * N or cand.shape != (N, KNN_CAND):
         raise ValueError("pos must hold `batches` meshes of xi's size; cand from knn_candidates(xi)")
     _knn_points_check(N, k, "knn_graph")
-    need = L.lib().mmpde_knn_graph_cand_scratch_bytes(batches, N)
-    if scratch is None or scratch.numel() * scratch.element_size() < need:
-        scratch = torch.empty((need,), dtype=torch.uint8, device=pos.device)
+    if cells is None:
+        cells = knn_moved_cells(pos, xi, batches)
+    scratch = _cand_scratch(scratch, batches, N, pos.device)
     nbr = torch.empty((n, k), dtype=torch.int32, device=pos.device)
     deg = torch.zeros((1,), dtype=torch.int32, device=pos.device) if count_degenerate else None
-    L.check(L.lib().mmpde_knn_graph_cand(L.ptr(pos), L.ptr(xi), batches, N, k, L.ptr(cand),
-                                         L.ptr(nbr), L.ptr(deg), L.ptr(scratch),
+    L.check(L.lib().mmpde_knn_graph_cand(L.ptr(pos), L.ptr(xi), L.ptr(cells), float(skip_above),
+                                         batches, N, k,
+                                         L.ptr(cand), L.ptr(nbr), L.ptr(deg), L.ptr(scratch),
                                          L.stream(pos.device)), "mmpde_knn_graph_cand")
     return (nbr, deg) if count_degenerate else nbr
 
@@ -178,30 +242,39 @@ def knn_query(src: torch.Tensor, qry: torch.Tensor, batches: int, k: int) -> tor
 
 
 def knn_query_moved(src: torch.Tensor, qry: torch.Tensor, xi: torch.Tensor, cand, batches: int,
-                    k: int, scratch: torch.Tensor | None = None) -> torch.Tensor:
+                    k: int, scratch: torch.Tensor | None = None, ref: torch.Tensor | None = None,
+                    cells: torch.Tensor | None = None, skip_above: float = 0.0) -> torch.Tensor:
     """knn_query of qry onto moved points src (every trajectory's mesh moved
     from the same xi [N, 2]; n_src = n_qry = N), bit for bit, answered from the
-    candidate table `cand` (knn_candidates(xi)) where a distance bound proves
-    it complete and by the full search elsewhere (reference
-    data_creator_2d.py:66-78 onto the DMM's moved mesh)."""
+    candidate table `cand` = knn_candidates(xi, ref) (ref: the fixed points the
+    queries sit at or near, default xi) where a distance bound proves it
+    complete and by the full search elsewhere (reference data_creator_2d.py:66-78
+    onto the DMM's moved mesh).  cells: knn_moved_cells(src, xi, batches) if
+    already computed; skip_above as for knn_graph_moved."""
     if cand is None:
         return knn_query(src, qry, batches, k)
-    L.require_device(src, qry)
+    L.require_device(src, qry, ref)
     src = L.f32c(src).reshape(-1, 2)
     qry = L.f32c(qry).reshape(-1, 2)
     xi = L.f32c(xi).reshape(-1, 2)
     N = xi.shape[0]
     if src.shape[0] != batches * N or qry.shape[0] != batches * N or cand.shape != (N, KNN_CAND):
         raise ValueError("src and qry must hold `batches` point sets of xi's size; "
-                         "cand from knn_candidates(xi)")
+                         "cand from knn_candidates(xi, ref)")
+    if ref is not None:
+        ref = L.f32c(ref).reshape(-1, 2)
+        if ref.shape[0] != N:
+            raise ValueError("ref must hold one reference point per xi point")
     _knn_points_check(N, k, "knn_query")
-    need = L.lib().mmpde_knn_graph_cand_scratch_bytes(batches, N)
-    if scratch is None or scratch.numel() * scratch.element_size() < need:
-        scratch = torch.empty((need,), dtype=torch.uint8, device=src.device)
+    if cells is None:
+        cells = knn_moved_cells(src, xi, batches)
+    scratch = _cand_scratch(scratch, batches, N, src.device)
     idx = torch.empty((batches * N, k), dtype=torch.int32, device=src.device)
-    L.check(L.lib().mmpde_knn_query_cand(L.ptr(src), L.ptr(qry), L.ptr(xi), batches, N, k,
-                                         L.ptr(cand), L.ptr(idx), L.ptr(scratch),
-                                         L.stream(src.device)), "mmpde_knn_query_cand")
+    L.check(L.lib().mmpde_knn_query_cand(L.ptr(src), L.ptr(qry), L.ptr(xi), L.ptr(ref),
+                                         L.ptr(cells), float(skip_above), batches, N, k,
+                                         L.ptr(cand), L.ptr(idx),
+                                         L.ptr(scratch), L.stream(src.device)),
+            "mmpde_knn_query_cand")
     return idx
 
 

@@ -73,13 +73,34 @@ class MMPDERollout:
                 itp.packed(mode)
             # the DMM head's grid side depends on xi and the weights only
             self.dmm_cache = dmm.head_cache(self.xi, workspace=self.ws_dmm)
-            # the moved-mesh graph from the 128 nearest of each xi point (exact:
-            # csrc/knn.hip knn_cand_kernel, full search where its bound fails)
+            # the moved-mesh graph from the 128 nearest of each xi point, the
+            # kNN-30 query of the fixed grid from the 128 nearest xi points of
+            # each grid point (exact: csrc/knn.hip knn_cand_kernel, full search
+            # where its bound fails).  Burgers' grid is in 'ij' order and xi in
+            # 'xy' order, so the query table is built for the grid's own order.
             self.knn_cand = ops.knn_candidates(self.xi)
-            nb = L.lib().mmpde_knn_graph_cand_scratch_bytes(batches, N)
+            self.knn_cand_q = (self.knn_cand if self.grid is self.xi
+                               else ops.knn_candidates(self.xi, ref=self.grid))
+            # trajectories moved further than these go straight to the full
+            # search (about half the table's lookups would fail; read once)
+            self.knn_skip = ops.knn_skip_threshold(self.xi, self.knn_cand, gc.n + 1)
+            self.knn_skip_q = ops.knn_skip_threshold(self.xi, self.knn_cand_q, 30, ref=self.grid)
+            nb = max(L.lib().mmpde_knn_graph_cand_scratch_bytes(batches, N), 1)
             self.knn_scratch = torch.empty((nb,), dtype=torch.uint8, device=self.device)
             # the kNN-30 query runs on side2 beside the graph: its own scratch
             self.knn_scratch_q = torch.empty((nb,), dtype=torch.uint8, device=self.device)
+            # per-step displacement record shared by both (ops.knn_moved_cells)
+            self.knn_cells = torch.empty((L.lib().mmpde_knn_moved_cells_bytes(batches) // 4,),
+                                         dtype=torch.float32, device=self.device)
+            if kind == "burgers":
+                # mode '1': kNN-30 of the moved mesh (near xi, 'xy' order) onto the
+                # fixed grid: a table of the 128 grid points nearest each xi point,
+                # and a displacement record of the unmoved grid (all zero)
+                # (rebuilt every step, which also zeroes its miss counters)
+                self.knn_cand_1 = ops.knn_candidates(self.grid, ref=self.xi)
+                self.knn_skip_1 = ops.knn_skip_threshold(self.grid, self.knn_cand_1, 30, ref=self.xi)
+                self.knn_cells_1 = torch.empty_like(self.knn_cells)
+                self.knn_scratch_1 = torch.empty((nb,), dtype=torch.uint8, device=self.device)
             # the fixed-grid model depends on u only: it runs on a side stream,
             # with its own workspace, beside the moving-mesh chain
             self.side = torch.cuda.Stream(self.device)
@@ -141,23 +162,26 @@ class MMPDERollout:
         u_flat = u.reshape(-1)
         self._set_t(self.pos_u, step_idx)
         if not self.moving_mesh:
-            return self.model(_Nodes(u_flat, self.pos_u, self.nbr_u), out=self.out_u,
+            return self.model(_Nodes(u_flat, self.pos_u, self.nbr_u, N), out=self.out_u,
                               workspace=self.ws_gnn, trace=self._trace()).reshape(u.shape)
         cur = torch.cuda.current_stream(self.device)
         side = self.side if self.overlap else cur
         side.wait_stream(cur)
         with torch.cuda.stream(side):
             u.record_stream(side)
-            out_u = self.model(_Nodes(u_flat, self.pos_u, self.nbr_u), out=self.out_u,
+            out_u = self.model(_Nodes(u_flat, self.pos_u, self.nbr_u, N), out=self.out_u,
                                workspace=self.ws_gnn_u, trace=self._trace())
         mesh = self.dmm.mesh(u, self.xi, out=self.mesh, workspace=self.ws_dmm,
                              head_cache=self.dmm_cache)
+        cells = ops.knn_moved_cells(mesh, self.xi, B, out=self.knn_cells) \
+            if self.knn_cand is not None else None
         side2 = self.side2 if self.overlap else cur
         side2.wait_stream(cur)
         with torch.cuda.stream(side2):
             u.record_stream(side2)
-            idx2 = ops.knn_query_moved(mesh, self.grid_rep, self.xi, self.knn_cand, B, 30,
-                                       self.knn_scratch_q)
+            self.idx2 = idx2 = ops.knn_query_moved(mesh, self.grid_rep, self.xi, self.knn_cand_q, B,
+                                                   30, self.knn_scratch_q, ref=self.grid,
+                                                   cells=cells, skip_above=self.knn_skip_q)
             if self.kind == "burgers":
                 res = self.itp.res_cut(u.reshape(B, 1, self.s, self.s)).reshape(-1)
             else:
@@ -166,19 +190,36 @@ class MMPDERollout:
             res.record_stream(cur)
         self.pos_m[:, 1:3] = mesh
         self._set_t(self.pos_m, step_idx)
-        nbr_m = ops.knn_graph_moved(mesh, self.xi, self.knn_cand, B, self.gc.n, self.knn_scratch)
+        self.nbr_m = nbr_m = ops.knn_graph_moved(mesh, self.xi, self.knn_cand, B, self.gc.n,
+                                                 self.knn_scratch, cells=cells,
+                                                 skip_above=self.knn_skip)
         if self.kind == "burgers":
-            idx1 = ops.knn_query(self.grid_rep, mesh, B, 30)
+            cells1 = ops.knn_moved_cells(self.grid_rep, self.grid, B, out=self.knn_cells_1)
+            self.idx1 = idx1 = ops.knn_query_moved(self.grid_rep, mesh, self.grid, self.knn_cand_1, B,
+                                                   30, self.knn_scratch_1, ref=self.xi, cells=cells1,
+                                                   skip_above=self.knn_skip_1)
             u_m = ops.itp_interp(self.grid_rep, u_flat, mesh, idx1, B, self.itp.packed("1"))
         else:
             u_m = u_flat
-        out_b = self.model_b(_Nodes(u_m, self.pos_m, nbr_m), out=self.out_b,
+        out_b = self.model_b(_Nodes(u_m, self.pos_m, nbr_m, N), out=self.out_b,
                              workspace=self.ws_gnn, trace=self._trace())
         cur.wait_stream(side2)
         interp = ops.itp_interp(mesh, out_b, self.grid_rep, idx2, B, self.itp.packed("2"),
                                 addend=res)
         cur.wait_stream(side)
         return torch.add(interp, out_u.reshape(-1)).reshape(u.shape)
+
+    def knn_table_share(self):
+        """(graph, query[, burgers mode-'1' query]): the share of the last step's
+        moved-mesh kNN lookups the candidate tables answered (the rest went to
+        the full search).  Diagnostics: synchronises the device."""
+        if not self.moving_mesh or self.knn_cand is None:
+            return None
+        torch.cuda.synchronize(self.device)
+        s = ops.knn_table_share(self.knn_cells, self.B, self.N).mean(0).tolist()
+        if self.kind == "burgers":
+            s.append(ops.knn_table_share(self.knn_cells_1, self.B, self.N)[:, 1].mean().item())
+        return tuple(s)
 
     def rollout(self, u0: torch.Tensor, start_step: int, n_steps: int):
         """Feed each prediction back as the next input; returns the final state."""
@@ -189,11 +230,12 @@ class MMPDERollout:
 
 
 class _Nodes:
-    """The three graph fields the solver reads (x, pos, nbr)."""
-    __slots__ = ("x", "pos", "nbr", "edge_index")
+    """The graph fields the solver reads (x, pos, nbr, seg_n = nodes per trajectory)."""
+    __slots__ = ("x", "pos", "nbr", "edge_index", "seg_n")
 
-    def __init__(self, x, pos, nbr):
+    def __init__(self, x, pos, nbr, seg_n=None):
         self.x = x.reshape(-1, 1)
         self.pos = pos
         self.nbr = nbr
         self.edge_index = None
+        self.seg_n = seg_n

@@ -55,34 +55,85 @@ def test_knn_graph_burgers_grid_ties_bit_exact(dev):
 
 @pytest.mark.parametrize("kind", ["cy", "burgers"])
 def test_knn_graph_moved_candidates_bit_exact(dev, kind):
-    """The candidate-table graph (mmpde_knn_graph_cand) against the oracle and
-    the full search: small displacements (the table answers), one trajectory
-    moved far (the bound fails, the full search answers), and the unmoved grid
-    (ties at the cut on the burgers lattice)."""
+    """The candidate-table graph and kNN-30 query (mmpde_knn_graph_cand /
+    mmpde_knn_query_cand) against the oracle and the full search, on
+    trajectories that exercise every branch: unmoved (ties at the cut on the
+    burgers lattice), small smooth and small random displacements (the table
+    answers), random displacements of 0.02 (mixed: some queries answered, the
+    rest by the full search in the same workgroups), one node moved far (the
+    per-cell bound keeps the table for the queries away from it) and a large
+    smooth displacement (the bound fails, the full search answers).  The
+    tables' answered shares are asserted so that each regime is really hit."""
     from mmpde_amd import ops
     from mmpde_amd.synth import burgers_grid_points, cy_synth_mesh
 
     xi = cy_synth_mesh() if kind == "cy" else burgers_grid_points()
+    N = xi.shape[0]
     gen = torch.Generator().manual_seed(5)
+    one_far = xi.clone()
+    one_far[N // 3] += torch.tensor([0.08, -0.05])
     moved = [xi, xi + 0.004 * torch.sin(9 * xi.flip(1)),
              xi + 0.002 * torch.randn(xi.shape, generator=gen),
+             xi + 0.02 * torch.randn(xi.shape, generator=gen),
+             one_far,
              xi + 0.3 * torch.sin(3 * xi.flip(1))]
     B = len(moved)
     pos = torch.cat(moved)
-    cand = ops.knn_candidates(xi.to(dev))
-    assert cand is not None and cand.shape == (xi.shape[0], ops.KNN_CAND)
-    nbr, deg = ops.knn_graph_moved(pos.to(dev), xi.to(dev), cand, B, 35, count_degenerate=True)
+    xd, pd = xi.to(dev), pos.to(dev)
+    cand = ops.knn_candidates(xd)
+    assert cand is not None and cand.shape == (N, ops.KNN_CAND)
+    cells = ops.knn_moved_cells(pd, xd, B)
+    nbr, deg = ops.knn_graph_moved(pd, xd, cand, B, 35, count_degenerate=True, cells=cells)
+    share = ops.knn_table_share(cells, B, N)[:, 0].cpu()
+    print(f"{kind} graph: table share per trajectory {share.tolist()}")
     _, ref, rdeg = refcpu.knn_graph(pos, 35, B)
     assert int(deg.item()) == rdeg
     assert torch.equal(nbr.cpu().long(), ref)
-    assert torch.equal(nbr, ops.knn_graph_nbr(pos.to(dev), B, 35))
-    # the kNN-30 query of the grid onto the moved meshes (queries = xi; and
-    # queries moved off xi, which the bound must account for)
-    for qry in (xi.repeat(B, 1), xi.repeat(B, 1) + 0.003 * torch.cos(5 * xi.repeat(B, 1))):
-        idx = ops.knn_query_moved(pos.to(dev), qry.to(dev), xi.to(dev), cand, B, 30)
-        assert torch.equal(idx, ops.knn_query(pos.to(dev), qry.to(dev), B, 30))
+    assert torch.equal(nbr, ops.knn_graph_nbr(pd, B, 35))
+    assert share[1] > 0.99 and share[2] > 0.99           # small displacements: the table
+    assert 0.0 < share[3] < 1.0                           # mixed
+    assert share[4] > 0.7                                 # one far node: its cells only
+    assert share[5] < 0.05                                # large: the full search
+    # the skip threshold sends the trajectories moved far (3 and 5; 4 moved
+    # one node far) straight to the full search, same tables bit for bit
+    thr = ops.knn_skip_threshold(xd, cand, 36)
+    assert 0.0 < thr < 0.1
+    cells = ops.knn_moved_cells(pd, xd, B)
+    nbr_s = ops.knn_graph_moved(pd, xd, cand, B, 35, cells=cells, skip_above=thr)
+    share_s = ops.knn_table_share(cells, B, N)[:, 0].cpu()
+    print(f"{kind} graph, skip above {thr:.4f}: table share {share_s.tolist()}")
+    assert torch.equal(nbr_s, nbr)
+    assert share_s[3] == 0.0 and share_s[4] == 0.0 and share_s[5] == 0.0
+    assert share_s[1] > 0.99 and share_s[2] > 0.99
+    # the kNN-30 query of fixed points onto the moved meshes: queries at xi
+    # (table of xi), moved off xi (the bound takes the offset), and the queries
+    # in another order than xi -- burgers: the 'ij' grid against the 'xy' xi,
+    # cy: a permutation -- once with a table built for that order (answered
+    # from the table) and once with xi's table (offsets large: full search)
+    if kind == "burgers":
+        s = int(round(N ** 0.5))
+        perm = torch.arange(N).reshape(s, s).t().reshape(-1)   # 'ij' index -> 'xy' index
+    else:
+        perm = torch.randperm(N, generator=gen)
+    other = xi[perm]
+    cand_o = ops.knn_candidates(xd, ref=other.to(dev))
+    cases = [(xi.repeat(B, 1), cand, None, 1),
+             (xi.repeat(B, 1) + 0.003 * torch.cos(5 * xi.repeat(B, 1)), cand, None, 1),
+             (other.repeat(B, 1), cand_o, other, 1),
+             (other.repeat(B, 1), cand, None, 0)]
+    for qry, cq, rq, expect_table in cases:
+        cells = ops.knn_moved_cells(pd, xd, B)             # fresh miss counters
+        idx = ops.knn_query_moved(pd, qry.to(dev), xd, cq, B, 30,
+                                  ref=None if rq is None else rq.to(dev), cells=cells)
+        qs = ops.knn_table_share(cells, B, N)[:, 1].cpu()
+        print(f"{kind} query: table share per trajectory {qs.tolist()}")
+        assert torch.equal(idx, ops.knn_query(pd, qry.to(dev), B, 30))
         ref_q = refcpu.knn_query(pos, qry, B, 30)
         assert torch.equal(idx.cpu().long().reshape(ref_q.shape), ref_q)
+        if expect_table:
+            assert qs[1] > 0.99 and qs[2] > 0.99
+        else:
+            assert qs[1] < 0.5
 
 
 def test_knn_graph_integer_lattice_golden(dev):
@@ -552,8 +603,30 @@ def test_full_size_step_matches_oracle_sampled(dev, edge_gemm):
     model.edge_gemm = model_b.edge_gemm = edge_gemm
     eng = MMPDERollout("cy", model, model_b, itp, dmm, gc, B, dev)
     pred = eng.step(data[:, 0].to(dev), step).cpu().reshape(B, N)
+    torch.cuda.synchronize()
     mesh = eng.mesh.cpu().reshape(B, N, 2)
-    nbr = ops.knn_graph_nbr(eng.mesh, B, 35).long().cpu().reshape(B, N, 35)
+    # the rollout's own moved-mesh tables (candidate path), whole batch against
+    # the full search, sampled trajectories against the oracle below
+    nbr = eng.nbr_m.long().cpu().reshape(B, N, 35)
+    idx2 = eng.idx2.long().cpu().reshape(B, N, 30)
+    assert torch.equal(eng.nbr_m, ops.knn_graph_nbr(eng.mesh, B, 35))
+    assert torch.equal(eng.idx2, ops.knn_query(eng.mesh, eng.grid_rep, B, 30))
+    share = eng.knn_table_share()
+    print(f"full size: candidate tables answered {share[0]:.4f} (graph) {share[1]:.4f} (query)")
+    # the same tables at bench geometry with one trajectory moved far: the
+    # fallback runs inside the B = 16 launch, bit for bit
+    far = eng.mesh.clone().reshape(B, N, 2)
+    far[5] += 0.04 * torch.sin(11 * far[5].flip(1))
+    far = far.reshape(-1, 2)
+    cells = ops.knn_moved_cells(far, eng.xi, B)
+    nbr_far = ops.knn_graph_moved(far, eng.xi, eng.knn_cand, B, 35, cells=cells)
+    fs = ops.knn_table_share(cells, B, N)[:, 0]
+    print(f"far trajectory: table share {fs[5].item():.3f}, others min {fs[torch.arange(B) != 5].min().item():.3f}")
+    assert fs[5] < 0.9
+    assert torch.equal(nbr_far, ops.knn_graph_nbr(far, B, 35))
+    idx_far = ops.knn_query_moved(far, eng.grid_rep, eng.xi, eng.knn_cand_q, B, 30, ref=eng.grid,
+                                  cells=cells)
+    assert torch.equal(idx_far, ops.knn_query(far, eng.grid_rep, B, 30))
     pick = [0, 7, 15]
     sub = data[pick]
     ref_x, ref_y = refcpu.moving_mesh_tri(sds["dmm"], sub.reshape(len(pick), -1),
@@ -564,6 +637,8 @@ def test_full_size_step_matches_oracle_sampled(dev, edge_gemm):
     for i, b in enumerate(pick):
         _, ref_nbr, _ = refcpu.knn_graph(mesh[b], 35, 1)
         assert torch.equal(nbr[b] - b * N, ref_nbr), f"kNN-35 rows of trajectory {b}"
+        ref_idx = refcpu.knn_query(mesh[b], grid, 1, 30)
+        assert torch.equal(idx2[b], ref_idx.reshape(N, 30)), f"kNN-30 rows of trajectory {b}"
     opde = refcpu.PDEConst("cy", [30, N], ori_grid=grid)
     ref, aux = refcpu.mmpde_step(opde, sds, sub, sub, [step] * len(pick),
                                  mesh_override=mesh[pick].reshape(-1, 2))
@@ -602,9 +677,21 @@ def test_full_size_burgers_step_properties_and_oracle(dev):
     p1 = eng.step(u0, step)
     mesh = eng.mesh.clone()
     out_u, out_b = eng.out_u.clone(), eng.out_b.clone()
+    # the rollout's own moved-mesh tables (candidate path): kNN-35 graph, kNN-30
+    # of the moved mesh onto the grid (mode '1') and of the grid onto the
+    # moved mesh (mode '2', the grid in 'ij' order against the 'xy' mesh)
+    torch.cuda.synchronize()
+    nbr_m, idx1, idx2 = eng.nbr_m.clone(), eng.idx1.clone(), eng.idx2.clone()
+    share = eng.knn_table_share()
+    print(f"burgers: candidate tables answered {share[0]:.4f} (graph) {share[1]:.4f} (query), "
+          f"{share[2]:.4f} (mode-1 query)")
+    assert share[1] > 0.9     # the query table is built for the grid's own order
+    assert torch.equal(nbr_m, ops.knn_graph_nbr(mesh, B, 35))
+    assert torch.equal(idx1, ops.knn_query(eng.grid_rep, mesh, B, 30))
+    assert torch.equal(idx2, ops.knn_query(mesh, eng.grid_rep, B, 30))
     p2 = eng.step(u0, step)
     assert torch.equal(p1, p2)                                  # bitwise deterministic
-    nbr = ops.knn_graph_nbr(mesh, B, 35).long().cpu()
+    nbr = nbr_m.long().cpu()
     rows = torch.arange(B * N)[:, None]
     assert ((nbr // N) == rows // N).all() and (nbr != rows).all()
     m = mesh.cpu().double()
@@ -618,9 +705,14 @@ def test_full_size_burgers_step_properties_and_oracle(dev):
     sub = data[pick]
     ox, oy = refcpu.moving_mesh(sds["dmm"], opde, sub.reshape(len(pick), s, s), s, s)
     _close(mesh_c[pick], torch.cat((ox, oy), -1), 0.0, 2e-6, "full-size burgers DMM mesh")
+    grid_c = eng.grid.cpu()
     for b in pick:
         _, ref_nbr, _ = refcpu.knn_graph(mesh_c[b], 35, 1)
         assert torch.equal(nbr.reshape(B, N, 35)[b] - b * N, ref_nbr), f"kNN-35 rows of {b}"
+        r1 = refcpu.knn_query(grid_c, mesh_c[b], 1, 30).reshape(N, 30)
+        assert torch.equal(idx1.long().cpu().reshape(B, N, 30)[b], r1), f"kNN-30 (mode 1) rows of {b}"
+        r2 = refcpu.knn_query(mesh_c[b], grid_c, 1, 30).reshape(N, 30)
+        assert torch.equal(idx2.long().cpu().reshape(B, N, 30)[b], r2), f"kNN-30 (mode 2) rows of {b}"
     ref, aux = refcpu.mmpde_step(opde, sds, sub, sub, [step] * len(pick),
                                  mesh_override=mesh_c[pick].reshape(-1, 2))
     _close(p1.cpu().reshape(B, N)[pick], ref, 2.5e-5, 1e-7, "full-size burgers step")

@@ -18,7 +18,7 @@
 #include <vector>
 
 int launch_edge_wave_diag(const float *a, const float *b, const int32_t *nbr, int64_t n, int k,
-                          const float *msg2_b, const char *pk, const uint32_t *amax_in, float *out,
+                          const float *msg2_b, const char *pk, const float *rng, float *out,
                           float *side, int cus, int diag, hipStream_t st);
 
 #define CK(x)                                                                          \
@@ -81,9 +81,23 @@ int main(int argc, char **argv) {
     float *a = dev_random(n * H, -1, 1, rng), *b = dev_random(n * H, -1, 1, rng);
     float *w2 = dev_random(128 * 128, -0.09f, 0.09f, rng), *b2 = dev_random(128, -0.09f, 0.09f, rng);
     std::vector<int32_t> hn(n * k);
-    std::uniform_int_distribution<int> di(0, N - 1);
+    // neighbour locality: "random" (uniform in the trajectory, like a mesh in
+    // random node order), "local" (within +-R of the target's index, like a
+    // space-filling-curve order), "self" (every neighbour is the target)
+    const char *mode = argc > 2 ? argv[2] : "random";
+    const int R = argc > 3 ? atoi(argv[3]) : 24;
+    std::uniform_int_distribution<int> di(0, N - 1), dl(-R, R);
     for (int64_t i = 0; i < n; ++i)
-        for (int e = 0; e < k; ++e) hn[i * k + e] = (int32_t)((i / N) * N + di(rng));
+        for (int e = 0; e < k; ++e) {
+            int64_t j;
+            if (!strcmp(mode, "self")) j = i;
+            else if (!strcmp(mode, "local")) {
+                const int64_t l = std::min<int64_t>(std::max<int64_t>(i % N + dl(rng), 0), N - 1);
+                j = (i / N) * N + l;
+            } else j = (i / N) * N + di(rng);
+            hn[i * k + e] = (int32_t)j;
+        }
+    printf("neighbours: %s (R = %d)\n", mode, R);
     int32_t *nbr;
     CK(hipMalloc(&nbr, n * k * 4));
     CK(hipMemcpy(nbr, hn.data(), n * k * 4, hipMemcpyHostToDevice));
@@ -97,10 +111,11 @@ int main(int argc, char **argv) {
     lp.upd1_w = w1big;
     lp.upd1_ld = 260;
     if (mmpde_gnn_pack_f16x3(&lp, 1, pack, 0) != 0) return 1;
-    uint32_t *amax;
-    CK(hipMalloc(&amax, 2 * kAmaxShards * 4));
+    // range records (layer.hpp): max |a| = max |b| = 1 in every node tile
+    float *amax;
     {
-        std::vector<uint32_t> hs(2 * kAmaxShards, 0x3f800000u);
+        std::vector<float> hs(4 * range_tiles(n), 1.0f);
+        CK(hipMalloc(&amax, hs.size() * 4));
         CK(hipMemcpy(amax, hs.data(), hs.size() * 4, hipMemcpyHostToDevice));
     }
     float *out, *side;
