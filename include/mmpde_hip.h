@@ -86,13 +86,14 @@ int mmpde_knn_candidates(const float *xi, const float *ref, int64_t n_per, int32
 int64_t mmpde_knn_moved_cells_bytes(int64_t batches);
 int mmpde_knn_moved_cells(const float *pos, const float *xi, int64_t batches, int64_t n_per,
                           float *cells_out, mmpde_stream_t stream);
-/* out[0] (device float) = half the median over the reference points p of
+/* out[0] (device float) = the median over the reference points p of
  * R128(p) - R_kk(p), the 128th and the kk-th nearest distance of ref_p in xi
- * (cand from mmpde_knn_candidates(xi, ref)): the skip_above of the calls below
- * (past that displacement about half the lookups cannot pass).  Once per
- * table. */
+ * (cand from mmpde_knn_candidates(xi, ref)), halved when the queries move with
+ * the mesh (moved_queries != 0: the graph, whose query x_p is itself
+ * displaced): the skip_above of the calls below (past that typical
+ * displacement about half the lookups cannot pass).  Once per table. */
 int mmpde_knn_skip_threshold(const float *xi, const float *ref, int64_t n_per, const int32_t *cand,
-                             int kk, float *out, mmpde_stream_t stream);
+                             int kk, int moved_queries, float *out, mmpde_stream_t stream);
 /* misses_out [batches, 2] int32 (device): per trajectory, the graph and the
  * query misses counted in the record (diagnostics; stream-ordered copy). */
 int mmpde_knn_table_misses(const float *cells, int64_t batches, int32_t *misses_out,
@@ -107,9 +108,9 @@ int mmpde_knn_table_misses(const float *cells, int64_t batches, int32_t *misses_
  * mmpde_knn_candidates(xi, NULL); cells from mmpde_knn_moved_cells(pos, xi);
  * scratch: device bytes from mmpde_knn_graph_cand_scratch_bytes (a flag per
  * query: the ones the full search answers).  skip_above > 0: a trajectory
- * whose largest displacement exceeds it goes straight to the full search
- * (mmpde_knn_skip_threshold gives the displacement beyond which half the
- * table's lookups must fail); <= 0: the table is always tried.  k <= 63 and 128 <= n_per <= 4096, else it
+ * whose median cell displacement (over the record's non-empty cells) exceeds
+ * it goes straight to the full search (mmpde_knn_skip_threshold); <= 0: the
+ * table is always tried.  k <= 63 and 128 <= n_per <= 4096, else it
  * is mmpde_knn_graph. */
 int64_t mmpde_knn_graph_cand_scratch_bytes(int64_t batches, int64_t n_per);
 int mmpde_knn_graph_cand(const float *pos, const float *xi, const float *cells, float skip_above,

@@ -48,6 +48,11 @@ __device__ __forceinline__ int32_t *cell_last_miss(const float *cells, int b) {
 __device__ __forceinline__ int32_t *cell_any_miss(const float *cells, int b) {
     return (int32_t *)(cells + (int64_t)b * kCellRec + kCells + 10);  // [role]
 }
+// set by knn_cand_kernel when the trajectory skipped the table (skip_above):
+// the fallback then answers all its queries without reading the flags
+__device__ __forceinline__ int32_t *cell_skipped(const float *cells, int b) {
+    return (int32_t *)(cells + (int64_t)b * kCellRec + kCells + 12);  // [role]
+}
 
 // fp32 squared distance as raw bits: the graph key, and the query's filter key.
 __device__ __forceinline__ uint32_t key_f32(float2 p, float2 q) {
@@ -368,6 +373,10 @@ __global__ __launch_bounds__(256) void knn_kernel(const float2 *__restrict__ pts
     const int b = blockIdx.y;
     int q_count = n_q;  // queries of this trajectory to answer
     __shared__ int sList[QPB];
+    if (miss && cell_skipped(cells, b)[role]) {  // workgroup-uniform: the plain search
+        if (blockIdx.x == 0 && threadIdx.x == 0) cell_last_miss(cells, b)[role] = n_q;
+        miss = nullptr;
+    }
     if (miss) {
         if (!cell_any_miss(cells, b)[role]) {  // workgroup-uniform
             if (blockIdx.x == 0 && threadIdx.x == 0) cell_last_miss(cells, b)[role] = 0;
@@ -675,11 +684,32 @@ __global__ __launch_bounds__(256) void knn_cells_kernel(const float2 *__restrict
     __syncthreads();
     float *r = rec + (int64_t)b * kCellRec;
     const uint32_t v = cell[tid];
-    r[tid] = v == 0u ? -1.0f : __uint_as_float(v - 1u);
-    const float dall = wave_max(v == 0u ? 0.0f : __uint_as_float(v - 1u));
+    const float dc = v == 0u ? -1.0f : __uint_as_float(v - 1u);
+    r[tid] = dc;
+    const float dall = wave_max(fmaxf(dc, 0.0f));
+    const int nonempty = __popcll(__ballot(v != 0u));
     __syncthreads();
-    if (lane == 0) red[wave][0] = dall;
+    if (lane == 0) {
+        red[wave][0] = dall;
+        red[wave][1] = __int_as_float(nonempty);
+    }
+    // the median over the non-empty cells of their largest displacement (the
+    // statistic skip_above is compared with): bitonic sort, empty cells last
+    float *srt = (float *)cell;
+    srt[tid] = v == 0u ? 3.0e38f : dc;
     __syncthreads();
+    for (int size = 2; size <= kCells; size <<= 1)
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            if (tid < kCells / 2) {
+                const int i = 2 * tid - (tid & (stride - 1)), l = i + stride;
+                const float a = srt[i], c = srt[l];
+                if ((a > c) == ((i & size) == 0)) {
+                    srt[i] = c;
+                    srt[l] = a;
+                }
+            }
+            __syncthreads();
+        }
     if (tid == 0) {
         const float eps = 1.0e-5f * fmaxf(x1 - x0, y1 - y0);
         r[kCells + 0] = x0;
@@ -688,9 +718,13 @@ __global__ __launch_bounds__(256) void knn_cells_kernel(const float2 *__restrict
         r[kCells + 3] = hy;
         r[kCells + 4] = eps;
         r[kCells + 5] = fmaxf(fmaxf(red[0][0], red[1][0]), fmaxf(red[2][0], red[3][0]));
+        const int ne = __float_as_int(red[0][1]) + __float_as_int(red[1][1]) + __float_as_int(red[2][1]) +
+                       __float_as_int(red[3][1]);
+        r[kCells + 6] = ne > 0 ? srt[ne / 2] : 0.0f;
         for (int i = 0; i < 2; ++i) {
             cell_last_miss(rec, b)[i] = 0;
             cell_any_miss(rec, b)[i] = 0;
+            cell_skipped(rec, b)[i] = 0;
         }
     }
 }
@@ -759,10 +793,16 @@ __global__ __launch_bounds__(256) void knn_cand_kernel(const float2 *__restrict_
     if (p >= n_tot) return;  // wave-uniform
     const int b = (int)(p / n_per);
     const int pl = (int)(p - (int64_t)b * n_per);
+    const float *rec = cells + (int64_t)b * kCellRec;
+    // a trajectory whose median cell displacement exceeds skip_above does not
+    // try the table: the fallback answers all its queries (wave-uniform)
+    if (skip_above > 0.0f && rec[kCells + 6] > skip_above) {
+        if (pl == 0 && lane == 0) cell_skipped(cells, b)[QUERY ? 1 : 0] = 1;
+        return;
+    }
     const float2 *X = x + (int64_t)b * n_per;
     const float2 q = QUERY ? qry[p] : X[pl];
     const int32_t *cr = cand + (int64_t)pl * kCandN;
-    const float *rec = cells + (int64_t)b * kCellRec;
     const float2 rp = ref[pl];
     const float rq = cand_rq(xi, rp, n_per, cr, q);
     const int kk = QUERY ? k : k + 1;
@@ -773,11 +813,7 @@ __global__ __launch_bounds__(256) void knn_cand_kernel(const float2 *__restrict_
             cell_any_miss(cells, b)[QUERY ? 1 : 0] = 1;
         }
     };
-    // a trajectory moved by more than skip_above: the table is not tried
-    if (skip_above > 0.0f && rec[kCells + 5] > skip_above) {
-        give_up();
-        return;
-    }
+
     // Given up (wave-uniform) when the bound proves nothing, or when already
     // the unmoved kk-th candidate lies beyond it: the moved one then almost
     // never passes, and the sort would be wasted.  A heuristic only -- the
@@ -899,13 +935,13 @@ extern "C" int mmpde_knn_moved_cells(const float *pos, const float *xi, int64_t 
     return MMPDE_OK;
 }
 
-// Half the median over reference points p of R128(p) - R_kk(p) (the 128th and
-// the kk-th candidate distance of r_p in xi): past that displacement about
-// half the table's lookups cannot pass.  One workgroup, bitonic sort in LDS.
+// The median over reference points p of R128(p) - R_kk(p) (the 128th and the
+// kk-th candidate distance of r_p in xi), times `scale`.  One workgroup,
+// bitonic sort in LDS.
 __global__ __launch_bounds__(256) void knn_margin_kernel(const float2 *__restrict__ xi,
                                                          const float2 *__restrict__ ref, int n_per,
                                                          const int32_t *__restrict__ cand, int kk,
-                                                         float *__restrict__ out) {
+                                                         float scale, float *__restrict__ out) {
     __shared__ float sm[4096];
     for (int p = threadIdx.x; p < 4096; p += 256) {
         float m = 3.0e38f;
@@ -930,7 +966,7 @@ __global__ __launch_bounds__(256) void knn_margin_kernel(const float2 *__restric
             }
             __syncthreads();
         }
-    if (threadIdx.x == 0) out[0] = 0.5f * sm[n_per / 2];
+    if (threadIdx.x == 0) out[0] = scale * sm[n_per / 2];
 }
 
 __global__ void knn_misses_kernel(const float *__restrict__ cells, int batches, int32_t *__restrict__ out) {
@@ -948,10 +984,13 @@ extern "C" int mmpde_knn_table_misses(const float *cells, int64_t batches, int32
 }
 
 extern "C" int mmpde_knn_skip_threshold(const float *xi, const float *ref, int64_t n_per, const int32_t *cand,
-                                        int kk, float *out, mmpde_stream_t stream) {
+                                        int kk, int moved_queries, float *out, mmpde_stream_t stream) {
     MMPDE_REQUIRE(xi && cand && out && n_per >= kCandN && n_per <= 4096 && kk >= 1 && kk <= kCandN);
+    // a moved query spends the margin twice (its own offset and its
+    // neighbours' displacement), a query at its reference point once
     hipLaunchKernelGGL(knn_margin_kernel, dim3(1), dim3(256), 0, as_stream(stream), (const float2 *)xi,
-                       (const float2 *)(ref ? ref : xi), (int)n_per, cand, kk, out);
+                       (const float2 *)(ref ? ref : xi), (int)n_per, cand, kk, moved_queries ? 0.5f : 1.0f,
+                       out);
     MMPDE_RET_LAUNCH();
     return MMPDE_OK;
 }

@@ -67,11 +67,13 @@ def knn_candidates(xi: torch.Tensor, ref: torch.Tensor | None = None):
     return cand
 
 
-def knn_skip_threshold(xi: torch.Tensor, cand, kk: int, ref: torch.Tensor | None = None) -> float:
+def knn_skip_threshold(xi: torch.Tensor, cand, kk: int, ref: torch.Tensor | None = None,
+                       moved_queries: bool = False) -> float:
     """The skip_above of knn_graph_moved / knn_query_moved for a table cand =
-    knn_candidates(xi, ref) and kk = k + 1 (graph) or k (query): half the median
-    of R128 - R_kk over the reference points (mmpde_knn_skip_threshold).  Reads
-    one float back to the host: call once per table, not per step."""
+    knn_candidates(xi, ref) and kk = k + 1 (graph) or k (query): the median of
+    R128 - R_kk over the reference points, halved for queries that move with
+    the mesh (the graph) (mmpde_knn_skip_threshold).  Reads one float back to
+    the host: call once per table, not per step."""
     if cand is None:
         return 0.0
     L.require_device(xi, cand, ref)
@@ -79,7 +81,8 @@ def knn_skip_threshold(xi: torch.Tensor, cand, kk: int, ref: torch.Tensor | None
     ref = None if ref is None else L.f32c(ref).reshape(-1, 2)
     out = torch.empty((1,), dtype=torch.float32, device=xi.device)
     L.check(L.lib().mmpde_knn_skip_threshold(L.ptr(xi), L.ptr(ref), xi.shape[0], L.ptr(cand), kk,
-                                             L.ptr(out), L.stream(xi.device)), "mmpde_knn_skip_threshold")
+                                             int(moved_queries), L.ptr(out), L.stream(xi.device)),
+            "mmpde_knn_skip_threshold")
     return float(out.item())
 
 

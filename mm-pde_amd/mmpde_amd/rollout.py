@@ -81,9 +81,9 @@ class MMPDERollout:
             self.knn_cand = ops.knn_candidates(self.xi)
             self.knn_cand_q = (self.knn_cand if self.grid is self.xi
                                else ops.knn_candidates(self.xi, ref=self.grid))
-            # trajectories moved further than these go straight to the full
-            # search (about half the table's lookups would fail; read once)
-            self.knn_skip = ops.knn_skip_threshold(self.xi, self.knn_cand, gc.n + 1)
+            # trajectories whose typical displacement exceeds these go straight
+            # to the full search (about half the lookups would fail; read once)
+            self.knn_skip = ops.knn_skip_threshold(self.xi, self.knn_cand, gc.n + 1, moved_queries=True)
             self.knn_skip_q = ops.knn_skip_threshold(self.xi, self.knn_cand_q, 30, ref=self.grid)
             nb = max(L.lib().mmpde_knn_graph_cand_scratch_bytes(batches, N), 1)
             self.knn_scratch = torch.empty((nb,), dtype=torch.uint8, device=self.device)
@@ -98,7 +98,8 @@ class MMPDERollout:
                 # and a displacement record of the unmoved grid (all zero)
                 # (rebuilt every step, which also zeroes its miss counters)
                 self.knn_cand_1 = ops.knn_candidates(self.grid, ref=self.xi)
-                self.knn_skip_1 = ops.knn_skip_threshold(self.grid, self.knn_cand_1, 30, ref=self.xi)
+                self.knn_skip_1 = ops.knn_skip_threshold(self.grid, self.knn_cand_1, 30, ref=self.xi,
+                                                         moved_queries=True)
                 self.knn_cells_1 = torch.empty_like(self.knn_cells)
                 self.knn_scratch_1 = torch.empty((nb,), dtype=torch.uint8, device=self.device)
             # the fixed-grid model depends on u only: it runs on a side stream,

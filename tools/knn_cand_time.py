@@ -32,7 +32,8 @@ dev = torch.device("cuda:0")
 xi = cy_synth_mesh().to(dev)
 N = xi.shape[0]
 cand = ops.knn_candidates(xi)
-thr_g, thr_q = ops.knn_skip_threshold(xi, cand, 36), ops.knn_skip_threshold(xi, cand, 30)
+thr_g = ops.knn_skip_threshold(xi, cand, 36, moved_queries=True)
+thr_q = ops.knn_skip_threshold(xi, cand, 30)
 print(f"skip thresholds: graph {thr_g:.4f}, query {thr_q:.4f}")
 need = L.lib().mmpde_knn_graph_cand_scratch_bytes(B, N)
 scr = torch.zeros((need,), dtype=torch.uint8, device=dev)
