@@ -510,6 +510,25 @@ int mmpde_itp_interp(const float *src, const float *vals, const float *qry, cons
                      int64_t batches, int64_t n_src, int64_t n_qry, const void *packed,
                      const float *addend, float *out, mmpde_stream_t stream);
 
+/* ------------------------------------------------------------------------
+ * DMM training (reference mesh/dmm_utils.py)
+ * ---------------------------------------------------------------------- */
+
+/* Softmax kernel smoother (reference mesh/dmm_utils.py:233-249 interpolate with
+ * scale = n on the n x n linspace grid, :251-267 interpolate_tri with scale =
+ * sqrt(n) on a mesh of n points): out[q] = sum_j vals[j] softmax_j(-scale *
+ * |pts[j] - qry[q]|).  pts [pts_sets, n_pts, 2], vals [val_sets, n_pts],
+ * qry [n_q, 2]: query q uses point set q / (n_q / pts_sets) and value set
+ * q / (n_q / val_sets) (both must divide n_q).  _grad: grad_qry [n_q, 2] =
+ * grad_out[q] * d out[q] / d qry[q] (the VJP torch.norm / softmax autograd
+ * gives, 0 for the direction of a point at distance 0). */
+int mmpde_softmax_interp(const float *pts, int64_t n_pts, int64_t pts_sets, const float *vals,
+                         int64_t val_sets, const float *qry, int64_t n_q, float scale, float *out,
+                         mmpde_stream_t stream);
+int mmpde_softmax_interp_grad(const float *pts, int64_t n_pts, int64_t pts_sets, const float *vals,
+                              int64_t val_sets, const float *qry, int64_t n_q, float scale,
+                              const float *grad_out, float *grad_qry, mmpde_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -142,6 +142,8 @@ _SIGS = {
     "mmpde_itp_pack_bytes": (_I64, []),
     "mmpde_itp_pack": (_I, [_P, _P, _P]),
     "mmpde_itp_interp": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _P, _P, _P, _P]),
+    "mmpde_softmax_interp": (_I, [_P, _I64, _I64, _P, _I64, _P, _I64, _F, _P, _P]),
+    "mmpde_softmax_interp_grad": (_I, [_P, _I64, _I64, _P, _I64, _P, _I64, _F, _P, _P, _P]),
 }
 
 EXPORTS = tuple(_SIGS)

@@ -13,8 +13,14 @@ returns exactly that through an analytic vector-Jacobian product
 (mmpde_dmm_mesh_graph / mmpde_dmm_mesh_array; derivation in dmm.hip).
 ``DMM.forward`` (phi, and rf=True's second output) runs the branch and the
 head on the same kernels (mmpde_dmm_branch_*, mmpde_dmm_phi); ``DenseNet`` /
-``ConvNet`` forwards run on the skinny-linear and conv kernels.  All are
-eval-mode (DMM training is outside the hot path).
+``ConvNet`` forwards run on the skinny-linear and conv kernels.
+
+In ``train()`` mode (DMM training, reference mesh/dmm_utils.py:391-1095,
+SURVEY.md §8(f) row 4: ``mmpde_amd.dmm_train``) every forward is the
+reference's computation as differentiable device torch ops -- BatchNorm on
+batch statistics, twice differentiable in the grid (the Monge-Ampere loss
+takes d2 phi / d xi2 through autograd) -- with the fixed grid's kNN-35 graph
+from the HIP kernel and the mean aggregation over its fixed in-degree.
 """
 from __future__ import annotations
 
@@ -29,10 +35,6 @@ from . import ops
 from .ops import knn_graph_nbr
 
 
-def _eval_only(m: nn.Module):
-    if m.training:
-        raise NotImplementedError("training-mode forward is out of scope (DMM training, "
-                                  "SURVEY.md §8(f) row 4); call .eval()")
 
 
 class DenseNet(nn.Module):
@@ -54,7 +56,13 @@ class DenseNet(nn.Module):
     def forward(self, x):
         """dmm_model.py:31-45 (normalize=False): (out, x) with x the last hidden
         activation (the input of the last Linear)."""
-        _eval_only(self)
+        if self.training:   # differentiable torch ops (DMM training)
+            for i, l in enumerate(self.layers):
+                if i != self.n_layers - 1:
+                    x = torch.tanh(l(x))
+                else:
+                    out = l(x)
+            return out, x
         for i, l in enumerate(self.layers):
             if i != self.n_layers - 1:
                 x = ops.linear_rows(x, l.weight, l.bias, L.ACT_TANH)
@@ -80,8 +88,12 @@ class ConvNet(nn.Module):
 
     def forward(self, x):
         """dmm_model.py:65-81: x [B, 1, s, s] -> [B, 512]."""
-        _eval_only(self)
         c = self.layers
+        if self.training:   # differentiable torch ops (DMM training)
+            x1 = torch.tanh(c[0](x))
+            x3 = torch.tanh(x1 + c[2](torch.tanh(c[1](x1))))
+            f = torch.flatten(torch.tanh(c[3](x3)), 1)
+            return self.fc3(torch.tanh(self.fc2(f)))
         x1 = ops.conv2d(x, c[0].weight, c[0].bias, 2, 2, L.ACT_TANH)
         x2 = ops.conv2d(x1, c[1].weight, c[1].bias, 1, 2, L.ACT_TANH)
         x3 = ops.conv2d(x2, c[2].weight, c[2].bias, 1, 2, L.ACT_TANH, residual=x1)
@@ -104,8 +116,18 @@ class GNN_Layer_FS_2D(nn.Module):  # noqa: N801 - reference name
         self.update_net_2 = nn.Sequential(nn.Linear(hidden_features, out_features), nn.Tanh())
         self.norm = BatchNorm(hidden_features)
 
-    def forward(self, *args, **kwargs):
-        raise NotImplementedError("runs inside mmpde_dmm_mesh_graph")
+    def forward(self, x, u, pos_x, pos_y, nbr):
+        """Training-mode layer (dmm_model.py:126-142) as differentiable torch ops:
+        tanh messages cat(x_i, x_j, u_i - u_j, dx, dy) over the target-major
+        neighbour table nbr [n, k] (every row k sources: PyG's mean is the mean
+        over them), update x + U2 tanh(U1 cat(x, m)), BatchNorm.  The eval
+        forward runs inside mmpde_dmm_mesh_graph."""
+        n, k = nbr.shape
+        j = nbr.reshape(-1).long()
+        i = torch.arange(n, device=x.device).repeat_interleave(k)
+        m = torch.cat((x[i], x[j], u[i] - u[j], pos_x[i] - pos_x[j], pos_y[i] - pos_y[j]), dim=-1)
+        m = self.message_net_2(self.message_net_1(m)).reshape(n, k, -1).mean(1)
+        return self.norm(x + self.update_net_2(self.update_net_1(torch.cat((x, m), dim=-1))))
 
 
 class DMM(nn.Module):
@@ -151,6 +173,8 @@ class DMM(nn.Module):
         Returns phi [B*m, 1], or (phi, second_out [B*m, L'], ones [B*m*L', 1])
         with rf=True."""
         L.require_device(u, grid)
+        if self.training:
+            return self._forward_train(u, grid, rf)
         bp, hd = self.device_params()
         u = L.f32c(u)
         grid = L.f32c(grid).reshape(-1, 2)
@@ -188,10 +212,41 @@ class DMM(nn.Module):
             return phi
         return phi, second, torch.ones_like(second).reshape(-1, 1)
 
+    def _forward_train(self, u, grid, rf=False):
+        """dmm_model.py:185-219 in train() mode: differentiable in the weights and
+        in `grid` (to any order), BatchNorm on batch statistics."""
+        B = u.shape[0]
+        if grid.shape[0] % B:
+            raise ValueError("grid rows must be a multiple of the batch size")
+        if self.mode == "array":
+            branch = self.branch(u.unsqueeze(1))
+        else:
+            og = torch.as_tensor(self.ori_grid).to(u.device, torch.float32).reshape(-1, 2)
+            N = og.shape[0]
+            nbr = self.grid_nbr(og.contiguous())                       # [N, 35] local
+            gnbr = (nbr[None].long() + N * torch.arange(B, device=u.device)[:, None, None])
+            gnbr = gnbr.reshape(B * N, -1)
+            x = u.reshape(-1, 1)
+            pos = og[None].expand(B, N, 2).reshape(-1, 2)
+            pos_x, pos_y = pos[:, :1], pos[:, 1:]
+            h = self.embedding_mlp(torch.cat((x, pos_x, pos_y), -1))
+            for layer in self.gnn_layers:
+                h = layer(h, x, pos_x, pos_y, gnbr)
+            h, _ = self.decoding_mlp(h)
+            branch = self.output_mlp(h.reshape(B, -1))
+        rep = grid.shape[0] // B
+        branch = branch[:, None, :].expand(B, rep, branch.shape[-1]).reshape(-1, branch.shape[-1])
+        trunk, _ = self.trunk(grid)
+        out, second = self.out_nn(torch.cat((branch, trunk.reshape(-1, branch.shape[-1])), dim=-1))
+        if not rf:
+            return out
+        return out, second, torch.ones_like(second).reshape(-1, 1)
+
     # ----------------------------------------------------------------- packing
     def _check(self):
         if self.training:
-            raise NotImplementedError("training-mode forward is out of scope; call .eval()")
+            raise NotImplementedError("the HIP head is eval-mode: call .eval() (train() "
+                                      "mode runs DMM.forward as torch ops)")
         tl = self.trunk.layers
         ol = self.out_nn.layers
         if len(tl) != 2 or len(ol) != 2 or ol[1].out_features != 1:

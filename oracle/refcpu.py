@@ -269,8 +269,9 @@ def basecnn(sd, dt, u, tw):
     return out.squeeze()
 
 
-def dmm_gnn_layer(sd, p, x, u, pos_x, pos_y, edge_index):
-    """DMM GNN_Layer_FS_2D (tanh), dmm_model.py:126-142."""
+def dmm_gnn_layer(sd, p, x, u, pos_x, pos_y, edge_index, train=False):
+    """DMM GNN_Layer_FS_2D (tanh), dmm_model.py:126-142 (train: BatchNorm on
+    batch statistics, the DMM training forward)."""
     n = x.shape[0]
 
     def message(i, j):
@@ -282,11 +283,14 @@ def dmm_gnn_layer(sd, p, x, u, pos_x, pos_y, edge_index):
     agg = propagate_mean(edge_index, n, message)
     upd = torch.tanh(_lin(sd, p + ".update_net_1.0", torch.cat((x, agg), dim=-1)))
     upd = torch.tanh(_lin(sd, p + ".update_net_2.0", upd))
-    return _bn(sd, p + ".norm.module", x + upd)
+    return _bn(sd, p + ".norm.module", x + upd, train=train)
 
 
-def dmm_forward(sd, mode, u, grid, ori_grid=None, hidden_layer=3, grid_edge_index=None):
-    """DMM.forward(u, grid), dmm_model.py:185-219.  `grid` is xi [B*N, 2]."""
+def dmm_forward(sd, mode, u, grid, ori_grid=None, hidden_layer=3, grid_edge_index=None,
+                train=False):
+    """DMM.forward(u, grid), dmm_model.py:185-219.  `grid` is xi [B*N, 2].
+    train=True: the train() forward of DMM training (BatchNorm on batch
+    statistics, running buffers of `sd` updated)."""
     B = u.shape[0]
     if mode == "array":
         branch = convnet(sd, "branch", u.unsqueeze(1)).unsqueeze(1)
@@ -302,10 +306,11 @@ def dmm_forward(sd, mode, u, grid, ori_grid=None, hidden_layer=3, grid_edge_inde
         pos_x = gpos[:, 0][:, None]
         pos_y = gpos[:, 1][:, None]
         h = _lin(sd, "embedding_mlp.0", torch.cat((x, pos_x, pos_y), -1))
-        h = torch.tanh(_bn(sd, "embedding_mlp.1", h))
-        h = _bn(sd, "embedding_mlp.4", _lin(sd, "embedding_mlp.3", h))
+        h = torch.tanh(_bn(sd, "embedding_mlp.1", h, train=train))
+        h = _bn(sd, "embedding_mlp.4", _lin(sd, "embedding_mlp.3", h), train=train)
         for i in range(hidden_layer):
-            h = dmm_gnn_layer(sd, f"gnn_layers.{i}", h, x, pos_x, pos_y, grid_edge_index)
+            h = dmm_gnn_layer(sd, f"gnn_layers.{i}", h, x, pos_x, pos_y, grid_edge_index,
+                              train=train)
         h, _ = densenet(sd, "decoding_mlp", h, 2)
         b = h.reshape(B, 1, -1)
         b = torch.tanh(_lin(sd, "output_mlp.0", b))

@@ -100,9 +100,8 @@ def test_densenet_convnet_forward_vs_oracle(dev):
     rbr = refcpu.convnet(sd_b, "branch", u)
     assert br.shape == rbr.shape == (3, 512)
     _close(br, rbr, 2e-5, 1e-6, "ConvNet.forward")
-    dmm_b.train()
-    with pytest.raises(NotImplementedError):
-        dmm_b.branch(u.to(dev))
+    dmm_b.train()       # DMM training's differentiable torch path (no BatchNorm inside)
+    _close(dmm_b.branch(u.to(dev)), rbr, 2e-5, 1e-6, "ConvNet.forward (train mode)")
 
 
 def _bilinear_f32(x, oh, ow):

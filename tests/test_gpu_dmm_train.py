@@ -1,0 +1,322 @@
+"""GPU parity of DMM training (reference mesh/dmm_utils.py)
+against the CPU restatement oracle/dmm_train_ref.py (fp64 torch, the
+reference's own [queries, points] tensor formulas and autograd):
+
+- the softmax kernel smoother (mmpde_softmax_interp) and its position VJP
+  (mmpde_softmax_interp_grad) for both of the reference's interpolations,
+  including a query on a lattice point (zero subgradient, as torch.norm);
+- the train()-mode DMM forward (BatchNorm on batch statistics) and its first
+  and second derivatives in the grid, graph (cy) and array (burgers) modes;
+- the samplers, draw for draw under the same numpy seed;
+- the Monge-Ampere objective and its parameter gradients;
+- one Adam epoch of train_MA_res (update = lr g'/(|g'| + eps) on the first
+  step) and an LBFGS epoch (runs, logs finite values);
+- evaluate_tri / evaluate.
+
+Bars are relative to max|ref| of each quantity; fp32 device arithmetic against
+fp64 (observed errors are printed).
+"""
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import dmm_train_ref as R
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(got, ref, rtol, atol=0.0, what=""):
+    got = got.detach().double().cpu().reshape(-1)
+    ref = ref.detach().double().cpu().reshape(-1)
+    assert got.shape == ref.shape, (what, got.shape, ref.shape)
+    if ref.numel() == 0:
+        return
+    d = (got - ref).abs()
+    err = d.max().item()
+    bound = rtol * ref.abs().max().item() + atol
+    at = int(d.argmax())
+    print(f"{what}: max|err| {err:.3e} at {at} bound {bound:.3e} max|ref| {ref.abs().max().item():.3e}")
+    assert err <= bound, (what, err, bound)
+
+
+def _models(kind):
+    from mmpde_amd.synth import build_models
+
+    pde, _, _, _, dmm, _ = build_models(kind, seed=3)
+    dmm.train()
+    return pde, dmm
+
+
+def _sd64(dmm):
+    """fp64 copy of the state dict: parameters as grad-requiring leaves."""
+    names = {n for n, _ in dmm.named_parameters()}
+    sd = {}
+    for k, v in dmm.state_dict().items():
+        t = v.detach().cpu().clone()
+        if t.is_floating_point():
+            t = t.double()
+        if k in names:
+            t.requires_grad_(True)
+        sd[k] = t
+    return sd
+
+
+def _phi(kind, pde, sd):
+    mode = "graph" if kind == "cy" else "array"
+    og = pde.ori_grid.double() if kind == "cy" else None
+    return R.phi_fn(sd, mode, ori_grid=og)
+
+
+def _data(kind, pde, T, seed=5):
+    """cy: all_u [T, N, 3] (x, y, u) with a per-snapshot perturbed mesh;
+    burgers: all_u [T, 48, 48]."""
+    from mmpde_amd.synth import burgers_grid_points, fields
+
+    if kind == "cy":
+        g = torch.Generator().manual_seed(seed)
+        u = fields(pde.ori_grid, 1, T, seed=seed)[0]                         # [T, N]
+        mesh = pde.ori_grid[None] + 1e-3 * torch.randn(T, *pde.ori_grid.shape, generator=g)
+        return torch.cat((mesh.clamp(0, 1), u[..., None]), -1).float()
+    return fields(burgers_grid_points(), 1, T, seed=seed)[0].reshape(T, 48, 48)
+
+
+def _args(kind, bx, bu, **kw):
+    a = dict(experiment=kind, bound_constraint="soft", batch_size_x_adam=bx, batch_size_u_adam=bu,
+             batch_size_x_lbfgs=bx, batch_size_u_lbfgs=bu, train_sample_grid=0, lr_adam=2e-4,
+             lr_lbfgs=1e-3, weight_decay=1e-5, gamma_adam=0.2, gamma_lbfgs=0.2, loss_weight0=1.0,
+             loss_weight1=1000.0, loss_weight2=1.0, loss_convex=True)
+    a.update(kw)
+    return SimpleNamespace(**a)
+
+
+# ----------------------------------------------------------------------------- smoother
+def test_softmax_interp_lattice_vs_oracle(dev):
+    from mmpde_amd import dmm_train as T
+
+    g = torch.Generator().manual_seed(1)
+    n, S, per = 48, 3, 257
+    u = torch.randn(S, n, n, generator=g)
+    q = torch.rand(S * per, 2, generator=g) * 1.2 - 0.1
+    q[5] = R.lattice(n, torch.float32)[30 * n + 12]      # on a lattice point (x_12, y_30)
+    ref_q = q.double().clone().requires_grad_(True)
+    ref = R.interpolate(u.double().repeat_interleave(per, 0), ref_q[:, :1], ref_q[:, 1:])
+    w = torch.randn(S * per, 1, generator=g)
+    (ref * w.double()).sum().backward()
+    qd = q.to(dev).requires_grad_(True)
+    got = T.interpolate(u.to(dev), qd[:, :1], qd[:, 1:])
+    assert got.shape == ref.shape
+    _close(got, ref, 1e-5, 1e-7, "interpolate (lattice, scale n)")
+    (got * w.to(dev)).sum().backward()
+    _close(qd.grad, ref_q.grad, 2e-5, 1e-6, "interpolate VJP in the query")
+
+
+def test_softmax_interp_tri_vs_oracle(dev):
+    from mmpde_amd import dmm_train as T
+
+    pde, _ = _models("cy")
+    g = torch.Generator().manual_seed(2)
+    N, S, per = pde.ori_grid.shape[0], 2, 300
+    mesh = pde.ori_grid[None] + 1e-3 * torch.randn(S, N, 2, generator=g)
+    u = torch.randn(S, N, generator=g)
+    q = torch.rand(S * per, 2, generator=g)
+    ref_q = q.double().clone().requires_grad_(True)
+    rep = lambda t: t.double().repeat_interleave(per, 0)  # noqa: E731
+    ref = R.interpolate_tri(rep(u), rep(mesh[..., :1]), rep(mesh[..., 1:]),
+                            ref_q[:, None, :1].expand(-1, N, 1), ref_q[:, None, 1:].expand(-1, N, 1))
+    ref.sum().backward()
+    qd = q.to(dev).requires_grad_(True)
+    got = T.interpolate_tri(u.to(dev), mesh.to(dev), qd[:, :1], qd[:, 1:])
+    _close(got, ref, 1e-5, 1e-7, "interpolate_tri (mesh, scale sqrt N)")
+    got.sum().backward()
+    _close(qd.grad, ref_q.grad, 2e-5, 1e-6, "interpolate_tri VJP in the query")
+    # the monitor's lattice derivatives (sample_train_data_tri / evaluate_tri)
+    rx, ry = R.tri_lattice_derivatives(u.double(), mesh.double())
+    n = int(np.sqrt(N))
+    lat = T.unit_lattice(n, dev)
+    gq = T.softmax_interp_grad_at(mesh.to(dev), u.to(dev), lat.repeat(S, 1), float(np.sqrt(N)))
+    gq = gq.reshape(S, n, n, 2)
+    _close(gq[..., 0], rx, 2e-5, 1e-6, "lattice d/dx of interpolate_tri")
+    _close(gq[..., 1], ry, 2e-5, 1e-6, "lattice d/dy of interpolate_tri")
+
+
+# ----------------------------------------------------------------------------- forward
+@pytest.mark.parametrize("kind", ["cy", "burgers"])
+def test_train_forward_and_grid_derivatives_vs_oracle(dev, kind):
+    pde, dmm = _models(kind)
+    sd = _sd64(dmm)
+    phi_ref = _phi(kind, pde, sd)
+    data = _data(kind, pde, 4)
+    u = data[:2, :, 2] if kind == "cy" else data[:2]
+    g = torch.Generator().manual_seed(4)
+    x = torch.rand(2 * 37, 2, generator=g)
+
+    def derivs(phi, u, x):
+        x1 = x[:, :1].clone().requires_grad_(True)
+        x2 = x[:, 1:].clone().requires_grad_(True)
+        out = phi(u, torch.cat((x1, x2), 1))
+        px, py = R._grad(out, x1), R._grad(out, x2)
+        return out, px, py, R._grad(px, x1), R._grad(px, x2), R._grad(py, x2)
+
+    ref = derivs(phi_ref, u.double(), x.double())
+    dmm.to(dev)
+    got = derivs(dmm, u.to(dev), x.to(dev))
+    for name, a, b in zip(("phi", "phi_x", "phi_y", "phi_xx", "phi_xy", "phi_yy"), got, ref):
+        _close(a, b, 1e-4, 1e-7, f"{kind} train-mode {name}")
+    # BatchNorm running statistics advanced as the reference's (momentum 0.1)
+    for k, v in dmm.state_dict().items():
+        if k.endswith("running_mean") or k.endswith("running_var"):
+            _close(v, sd[k], 1e-4, 1e-7, f"{kind} {k}")
+
+
+# ----------------------------------------------------------------------------- samplers
+@pytest.mark.parametrize("kind", ["cy", "burgers"])
+def test_samplers_vs_oracle(dev, kind):
+    from mmpde_amd import dmm_train as T
+
+    pde, _ = _models(kind)
+    all_u = _data(kind, pde, 6)
+    bx, bu = 8, (10 if kind == "cy" else 4)
+    args = _args(kind, bx, bu)
+    np.random.seed(11)
+    got = T._sample(args, all_u, bx, bu, dev)
+    np.random.seed(11)
+    ref = (R.sample_tri if kind == "cy" else R.sample_arr)(all_u, bx, bu)
+    for name, a, b in zip(("u", "ux", "uy", "alpha", "RHS"), got[:5], ref[:5]):
+        _close(a, b, 2e-5, 1e-6, f"{kind} sample {name}")
+    assert torch.equal(got[5].cpu().double(), ref[5]), "sampled points differ"
+    for k in range(4):
+        assert torch.equal(got[6][k].cpu().double(), ref[6][k])
+        assert torch.equal(got[7][k].cpu().double(), ref[7][k].float().double())
+    with pytest.raises(ValueError):
+        T._sample(args, all_u, bx, bu + 2, dev)
+
+
+# ----------------------------------------------------------------------------- loss
+@pytest.mark.parametrize("kind", ["cy", "burgers"])
+def test_objective_and_parameter_grads_vs_oracle(dev, kind):
+    from mmpde_amd import dmm_train as T
+
+    pde, dmm = _models(kind)
+    sd = _sd64(dmm)
+    all_u = _data(kind, pde, 6)
+    bx, bu = 8, (10 if kind == "cy" else 4)
+    args = _args(kind, bx, bu)
+    dmm.to(dev)
+    np.random.seed(3)
+    sample = T._sample(args, all_u, bx, bu, dev)
+    loss, li, lb, lc, lhs, rhs = T.objective(dmm, args, sample, bx, False, dev)
+    dmm.zero_grad()
+    loss.backward()
+    s64 = tuple(t.detach().double().cpu() if torch.is_tensor(t) else [b.detach().double().cpu() for b in t]
+                for t in sample)
+    rl, rli, rlb, rlc = R.total_loss(_phi(kind, pde, sd), s64, bx)
+    rl.backward()
+    for name, a, b in (("loss", loss, rl), ("loss_in", li, rli), ("loss_bound", lb, rlb),
+                       ("loss_convex", lc, rlc)):
+        _close(a, b, 1e-4, 1e-9, f"{kind} {name}")
+    # parameters outside this mode's forward (array mode: the graph branch) get
+    # no gradient on either side; a bias feeding a BatchNorm has an analytic
+    # gradient of 0 and fp32 rounding noise, so the bar carries 1e-5 of the
+    # largest gradient of the model as its absolute part
+    G = max(sd[n].grad.abs().max().item() for n, _ in dmm.named_parameters() if sd[n].grad is not None)
+    worst = 0.0
+    for n, p in dmm.named_parameters():
+        ref = sd[n].grad
+        if ref is None:
+            assert p.grad is None or not bool(p.grad.any()), n
+            continue
+        err = (p.grad.double().cpu() - ref).abs().max().item()
+        worst = max(worst, err / max(ref.abs().max().item(), 1e-5 * G))
+        _close(p.grad, ref, 2e-3, 1e-5 * G, f"{kind} d loss / d {n}")
+    print(f"{kind}: worst relative gradient error {worst:.3e}")
+
+
+# ----------------------------------------------------------------------------- training loop
+def test_train_MA_res_adam_step_vs_oracle(dev, tmp_path):  # noqa: N802
+    from mmpde_amd import dmm_train as T
+
+    kind = "cy"
+    pde, dmm = _models(kind)
+    sd = _sd64(dmm)
+    p0 = {n: p.detach().double().clone() for n, p in dmm.named_parameters()}
+    all_u = _data(kind, pde, 6)
+    bx, bu = 8, 10
+    args = _args(kind, bx, bu)
+    dmm.to(dev)
+    np.random.seed(21)
+    out = T.train_MA_res(all_u, all_u, all_u, args, dmm, False, 1, 0, dev, save_dir=str(tmp_path))
+    assert len(out) == 15 and out[0] is dmm
+    assert (tmp_path / "dmm_cy_epoch1.pt").exists()
+    np.random.seed(21)
+    s64 = R.sample_tri(all_u, bx, bu)
+    rl, rli, _, _ = R.total_loss(_phi(kind, pde, sd), s64, bx)
+    rl.backward()
+    assert abs(out[1][0] - rli.item()) <= 1e-4 * abs(rli.item()), (out[1][0], rli.item())
+    G = max(sd[n].grad.abs().max().item() for n in p0 if sd[n].grad is not None)
+    for n, p in dmm.named_parameters():
+        if sd[n].grad is None:     # outside the graph-mode forward: Adam skips it
+            assert torch.equal(p.detach().double().cpu(), p0[n]), n
+            continue
+        g = sd[n].grad + args.weight_decay * p0[n]
+        step = -args.lr_adam * g / (g.abs() + 1e-8)
+        got = p.detach().double().cpu() - p0[n]
+        # components whose gradient stands above the fp32 noise floor (a bias
+        # feeding a BatchNorm has gradient 0 + rounding noise + the decay term)
+        big = g.abs() > 1e-3 * max(g.abs().max().item(), G)
+        _close(got[big], step[big], 1e-3, 0.0, f"Adam step {n}")
+        assert float(got.abs().max()) <= args.lr_adam * (1 + 1e-3)
+    # equation residual of the logged draw: LHS [P, 1] / RHS [nu] - 1
+    assert len(out[4]) == 1 and np.isfinite(out[4][0])
+
+
+def test_train_MA_res_lbfgs_epoch_runs(dev):  # noqa: N802
+    from mmpde_amd import dmm_train as T
+
+    pde, dmm = _models("burgers")
+    all_u = _data("burgers", pde, 6)
+    args = _args("burgers", 8, 4)
+    dmm.to(dev)
+    np.random.seed(5)
+    out = T.train_MA_res(all_u, all_u, all_u[:2], args, dmm, False, 0, 1, dev, save_dir=False)
+    # LBFGS redraws inside its closure (max_iter 20 evaluations), logs the first
+    assert len(out[1]) == 1 and np.isfinite(out[1][0]) and np.isfinite(out[2][0])
+    assert len(out[8]) == 1 and all(np.isfinite(v) for v in (out[8][0], out[9][0], out[10][0]))
+    assert all(torch.isfinite(p).all() for p in dmm.parameters())
+
+
+# ----------------------------------------------------------------------------- evaluation
+def test_evaluate_tri_vs_oracle(dev):
+    from scipy.spatial import Delaunay
+
+    from mmpde_amd import dmm_train as T
+
+    pde, dmm = _models("cy")
+    sd = _sd64(dmm)
+    all_u = _data("cy", pde, 3)
+    u1 = all_u[[1], :, 2]
+    grid = all_u[0, :, :2]
+    dmm.to(dev)
+    np.random.seed(0)
+    got = T.evaluate_tri(dmm, u1, grid, dev)
+    tris = torch.from_numpy(Delaunay(grid.numpy()).simplices.astype(np.int64))
+    ref = R.evaluate_tri_one(_phi("cy", pde, sd), u1.double(), grid.double(), tris)
+    for name, a, b in zip(("mean", "std", "minmax"), got, ref):
+        _close(torch.tensor([a]), torch.tensor([b]), 2e-4, 0.0, f"evaluate_tri {name}")
+
+
+def test_evaluate_vs_oracle(dev):
+    from mmpde_amd import dmm_train as T
+
+    pde, dmm = _models("burgers")
+    sd = _sd64(dmm)
+    all_u = _data("burgers", pde, 2)
+    dmm.to(dev)
+    np.random.seed(0)
+    got = T.evaluate(dmm, all_u, dev)
+    phi = _phi("burgers", pde, sd)
+    per = [R.evaluate_one(phi, all_u[[t]].double(), 48) for t in range(2)]
+    ref = [float(np.mean([p[i] for p in per])) for i in range(3)]
+    for name, a, b in zip(("mean", "std", "minmax"), got, ref):
+        _close(torch.tensor([a]), torch.tensor([b]), 2e-4, 0.0, f"evaluate {name}")
