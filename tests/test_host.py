@@ -79,6 +79,24 @@ def test_training_mode_needs_device_tensors():
         model(g)
 
 
+def test_dmm_training_needs_device_tensors():
+    """DMM training (mmpde_amd.dmm_train): the train()-mode DMM forward and the
+    softmax smoother refuse host tensors; the samplers keep the reference's
+    batch-size constraints (nu a multiple of 4 / 10) as errors."""
+    from mmpde_amd import dmm_train as T
+
+    _, _, _, _, dmm, _ = build_models("cy", grid=torch.rand(100, 2))
+    dmm.train()
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        dmm(torch.zeros(1, 100), torch.rand(100, 2))
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        T.interpolate(torch.zeros(2, 8, 8), torch.rand(4, 1), torch.rand(4, 1))
+    with pytest.raises(ValueError):
+        T.sample_train_data(torch.zeros(5, 8, 8), 8, 6, "cpu")
+    with pytest.raises(ValueError):
+        T.sample_train_data_tri(torch.zeros(5, 100, 3), 8, 12, "cpu")
+
+
 def test_pde_constants():
     c = cy(ori_grid=torch.zeros(3, 2))
     assert c.tmax == 2.9 and c.grid_size == (30, 2521) and abs(c.dt - 0.1) < 1e-12
