@@ -576,8 +576,7 @@ __device__ __forceinline__ void prep(const float *src, int64_t lds, int64_t row0
         }
         if (div_k > 0) {
             const float d = div_deg ? (float)max(div_deg[srow], 1) : (float)div_k;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) x[q] = make_float4(x[q].x / d, x[q].y / d, x[q].z / d, x[q].w / d);
+            div_rows_rn(x, d);
         }
         if (copy) {
 #pragma unroll

@@ -24,7 +24,7 @@ import torch
 from torch import nn
 
 from . import _lib as L
-from .ops import nbr_from_edge_index, nbr_table_from_edge_index, reverse_adjacency
+from .ops import nbr_table_from_edge_index, reverse_adjacency
 
 
 class BatchNorm(nn.Module):
@@ -184,16 +184,19 @@ class GNN_Layer_FS_2D(nn.Module):  # noqa: N801 - reference name
         return self.norm(h + upd)
 
     def forward(self, x, u, pos_x, pos_y, variables, edge_index, batch):
-        """Layer-level API of the reference (gnn_2d.py:53-57)."""
-        if self.training:
-            L.require_device(x, u, pos_x, pos_y, variables)
-            nbr, deg = nbr_table_from_edge_index(edge_index, x.shape[0])
-            return self.train_forward(x, u, pos_x, pos_y, variables, EdgeGraph(nbr, deg))
-        if not self.supported():
-            raise NotImplementedError("HIP layer supports hidden 128, time_window 1, 1 variable")
+        """Layer-level API of the reference (gnn_2d.py:53-57), any edge_index.
+        The fused one-launch layer (mmpde_gnn_layer) takes time_window 1, one
+        variable and a grouped fixed-degree graph (knn_graph's layout); any
+        other time_window / variable count / ragged or ungrouped edge_index runs
+        the two node GEMMs as device torch ops and the edge stage on the HIP
+        EdgeMean kernels (the train() path; in-degree 0 gives the PyG mean 0)."""
         L.require_device(x, u, pos_x, pos_y, variables)
         n = x.shape[0]
-        nbr = nbr_from_edge_index(edge_index, n)
+        nbr, deg = nbr_table_from_edge_index(edge_index, n)
+        if self.training or not self.supported() or deg is not None:
+            if u.dim() == 1:
+                u = u[:, None]
+            return self.train_forward(x, u, pos_x, pos_y, variables, EdgeGraph(nbr, deg))
         pos = torch.cat((variables, pos_x, pos_y), dim=-1).float().contiguous()
         ws = torch.empty((4 * n * 128,), dtype=torch.float32, device=x.device)
         out = torch.empty((n, 128), dtype=torch.float32, device=x.device)

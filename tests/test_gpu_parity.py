@@ -301,6 +301,36 @@ def test_gnn_layer_api_and_edge_index_input(dev):
     _close(model(g()), ref2, 1e-5, 1e-9, "gnn edge_index input")
 
 
+@pytest.mark.parametrize("tw", [1, 3])
+def test_gnn_layer_api_any_time_window_ragged_edge_index(dev, tw):
+    """The layer API on what the fused launch does not take: time_window 3, and
+    a ragged, ungrouped edge_index (every 7th edge dropped, edges shuffled, one
+    node without in-edges): the HIP EdgeMean path, against the oracle."""
+    from mmpde_amd.gnn_2d import GNN_Layer_FS_2D
+
+    torch.manual_seed(4)
+    layer = GNN_Layer_FS_2D(128, 128, 128, time_window=tw, n_variables=1).eval()
+    with torch.no_grad():
+        layer.norm.module.running_mean.normal_(0, 0.1)
+        layer.norm.module.running_var.uniform_(0.5, 1.5)
+    sd = {"L." + k: v.detach() for k, v in layer.state_dict().items()}
+    n, k = 700, 12
+    g = torch.Generator().manual_seed(5)
+    pts = torch.rand(n, 2, generator=g)
+    ei, _, _ = refcpu.knn_graph(pts, k, 1)
+    keep = torch.ones(ei.shape[1], dtype=torch.bool)
+    keep[::7] = False
+    keep[ei[1] == 5] = False                       # node 5: no in-edges (mean 0)
+    ei = ei[:, keep][:, torch.randperm(int(keep.sum()), generator=g)]
+    h = torch.randn(n, 128, generator=g)
+    u = torch.randn(n, tw, generator=g)
+    px, py, pt = pts[:, :1], pts[:, 1:], torch.rand(n, 1, generator=g)
+    ref = refcpu.gnn_layer(sd, "L", h, u, px, py, pt, ei)
+    layer.to(dev)
+    got = layer(h.to(dev), u.to(dev), px.to(dev), py.to(dev), pt.to(dev), ei.to(dev), None)
+    _close(got, ref, 2e-5, 1e-6, f"gnn layer tw={tw}, ragged edge_index")
+
+
 def test_edge_mean_vs_torch_fp32(dev):
     """The hot kernel alone against a plain torch fp32 evaluation of
     mean_e relu(W2 relu(a_i + b_nbr) + b2)."""
