@@ -217,10 +217,16 @@ int mmpde_conv2d_ex(const float *x, int64_t batches, int cin, int h, int w, cons
  * Node inputs: u [n, tw] fp32 (data.x), pos [n, 3] fp32 = (t, x, y) (data.pos).
  * time_window tw (1 .. 16) is supported by mmpde_gnn_forward[_ex]; the
  * per-stage entry points (mmpde_gnn_embed / _layer) take tw = 1.
+ * pos_xy != 0: pos is [n, 2] = (x, y) and every node's t is *t_ptr (a device
+ * scalar, e.g. a graph-captured step's slot) or, with t_ptr NULL, t -- the
+ * rollout's form (one t per step, the moved mesh used as the positions as is).
  * ---------------------------------------------------------------------- */
 typedef struct {
     float inv_lx, inv_ly, inv_tmax; /* 1/pde.Lx, 1/pde.Ly, 1/pde.tmax (gnn_2d.py:122-124) */
     int tw;                         /* time_window: channels of u (0 is read as 1) */
+    int pos_xy;                     /* 0: pos = (t, x, y) rows; else (x, y) rows + t below */
+    float t;                        /* pos_xy: the nodes' t when t_ptr is NULL */
+    const float *t_ptr;             /* pos_xy: device scalar holding t (nullable) */
 } mmpde_gnn_scales;
 
 typedef struct {
@@ -509,6 +515,12 @@ int mmpde_itp_pack(const mmpde_itp_mlp *mlp, void *packed, mmpde_stream_t stream
 int mmpde_itp_interp(const float *src, const float *vals, const float *qry, const int32_t *idx,
                      int64_t batches, int64_t n_src, int64_t n_qry, const void *packed,
                      const float *addend, float *out, mmpde_stream_t stream);
+/* The same with a second addend, added last: out = (addend + sum) + addend2
+ * (the rollout's pred = interpolate_pred(...) + model(graph_uniform),
+ * train_helper_2d.py:178-185, in one launch); both nullable. */
+int mmpde_itp_interp_ex(const float *src, const float *vals, const float *qry, const int32_t *idx,
+                        int64_t batches, int64_t n_src, int64_t n_qry, const void *packed,
+                        const float *addend, const float *addend2, float *out, mmpde_stream_t stream);
 
 /* ------------------------------------------------------------------------
  * DMM training (reference mesh/dmm_utils.py)

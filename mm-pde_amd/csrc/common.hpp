@@ -118,6 +118,18 @@ __device__ __forceinline__ void div_rows_rn(float4 (&x)[N], float d) {
     for (int q = 0; q < N; ++q) x[q] = y[q];
 }
 
+// Node position fields of the GNN (mmpde_gnn_scales.pos_xy: (t, x, y) rows, or
+// (x, y) rows with one t for every node), unscaled.
+__device__ __forceinline__ float node_t(const mmpde_gnn_scales &sc, const float *pos, int64_t row) {
+    return sc.pos_xy ? (sc.t_ptr ? *sc.t_ptr : sc.t) : pos[row * 3];
+}
+__device__ __forceinline__ float node_x(const mmpde_gnn_scales &sc, const float *pos, int64_t row) {
+    return sc.pos_xy ? pos[row * 2] : pos[row * 3 + 1];
+}
+__device__ __forceinline__ float node_y(const mmpde_gnn_scales &sc, const float *pos, int64_t row) {
+    return sc.pos_xy ? pos[row * 2 + 1] : pos[row * 3 + 2];
+}
+
 static inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
 // library-internal entry points shared between translation units

@@ -58,7 +58,86 @@ __global__ __launch_bounds__(256) void dmm_embed_kernel(const float *__restrict_
 
 // DMM GNN_Layer_FS_2D (dmm_model.py:94-142): message cat(x_i, x_j, u_i-u_j,
 // px_i-px_j, py_i-py_j) (11) -> 4 tanh -> 4 tanh; mean; update cat(x, m) (8) ->
-// 4 tanh -> 4 tanh; x + upd; BN.
+// 4 tanh -> 4 tanh; x + upd; BN.  Four lanes per node: lane `sub` of the quad
+// takes edges sub, sub + 4, ..., the quad's sums meet by two xor shuffles.  The
+// arithmetic lives in these helpers, shared by the two kernels below (identical
+// results).
+struct DmmGnnSmem {
+    float W1[44], B1[4], W2[16], B2[4], V1[32], C1[4], V2[16], C2[4];
+    __device__ void load(const float *w1, const float *b1, const float *w2, const float *b2, const float *v1,
+                         const float *c1, const float *v2, const float *c2) {
+        const int t = threadIdx.x;
+        if (t < 44) W1[t] = w1[t];
+        if (t < 16) {
+            W2[t] = w2[t];
+            V2[t] = v2[t];
+        }
+        if (t < 32) V1[t] = v1[t];
+        if (t < 4) {
+            B1[t] = b1[t];
+            B2[t] = b2[t];
+            C1[t] = c1[t];
+            C2[t] = c2[t];
+        }
+    }
+};
+
+// sum[o] += message(i, j)[o]
+__device__ __forceinline__ void dmm_edge_acc(const DmmGnnSmem &w, const float (&hi)[4], float ui, float2 gi,
+                                             float4 hj4, float uj, float2 gj, float (&sum)[4]) {
+    const float in[11] = {hi[0], hi[1], hi[2], hi[3], hj4.x, hj4.y, hj4.z, hj4.w,
+                          ui - uj, gi.x - gj.x, gi.y - gj.y};
+    float m1[4];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+        float v = w.B1[o];
+#pragma unroll
+        for (int t = 0; t < 11; ++t) v += w.W1[o * 11 + t] * in[t];
+        m1[o] = tanhf(v);
+    }
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+        float v = w.B2[o];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) v += w.W2[o * 4 + t] * m1[t];
+        sum[o] += tanhf(v);
+    }
+}
+
+// the quad's sums -> mean -> update -> BN (every lane of the quad returns it)
+__device__ __forceinline__ float4 dmm_node_update(const DmmGnnSmem &w, const float (&hi)[4], float (&sum)[4],
+                                                  int k, const float *bnw, const float *bnb,
+                                                  const float *bnrm, const float *bnrv, float eps) {
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+        sum[o] += __shfl_xor(sum[o], 1, 64);
+        sum[o] += __shfl_xor(sum[o], 2, 64);
+    }
+    float cat[8];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+        cat[o] = hi[o];
+        cat[4 + o] = sum[o] / (float)k;
+    }
+    float up1[4], res[4];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+        float v = w.C1[o];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v += w.V1[o * 8 + t] * cat[t];
+        up1[o] = tanhf(v);
+    }
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+        float v = w.C2[o];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) v += w.V2[o * 4 + t] * up1[t];
+        res[o] = bn_eval(hi[o] + tanhf(v), bnrm[o], bnrv[o], bnw[o], bnb[o], eps);
+    }
+    return make_float4(res[0], res[1], res[2], res[3]);
+}
+
+// Every source read from global memory (L2): any trajectory size.
 __global__ __launch_bounds__(256) void dmm_gnn_kernel(const float4 *__restrict__ h,
                                                       const float *__restrict__ u,
                                                       const float2 *__restrict__ grid,
@@ -77,21 +156,9 @@ __global__ __launch_bounds__(256) void dmm_gnn_kernel(const float4 *__restrict__
                                                       const float *__restrict__ bnrm,
                                                       const float *__restrict__ bnrv, float eps,
                                                       float4 *__restrict__ h_out) {
-    __shared__ float sW1[44], sB1[4], sW2[16], sB2[4], sV1[32], sC1[4], sV2[16], sC2[4];
-    if (threadIdx.x < 44) sW1[threadIdx.x] = w1[threadIdx.x];
-    if (threadIdx.x < 16) {
-        sW2[threadIdx.x] = w2[threadIdx.x];
-        sV2[threadIdx.x] = v2[threadIdx.x];
-    }
-    if (threadIdx.x < 32) sV1[threadIdx.x] = v1[threadIdx.x];
-    if (threadIdx.x < 4) {
-        sB1[threadIdx.x] = b1[threadIdx.x];
-        sB2[threadIdx.x] = b2[threadIdx.x];
-        sC1[threadIdx.x] = c1[threadIdx.x];
-        sC2[threadIdx.x] = c2[threadIdx.x];
-    }
+    __shared__ DmmGnnSmem w;
+    w.load(w1, b1, w2, b2, v1, c1, v2, c2);
     __syncthreads();
-    // four lanes per node: lane `sub` of the quad takes edges sub, sub + 4, ...
     const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 2;
     const int sub = threadIdx.x & 3;
     if (i >= n_tot) return;  // whole quads leave together
@@ -106,53 +173,69 @@ __global__ __launch_bounds__(256) void dmm_gnn_kernel(const float4 *__restrict__
     for (int e = sub; e < k; e += 4) {
         const int64_t jl = min((uint32_t)nr[e], (uint32_t)(n_per - 1));
         const int64_t j = b * n_per + jl;
-        const float4 hj4 = h[j];
-        const float2 gj = grid[jl];
-        const float in[11] = {hi[0], hi[1], hi[2], hi[3], hj4.x, hj4.y, hj4.z, hj4.w,
-                              ui - u[j], gi.x - gj.x, gi.y - gj.y};
-        float m1[4];
-#pragma unroll
-        for (int o = 0; o < 4; ++o) {
-            float v = sB1[o];
-#pragma unroll
-            for (int t = 0; t < 11; ++t) v += sW1[o * 11 + t] * in[t];
-            m1[o] = tanhf(v);
-        }
-#pragma unroll
-        for (int o = 0; o < 4; ++o) {
-            float v = sB2[o];
-#pragma unroll
-            for (int t = 0; t < 4; ++t) v += sW2[o * 4 + t] * m1[t];
-            sum[o] += tanhf(v);
-        }
+        dmm_edge_acc(w, hi, ui, gi, h[j], u[j], grid[jl], sum);
     }
-#pragma unroll
-    for (int o = 0; o < 4; ++o) {
-        sum[o] += __shfl_xor(sum[o], 1, 64);
-        sum[o] += __shfl_xor(sum[o], 2, 64);
+    const float4 r = dmm_node_update(w, hi, sum, k, bnw, bnb, bnrm, bnrv, eps);
+    if (sub == 0) h_out[i] = r;
+}
+
+// The same layer with the trajectory's h, u and the grid staged in LDS
+// (28 B per point, dynamic): workgroup (x, b) takes kDmmLdsTargets targets of
+// trajectory b, so every neighbour read is an LDS read instead of an L2
+// round trip (the global kernel waits on its gathers, not on its tanh).
+constexpr int kDmmLdsTargets = 128;   // 512 threads: four lanes per target
+__global__ __launch_bounds__(512) void dmm_gnn_lds_kernel(const float4 *__restrict__ h,
+                                                          const float *__restrict__ u,
+                                                          const float2 *__restrict__ grid,
+                                                          const int32_t *__restrict__ nbr, int k,
+                                                          int n_per,
+                                                          const float *__restrict__ w1,
+                                                          const float *__restrict__ b1,
+                                                          const float *__restrict__ w2,
+                                                          const float *__restrict__ b2,
+                                                          const float *__restrict__ v1,
+                                                          const float *__restrict__ c1,
+                                                          const float *__restrict__ v2,
+                                                          const float *__restrict__ c2,
+                                                          const float *__restrict__ bnw,
+                                                          const float *__restrict__ bnb,
+                                                          const float *__restrict__ bnrm,
+                                                          const float *__restrict__ bnrv, float eps,
+                                                          float4 *__restrict__ h_out) {
+    extern __shared__ float4 dyn[];
+    float4 *sh = dyn;
+    float2 *sg = (float2 *)(sh + n_per);
+    float *su = (float *)(sg + n_per);
+    __shared__ DmmGnnSmem w;
+    w.load(w1, b1, w2, b2, v1, c1, v2, c2);
+    const int64_t base = (int64_t)blockIdx.y * n_per;
+    for (int t = threadIdx.x; t < n_per; t += 512) {
+        sh[t] = h[base + t];
+        sg[t] = grid[t];
+        su[t] = u[base + t];
     }
-    float cat[8];
-#pragma unroll
-    for (int o = 0; o < 4; ++o) {
-        cat[o] = hi[o];
-        cat[4 + o] = sum[o] / (float)k;
+    __syncthreads();
+    const int p = blockIdx.x * kDmmLdsTargets + (threadIdx.x >> 2);
+    const int sub = threadIdx.x & 3;
+    if (p >= n_per) return;  // whole quads leave together
+    const float4 hi4 = sh[p];
+    const float hi[4] = {hi4.x, hi4.y, hi4.z, hi4.w};
+    const float ui = su[p];
+    const float2 gi = sg[p];
+    float sum[4] = {0.f, 0.f, 0.f, 0.f};
+    const int32_t *nr = nbr + (int64_t)p * k;
+    for (int e = sub; e < k; e += 4) {
+        const int jl = (int)min((uint32_t)nr[e], (uint32_t)(n_per - 1));
+        dmm_edge_acc(w, hi, ui, gi, sh[jl], su[jl], sg[jl], sum);
     }
-    float up1[4], res[4];
-#pragma unroll
-    for (int o = 0; o < 4; ++o) {
-        float v = sC1[o];
-#pragma unroll
-        for (int t = 0; t < 8; ++t) v += sV1[o * 8 + t] * cat[t];
-        up1[o] = tanhf(v);
-    }
-#pragma unroll
-    for (int o = 0; o < 4; ++o) {
-        float v = sC2[o];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) v += sV2[o * 4 + t] * up1[t];
-        res[o] = bn_eval(hi[o] + tanhf(v), bnrm[o], bnrv[o], bnw[o], bnb[o], eps);
-    }
-    if (sub == 0) h_out[i] = make_float4(res[0], res[1], res[2], res[3]);
+    const float4 r = dmm_node_update(w, hi, sum, k, bnw, bnb, bnrm, bnrv, eps);
+    if (sub == 0) h_out[base + p] = r;
+}
+
+// LDS bytes of dmm_gnn_lds_kernel's staging (0: too large, use dmm_gnn_kernel)
+static size_t dmm_gnn_lds_bytes(int64_t n_per) {
+    const int64_t b = n_per * (16 + 8 + 4);
+    return b <= 120 * 1024 ? (size_t)b : 0;
 }
 
 // decoding_mlp DenseNet([4, 128, 1]) (dmm_model.py:173,209): d = W1 tanh(W0 h + b0) + b1
@@ -520,12 +603,26 @@ int graph_branch(const float *u, const float *grid, int64_t batches, int64_t n_p
     hipLaunchKernelGGL(dmm_embed_kernel, g1, dim3(256), 0, st, u, (const float2 *)grid, nt, n_per,
                        *br, h0, (unsigned *)sk, nz);
     MMPDE_RET_LAUNCH();
+    size_t lds = batches <= 65535 ? dmm_gnn_lds_bytes(n_per) : 0;
+    if (lds > 64 * 1024 &&
+        hipFuncSetAttribute((const void *)dmm_gnn_lds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds) != hipSuccess)
+        lds = 0;  // the global-memory kernel
     for (int l = 0; l < br->n_gnn_layers; ++l) {
-        hipLaunchKernelGGL(dmm_gnn_kernel, g4, dim3(256), 0, st, h0, u, (const float2 *)grid,
-                           grid_nbr, k, nt, n_per, br->g_msg1_w[l], br->g_msg1_b[l],
-                           br->g_msg2_w[l], br->g_msg2_b[l], br->g_upd1_w[l], br->g_upd1_b[l],
-                           br->g_upd2_w[l], br->g_upd2_b[l], br->g_bn_w[l], br->g_bn_b[l],
-                           br->g_bn_rm[l], br->g_bn_rv[l], br->eps, h1);
+        if (lds) {
+            const dim3 gl((unsigned)ceil_div(n_per, kDmmLdsTargets), (unsigned)batches);
+            hipLaunchKernelGGL(dmm_gnn_lds_kernel, gl, dim3(512), lds, st, h0, u, (const float2 *)grid,
+                               grid_nbr, k, (int)n_per, br->g_msg1_w[l], br->g_msg1_b[l],
+                               br->g_msg2_w[l], br->g_msg2_b[l], br->g_upd1_w[l], br->g_upd1_b[l],
+                               br->g_upd2_w[l], br->g_upd2_b[l], br->g_bn_w[l], br->g_bn_b[l],
+                               br->g_bn_rm[l], br->g_bn_rv[l], br->eps, h1);
+        } else {
+            hipLaunchKernelGGL(dmm_gnn_kernel, g4, dim3(256), 0, st, h0, u, (const float2 *)grid,
+                               grid_nbr, k, nt, n_per, br->g_msg1_w[l], br->g_msg1_b[l],
+                               br->g_msg2_w[l], br->g_msg2_b[l], br->g_upd1_w[l], br->g_upd1_b[l],
+                               br->g_upd2_w[l], br->g_upd2_b[l], br->g_bn_w[l], br->g_bn_b[l],
+                               br->g_bn_rm[l], br->g_bn_rv[l], br->eps, h1);
+        }
         MMPDE_RET_LAUNCH();
         float4 *t = h0;
         h0 = h1;

@@ -40,9 +40,9 @@ __global__ __launch_bounds__(256) void embed0_kernel(const float *__restrict__ u
     const int64_t i = e >> 7;
     const int c = (int)(e & (H - 1));
     const float in0 = u[i];
-    const float in1 = pos[i * 3 + 1] * sc.inv_lx;
-    const float in2 = pos[i * 3 + 2] * sc.inv_ly;
-    const float in3 = pos[i * 3 + 0] * sc.inv_tmax;
+    const float in1 = node_x(sc, pos, i) * sc.inv_lx;
+    const float in2 = node_y(sc, pos, i) * sc.inv_ly;
+    const float in3 = node_t(sc, pos, i) * sc.inv_tmax;
     const float *w = p.w0 + c * 4;
     float v = p.b0[c] + w[0] * in0 + w[1] * in1 + w[2] * in2 + w[3] * in3;
     v = bn_eval(v, p.bn1_rm[c], p.bn1_rv[c], p.bn1_w[c], p.bn1_b[c], p.eps);
@@ -66,12 +66,12 @@ struct EpiProj {  // message_net_1 split (see header comment)
             const int64_t row = row0 + acc_row(r, lane);
             if (row < m) {
                 const float uu = u[row];
-                const float px = pos[row * 3 + 1] * sc.inv_lx;
-                const float py = pos[row * 3 + 2] * sc.inv_ly;
+                const float px = node_x(sc, pos, row) * sc.inv_lx;
+                const float py = node_y(sc, pos, row) * sc.inv_ly;
                 const float node = wdu * uu + wdx * px + wdy * py;
                 float v;
                 if (part == 0) {
-                    const float pt = pos[row * 3 + 0] * sc.inv_tmax;
+                    const float pt = node_t(sc, pos, row) * sc.inv_tmax;
                     v = acc[r] + node + wt * pt + bb;
                 } else {
                     v = acc[r] - node;
@@ -87,7 +87,7 @@ struct EpiUpd1 {  // relu(U1 [h | mean | t] + c1), gnn_2d.py:67
     const float *c1, *w_t;  // w_t: column 256 of U1 (stride ldw1)
     int64_t ldw1;
     const float *pos;
-    float inv_tmax;
+    mmpde_gnn_scales sc;
     __device__ void operator()(const f32x16 &acc, int64_t row0, int col0, int lane, int64_t m,
                                int) const {
         const int c = col0 + (lane & 31);
@@ -96,7 +96,7 @@ struct EpiUpd1 {  // relu(U1 [h | mean | t] + c1), gnn_2d.py:67
         for (int r = 0; r < 16; ++r) {
             const int64_t row = row0 + acc_row(r, lane);
             if (row < m) {
-                const float pt = pos[row * 3 + 0] * inv_tmax;
+                const float pt = node_t(sc, pos, row) * sc.inv_tmax;
                 out[row * H + c] = fmaxf(acc[r] + wt * pt + bb, 0.0f);
             }
         }
@@ -423,7 +423,7 @@ static int gnn_layer_impl(const float *h_in, const float *u, const float *pos, i
     {
         const int64_t ld = p->upd1_ld;
         GemmArgs g{n, h_in, wm, H, p->upd1_w, p->upd1_w + 128, ld, 128};
-        EpiUpd1 epi{wv, p->upd1_b, p->upd1_w + 256, ld, pos, sc.inv_tmax};
+        EpiUpd1 epi{wv, p->upd1_b, p->upd1_w + 256, ld, pos, sc};
         rc = launch_gemm(g, 1, epi, st);
         if (rc) return rc;
     }

@@ -64,7 +64,8 @@ constexpr int kItpThreads = 512;
 __global__ __launch_bounds__(kItpThreads, 4) void itp_interp_kernel(
     const float *__restrict__ src, const float *__restrict__ vals, const float *__restrict__ qry,
     const int32_t *__restrict__ idx, int64_t batches, int64_t n_src, int64_t n_qry,
-    const float *__restrict__ pk, const float *__restrict__ addend, float *__restrict__ out) {
+    const float *__restrict__ pk, const float *__restrict__ addend, const float *__restrict__ addend2,
+    float *__restrict__ out) {
     __shared__ float4 img[(kImg0 + kImg1) / 4];  // 64 KB
     {
         const float4 *gsrc = (const float4 *)pk;
@@ -159,7 +160,11 @@ __global__ __launch_bounds__(kItpThreads, 4) void itp_interp_kernel(
             }
         sum += __shfl_xor(sum, 16, 64);
         sum += __shfl_xor(sum, 32, 64);
-        if (g == 0 && valid) out[qrow] = addend ? addend[qrow] + sum : sum;
+        if (g == 0 && valid) {
+            float o = addend ? addend[qrow] + sum : sum;
+            if (addend2) o = o + addend2[qrow];  // (interp + res) + model(graph_uniform)
+            out[qrow] = o;
+        }
     }
 }
 
@@ -179,6 +184,14 @@ extern "C" int mmpde_itp_interp(const float *src, const float *vals, const float
                                 const int32_t *idx, int64_t batches, int64_t n_src,
                                 int64_t n_qry, const void *packed, const float *addend,
                                 float *out, mmpde_stream_t stream) {
+    return mmpde_itp_interp_ex(src, vals, qry, idx, batches, n_src, n_qry, packed, addend, nullptr, out,
+                               stream);
+}
+
+extern "C" int mmpde_itp_interp_ex(const float *src, const float *vals, const float *qry,
+                                   const int32_t *idx, int64_t batches, int64_t n_src,
+                                   int64_t n_qry, const void *packed, const float *addend,
+                                   const float *addend2, float *out, mmpde_stream_t stream) {
     MMPDE_REQUIRE(src && vals && qry && idx && packed && out);
     MMPDE_REQUIRE(batches > 0 && n_src >= kNb && n_qry > 0);
     const int64_t tiles = ((n_qry + 15) / 16) * batches;
@@ -189,7 +202,7 @@ extern "C" int mmpde_itp_interp(const float *src, const float *vals, const float
     int64_t blocks = 2 * (int64_t)cus;               // two resident workgroups per CU
     if (blocks > tiles) blocks = tiles;
     hipLaunchKernelGGL(itp_interp_kernel, dim3((unsigned)blocks), dim3(kItpThreads), 0, as_stream(stream), src, vals,
-                       qry, idx, batches, n_src, n_qry, (const float *)packed, addend, out);
+                       qry, idx, batches, n_src, n_qry, (const float *)packed, addend, addend2, out);
     MMPDE_RET_LAUNCH();
     return MMPDE_OK;
 }

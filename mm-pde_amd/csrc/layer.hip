@@ -781,9 +781,9 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs p) {
     // epilogue waits on a memory round trip
     if (tid < ROWS) {
         const int64_t row = min(row0 + tid, p.n - 1);
-        rowv[0][tid] = p.pos[row * 3 + 0] * p.sc.inv_tmax;
-        rowv[1][tid] = p.pos[row * 3 + 1] * p.sc.inv_lx;
-        rowv[2][tid] = p.pos[row * 3 + 2] * p.sc.inv_ly;
+        rowv[0][tid] = node_t(p.sc, p.pos, row) * p.sc.inv_tmax;
+        rowv[1][tid] = node_x(p.sc, p.pos, row) * p.sc.inv_lx;
+        rowv[2][tid] = node_y(p.sc, p.pos, row) * p.sc.inv_ly;
         for (int c = 0; c < tw; ++c) rowv[3 + c][tid] = p.u[row * tw + c];
     }
     const float u1_wt = wu1[256], u1_b = p.c1[col];
@@ -915,9 +915,9 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_embed_kernel(EmbedArgs p) {
     const int tw = p.sc.tw > 1 ? p.sc.tw : 1;
     if (tid < ROWS) {
         const int64_t row = min(row0 + tid, p.n - 1);
-        rowv[0][tid] = p.pos[row * 3 + 0] * p.sc.inv_tmax;
-        rowv[1][tid] = p.pos[row * 3 + 1] * p.sc.inv_lx;
-        rowv[2][tid] = p.pos[row * 3 + 2] * p.sc.inv_ly;
+        rowv[0][tid] = node_t(p.sc, p.pos, row) * p.sc.inv_tmax;
+        rowv[1][tid] = node_x(p.sc, p.pos, row) * p.sc.inv_lx;
+        rowv[2][tid] = node_y(p.sc, p.pos, row) * p.sc.inv_ly;
         for (int c = 0; c < tw; ++c) rowv[3 + c][tid] = p.u[row * tw + c];
     }
     const mmpde_gnn_embed_params &e = p.e;

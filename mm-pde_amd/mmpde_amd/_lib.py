@@ -13,7 +13,7 @@ import os
 import torch
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libmmpde_hip.so")
-ABI_VERSION = 11200
+ABI_VERSION = 11300
 
 ACT_NONE, ACT_TANH, ACT_RELU, ACT_ELU = 0, 1, 2, 3
 PAD_ZEROS, PAD_CIRCULAR = 0, 1
@@ -36,7 +36,8 @@ class MmpdeError(RuntimeError):
 
 # --------------------------------------------------------------------------- structs
 class GnnScales(ctypes.Structure):
-    _fields_ = [("inv_lx", _F), ("inv_ly", _F), ("inv_tmax", _F), ("tw", _I)]
+    _fields_ = [("inv_lx", _F), ("inv_ly", _F), ("inv_tmax", _F), ("tw", _I), ("pos_xy", _I),
+                ("t", _F), ("t_ptr", _P)]
 
 
 class GnnEmbedParams(ctypes.Structure):
@@ -142,6 +143,7 @@ _SIGS = {
     "mmpde_itp_pack_bytes": (_I64, []),
     "mmpde_itp_pack": (_I, [_P, _P, _P]),
     "mmpde_itp_interp": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _P, _P, _P, _P]),
+    "mmpde_itp_interp_ex": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _P, _P, _P, _P, _P]),
     "mmpde_softmax_interp": (_I, [_P, _I64, _I64, _P, _I64, _P, _I64, _F, _P, _P]),
     "mmpde_softmax_interp_grad": (_I, [_P, _I64, _I64, _P, _I64, _P, _I64, _F, _P, _P, _P]),
 }

@@ -324,6 +324,16 @@ class MP_PDE_Solver_2D(nn.Module):  # noqa: N801 - reference name
         u = L.f32c(u).reshape(-1)
         pos = L.f32c(pos)
         sc, emb, arr, head = self.device_params()
+        if pos.shape[-1] == 2:   # (x, y) rows, one t for every node (the rollout's form)
+            t, t_slot = getattr(data, "t", None), getattr(data, "t_slot", None)
+            if t is None and t_slot is None:
+                raise ValueError("pos with 2 columns needs data.t or data.t_slot")
+            if t_slot is not None:
+                L.require_device(t_slot)
+            sc = L.GnnScales(sc.inv_lx, sc.inv_ly, sc.inv_tmax, sc.tw, 1, float(t or 0.0),
+                             L.ptr(L.f32c(t_slot)) if t_slot is not None else None)
+        elif pos.shape[-1] != 3:
+            raise ValueError("pos must be [n, 3] (t, x, y) or [n, 2] (x, y)")
         if workspace is None:
             workspace = torch.empty((L.lib().mmpde_gnn_workspace_bytes(n) // 4,),
                                     dtype=torch.float32, device=u.device)

@@ -358,9 +358,10 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, b, stride: int, pad: int, act: int,
     return y
 
 
-def itp_interp(src, vals, qry, idx, batches: int, packed: torch.Tensor, addend=None):
+def itp_interp(src, vals, qry, idx, batches: int, packed: torch.Tensor, addend=None, addend2=None):
     """ItpNet weights + weighted neighbour sum (interpolate.py:77-93,
-    data_creator_2d.py:80-83).  Returns [batches * n_qry] fp32."""
+    data_creator_2d.py:80-83), + addend, then + addend2 (both optional).
+    Returns [batches * n_qry] fp32."""
     L.require_device(src, vals, qry, idx, packed)
     src = L.f32c(src).reshape(-1, 2)
     qry = L.f32c(qry).reshape(-1, 2)
@@ -368,9 +369,10 @@ def itp_interp(src, vals, qry, idx, batches: int, packed: torch.Tensor, addend=N
     ns, nq = src.shape[0] // batches, qry.shape[0] // batches
     out = torch.empty((batches * nq,), dtype=torch.float32, device=src.device)
     add = L.f32c(addend).reshape(-1) if addend is not None else None
-    L.check(L.lib().mmpde_itp_interp(L.ptr(src), L.ptr(vals), L.ptr(qry), L.ptr(idx.contiguous()),
-                                     batches, ns, nq, L.ptr(packed), L.ptr(add), L.ptr(out),
-                                     L.stream(src.device)), "mmpde_itp_interp")
+    add2 = L.f32c(addend2).reshape(-1) if addend2 is not None else None
+    L.check(L.lib().mmpde_itp_interp_ex(L.ptr(src), L.ptr(vals), L.ptr(qry), L.ptr(idx.contiguous()),
+                                        batches, ns, nq, L.ptr(packed), L.ptr(add), L.ptr(add2),
+                                        L.ptr(out), L.stream(src.device)), "mmpde_itp_interp_ex")
     return out
 
 

@@ -52,9 +52,6 @@ class MMPDERollout:
         self.nbr_u = gc.fixed_graph_nbr(self.grid, batches)
         self.t = gc.time_grid()
         f32 = dict(dtype=torch.float32, device=self.device)
-        self.pos_u = torch.empty((n, 3), **f32)
-        self.pos_u[:, 1:3] = self.grid_rep
-        self.pos_m = torch.empty((n, 3), **f32)
         self.out_u = torch.empty((n, 1), **f32)
         self.out_b = torch.empty((n, 1), **f32)
         self.ws_gnn = torch.empty((L.lib().mmpde_gnn_workspace_bytes(n) // 4,), **f32)
@@ -119,11 +116,13 @@ class MMPDERollout:
     def _trace(self):
         return self.trace_hook() if self.trace_hook is not None else None
 
-    def _set_t(self, pos, step_idx):
-        if isinstance(step_idx, torch.Tensor):  # graph capture: t read from a device slot
-            pos[:, 0].copy_(step_idx.expand(pos.shape[0]))
-        else:
-            pos[:, 0].fill_(float(self.t[step_idx]))
+    def _nodes(self, u, xy, nbr, step_idx):
+        """The GNN's node inputs with (x, y) positions and one t for every node
+        (mmpde_gnn_scales.pos_xy): no (t, x, y) array is filled per step.  Graph
+        capture passes the device slot holding t."""
+        if isinstance(step_idx, torch.Tensor):
+            return _Nodes(u, xy, nbr, self.N, t_slot=step_idx)
+        return _Nodes(u, xy, nbr, self.N, t=float(self.t[step_idx]))
 
     # ------------------------------------------------------------ hipGraph
     def enable_graph(self, u_like: torch.Tensor) -> None:
@@ -161,16 +160,15 @@ class MMPDERollout:
         B, N = self.B, self.N
         u = u.contiguous()
         u_flat = u.reshape(-1)
-        self._set_t(self.pos_u, step_idx)
         if not self.moving_mesh:
-            return self.model(_Nodes(u_flat, self.pos_u, self.nbr_u, N), out=self.out_u,
+            return self.model(self._nodes(u_flat, self.grid_rep, self.nbr_u, step_idx), out=self.out_u,
                               workspace=self.ws_gnn, trace=self._trace()).reshape(u.shape)
         cur = torch.cuda.current_stream(self.device)
         side = self.side if self.overlap else cur
         side.wait_stream(cur)
         with torch.cuda.stream(side):
             u.record_stream(side)
-            out_u = self.model(_Nodes(u_flat, self.pos_u, self.nbr_u, N), out=self.out_u,
+            out_u = self.model(self._nodes(u_flat, self.grid_rep, self.nbr_u, step_idx), out=self.out_u,
                                workspace=self.ws_gnn_u, trace=self._trace())
         mesh = self.dmm.mesh(u, self.xi, out=self.mesh, workspace=self.ws_dmm,
                              head_cache=self.dmm_cache)
@@ -189,8 +187,6 @@ class MMPDERollout:
                 res = self.itp.res_cut(u.reshape(B, N)).reshape(-1)
             idx2.record_stream(cur)
             res.record_stream(cur)
-        self.pos_m[:, 1:3] = mesh
-        self._set_t(self.pos_m, step_idx)
         self.nbr_m = nbr_m = ops.knn_graph_moved(mesh, self.xi, self.knn_cand, B, self.gc.n,
                                                  self.knn_scratch, cells=cells,
                                                  skip_above=self.knn_skip)
@@ -202,13 +198,15 @@ class MMPDERollout:
             u_m = ops.itp_interp(self.grid_rep, u_flat, mesh, idx1, B, self.itp.packed("1"))
         else:
             u_m = u_flat
-        out_b = self.model_b(_Nodes(u_m, self.pos_m, nbr_m, N), out=self.out_b,
+        out_b = self.model_b(self._nodes(u_m, mesh, nbr_m, step_idx), out=self.out_b,
                              workspace=self.ws_gnn, trace=self._trace())
         cur.wait_stream(side2)
-        interp = ops.itp_interp(mesh, out_b, self.grid_rep, idx2, B, self.itp.packed("2"),
-                                addend=res)
         cur.wait_stream(side)
-        return torch.add(interp, out_u.reshape(-1)).reshape(u.shape)
+        # interpolate_pred(...) + model(graph_uniform) (train_helper_2d.py:178-185):
+        # (interp + res_cut) + out_u in the interpolation kernel's epilogue
+        pred = ops.itp_interp(mesh, out_b, self.grid_rep, idx2, B, self.itp.packed("2"),
+                              addend=res, addend2=out_u.reshape(-1))
+        return pred.reshape(u.shape)
 
     def knn_table_share(self):
         """(graph, query[, burgers mode-'1' query]): the share of the last step's
@@ -231,12 +229,16 @@ class MMPDERollout:
 
 
 class _Nodes:
-    """The graph fields the solver reads (x, pos, nbr, seg_n = nodes per trajectory)."""
-    __slots__ = ("x", "pos", "nbr", "edge_index", "seg_n")
+    """The graph fields the solver reads (x, pos, nbr, seg_n = nodes per
+    trajectory); pos [n, 2] = (x, y) with t (host float) or t_slot (device
+    scalar) for every node, or the reference's [n, 3] (t, x, y)."""
+    __slots__ = ("x", "pos", "nbr", "edge_index", "seg_n", "t", "t_slot")
 
-    def __init__(self, x, pos, nbr, seg_n=None):
+    def __init__(self, x, pos, nbr, seg_n=None, t=None, t_slot=None):
         self.x = x.reshape(-1, 1)
         self.pos = pos
         self.nbr = nbr
         self.edge_index = None
         self.seg_n = seg_n
+        self.t = t
+        self.t_slot = t_slot

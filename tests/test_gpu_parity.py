@@ -280,6 +280,17 @@ def test_gnn_forward_matches_oracle(dev, kind):
     out = model(_Nodes(u.to(dev), pos.to(dev), nbr.int().to(dev)))
     # fp32 tolerance for 6 BN'd layers + head: 1e-5 of the output range
     _close(out, ref, 1e-5, 1e-9, f"gnn {kind}")
+    # the rollout's position form: (x, y) rows + one t (host value or device
+    # slot) gives the same bits as the (t, x, y) rows, in both GEMM modes
+    t = float(pos[0, 0])
+    xy = pos[:, 1:].contiguous().to(dev)
+    for mode in ("f32", "f16x3"):
+        model.edge_gemm = mode
+        full = model(_Nodes(u.to(dev), pos.to(dev), nbr.int().to(dev), seg_n=pos.shape[0] // 2))
+        a = model(_Nodes(u.to(dev), xy, nbr.int().to(dev), seg_n=pos.shape[0] // 2, t=t))
+        b = model(_Nodes(u.to(dev), xy, nbr.int().to(dev), seg_n=pos.shape[0] // 2,
+                         t_slot=torch.tensor([t], device=dev)))
+        assert torch.equal(a, full) and torch.equal(b, full), mode
 
 
 def test_gnn_layer_api_and_edge_index_input(dev):
