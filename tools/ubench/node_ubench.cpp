@@ -72,15 +72,14 @@ int main(int argc, char **argv) {
     char *pack;
     CK(hipMalloc(&pack, mmpde_gnn_pack_bytes(2)));
     if (mmpde_gnn_pack_f16x3(two, 2, pack, 0) != 0) return 1;
-    uint32_t *amax;
-    CK(hipMalloc(&amax, 4 * 2 * kAmaxShards * 4));
-    CK(hipMemset(amax, 0, 4 * 2 * kAmaxShards * 4));
+    float *rng_rec;  // range records written by the node stage (layer.hpp)
+    CK(hipMalloc(&rng_rec, 4 * range_tiles(n) * 4));
     CK(hipDeviceSynchronize());
     mmpde_gnn_scales sc{1.0f, 1.0f, 1.0f / 2.9f, 1};
     const int cus = device_cus(), it = 20;
     printf("n=%lld parts=%d cus=%d (us per launch, median of 7)\n", (long long)n, parts, cus);
     NodeArgs nd{h, mean, n, u1, c1, 260, u2, c2, bnw, bnb, bnm, bnv, 1e-5f, ho[1], w1, b1, 260, ao[1], bo[1],
-                u, pos, sc, pack, pack + kLayerPack, amax + 2 * kAmaxShards, parts, n * H};
+                u, pos, sc, pack, pack + kLayerPack, rng_rec, N, parts, n * H};
     nd.div_k = 35;  // the wave edge kernel's buffers hold sums (production)
     NodeArgs nt = nd;
     nt.h_out = ho[0];
