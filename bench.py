@@ -40,6 +40,10 @@ METRIC = "MM-PDE rollout node-updates/sec, cylinder 2521-node mesh, 1/2/4/8 GPUs
 F32_MFMA_PEAK_TFLOPS = 157.3          # MI355X_MICROARCH.md: dense fp32 matrix peak
 F16_MFMA_PEAK_TFLOPS = 2516.6         # 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz (~2.5 PF dense)
 HBM_PEAK_GBS = 8000.0
+# counter records regenerated on the current kernels (tools/gpu_pmc.sh with
+# PMC_NAME=edge_pmc_r03; tools/gpu_configs.sh with STEP_HBM=r03_cy_gnn_step_hbm)
+EDGE_PMC_RECORD = "edge_pmc_r03.json"
+STEP_HBM_RECORD = "r03_cy_gnn_step_hbm.json"
 CONFIGS = {
     # name: (kind, moving_mesh, default trajectories per GPU, BASELINE.json config,
     #        Burgers grid side: 48 = the MM-PDE --base_resolution, 96 = PDEs.py's default)
@@ -282,7 +286,7 @@ def main():
     # fp32-equivalent peak is the dense fp16 MFMA peak / 3.
     peak = F32_MFMA_PEAK_TFLOPS if args.edge_gemm == "f32" else F16_MFMA_PEAK_TFLOPS / 3
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", "edge_pmc_r02.json")   # tools/gpu_pmc.sh, this round's kernels
+    pmc = os.path.join(ROOT, "profiles", EDGE_PMC_RECORD)   # tools/gpu_pmc.sh on this round's kernels
     if os.path.exists(pmc):
         with open(pmc) as f:
             rec = json.load(f)
@@ -335,7 +339,7 @@ def main():
                "algorithmic_bytes_per_step": alg, "achieved": alg / step_s / 1e9,
                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": alg / step_s / 1e9 / HBM_PEAK_GBS,
                "measured_bytes_per_step": None}
-        rec_path = os.path.join(ROOT, "profiles", "r02_cy_gnn_step_hbm.json")
+        rec_path = os.path.join(ROOT, "profiles", STEP_HBM_RECORD)
         if os.path.exists(rec_path):
             with open(rec_path) as f:
                 rec = json.load(f)

@@ -22,4 +22,4 @@ for c in FETCH_SIZE WRITE_SIZE; do
       --config cy-gnn --steps 2 --warmup 1 --no-cpu-baseline --no-f32-exact --serial > "$OUT/pmc.$c.log" 2>&1 \
       || { tail -20 "$OUT/pmc.$c.log"; exit 1; }
 done
-python3 tools/step_hbm.py "$OUT/cy_gnn_step_hbm.json" cy-gnn 20168 6 "$OUT/pmc"
+python3 tools/step_hbm.py "$OUT/${STEP_HBM:-r03_cy_gnn_step_hbm}.json" cy-gnn 20168 6 "$OUT/pmc"

@@ -20,4 +20,4 @@ for mode in f16x3 f32; do
     if [ $rc -ne 0 ]; then tail -20 "$OUT/$mode.$c.log"; exit $rc; fi
   done
 done
-python3 tools/pmc_summary.py ${PMC_NAME:-edge_pmc_r02} cy-mmpde 40336 f16x3="$OUT/f16x3" f32="$OUT/f32"
+python3 tools/pmc_summary.py ${PMC_NAME:-edge_pmc_r03} cy-mmpde 40336 f16x3="$OUT/f16x3" f32="$OUT/f32"
