@@ -45,6 +45,17 @@ namespace {
 constexpr int LH = 128;  // hidden width
 constexpr int ET = 16;   // targets per tile
 
+// Split placement (body below).  1: every MFMA gap carries at most 8 issue
+// cycles of VALU: per pair j, group 2j = [relu-sum | fmas | cvt + relu of pair
+// j - 1's hi], group 2j + 1 = [relu-sum | mixlo | mixhi (+ a b-row refill)]
+// (v_fma_mix* issue for 8 cycles, tools/ubench/gapcost.hip).  0: the round-2
+// placement, cvt + mixlo and mixhi + pk_max (12 cycles each) in one gap.
+#ifndef MMPDE_EDGE_PLACE
+#define MMPDE_EDGE_PLACE 1
+#endif
+constexpr bool kPlace8 = MMPDE_EDGE_PLACE == 1;
+
+
 struct WaveArgs {
     const float *a, *b;
     const int32_t *nbr;
@@ -282,14 +293,20 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
                 atile = st;
             }
         }
-        // Per-MFMA placement: every MFMA gap carries at most one 2-instruction
-        // VALU unit (8 issue cycles beside the MFMA's 8 of 16), pinned by
-        // sched_barriers.  Group G = 4 c + s (the 3 MFMAs of column tile c, K
-        // step s): gap 0 the relu-sum of value G, gaps 1 / 2 split pair G >> 1
-        // (G even: its two fmas, then cvt_pkrtz + mixlo; G odd: mixhi + pk_max,
-        // then at G = 4 p + 3 the refill of piece p, whose last pair (4 p + 2)
-        // has read it).  The relu-sums trail their tile's MFMAs by six groups
-        // (groups 0-5: the previous slot's tiles 6 and 7).
+        // Per-MFMA placement (kPlace8): every MFMA gap carries at most 8 issue
+        // cycles of VALU beside the MFMA's 8 of 16, pinned by sched_barriers on
+        // both sides of each MFMA.  Group G = 4 c + s (the 3 MFMAs of column
+        // tile c, K step s): gap 0 the relu-sum of value G (max + add); split
+        // pair j = G >> 1 over its two groups: G even gap 1 its two fmas
+        // (relu(a + b) input), gap 2 cvt_pkrtz (hi) + the relu of pair j - 1's
+        // hi; G odd gap 1 mixlo, gap 2 mixhi (the v_fma_mix* issue for 8 cycles
+        // each) and at G = 4 p + 3 the refill of piece p, whose last pair
+        // (4 p + 2) has read it.  The relu-sums trail their tile's MFMAs by six
+        // groups (groups 0-5: the previous slot's tiles 6 and 7).  Measured
+        // (tools/ubench/gapcost.hip: 2 v_fma_mix in one gap cost 1.48x an MFMA,
+        // cvt + mix 1.32x, any 8-cycle pair 1.03-1.07x): 105.9 vs 111.8 us per
+        // launch for the round-2 placement (kPlace8 = 0: cvt + mixlo and
+        // mixhi + pk_max in one gap each).
         f32x4 acc[8];
         float xs0 = 0.0f, xs1 = 0.0f;
 #pragma unroll
@@ -300,6 +317,7 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
                 const half8 ah = __builtin_bit_cast(half8, h[s]), al = __builtin_bit_cast(half8, l[s]);
                 const int G = 4 * c + s, j = G >> 1;
                 acc[c] = mfma_f16(ah, wh[c][s], acc[c]);
+                if (kPlace8) __builtin_amdgcn_sched_barrier(0);  // the gap's unit after its MFMA
                 {
                     f32x4 &Sc = G >= 6 ? S[(G - 6) >> 2] : (G < 2 ? S[6] : S[7]);
                     const int t = G >= 6 ? (G - 6) & 3 : (G < 2 ? G + 2 : G - 2);
@@ -310,22 +328,38 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 acc[c] = mfma_f16(ah, wl[c][s], acc[c]);
+                if (kPlace8) __builtin_amdgcn_sched_barrier(0);  // the gap's unit after its MFMA
                 if (!(DIAG & 1)) {
                     if ((G & 1) == 0) {
                         const float4 &ap = av[a_piece(j)];
                         const float4 &bb = X[a_piece(j)];
                         xs0 = (j & 1) ? fmaf(bb.z, sc, ap.z) : fmaf(bb.x, sc, ap.x);
                         xs1 = (j & 1) ? fmaf(bb.w, sc, ap.w) : fmaf(bb.y, sc, ap.y);
+                    } else if (kPlace8) {
+                        split_l(xs0, nh[j >> 2][j & 3], nl[j >> 2][j & 3]);
                     } else {
                         split2_relu_rtz_b(xs1, nh[j >> 2][j & 3], nl[j >> 2][j & 3]);
                     }
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 acc[c] = mfma_f16(al, wh[c][s], acc[c]);
+                if (kPlace8) __builtin_amdgcn_sched_barrier(0);  // the gap's unit after its MFMA
                 if ((G & 1) == 0) {
-                    if (!(DIAG & 1)) split2_relu_rtz_a(xs0, xs1, nh[j >> 2][j & 3], nl[j >> 2][j & 3]);
-                } else if ((G & 3) == 3 && !(DIAG & 4)) {
-                    X[G >> 2] = *(const float4 *)(brow + piece(G >> 2));
+                    if (DIAG & 1) {
+                    } else if (kPlace8) {
+                        split_c(xs0, xs1, nh[j >> 2][j & 3]);
+                        // relu of the previous pair's hi (pair 15 of the split
+                        // made in the previous body: this body's operand h, first
+                        // read by group 3; applying it again to the prologue's
+                        // split is harmless, relu is idempotent)
+                        if (j == 0) split_p(h[3][3]);
+                        else split_p(nh[(j - 1) >> 2][(j - 1) & 3]);
+                    } else {
+                        split2_relu_rtz_a(xs0, xs1, nh[j >> 2][j & 3], nl[j >> 2][j & 3]);
+                    }
+                } else {
+                    if (kPlace8 && !(DIAG & 1)) split_h(xs1, nh[j >> 2][j & 3], nl[j >> 2][j & 3]);
+                    if ((G & 3) == 3 && !(DIAG & 4)) X[G >> 2] = *(const float4 *)(brow + piece(G >> 2));
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 if (G == 5 && close_prev) {  // the previous unit is complete: write, restart

@@ -183,6 +183,25 @@ __device__ __forceinline__ void split2_relu_rtz_b(float x1, uint32_t &hi, uint32
         : "v"(x1));
 }
 
+// split2_relu_rtz as four single-instruction steps, for schedules that give
+// every MFMA gap at most 8 issue cycles (tools/ubench/gapcost.hip: v_fma_mix*
+// issue for 8 cycles, cvt / pk_max / fma for 4): C = hi (RTZ, before the
+// relu), L = low word of lo, H = high word of lo (both read the pre-relu hi),
+// P = the relu of hi (after L and H).  The caller keeps two instructions
+// between P and the first MFMA that reads hi / lo.
+__device__ __forceinline__ void split_c(float x0, float x1, uint32_t &hi) {
+    asm("v_cvt_pkrtz_f16_f32 %0, %1, %2" : "=v"(hi) : "v"(x0), "v"(x1));
+}
+__device__ __forceinline__ void split_l(float x0, uint32_t hi, uint32_t &lo) {
+    asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1] clamp" : "=&v"(lo) : "v"(x0), "v"(hi));
+}
+__device__ __forceinline__ void split_h(float x1, uint32_t hi, uint32_t &lo) {
+    asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1] clamp" : "+v"(lo) : "v"(x1), "v"(hi));
+}
+__device__ __forceinline__ void split_p(uint32_t &hi) {
+    asm("v_pk_max_f16 %0, %0, 0" : "+v"(hi));
+}
+
 __device__ __forceinline__ float absmax4(float m, const float4 &v) {
     return fmaxf(fmaxf(fmaxf(m, fabsf(v.x)), fmaxf(fabsf(v.y), fabsf(v.z))), fabsf(v.w));
 }
