@@ -534,6 +534,96 @@ constexpr int NODE_WPE = MMPDE_NODE_WPE;  // node / embed launch bounds: waves p
 // buffer order (the edge stage's per-part sums); div_k > 0: the total is then
 // divided by the row's degree max(div_deg[row], 1), or by div_k (IEEE division:
 // torch_scatter's mean = sum / count).
+// The (row, part) item of prep's work index idx: a wave takes 8 rows x 8 parts,
+// lane = 8 part + row: the 8 lanes of one ds_write_b128 group write 8
+// consecutive image rows (conflict-free).
+__device__ __forceinline__ void prep_item(int idx, int &row, int &part) {
+    row = (idx >> 6) * 8 + (idx & 7);
+    part = (idx >> 3) & 7;
+}
+
+// prep, first half: the 16 values of item (row, part) of rows src (row stride
+// lds; global rows row0 + row clamped to nrows_valid - 1, else LDS rows).
+__device__ __forceinline__ void prep_fetch(const float *src, int64_t lds, int64_t row0, int64_t nrows_valid,
+                                           bool global, int row, int part, float4 (&x)[4]) {
+    const int64_t srow = global ? min(row0 + row, nrows_valid - 1) : row;
+    const float *sp = src + srow * lds + 16 * part;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) x[q] = *(const float4 *)(sp + 4 * q);
+}
+
+// prep, second half: the fetched values x of item (row, part) (global row srow
+// when global) -> the image (and copy, rs), after the optional side-block sums
+// and degree division (see prep).
+template <bool F16X3>
+__device__ __forceinline__ void prep_finish(float4 (&x)[4], const float *src, int64_t srow, int row, int part,
+                                            float4 *img, int KT, int kofs, float *rs, float *copy, int nsum,
+                                            int64_t sum_stride, const int32_t *div_deg, int div_k,
+                                            const EdgeSplit *split) {
+    const float *sp = src + srow * LH + 16 * part;
+    for (int ps = 1; ps < nsum; ++ps) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float4 y = *(const float4 *)(sp + ps * sum_stride + 4 * q);
+            x[q] = make_float4(x[q].x + y.x, x[q].y + y.y, x[q].z + y.z, x[q].w + y.w);
+        }
+    }
+    if (split && split->units > 0) {
+        // side blocks of the units u of this row's segment whose first slot
+        // s0(u) = floor(u S / U) lies strictly inside the row's 16-row tile
+        // t (local): t k < s0(u) < (t + 1) k
+        const int64_t sg = srow / split->seg_n, q = srow - sg * split->seg_n, t = q / 16;
+        const int64_t S = split->S, G = split->units, kk = split->k;
+        const int64_t lo = max(((t * kk + 1) * G + S - 1) / S, (int64_t)1);
+        const int64_t hi = min(((t + 1) * kk * G + S - 1) / S - 1, G - 1);
+        for (int64_t w = lo; w <= hi; ++w) {
+            const float *q4 = split->side + ((sg * G + w) * 16 + (q & 15)) * 128 + 16 * part;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 y = *(const float4 *)(q4 + 4 * q);
+                x[q] = make_float4(x[q].x + y.x, x[q].y + y.y, x[q].z + y.z, x[q].w + y.w);
+            }
+        }
+    }
+    if (div_k > 0) {
+        const float d = div_deg ? (float)max(div_deg[srow], 1) : (float)div_k;
+        div_rows_rn(x, d);
+    }
+    if (copy) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) *(float4 *)(copy + row * NLD + 16 * part + 4 * q) = x[q];
+    }
+    const int rb = row >> 4, rr = row & 15;
+    if (F16X3) {
+        float m = 0.0f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) m = absmax4(m, x[q]);
+        m = fmaxf(m, __shfl_xor(m, 8, 64));
+        m = fmaxf(m, __shfl_xor(m, 16, 64));
+        m = fmaxf(m, __shfl_xor(m, 32, 64));
+        const float s = split_scale(m);
+        if (part == 0) rs[row] = s;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) x[q] = make_float4(x[q].x * s, x[q].y * s, x[q].z * s, x[q].w * s);
+        const int KS = KT / 32;
+        const int ks = (kofs + 16 * part) >> 5;
+        const int g0 = 2 * (part & 1);
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            half8 hi, lo;
+            split8_rn(x[2 * hh], x[2 * hh + 1], hi, lo);
+            float4 *d = img + ((rb * KS + ks) * 2) * 64 + 16 * (g0 + hh) + rr;
+            d[0] = *(const float4 *)&hi;
+            d[64] = *(const float4 *)&lo;
+        }
+    } else {
+        const int KJ = KT / 16;
+        const int j = (kofs >> 4) + part;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) img[(rb * KJ + j) * 64 + 16 * q + rr] = x[q];
+    }
+}
+
 template <bool F16X3, int ROWS>
 __device__ __forceinline__ void prep(const float *src, int64_t lds, int64_t row0, int64_t nrows_valid,
                                      bool global, float4 *img, int KT, int kofs, float *rs,
@@ -542,75 +632,13 @@ __device__ __forceinline__ void prep(const float *src, int64_t lds, int64_t row0
                                      int div_k = 0, const EdgeSplit *split = nullptr) {
     // threads t0 .. t0 + nthr (default: the whole workgroup) share the rows
     for (int idx = t0 < 0 ? (int)threadIdx.x : (int)threadIdx.x - t0; idx < ROWS * 8; idx += nthr) {
-        // a wave takes 8 rows x 8 parts, lane = 8 part + row: the 8 lanes of one
-        // ds_write_b128 group write 8 consecutive image rows (conflict-free)
-        const int row = (idx >> 6) * 8 + (idx & 7), part = (idx >> 3) & 7;
-        const int64_t srow = global ? min(row0 + row, nrows_valid - 1) : row;
-        const float *sp = src + srow * lds + 16 * part;
+        int row, part;
+        prep_item(idx, row, part);
         float4 x[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) x[q] = *(const float4 *)(sp + 4 * q);
-        for (int ps = 1; ps < nsum; ++ps) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float4 y = *(const float4 *)(sp + ps * sum_stride + 4 * q);
-                x[q] = make_float4(x[q].x + y.x, x[q].y + y.y, x[q].z + y.z, x[q].w + y.w);
-            }
-        }
-        if (split && split->units > 0) {
-            // side blocks of the units u of this row's segment whose first slot
-            // s0(u) = floor(u S / U) lies strictly inside the row's 16-row tile
-            // t (local): t k < s0(u) < (t + 1) k
-            const int64_t sg = srow / split->seg_n, q = srow - sg * split->seg_n, t = q / 16;
-            const int64_t S = split->S, G = split->units, kk = split->k;
-            const int64_t lo = max(((t * kk + 1) * G + S - 1) / S, (int64_t)1);
-            const int64_t hi = min(((t + 1) * kk * G + S - 1) / S - 1, G - 1);
-            for (int64_t w = lo; w <= hi; ++w) {
-                const float *q4 = split->side + ((sg * G + w) * 16 + (q & 15)) * 128 + 16 * part;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const float4 y = *(const float4 *)(q4 + 4 * q);
-                    x[q] = make_float4(x[q].x + y.x, x[q].y + y.y, x[q].z + y.z, x[q].w + y.w);
-                }
-            }
-        }
-        if (div_k > 0) {
-            const float d = div_deg ? (float)max(div_deg[srow], 1) : (float)div_k;
-            div_rows_rn(x, d);
-        }
-        if (copy) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) *(float4 *)(copy + row * NLD + 16 * part + 4 * q) = x[q];
-        }
-        const int rb = row >> 4, rr = row & 15;
-        if (F16X3) {
-            float m = 0.0f;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) m = absmax4(m, x[q]);
-            m = fmaxf(m, __shfl_xor(m, 8, 64));
-            m = fmaxf(m, __shfl_xor(m, 16, 64));
-            m = fmaxf(m, __shfl_xor(m, 32, 64));
-            const float s = split_scale(m);
-            if (part == 0) rs[row] = s;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) x[q] = make_float4(x[q].x * s, x[q].y * s, x[q].z * s, x[q].w * s);
-            const int KS = KT / 32;
-            const int ks = (kofs + 16 * part) >> 5;
-            const int g0 = 2 * (part & 1);
-#pragma unroll
-            for (int hh = 0; hh < 2; ++hh) {
-                half8 hi, lo;
-                split8_rn(x[2 * hh], x[2 * hh + 1], hi, lo);
-                float4 *d = img + ((rb * KS + ks) * 2) * 64 + 16 * (g0 + hh) + rr;
-                d[0] = *(const float4 *)&hi;
-                d[64] = *(const float4 *)&lo;
-            }
-        } else {
-            const int KJ = KT / 16;
-            const int j = (kofs >> 4) + part;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) img[(rb * KJ + j) * 64 + 16 * q + rr] = x[q];
-        }
+        prep_fetch(src, lds, row0, nrows_valid, global, row, part, x);
+        const int64_t srow = global ? min(row0 + row, nrows_valid - 1) : row;
+        prep_finish<F16X3>(x, src, srow, row, part, img, KT, kofs, rs, copy, nsum, sum_stride, div_deg, div_k,
+                           split);
     }
 }
 
@@ -696,14 +724,17 @@ __device__ __forceinline__ void proj_phase(const BOps<F16X3, F16X3 ? 4 : 8> &bA,
                                            const float *rs, const float *rowv, const W1C &w,
                                            const char *pk, const float *w1r, int tw, int64_t row0,
                                            int64_t n, int64_t seg_n, float *a_out, float *b_out,
-                                           float *rng_out, int wave, int lane) {
+                                           float *rng_out, int wave, int lane,
+                                           const BOps<F16X3, F16X3 ? 4 : 8> *bBpre = nullptr) {
     constexpr int ROWS = 16 * RB, S1 = F16X3 ? 4 : 8;
     const int col = 16 * wave + (lane & 15), g = lane >> 4;
     f32x4 aA[RB], aB[RB];
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) aA[rb] = aB[rb] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
     gemm_tile<F16X3, RB, S1>(aA, img, 128, 0, bA, lane);
-    {
+    if (bBpre) {  // operands of b preloaded (the weight-stationary node kernel)
+        gemm_tile<F16X3, RB, S1>(aB, img, 128, 0, *bBpre, lane);
+    } else {
         BOps<F16X3, S1> bB;
         bB.load(pk + kPkW1, 4, 8 + wave, 0, w1r, 128, lane);
         gemm_tile<F16X3, RB, S1>(aB, img, 128, 0, bB, lane);

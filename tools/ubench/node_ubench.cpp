@@ -95,6 +95,7 @@ int main(int argc, char **argv) {
     std::vector<V> vs;
     vs.push_back({"tiled RB2", tiled(gnn_node_kernel<true, true, 2>, 32)});
     vs.push_back({"tiled RB4", tiled(gnn_node_kernel<true, true, 4>, 64)});
+    vs.push_back({"tiled RB2 last layer", tiled(gnn_node_kernel<false, true, 2>, 32)});
     const int reps = 7;
     std::vector<std::vector<float>> t(vs.size());
     for (int r = 0; r < reps; ++r)
@@ -104,10 +105,18 @@ int main(int argc, char **argv) {
         printf("node %-18s median %6.1f  min %6.1f  max %6.1f\n", vs[v].name, t[v][reps / 2], t[v][0],
                t[v][reps - 1]);
     }
-    {   // bitwise: tiled RB2 (outputs 0) vs tiled RB4 (outputs 1)
+    // bitwise: tiled RB2 (outputs 0) against tiled RB4 and the weight-stationary kernel (outputs 1)
+    auto compare = [&](const char *name, std::function<void()> other) -> int {
+        CK(hipMemset(ho[1], 0, n * H * 4));
+        CK(hipMemset(ao[1], 0, n * H * 4));
+        CK(hipMemset(bo[1], 0, n * H * 4));
         hipLaunchKernelGGL((gnn_node_kernel<true, true, 2>), dim3(ceil_div(n, 32)), dim3(512), 0, 0, nt);
-        hipLaunchKernelGGL((gnn_node_kernel<true, true, 4>), dim3(ceil_div(n, 64)), dim3(512), 0, 0, nd);
         CK(hipDeviceSynchronize());
+        std::vector<float> rec0(4 * range_tiles(n)), rec1(4 * range_tiles(n));
+        CK(hipMemcpy(rec0.data(), rng_rec, rec0.size() * 4, hipMemcpyDeviceToHost));
+        other();
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(rec1.data(), rng_rec, rec1.size() * 4, hipMemcpyDeviceToHost));
         for (int q = 0; q < 3; ++q) {
             std::vector<float> x(n * H), y(n * H);
             float *p0 = q == 0 ? ho[0] : q == 1 ? ao[0] : bo[0], *p1 = q == 0 ? ho[1] : q == 1 ? ao[1] : bo[1];
@@ -115,9 +124,15 @@ int main(int argc, char **argv) {
             CK(hipMemcpy(y.data(), p1, n * H * 4, hipMemcpyDeviceToHost));
             size_t nb = 0;
             for (size_t i = 0; i < x.size(); ++i) nb += memcmp(&x[i], &y[i], 4) != 0;
-            printf("RB4 vs RB2 array %d (h', a', b'): %zu differing words\n", q, nb);
+            printf("%s vs RB2 array %d (h', a', b'): %zu differing words\n", name, q, nb);
         }
-    }
+        size_t nr = 0;
+        for (size_t i = 0; i < rec0.size(); ++i) nr += memcmp(&rec0[i], &rec1[i], 4) != 0;
+        printf("%s vs RB2 range records: %zu differing words\n", name, nr);
+        return 0;
+    };
+    if (compare("RB4", [&] { hipLaunchKernelGGL((gnn_node_kernel<true, true, 4>), dim3(ceil_div(n, 64)), dim3(512), 0, 0, nd); }))
+        return 1;
     CK(hipGetLastError());
     return 0;
 }
