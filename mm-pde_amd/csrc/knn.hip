@@ -832,8 +832,35 @@ __global__ __launch_bounds__(256) void knn_cand_kernel(const float2 *__restrict_
         }
     }
     int i0 = min(max(cr[lane], 0), n_per - 1), i1 = min(max(cr[64 + lane], 0), n_per - 1);
-    key_t k0 = KT::key(X[i0], q), k1 = KT::key(X[i1], q);
-    wave_sort128(k0, i0, k1, i1, lane);
+    key_t k0 = 0, k1 = 0;
+    bool sorted = false;
+    if constexpr (QUERY) if (kk < 64) {
+        // sklearn's fp64 order, found by the cheaper fp32 (key, index) sort and
+        // checked exactly: ranks 0 .. kk-1 must be in fp64 (key, index) order
+        // (adjacent pairs compared on their exact keys), and the fp32 key of
+        // rank kk must exceed rank kk-1's by the 64-ulp filter margin
+        // (KeyTraits<true>::filter_threshold: the fp32 key is within 2^-22
+        // relative of the fp64 one), so no later candidate's fp64 key can be
+        // below rank kk-1's.  Otherwise (ties, near-ties) the fp64 sort below.
+        uint32_t f0 = key_f32(X[i0], q), f1 = key_f32(X[i1], q);
+        int j0 = i0, j1 = i1;
+        wave_sort128(f0, j0, f1, j1, lane);
+        const uint64_t e0 = KT::key(X[j0], q);
+        const uint64_t en = __shfl(e0, (lane + 1) & 63, 64);
+        const int jn = __shfl(j0, (lane + 1) & 63, 64);
+        const bool pair_ok = lane >= kk - 1 || ki_less(e0, j0, en, jn);
+        const uint32_t fk = __shfl(f0, kk, 64), fk1 = __shfl(f0, kk - 1, 64);
+        if (__ballot(!pair_ok) == 0ull && fk > KT::filter_threshold(fk1)) {
+            k0 = e0;
+            i0 = j0;
+            sorted = true;
+        }
+    }
+    if (!sorted) {
+        k0 = KT::key(X[i0], q);
+        k1 = KT::key(X[i1], q);
+        wave_sort128(k0, i0, k1, i1, lane);
+    }
     const key_t key_kk = __shfl(k0, kk - 1, 64);
     float d_kk;
     if constexpr (QUERY)
