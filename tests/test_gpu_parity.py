@@ -53,6 +53,49 @@ def test_knn_graph_burgers_grid_ties_bit_exact(dev):
     _graph_case(burgers_grid_points().repeat(2, 1), 2, dev)   # linspace grid: ties at the cut
 
 
+@pytest.mark.gpu
+def test_knn_moved_cells_record_vs_numpy(dev):
+    """The per-trajectory displacement record of the candidate path
+    (mmpde_knn_moved_cells): per 16 x 16 cell of xi's box the largest |x_j - xi_j|
+    (empty: -1), the trajectory's largest, and the median over the non-empty
+    cells (the skip threshold's statistic) against a numpy restatement.  The
+    kernel rounds each distance up by 2^-20 relative (a bound), so values match
+    to that factor."""
+    from mmpde_amd import ops
+    from mmpde_amd.synth import cy_synth_mesh
+
+    xi = cy_synth_mesh()
+    N, B = xi.shape[0], 3
+    g = torch.Generator().manual_seed(7)
+    disp = torch.stack([0.004 * torch.randn((N, 2), generator=g),
+                        0.02 * torch.randn((N, 2), generator=g),
+                        torch.zeros((N, 2))])
+    disp[2, 11] = 0.3                                       # one far-moved node
+    pos = (xi[None] + disp).reshape(-1, 2)
+    rec = ops.knn_moved_cells(pos.to(dev), xi.to(dev), B).cpu().numpy().reshape(B, -1)
+    x32 = xi.numpy().astype(np.float32)
+    lo, hi = x32.min(0), x32.max(0)
+    h = ((hi - lo) / np.float32(16)).astype(np.float32)    # the kernel's fp32 cell assignment
+    ih = (np.float32(1) / h).astype(np.float32)
+    cell = np.clip(((x32 - lo) * ih).astype(np.int64), 0, 15)
+    cid = cell[:, 1] * 16 + cell[:, 0]
+    x = x32.astype(np.float64)
+    for b in range(B):
+        d = np.sqrt(((pos.numpy()[b * N:(b + 1) * N].astype(np.float64) - x) ** 2).sum(1))
+        dcell = np.full(256, -1.0)
+        for c in range(256):
+            m = cid == c
+            if m.any():
+                dcell[c] = d[m].max()
+        got = rec[b, :256]
+        assert np.array_equal(got < 0, dcell < 0), f"empty cells of trajectory {b}"
+        ne = dcell >= 0
+        np.testing.assert_allclose(got[ne], dcell[ne], rtol=4e-6, atol=1e-9)
+        np.testing.assert_allclose(rec[b, 256 + 5], d.max(), rtol=4e-6, atol=1e-9)
+        med = np.sort(dcell[ne])[ne.sum() // 2]
+        np.testing.assert_allclose(rec[b, 256 + 6], med, rtol=4e-6, atol=1e-9)
+
+
 @pytest.mark.parametrize("kind", ["cy", "burgers"])
 def test_knn_graph_moved_candidates_bit_exact(dev, kind):
     """The candidate-table graph and kNN-30 query (mmpde_knn_graph_cand /
