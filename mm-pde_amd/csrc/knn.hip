@@ -639,14 +639,20 @@ __global__ __launch_bounds__(256) void knn_table_kernel(const float2 *__restrict
 // hx, hy, their inverses, a margin eps that covers the rounding of the cell
 // assignment) and dcell[c] >= max |x_bj - xi_j| over the points j with xi_j in
 // cell c (-1: empty cell).  rec[b] = {dcell[256], box[8]}.
-__global__ __launch_bounds__(256) void knn_cells_kernel(const float2 *__restrict__ x,
-                                                        const float2 *__restrict__ xi, int n_per,
-                                                        float *__restrict__ rec) {
-    __shared__ float red[4][4];
+// 1024 threads (16 waves): the point loops are 2.5 iterations per thread at
+// N = 2521, and the median is a rank count (256 broadcast LDS reads per cell)
+// instead of a 36-stage bitonic network with a barrier per stage.
+constexpr int kCellThreads = 1024;
+__global__ __launch_bounds__(kCellThreads) void knn_cells_kernel(const float2 *__restrict__ x,
+                                                                 const float2 *__restrict__ xi, int n_per,
+                                                                 float *__restrict__ rec) {
+    constexpr int NW = kCellThreads / 64;
+    __shared__ float red[NW][4];
     __shared__ uint32_t cell[kCells];
+    __shared__ float srt[kCells];
     const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     float mnx = 3.0e38f, mny = 3.0e38f, mxx = -3.0e38f, mxy = -3.0e38f;
-    for (int i = tid; i < n_per; i += 256) {
+    for (int i = tid; i < n_per; i += kCellThreads) {
         const float2 c = xi[i];
         mnx = fminf(mnx, c.x);
         mny = fminf(mny, c.y);
@@ -663,15 +669,19 @@ __global__ __launch_bounds__(256) void knn_cells_kernel(const float2 *__restrict
         red[wave][2] = mxx;
         red[wave][3] = mxy;
     }
-    cell[tid] = 0u;  // empty (kCells == 256 threads)
+    if (tid < kCells) cell[tid] = 0u;  // empty
     __syncthreads();
-    const float x0 = fminf(fminf(red[0][0], red[1][0]), fminf(red[2][0], red[3][0]));
-    const float y0 = fminf(fminf(red[0][1], red[1][1]), fminf(red[2][1], red[3][1]));
-    const float x1 = fmaxf(fmaxf(red[0][2], red[1][2]), fmaxf(red[2][2], red[3][2]));
-    const float y1 = fmaxf(fmaxf(red[0][3], red[1][3]), fmaxf(red[2][3], red[3][3]));
+    float x0 = red[0][0], y0 = red[0][1], x1 = red[0][2], y1 = red[0][3];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) {
+        x0 = fminf(x0, red[w][0]);
+        y0 = fminf(y0, red[w][1]);
+        x1 = fmaxf(x1, red[w][2]);
+        y1 = fmaxf(y1, red[w][3]);
+    }
     const float hx = (x1 - x0) / kCellG, hy = (y1 - y0) / kCellG;
     const float ihx = hx > 0.0f ? 1.0f / hx : 0.0f, ihy = hy > 0.0f ? 1.0f / hy : 0.0f;
-    for (int i = tid; i < n_per; i += 256) {
+    for (int i = tid; i < n_per; i += kCellThreads) {
         const float2 a = x[(int64_t)b * n_per + i], c = xi[i];
         const float dx = a.x - c.x, dy = a.y - c.y;
         const float d = sqrtf(dx * dx + dy * dy) * kUp;
@@ -683,33 +693,36 @@ __global__ __launch_bounds__(256) void knn_cells_kernel(const float2 *__restrict
     }
     __syncthreads();
     float *r = rec + (int64_t)b * kCellRec;
-    const uint32_t v = cell[tid];
+    // cells on threads 0 .. 255 (waves 0 - 3)
+    const uint32_t v = tid < kCells ? cell[tid] : 0u;
     const float dc = v == 0u ? -1.0f : __uint_as_float(v - 1u);
-    r[tid] = dc;
+    if (tid < kCells) {
+        r[tid] = dc;
+        // the median over the non-empty cells of their largest displacement (the
+        // statistic skip_above is compared with), empty cells last
+        srt[tid] = v == 0u ? 3.0e38f : dc;
+    }
     const float dall = wave_max(fmaxf(dc, 0.0f));
     const int nonempty = __popcll(__ballot(v != 0u));
-    __syncthreads();
-    if (lane == 0) {
+    __syncthreads();  // red (read above) and srt
+    if (lane == 0 && wave < kCells / 64) {
         red[wave][0] = dall;
         red[wave][1] = __int_as_float(nonempty);
     }
-    // the median over the non-empty cells of their largest displacement (the
-    // statistic skip_above is compared with): bitonic sort, empty cells last
-    float *srt = (float *)cell;
-    srt[tid] = v == 0u ? 3.0e38f : dc;
     __syncthreads();
-    for (int size = 2; size <= kCells; size <<= 1)
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            if (tid < kCells / 2) {
-                const int i = 2 * tid - (tid & (stride - 1)), l = i + stride;
-                const float a = srt[i], c = srt[l];
-                if ((a > c) == ((i & size) == 0)) {
-                    srt[i] = c;
-                    srt[l] = a;
-                }
-            }
-            __syncthreads();
+    const int ne = __float_as_int(red[0][1]) + __float_as_int(red[1][1]) + __float_as_int(red[2][1]) +
+                   __float_as_int(red[3][1]);
+    if (tid < kCells) {
+        // rank of this cell's value in (value, cell) order; the one of rank
+        // ne / 2 is element ne / 2 of the sorted list
+        const float mine = srt[tid];
+        int rank = 0;
+        for (int u = 0; u < kCells; ++u) {
+            const float o = srt[u];
+            rank += (o < mine || (o == mine && u < tid)) ? 1 : 0;
         }
+        if (ne > 0 && rank == ne / 2) r[kCells + 6] = mine;
+    }
     if (tid == 0) {
         const float eps = 1.0e-5f * fmaxf(x1 - x0, y1 - y0);
         r[kCells + 0] = x0;
@@ -718,9 +731,7 @@ __global__ __launch_bounds__(256) void knn_cells_kernel(const float2 *__restrict
         r[kCells + 3] = hy;
         r[kCells + 4] = eps;
         r[kCells + 5] = fmaxf(fmaxf(red[0][0], red[1][0]), fmaxf(red[2][0], red[3][0]));
-        const int ne = __float_as_int(red[0][1]) + __float_as_int(red[1][1]) + __float_as_int(red[2][1]) +
-                       __float_as_int(red[3][1]);
-        r[kCells + 6] = ne > 0 ? srt[ne / 2] : 0.0f;
+        if (ne == 0) r[kCells + 6] = 0.0f;
         for (int i = 0; i < 2; ++i) {
             cell_last_miss(rec, b)[i] = 0;
             cell_any_miss(rec, b)[i] = 0;
@@ -956,7 +967,7 @@ extern "C" int mmpde_knn_moved_cells(const float *pos, const float *xi, int64_t 
                                      float *cells_out, mmpde_stream_t stream) {
     MMPDE_REQUIRE(pos && xi && cells_out && batches >= 1 && batches <= 65535 && n_per >= 1 &&
                   n_per <= INT32_MAX);
-    hipLaunchKernelGGL(knn_cells_kernel, dim3((unsigned)batches), dim3(256), 0, as_stream(stream),
+    hipLaunchKernelGGL(knn_cells_kernel, dim3((unsigned)batches), dim3(kCellThreads), 0, as_stream(stream),
                        (const float2 *)pos, (const float2 *)xi, (int)n_per, cells_out);
     MMPDE_RET_LAUNCH();
     return MMPDE_OK;

@@ -739,16 +739,20 @@ __device__ __forceinline__ void proj_phase(const BOps<F16X3, F16X3 ? 4 : 8> &bA,
         bB.load(pk + kPkW1, 4, 8 + wave, 0, w1r, 128, lane);
         gemm_tile<F16X3, RB, S1>(aB, img, 128, 0, bB, lane);
     }
-    // |a|, |b| maxima of the rows in the tile's first segment (0) and in the
-    // next one (1) for the range record (seg_n >= ROWS: at most two segments)
-    float amx[2] = {0.0f, 0.0f}, bmx[2] = {0.0f, 0.0f};
-    const int64_t seg1 = (row0 / seg_n + 1) * seg_n;  // first row of the next segment
+    // |a|, |b| maxima of each 16-row block's rows in the block's first segment
+    // (0) and in the next one (1), for the block's range record (layer.hpp:
+    // kRangeRows = 16; seg_n >= 16: a block touches at most two segments)
+    float amx[RB][2], bmx[RB][2];
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) amx[rb][0] = amx[rb][1] = bmx[rb][0] = bmx[rb][1] = 0.0f;
     // stores at immediate offsets from one base per lane; the row test only
     // for a tile that runs past n (wave-uniform)
     const bool full = row0 + ROWS <= n;
     float *ap = a_out + (row0 + 4 * g) * LH + col, *bp = b_out + (row0 + 4 * g) * LH + col;
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) {
+        const int64_t rb0 = row0 + 16 * rb;
+        const int64_t seg1 = (rb0 / seg_n + 1) * seg_n;  // first row of the next segment
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int lr = 16 * rb + 4 * g + q;
@@ -767,27 +771,33 @@ __device__ __forceinline__ void proj_phase(const BOps<F16X3, F16X3 ? 4 : 8> &bA,
                 ap[(16 * rb + q) * LH] = va;
                 bp[(16 * rb + q) * LH] = vb;
                 const int sx = row0 + lr >= seg1;
-                amx[sx] = fmaxf(amx[sx], fabsf(va));
-                bmx[sx] = fmaxf(bmx[sx], fabsf(vb));
+                amx[rb][sx] = fmaxf(amx[rb][sx], fabsf(va));
+                bmx[rb][sx] = fmaxf(bmx[rb][sx], fabsf(vb));
             }
         }
     }
     if (rng_out) {
-        // wave maxima, then the workgroup's through LDS: one float4 record
-        __shared__ float red[8][4];
-        const float m0 = wave_max(amx[0]), m1 = wave_max(bmx[0]), m2 = wave_max(amx[1]), m3 = wave_max(bmx[1]);
-        if (lane == 0) {
-            red[wave][0] = m0;
-            red[wave][1] = m1;
-            red[wave][2] = m2;
-            red[wave][3] = m3;
+        // wave maxima, then the workgroup's through LDS: one float4 record per
+        // 16-row block
+        __shared__ float red[8][RB][4];
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+            const float m0 = wave_max(amx[rb][0]), m1 = wave_max(bmx[rb][0]), m2 = wave_max(amx[rb][1]),
+                        m3 = wave_max(bmx[rb][1]);
+            if (lane == 0) {
+                red[wave][rb][0] = m0;
+                red[wave][rb][1] = m1;
+                red[wave][rb][2] = m2;
+                red[wave][rb][3] = m3;
+            }
         }
         __syncthreads();
-        if (wave == 0 && lane < 4) {
-            float m = red[0][lane];
+        if (wave == 0 && lane < 4 * RB) {
+            const int rb = lane >> 2, e = lane & 3;
+            float m = red[0][rb][e];
 #pragma unroll
-            for (int w = 1; w < 8; ++w) m = fmaxf(m, red[w][lane]);
-            rng_out[4 * (row0 / ROWS) + lane] = m;
+            for (int w = 1; w < 8; ++w) m = fmaxf(m, red[w][rb][e]);
+            if (row0 + 16 * rb < n) rng_out[4 * (row0 / 16 + rb) + e] = m;
         }
     }
 }
@@ -1056,7 +1066,7 @@ int device_cus() {
 #define MMPDE_NODE_RB 2
 #endif
 
-static_assert(16 * MMPDE_NODE_RB == kRangeRows, "range records are per node tile");
+static_assert(16 * MMPDE_NODE_RB % kRangeRows == 0, "range records are per 16-row block of a node tile");
 
 int launch_edge_stage(const float *a, const float *b, const int32_t *nbr, const int32_t *deg,
                       int64_t n, int k, int64_t seg_n, const mmpde_gnn_layer_params *p, const char *pk,

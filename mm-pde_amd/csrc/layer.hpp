@@ -3,20 +3,20 @@
 #pragma once
 #include "common.hpp"
 
-// F16X3 range records: the node / embed stage writes, per 32-row node tile
-// (kRangeRows rows; tile index = row / kRangeRows), the max |a| and max |b| of
+// F16X3 range records: the node / embed stage writes, per 16-row block
+// (kRangeRows rows; block index = row / kRangeRows), the max |a| and max |b| of
 // its rows in each of the (at most two) trajectory segments the tile touches:
 // rng[tile] = {max|a| seg0, max|b| seg0, max|a| seg1, max|b| seg1}, seg0 =
 // first row / seg_n (the seg1 entries are 0 when the tile lies in one
 // segment).  The wave edge kernel takes its split scale from the records of
 // its own segment only, so a trajectory's f16x3 result does not depend on the
 // trajectories launched beside it.  Plain stores, no atomics, no zeroing.
-constexpr int kRangeRows = 32;
+constexpr int kRangeRows = 16;
 inline int64_t range_tiles(int64_t n) { return (n + kRangeRows - 1) / kRangeRows; }
 
 // max |a| + max |b| over segment s from the range records of the node tiles
-// that hold its rows (layer.hpp kRangeRows): a tile whose first row lies in s
-// gives its seg0 entries, the tile straddling into s from s - 1 its seg1 ones.
+// that hold its rows (layer.hpp kRangeRows): a block whose first row lies in s
+// gives its seg0 entries, the block straddling into s from s - 1 its seg1 ones.
 __device__ __forceinline__ float segment_range(const float *rng, int64_t seg_n, int64_t s) {
     const int64_t r0 = s * seg_n, t0 = r0 / kRangeRows, t1 = (r0 + seg_n - 1) / kRangeRows;
     float ma = 0.0f, mb = 0.0f;

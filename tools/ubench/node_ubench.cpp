@@ -95,6 +95,7 @@ int main(int argc, char **argv) {
     std::vector<V> vs;
     vs.push_back({"tiled RB2", tiled(gnn_node_kernel<true, true, 2>, 32)});
     vs.push_back({"tiled RB4", tiled(gnn_node_kernel<true, true, 4>, 64)});
+
     vs.push_back({"tiled RB2 last layer", tiled(gnn_node_kernel<false, true, 2>, 32)});
     const int reps = 7;
     std::vector<std::vector<float>> t(vs.size());
@@ -133,6 +134,7 @@ int main(int argc, char **argv) {
     };
     if (compare("RB4", [&] { hipLaunchKernelGGL((gnn_node_kernel<true, true, 4>), dim3(ceil_div(n, 64)), dim3(512), 0, 0, nd); }))
         return 1;
+
     CK(hipGetLastError());
     return 0;
 }
