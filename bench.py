@@ -114,13 +114,20 @@ class EdgeTracer:
         self.traces.append((t, arr))
         return t
 
-    def launch_times_ms(self):
-        """[(layer index, edge-stage ms, node-stage ms)] for every traced layer."""
+    def launch_times_ms(self, paired=False):
+        """[(layer index, edge-stage ms, node-stage ms)] for every traced layer.
+        paired: consecutive forwards (model, model_b of one step) shared one
+        node-stage launch per layer (gnn_2d.forward_pair), which starts after
+        model_b's edge stage: each gets half of that launch."""
         out = []
-        for _, (beg, mid, end) in self.traces:
+        for i, (_, (beg, mid, end)) in enumerate(self.traces):
             for l in range(self.L):
-                out.append((l, self.pool.elapsed_ms(beg[l], mid[l]),
-                            self.pool.elapsed_ms(mid[l], end[l])))
+                if paired:
+                    _, (_, mid_b, end_b) = self.traces[i | 1]
+                    node = 0.5 * self.pool.elapsed_ms(mid_b[l], end_b[l])
+                else:
+                    node = self.pool.elapsed_ms(mid[l], end[l])
+                out.append((l, self.pool.elapsed_ms(beg[l], mid[l]), node))
         return out
 
 
@@ -265,7 +272,7 @@ def main():
         exact = {"value": (hi - lo) * world * n_nodes * args.steps / el32,
                  "ms_per_step": 1e3 * el32 / args.steps,
                  "final_state_max_rel_diff_vs_main": rel}
-    launches = tracer.launch_times_ms()
+    launches = tracer.launch_times_ms(paired=moving and eng.pair)
     tracer.pool.close()
 
     if rank != 0:

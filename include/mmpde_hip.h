@@ -395,6 +395,32 @@ int mmpde_gnn_forward_ex(const float *u, const float *pos, int64_t n, int k, con
                          const mmpde_gnn_head_params *head, void *workspace, float *out,
                          const mmpde_gnn_exec *exec, mmpde_stream_t stream);
 
+/* One mmpde_gnn_forward_ex call's arguments (mmpde_gnn_forward_pair). */
+typedef struct {
+    const float *u, *pos;
+    int64_t n;
+    int k;
+    const int32_t *nbr;
+    mmpde_gnn_scales sc;
+    const mmpde_gnn_embed_params *emb;
+    const mmpde_gnn_layer_params *layers;
+    int n_layers;
+    const mmpde_gnn_head_params *head;
+    void *workspace; /* mmpde_gnn_workspace_bytes(n), one per call */
+    float *out;
+    const mmpde_gnn_exec *exec;
+} mmpde_gnn_call;
+
+/* Two independent GNN forwards -- the MM-PDE step's `model(graph_uniform)` and
+ * `model_b(graph)` (reference train_helper_2d.py:174-185) -- as one sequence of
+ * launches: one embedding launch over both problems' rows, per layer the two
+ * edge stages then ONE node-stage launch over both, one head launch.  Each
+ * output equals mmpde_gnn_forward_ex's for its call, bit for bit.  Both calls:
+ * F16X3 with exec->packed images, the same n_layers (>= 1) and time window;
+ * their events are recorded around their own edge stages and after the shared
+ * node stage. */
+int mmpde_gnn_forward_pair(const mmpde_gnn_call *calls, mmpde_stream_t stream);
+
 /* ------------------------------------------------------------------------
  * DMM mesh mover (reference mesh/dmm_model.py, data_creator_2d.py:88-137)
  * ---------------------------------------------------------------------- */

@@ -802,9 +802,18 @@ __device__ __forceinline__ void proj_phase(const BOps<F16X3, F16X3 ? 4 : 8> &bA,
     }
 }
 
+// One or two problems per launch (launch_node_stages): workgroups below
+// tiles0 take problem 0's row tiles, the rest problem 1's.
+struct NodeArgs2 {
+    NodeArgs a[2];
+    int64_t tiles0;
+};
+
 template <bool NEXT, bool F16X3, int RB>
-__global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs p) {
+__global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs2 pp) {
     constexpr int ROWS = 16 * RB;
+    const bool second = (int64_t)blockIdx.x >= pp.tiles0;  // workgroup-uniform
+    const NodeArgs &p = pp.a[second ? 1 : 0];
     __shared__ float4 img[RB * 16 * 64];        // operand image, K = 256 (h | mean), then 128
     __shared__ float stage[ROWS * NLD];         // fp32 v, then h'
     __shared__ float hres[ROWS * NLD];          // fp32 h (residual)
@@ -812,7 +821,7 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs p) {
     __shared__ float rowv[3 + MAX_TW][ROWS];    // per row: t / tmax, x / Lx, y / Ly, u_0 .. u_{tw-1}
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int r = lane & 15, g = lane >> 4;
-    const int64_t row0 = (int64_t)blockIdx.x * ROWS;
+    const int64_t row0 = ((int64_t)blockIdx.x - (second ? pp.tiles0 : 0)) * ROWS;
     const int col = 16 * wave + r;  // this lane's output column (tile = wave)
     const int tw = p.sc.tw > 1 ? p.sc.tw : 1;
     constexpr int S1 = F16X3 ? 4 : 8;    // K steps per 128 columns of K
@@ -940,9 +949,16 @@ struct EmbedArgs {
     int64_t seg_n;         // rows per trajectory segment (range records)
 };
 
+struct EmbedArgs2 {
+    EmbedArgs a[2];
+    int64_t tiles0;
+};
+
 template <bool F16X3, int RB>
-__global__ __launch_bounds__(512, NODE_WPE) void gnn_embed_kernel(EmbedArgs p) {
+__global__ __launch_bounds__(512, NODE_WPE) void gnn_embed_kernel(EmbedArgs2 pp) {
     constexpr int ROWS = 16 * RB;
+    const bool second = (int64_t)blockIdx.x >= pp.tiles0;  // workgroup-uniform
+    const EmbedArgs &p = pp.a[second ? 1 : 0];
     constexpr int S1 = F16X3 ? 4 : 8;
     __shared__ float4 img[RB * 8 * 64];   // K = 128 operand image
     __shared__ float stage[ROWS * NLD];   // fp32 z, then h0
@@ -951,7 +967,7 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_embed_kernel(EmbedArgs p) {
     __shared__ float rowv[3 + MAX_TW][ROWS];  // per row: t / tmax, x / Lx, y / Ly, u_0 .. u_{tw-1}
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int g = lane >> 4;
-    const int64_t row0 = (int64_t)blockIdx.x * ROWS;
+    const int64_t row0 = ((int64_t)blockIdx.x - (second ? pp.tiles0 : 0)) * ROWS;
     const int col = 16 * wave + (lane & 15);
     const int tw = p.sc.tw > 1 ? p.sc.tw : 1;
     if (tid < ROWS) {
@@ -1101,39 +1117,105 @@ int launch_edge_stage(const float *a, const float *b, const int32_t *nbr, const 
     return MMPDE_OK;
 }
 
+// The kernel arguments of one node-stage call (validated); *next_out / *f16
+// select the kernel instance.
+static int node_args(const NodeStageCall &c, NodeArgs *out) {
+    const bool sums = c.split && c.split->units > 0;
+    MMPDE_REQUIRE(!sums || (c.split->side && c.split->S > 0 && c.split->k > 0 && c.split->seg_n > 0 &&
+                            c.n % c.split->seg_n == 0));
+    MMPDE_REQUIRE(!c.rng_out || al16(c.rng_out));
+    MMPDE_REQUIRE(c.h && c.mean && c.u && c.pos && c.p && c.h_out && c.n > 0);
+    MMPDE_REQUIRE(al16(c.h) && al16(c.mean) && al16(c.h_out));
+    MMPDE_REQUIRE(c.p->upd1_ld >= 257 && (c.p->upd1_ld & 3) == 0 && al16(c.p->upd1_w) && al16(c.p->upd2_w));
+    MMPDE_REQUIRE(!c.pk || (al16(c.pk) && (!c.next || c.pkn)));
+    const mmpde_gnn_layer_params *p = c.p;
+    NodeArgs a{c.h, c.mean, c.n, p->upd1_w, p->upd1_b, p->upd1_ld, p->upd2_w, p->upd2_b, p->bn_w, p->bn_b,
+               p->bn_rm, p->bn_rv, p->eps, c.h_out, nullptr, nullptr, 0, c.a_out, c.b_out, c.u, c.pos, c.sc,
+               c.pk, c.pkn, c.rng_out, effective_seg(c.n, c.seg_n), 1, 0, sums ? c.deg : nullptr,
+               sums ? c.split->k : 0};
+    if (sums) a.split = *c.split;
+    if (c.next) {
+        MMPDE_REQUIRE(c.a_out && c.b_out && c.next->msg1_ld >= 260 && (c.next->msg1_ld & 3) == 0 &&
+                      al16(c.next->msg1_w));
+        a.w1n = c.next->msg1_w;
+        a.b1n = c.next->msg1_b;
+        a.ld_w1n = c.next->msg1_ld;
+    }
+    *out = a;
+    return MMPDE_OK;
+}
+
+int launch_node_stages(const NodeStageCall *calls, int count, hipStream_t st) {
+    MMPDE_REQUIRE(calls && (count == 1 || count == 2));
+    constexpr int RB = MMPDE_NODE_RB;
+    NodeArgs2 pp;
+    int rc = node_args(calls[0], &pp.a[0]);
+    if (rc) return rc;
+    const bool next = calls[0].next != nullptr, f16 = calls[0].pk != nullptr;
+    pp.tiles0 = ceil_div(calls[0].n, 16 * RB);
+    int64_t tiles = pp.tiles0;
+    if (count == 2) {
+        MMPDE_REQUIRE((calls[1].next != nullptr) == next && (calls[1].pk != nullptr) == f16);
+        rc = node_args(calls[1], &pp.a[1]);
+        if (rc) return rc;
+        tiles += ceil_div(calls[1].n, 16 * RB);
+    } else {
+        pp.a[1] = pp.a[0];
+    }
+    MMPDE_REQUIRE(tiles < (int64_t)INT32_MAX);
+    const dim3 grid((unsigned)tiles);
+#define MMPDE_NODE(NX, SPLIT) \
+    hipLaunchKernelGGL((gnn_node_kernel<NX, SPLIT, RB>), grid, dim3(512), 0, st, pp)
+    if (next && f16) MMPDE_NODE(true, true);
+    else if (next) MMPDE_NODE(true, false);
+    else if (f16) MMPDE_NODE(false, true);
+    else MMPDE_NODE(false, false);
+#undef MMPDE_NODE
+    MMPDE_RET_LAUNCH();
+    return MMPDE_OK;
+}
+
 int launch_node_stage(const float *h, const float *mean, const EdgeSplit *split, const int32_t *deg,
                       const float *u, const float *pos, int64_t n, int64_t seg_n, mmpde_gnn_scales sc,
                       const mmpde_gnn_layer_params *p, const mmpde_gnn_layer_params *next,
                       const char *pk, const char *pkn, float *rng_out, float *h_out, float *a_out,
                       float *b_out, hipStream_t st) {
-    const bool sums = split && split->units > 0;
-    MMPDE_REQUIRE(!sums || (split->side && split->S > 0 && split->k > 0 && split->seg_n > 0 &&
-                            n % split->seg_n == 0));
-    MMPDE_REQUIRE(!rng_out || al16(rng_out));
-    MMPDE_REQUIRE(h && mean && u && pos && p && h_out && n > 0);
-    MMPDE_REQUIRE(al16(h) && al16(mean) && al16(h_out));
-    MMPDE_REQUIRE(p->upd1_ld >= 257 && (p->upd1_ld & 3) == 0 && al16(p->upd1_w) && al16(p->upd2_w));
-    MMPDE_REQUIRE(!pk || (al16(pk) && (!next || pkn)));
-    NodeArgs a{h, mean, n, p->upd1_w, p->upd1_b, p->upd1_ld, p->upd2_w, p->upd2_b, p->bn_w, p->bn_b,
-               p->bn_rm, p->bn_rv, p->eps, h_out, nullptr, nullptr, 0, a_out, b_out, u, pos, sc,
-               pk, pkn, rng_out, effective_seg(n, seg_n), 1, 0, sums ? deg : nullptr, sums ? split->k : 0};
-    if (sums) a.split = *split;
-    if (next) {
-        MMPDE_REQUIRE(a_out && b_out && next->msg1_ld >= 260 && (next->msg1_ld & 3) == 0 &&
-                      al16(next->msg1_w));
-        a.w1n = next->msg1_w;
-        a.b1n = next->msg1_b;
-        a.ld_w1n = next->msg1_ld;
-    }
+    const NodeStageCall c{h, mean, split, deg, u, pos, n, seg_n, sc, p, next, pk, pkn, rng_out, h_out, a_out,
+                          b_out};
+    return launch_node_stages(&c, 1, st);
+}
+
+static int embed_args(const EmbedStageCall &c, EmbedArgs *out) {
+    MMPDE_REQUIRE(c.u && c.pos && c.e && c.l0 && c.h_out && c.a_out && c.b_out && c.n > 0);
+    MMPDE_REQUIRE(al16(c.e->w3) && al16(c.h_out) && al16(c.a_out) && al16(c.b_out));
+    MMPDE_REQUIRE(c.l0->msg1_ld >= 260 && (c.l0->msg1_ld & 3) == 0 && al16(c.l0->msg1_w));
+    MMPDE_REQUIRE(!c.pk0 || (al16(c.pk0) && c.rng_out && al16(c.rng_out)));
+    *out = EmbedArgs{c.u, c.pos, c.n, c.sc, *c.e, c.h_out, c.l0->msg1_w, c.l0->msg1_b, c.l0->msg1_ld, c.a_out,
+                     c.b_out, c.pk0, c.rng_out, effective_seg(c.n, c.seg_n)};
+    return MMPDE_OK;
+}
+
+int launch_embed_stages(const EmbedStageCall *calls, int count, hipStream_t st) {
+    MMPDE_REQUIRE(calls && (count == 1 || count == 2));
     constexpr int RB = MMPDE_NODE_RB;
-    const dim3 grid((unsigned)ceil_div(n, 16 * RB));
-#define MMPDE_NODE(NX, SPLIT) \
-    hipLaunchKernelGGL((gnn_node_kernel<NX, SPLIT, RB>), grid, dim3(512), 0, st, a)
-    if (next && pk) MMPDE_NODE(true, true);
-    else if (next) MMPDE_NODE(true, false);
-    else if (pk) MMPDE_NODE(false, true);
-    else MMPDE_NODE(false, false);
-#undef MMPDE_NODE
+    EmbedArgs2 pp;
+    int rc = embed_args(calls[0], &pp.a[0]);
+    if (rc) return rc;
+    const bool f16 = calls[0].pk0 != nullptr;
+    pp.tiles0 = ceil_div(calls[0].n, 16 * RB);
+    int64_t tiles = pp.tiles0;
+    if (count == 2) {
+        MMPDE_REQUIRE((calls[1].pk0 != nullptr) == f16);
+        rc = embed_args(calls[1], &pp.a[1]);
+        if (rc) return rc;
+        tiles += ceil_div(calls[1].n, 16 * RB);
+    } else {
+        pp.a[1] = pp.a[0];
+    }
+    MMPDE_REQUIRE(tiles < (int64_t)INT32_MAX);
+    const dim3 grid((unsigned)tiles);
+    if (f16) hipLaunchKernelGGL((gnn_embed_kernel<true, RB>), grid, dim3(512), 0, st, pp);
+    else hipLaunchKernelGGL((gnn_embed_kernel<false, RB>), grid, dim3(512), 0, st, pp);
     MMPDE_RET_LAUNCH();
     return MMPDE_OK;
 }
@@ -1142,16 +1224,6 @@ int launch_embed_stage(const float *u, const float *pos, int64_t n, int64_t seg_
                        const mmpde_gnn_embed_params *e, const mmpde_gnn_layer_params *l0,
                        const char *pk0, float *rng_out, float *h_out, float *a_out,
                        float *b_out, hipStream_t st) {
-    MMPDE_REQUIRE(u && pos && e && l0 && h_out && a_out && b_out && n > 0);
-    MMPDE_REQUIRE(al16(e->w3) && al16(h_out) && al16(a_out) && al16(b_out));
-    MMPDE_REQUIRE(l0->msg1_ld >= 260 && (l0->msg1_ld & 3) == 0 && al16(l0->msg1_w));
-    MMPDE_REQUIRE(!pk0 || (al16(pk0) && rng_out && al16(rng_out)));
-    EmbedArgs a{u, pos, n, sc, *e, h_out, l0->msg1_w, l0->msg1_b, l0->msg1_ld, a_out, b_out, pk0,
-                rng_out, effective_seg(n, seg_n)};
-    constexpr int RB = MMPDE_NODE_RB;
-    const dim3 grid((unsigned)ceil_div(n, 16 * RB));
-    if (pk0) hipLaunchKernelGGL((gnn_embed_kernel<true, RB>), grid, dim3(512), 0, st, a);
-    else hipLaunchKernelGGL((gnn_embed_kernel<false, RB>), grid, dim3(512), 0, st, a);
-    MMPDE_RET_LAUNCH();
-    return MMPDE_OK;
+    const EmbedStageCall c{u, pos, n, seg_n, sc, e, l0, pk0, rng_out, h_out, a_out, b_out};
+    return launch_embed_stages(&c, 1, st);
 }

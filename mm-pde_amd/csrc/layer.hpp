@@ -98,6 +98,24 @@ int launch_node_stage(const float *h, const float *mean, const EdgeSplit *split,
                       const char *pk, const char *pkn, float *rng_out, float *h_out, float *a_out,
                       float *b_out, hipStream_t st);
 
+// The arguments of one launch_node_stage call; launch_node_stages runs one or
+// two of them (two independent problems, e.g. the MM-PDE step's two GNNs) in
+// ONE launch: problem 0's row tiles, then problem 1's, each workgroup reading
+// its own problem's arguments.  Both must take the same kernel (next and pk
+// both set or both null).
+struct NodeStageCall {
+    const float *h, *mean;
+    const EdgeSplit *split;
+    const int32_t *deg;
+    const float *u, *pos;
+    int64_t n, seg_n;
+    mmpde_gnn_scales sc;
+    const mmpde_gnn_layer_params *p, *next;
+    const char *pk, *pkn;
+    float *rng_out, *h_out, *a_out, *b_out;
+};
+int launch_node_stages(const NodeStageCall *calls, int count, hipStream_t st);
+
 // Embedding (gnn_2d.py:99-106) + layer 0's message_net_1 node halves in one
 // launch: h_out = embedding_mlp(cat(u, x/Lx, y/Ly, t/tmax)), a_out / b_out as
 // launch_node_stage's.  F16X3 projection when pk0 (layer 0's images) != nullptr.
@@ -105,3 +123,16 @@ int launch_embed_stage(const float *u, const float *pos, int64_t n, int64_t seg_
                        const mmpde_gnn_embed_params *e, const mmpde_gnn_layer_params *l0,
                        const char *pk0, float *rng_out, float *h_out, float *a_out,
                        float *b_out, hipStream_t st);
+
+// launch_embed_stage's arguments; launch_embed_stages: one or two problems in
+// one launch, as launch_node_stages (pk0 both set or both null).
+struct EmbedStageCall {
+    const float *u, *pos;
+    int64_t n, seg_n;
+    mmpde_gnn_scales sc;
+    const mmpde_gnn_embed_params *e;
+    const mmpde_gnn_layer_params *l0;
+    const char *pk0;
+    float *rng_out, *h_out, *a_out, *b_out;
+};
+int launch_embed_stages(const EmbedStageCall *calls, int count, hipStream_t st);

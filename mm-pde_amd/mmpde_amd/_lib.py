@@ -13,7 +13,7 @@ import os
 import torch
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libmmpde_hip.so")
-ABI_VERSION = 11300
+ABI_VERSION = 11400
 
 ACT_NONE, ACT_TANH, ACT_RELU, ACT_ELU = 0, 1, 2, 3
 PAD_ZEROS, PAD_CIRCULAR = 0, 1
@@ -64,6 +64,13 @@ class GnnExec(ctypes.Structure):
     _fields_ = [("edge_begin", ctypes.POINTER(_P)), ("edge_end", ctypes.POINTER(_P)),
                 ("edge_gemm", _I), ("packed", _P), ("node_end", ctypes.POINTER(_P)),
                 ("degree", _P), ("seg_n", _I64)]
+
+
+class GnnCall(ctypes.Structure):
+    """mmpde_gnn_call: one mmpde_gnn_forward_ex call's arguments (mmpde_gnn_forward_pair)."""
+    _fields_ = [("u", _P), ("pos", _P), ("n", _I64), ("k", _I), ("nbr", _P), ("sc", GnnScales),
+                ("emb", _P), ("layers", _P), ("n_layers", _I), ("head", _P), ("workspace", _P),
+                ("out", _P), ("exec", _P)]
 
 
 class DmmGraphBranch(ctypes.Structure):
@@ -128,6 +135,7 @@ _SIGS = {
     "mmpde_gnn_pack_f16x3": (_I, [_P, _I, _P, _P]),
     "mmpde_gnn_forward_ex": (_I, [_P, _P, _I64, _I, _P, GnnScales, _P, _P, _I, _P, _P, _P, _P,
                                   _P]),
+    "mmpde_gnn_forward_pair": (_I, [_P, _P]),
     "mmpde_dmm_workspace_bytes": (_I64, [_I64, _I64, _I, _I]),
     "mmpde_dmm_mesh_graph": (_I, [_P, _P, _I64, _I64, _P, _I, _P, _P, _P, _P, _P]),
     "mmpde_dmm_mesh_array": (_I, [_P, _P, _I64, _I64, _P, _P, _P, _P, _P]),

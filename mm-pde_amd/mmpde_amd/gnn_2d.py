@@ -310,6 +310,15 @@ class MP_PDE_Solver_2D(nn.Module):  # noqa: N801 - reference name
         (its edge_gemm field is set from self.edge_gemm)."""
         if self.training:
             return self.train_forward(data)
+        call, out, _keep = self._call(data, out, workspace, trace)
+        L.check(L.lib().mmpde_gnn_forward_ex(
+            call.u, call.pos, call.n, call.k, call.nbr, call.sc, call.emb, call.layers,
+            call.n_layers, call.head, call.workspace, call.out, call.exec, L.stream(data.x.device)),
+            "mmpde_gnn_forward")
+        return out
+
+    def _call(self, data, out, workspace, trace):
+        """(mmpde_gnn_call, out, keep-alive) of one eval forward (see forward)."""
         self.check_supported()
         u, pos = data.x, data.pos
         L.require_device(u, pos)
@@ -324,14 +333,16 @@ class MP_PDE_Solver_2D(nn.Module):  # noqa: N801 - reference name
         u = L.f32c(u).reshape(-1)
         pos = L.f32c(pos)
         sc, emb, arr, head = self.device_params()
+        t_slot = None
         if pos.shape[-1] == 2:   # (x, y) rows, one t for every node (the rollout's form)
             t, t_slot = getattr(data, "t", None), getattr(data, "t_slot", None)
             if t is None and t_slot is None:
                 raise ValueError("pos with 2 columns needs data.t or data.t_slot")
             if t_slot is not None:
                 L.require_device(t_slot)
+                t_slot = L.f32c(t_slot)
             sc = L.GnnScales(sc.inv_lx, sc.inv_ly, sc.inv_tmax, sc.tw, 1, float(t or 0.0),
-                             L.ptr(L.f32c(t_slot)) if t_slot is not None else None)
+                             L.ptr(t_slot) if t_slot is not None else None)
         elif pos.shape[-1] != 3:
             raise ValueError("pos must be [n, 3] (t, x, y) or [n, 2] (x, y)")
         if workspace is None:
@@ -349,12 +360,11 @@ class MP_PDE_Solver_2D(nn.Module):  # noqa: N801 - reference name
         trace.seg_n = int(seg) if seg else 0
         trace.packed = (L.ptr(self.packed_f16x3(u.device)) if self.edge_gemm == "f16x3"
                         else None)
-        L.check(L.lib().mmpde_gnn_forward_ex(
-            L.ptr(u), L.ptr(pos), n, nbr.shape[1], L.ptr(nbr), sc, ctypes.byref(emb), arr,
-            len(arr), ctypes.byref(head), L.ptr(workspace), L.ptr(out),
-            ctypes.byref(trace), L.stream(u.device)),
-            "mmpde_gnn_forward")
-        return out
+        call = L.GnnCall(L.ptr(u), L.ptr(pos), n, nbr.shape[1], L.ptr(nbr), sc,
+                         ctypes.addressof(emb), ctypes.addressof(arr), len(arr),
+                         ctypes.addressof(head), L.ptr(workspace), L.ptr(out), ctypes.addressof(trace))
+        return call, out, (u, pos, nbr, deg, t_slot, workspace, out, trace, emb, arr, head)
+
 
     # ----------------------------------------------------------------- training
     def train_forward(self, data):
@@ -373,3 +383,26 @@ class MP_PDE_Solver_2D(nn.Module):  # noqa: N801 - reference name
             h = layer.train_forward(h, u, pos_x, pos_y, variables, graph)
         diff = self.output_mlp(h[:, None]).squeeze(1)
         return self.out_scales()[None].to(h.device) * diff
+
+
+def forward_pair(model_a: "MP_PDE_Solver_2D", data_a, model_b: "MP_PDE_Solver_2D", data_b,
+                 out_a=None, out_b=None, workspace_a=None, workspace_b=None, trace_a=None,
+                 trace_b=None):
+    """model_a(data_a), model_b(data_b) -- e.g. the MM-PDE step's model(graph_uniform)
+    and model_b(graph) (train_helper_2d.py:174-185) -- through mmpde_gnn_forward_pair:
+    one embedding, node-stage and head launch for both (bitwise the two separate
+    forwards).  Both in eval mode with edge_gemm 'f16x3' and the same layer count and
+    time window; otherwise the two forwards run one after the other."""
+    paired = (not model_a.training and not model_b.training and
+              model_a.edge_gemm == "f16x3" and model_b.edge_gemm == "f16x3" and
+              len(model_a.gnn_layers) == len(model_b.gnn_layers) >= 1 and
+              model_a.time_window == model_b.time_window)
+    if not paired:
+        return (model_a(data_a, out=out_a, workspace=workspace_a, trace=trace_a),
+                model_b(data_b, out=out_b, workspace=workspace_b, trace=trace_b))
+    ca, oa, ka = model_a._call(data_a, out_a, workspace_a, trace_a)
+    cb, ob, kb = model_b._call(data_b, out_b, workspace_b, trace_b)
+    calls = (L.GnnCall * 2)(ca, cb)
+    L.check(L.lib().mmpde_gnn_forward_pair(calls, L.stream(data_a.x.device)), "mmpde_gnn_forward_pair")
+    del ka, kb
+    return oa, ob

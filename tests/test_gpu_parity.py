@@ -576,6 +576,35 @@ def test_graph_creator_api_equals_engine(dev):
     assert torch.equal(ei[0].reshape(-1, 35).int(), graph.nbr)
 
 
+@pytest.mark.parametrize("edge_gemm", ["f16x3", "f32"])
+def test_paired_gnn_forward_equals_separate(dev, edge_gemm):
+    """The rollout's paired GNN forward (MMPDERollout.pair: gnn_2d.forward_pair ->
+    mmpde_gnn_forward_pair, one embedding / node-stage / head launch over
+    model's and model_b's rows) against the two separate forwards, bit for bit,
+    over two autoregressive steps at the bench geometry (16 cylinder
+    trajectories).  In f32 mode forward_pair falls back to two forwards."""
+    from mmpde_amd.rollout import MMPDERollout
+    from mmpde_amd.synth import build_models, fields
+
+    pde, model, model_b, itp, dmm, gc = build_models("cy")
+    for m in (model, model_b, itp, dmm):
+        m.to(dev)
+    for m in (model, model_b):
+        m.edge_gemm = edge_gemm
+    B = 16
+    u0 = fields(pde.ori_grid, B, 30)[:, 0].to(dev)
+    outs = []
+    for pair in (True, False):
+        eng = MMPDERollout("cy", model, model_b, itp, dmm, gc, B, dev)
+        eng.pair = pair
+        p1 = eng.step(u0, 1).clone()
+        o = (eng.out_u.clone(), eng.out_b.clone())
+        p2 = eng.step(p1, 2).clone()
+        outs.append((p1, p2) + o)
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+
+
 # ============================================================================ full size
 def test_full_size_properties(dev):
     """BASELINE config 4 size (16 x 2521 nodes): properties the oracle is too slow

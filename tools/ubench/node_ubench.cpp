@@ -85,8 +85,15 @@ int main(int argc, char **argv) {
     nt.h_out = ho[0];
     nt.a_out = ao[0];
     nt.b_out = bo[0];
+    // the kernels take one or two problems (NodeArgs2): one here
+    auto one = [&](const NodeArgs &a, int rows) {
+        NodeArgs2 q;
+        q.a[0] = q.a[1] = a;
+        q.tiles0 = ceil_div(n, rows);
+        return q;
+    };
     auto tiled = [&](auto kern, int rows) {
-        return [&, kern, rows] { hipLaunchKernelGGL(kern, dim3(ceil_div(n, rows)), dim3(512), 0, 0, nt); };
+        return [&, kern, rows] { hipLaunchKernelGGL(kern, dim3(ceil_div(n, rows)), dim3(512), 0, 0, one(nt, rows)); };
     };
     struct V {
         const char *name;
@@ -111,7 +118,7 @@ int main(int argc, char **argv) {
         CK(hipMemset(ho[1], 0, n * H * 4));
         CK(hipMemset(ao[1], 0, n * H * 4));
         CK(hipMemset(bo[1], 0, n * H * 4));
-        hipLaunchKernelGGL((gnn_node_kernel<true, true, 2>), dim3(ceil_div(n, 32)), dim3(512), 0, 0, nt);
+        hipLaunchKernelGGL((gnn_node_kernel<true, true, 2>), dim3(ceil_div(n, 32)), dim3(512), 0, 0, one(nt, 32));
         CK(hipDeviceSynchronize());
         std::vector<float> rec0(4 * range_tiles(n)), rec1(4 * range_tiles(n));
         CK(hipMemcpy(rec0.data(), rng_rec, rec0.size() * 4, hipMemcpyDeviceToHost));
@@ -132,7 +139,7 @@ int main(int argc, char **argv) {
         printf("%s vs RB2 range records: %zu differing words\n", name, nr);
         return 0;
     };
-    if (compare("RB4", [&] { hipLaunchKernelGGL((gnn_node_kernel<true, true, 4>), dim3(ceil_div(n, 64)), dim3(512), 0, 0, nd); }))
+    if (compare("RB4", [&] { hipLaunchKernelGGL((gnn_node_kernel<true, true, 4>), dim3(ceil_div(n, 64)), dim3(512), 0, 0, one(nd, 64)); }))
         return 1;
 
     CK(hipGetLastError());
