@@ -183,6 +183,24 @@ int mmpde_linear_skinny_ws(const float *x, int64_t ldx, int64_t m, int64_t k, co
                            int64_t ldw, const float *b, int64_t n, int act, float *y, int64_t ldy,
                            float *workspace, int64_t workspace_bytes, mmpde_stream_t stream);
 
+/* A chain of nl <= 4 skinny linears in ONE launch (the res_cut MLP,
+ * interpolate.py:66-74 / :95-97; the DMM output_mlp, mesh/dmm_model.py:175-181):
+ *   x_0 = x [m, dims[0]],  x_{l+1} = act[l](x_l . w[l]^T + b[l])   (w[l]: [dims[l+1], dims[l]],
+ *   row stride ldw[l] or dims[l] when ldw is NULL; b NULL or b[l] NULL: no bias),
+ * y = x_nl [m, dims[nl]] (row stride ldy).  m <= 64.  A persistent grid walks
+ * each layer's (16 x 16 tile, K split) items and meets at a grid barrier
+ * between layers, issuing its next weights before it waits.  Per item the
+ * arithmetic is mmpde_linear_skinny_ws's (exact fp32 MFMA products, fixed
+ * summation order, a K split that depends on (n, k) only).  workspace: at
+ * least mmpde_linear_chain_workspace_bytes(m, nl, dims) bytes, 4-B aligned,
+ * ZEROED before its first use and reused (each call leaves its first 4096
+ * words at zero again; the intermediate activations live after them). */
+int64_t mmpde_linear_chain_workspace_bytes(int64_t m, int nl, const int64_t *dims);
+int mmpde_linear_chain_ws(const float *x, int64_t ldx, int64_t m, int nl, const int64_t *dims,
+                          const float *const *w, const int64_t *ldw, const float *const *b,
+                          const int *act, float *y, int64_t ldy, void *workspace,
+                          int64_t workspace_bytes, mmpde_stream_t stream);
+
 /* out[b] = mean_i (pred[b, i] - labels[b, i])^2 per trajectory b (n_per values
  * each): the loss of mmpde.py:33-36 (MSELoss) kept per trajectory for the
  * sharded teacher-forced evaluation (train_helper_2d.py:184-185,193-198).
@@ -310,6 +328,17 @@ int mmpde_gnn_edge_backward(const float *a, const float *b, const int32_t *nbr, 
                             int64_t n, int k, const float *msg2_w, const float *msg2_b,
                             const float *grad_mean, float *grad_a, float *grad_edge,
                             float *partials, float *grad_w2, float *grad_b2, mmpde_stream_t stream);
+/* The same with the GEMM arithmetic chosen by edge_gemm: MMPDE_EDGE_GEMM_F32
+ * (the call above) or MMPDE_EDGE_GEMM_F16X3 (the z2, gm1 and dW2 GEMMs in the
+ * fp16x3 split with fp32 accumulation, as the forward's f16x3 edge stage:
+ * relu(z1) and gz2 scaled by powers of two from max|a| + max|b| and max|g|,
+ * W2 per column; k <= 64, else the F32 kernel).  Same outputs, same partials
+ * scratch, deterministic. */
+int mmpde_gnn_edge_backward_ex(const float *a, const float *b, const int32_t *nbr, const int32_t *deg,
+                               int64_t n, int k, const float *msg2_w, const float *msg2_b,
+                               const float *grad_mean, float *grad_a, float *grad_edge,
+                               float *partials, float *grad_w2, float *grad_b2, int edge_gemm,
+                               mmpde_stream_t stream);
 /* grad_b[j] = sum over q in [rev_off[j], rev_off[j+1]) of grad_edge[rev_edge[q]]
  * (rev_*: the reverse adjacency, slot ids i*k+e grouped by source j, in the
  * order given: deterministic). */

@@ -162,6 +162,261 @@ __global__ __launch_bounds__(kSkW * 64) void linear_skinny_kernel(const float *_
     }
 }
 
+// ---------------------------------------------------------------------------
+// A chain of skinny linears in ONE launch (res_cut's 4-layer MLP,
+// interpolate.py:66-74; the DMM output_mlp + P = Wb . branch,
+// mesh/dmm_model.py:175-181): a persistent grid walks each layer's work items
+// (16 x 16 output tile x K split, the linear_skinny_kernel item above, same
+// per-item arithmetic), then meets at a grid barrier before the next layer.
+// What the fusion buys is the barrier's shadow: before waiting, every
+// workgroup issues the weight loads of its first item of the next layer
+// (weights do not depend on the activations), so a layer's weight stream
+// starts while the previous layer drains.  Activations written inside the
+// launch go through write-through agent-scope stores and are read back with
+// agent-scope loads (no release / acquire fences: the XCD L2s are not
+// coherent, the sc1 path is); every buffer is written once per launch.
+// The barrier counter and exit counter reset themselves: the last workgroup to
+// leave zeroes both, so a zeroed workspace serves every later launch.
+constexpr int kChainMax = 4;           // layers per launch
+constexpr int kChainTickets = 1008;    // ticket words per layer (output tiles)
+constexpr int kChainCtl = 64;          // control words before the tickets (4096 words in all)
+
+struct ChainLayer {
+    const float *w, *b;
+    float *y, *part;   // output (row stride ldy); split-K partials (z > 1)
+    int64_t ldw, ldy, n, k;
+    int act, z, nchz, ctiles, items;
+};
+
+struct ChainArgs {
+    ChainLayer L[kChainMax];
+    const float *x;
+    int64_t ldx, m;
+    int nl, rtiles;
+    unsigned *ctl;     // [0] barrier arrivals, [1] exits, [2] sticky barrier timeout; tickets from kChainCtl
+};
+
+__device__ __forceinline__ float ld_agent(const float *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(float *p, float v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// item -> (column tile, row tile, split): the split is the slowest index
+struct ChainItem {
+    int64_t col0, row0;
+    int zz, c0, nch;
+};
+__device__ __forceinline__ ChainItem chain_item(const ChainLayer &Ly, int rtiles, int it, int C) {
+    ChainItem c;
+    const int T = Ly.ctiles * rtiles;
+    c.zz = it / T;
+    const int t = it - c.zz * T;
+    c.col0 = (int64_t)(t % Ly.ctiles) * 16;
+    c.row0 = (int64_t)(t / Ly.ctiles) * 16;
+    c.c0 = c.zz * Ly.nchz;
+    c.nch = min(((int)Ly.k + C - 1) / C - c.c0, Ly.nchz);
+    return c;
+}
+
+template <int kSkW>
+__device__ __forceinline__ void chain_loadw(const ChainLayer &Ly, int64_t col0, int kc, float (&lw)[16]) {
+    const int kk = kc + (int)threadIdx.x;
+    const bool ok = kk < Ly.k;
+    const int o = ok ? kk : 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const float a = Ly.w[min(col0 + i, Ly.n - 1) * Ly.ldw + o];
+        lw[i] = ok ? a : 0.0f;
+    }
+}
+
+// one layer's items of this workgroup; lw may already hold the first chunk of
+// the first item's weights (wpre)
+template <int kSkW>
+__device__ __forceinline__ void chain_layer(const ChainArgs &a, const ChainLayer &Ly, const float *x,
+                                            int64_t ldx, bool coh, bool last, unsigned *tickets,
+                                            float (&lw)[16], bool wpre, float *sw, float *sx) {
+    constexpr int C = 64 * kSkW, LD = C + 4;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int r = lane & 15, g = lane >> 4;
+    const int K = (int)Ly.k;
+    const int64_t m = a.m, n = Ly.n;
+    float lx[16];
+    auto loadx = [&](int64_t row0, int kc) {
+        const int kk = kc + tid;
+        const bool ok = kk < K;
+        const int o = ok ? kk : 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const float *p = x + min(row0 + i, m - 1) * ldx + o;
+            const float c = coh ? ld_agent(p) : *p;
+            lx[i] = ok ? c : 0.0f;
+        }
+    };
+    for (int it = blockIdx.x; it < Ly.items; it += gridDim.x) {
+        const ChainItem ci = chain_item(Ly, a.rtiles, it, C);
+        if (!wpre) chain_loadw<kSkW>(Ly, ci.col0, ci.c0 * C, lw);
+        wpre = false;
+        loadx(ci.row0, ci.c0 * C);
+        f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+        for (int c = 0; c < ci.nch; ++c) {
+            if (c) __syncthreads();  // chunk c - 1 consumed
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                sw[i * LD + tid] = lw[i];
+                sx[i * LD + tid] = lx[i];
+            }
+            __syncthreads();
+            if (c + 1 < ci.nch) {
+                chain_loadw<kSkW>(Ly, ci.col0, (ci.c0 + c + 1) * C, lw);
+                loadx(ci.row0, (ci.c0 + c + 1) * C);
+            }
+            const float *aw = sw + r * LD + 64 * wave + 4 * g;
+            const float *ax = sx + r * LD + 64 * wave + 4 * g;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 wv = *(const float4 *)(aw + 16 * q);
+                const float4 xv = *(const float4 *)(ax + 16 * q);
+                acc = mfma16(xv.x, wv.x, acc);
+                acc = mfma16(xv.y, wv.y, acc);
+                acc = mfma16(xv.z, wv.z, acc);
+                acc = mfma16(xv.w, wv.w, acc);
+            }
+        }
+        __syncthreads();
+        f32x4 *wpart = (f32x4 *)sw;  // [wave][lane]
+        wpart[wave * 64 + lane] = acc;
+        __syncthreads();
+        if (wave == 0) {
+            f32x4 s = wpart[lane];
+#pragma unroll
+            for (int v = 1; v < kSkW; ++v) s += wpart[v * 64 + lane];
+            const int64_t col = ci.col0 + r;
+            bool write = true;
+            if (Ly.z > 1) {
+                // split-K hand-off as in linear_skinny_kernel (sc1 partials, a
+                // ticket per tile, the last slice adds the slices in z order)
+                float *pz = Ly.part + (int64_t)ci.zz * m * n;
+                if (col < n) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int64_t row = ci.row0 + 4 * g + q;
+                        if (row < m) st_agent(pz + row * n + col, s[q]);
+                    }
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                const int T = Ly.ctiles * a.rtiles;
+                unsigned *tk = tickets + (it - ci.zz * T);
+                unsigned ticket = 0u;
+                if (lane == 0) ticket = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ticket = __builtin_amdgcn_readfirstlane(ticket);
+                write = ticket == (unsigned)(Ly.z - 1);
+                if (write) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    const int64_t cc = min(col, n - 1);
+                    float v[kSkMaxZ][4];
+#pragma unroll
+                    for (int zz = 0; zz < kSkMaxZ; ++zz) {
+                        if (zz < Ly.z) {
+                            const float *pq = Ly.part + (int64_t)zz * m * n + cc;
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) v[zz][q] = ld_agent(pq + min(ci.row0 + 4 * g + q, m - 1) * n);
+                        }
+                    }
+                    f32x4 t = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+                    for (int zz = 0; zz < kSkMaxZ; ++zz) {
+                        if (zz < Ly.z) {
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) t[q] += v[zz][q];
+                        }
+                    }
+                    if (lane == 0) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    s = t;
+                }
+            }
+            if (write && col < n) {
+                const float bb = Ly.b ? Ly.b[col] : 0.0f;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int64_t row = ci.row0 + 4 * g + q;
+                    if (row < m) {
+                        const float v = act_apply(s[q] + bb, Ly.act);
+                        if (last) Ly.y[row * Ly.ldy + col] = v;
+                        else st_agent(Ly.y + row * Ly.ldy + col, v);
+                    }
+                }
+            }
+        }
+        __syncthreads();  // wpart (sw) read before the next item's chunk store
+    }
+}
+
+template <int kSkW>
+__global__ __launch_bounds__(kSkW * 64, 4) void linear_chain_kernel(ChainArgs a) {
+    constexpr int C = 64 * kSkW, LD = C + 4;
+    __shared__ float sw[16 * LD], sx[16 * LD];
+    // control words through a VGPR base: vector-memory atomics only
+    int vzero;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(vzero));
+    unsigned *ctl = a.ctl + vzero;
+    float lw[16];
+    bool wpre = false;
+    const unsigned G = gridDim.x;
+#pragma unroll
+    for (int l = 0; l < kChainMax; ++l) {
+        if (l >= a.nl) break;
+        const bool last = l + 1 == a.nl;
+        chain_layer<kSkW>(a, a.L[l], l ? a.L[l - 1].y : a.x, l ? a.L[l - 1].ldy : a.ldx, l > 0, last,
+                          ctl + kChainCtl + l * kChainTickets, lw, wpre, sw, sx);
+        wpre = false;
+        if (last) break;
+        // arrive (this workgroup's stores are all wave 0's, drained in
+        // chain_layer before its tickets or here), then prefetch the next
+        // layer's first weights, then wait for every workgroup
+        if (threadIdx.x < 64) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (threadIdx.x == 0) __hip_atomic_fetch_add(ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        const ChainLayer &nx = a.L[l + 1];
+        if ((int)blockIdx.x < nx.items) {
+            const ChainItem ci = chain_item(nx, a.rtiles, blockIdx.x, C);
+            chain_loadw<kSkW>(nx, ci.col0, ci.c0 * C, lw);
+            wpre = true;
+        }
+        if (threadIdx.x == 0) {
+            const unsigned target = (unsigned)(l + 1) * G;
+            // bounded spin (every workgroup of the grid is resident: G <= the
+            // occupancy-derived capacity; 100 ms of the 100 MHz real-time
+            // clock), so a fault cannot hang the queue: a timeout sets the
+            // sticky word ctl[2]
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            while (__hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                __builtin_amdgcn_s_sleep(2);
+                if (__builtin_amdgcn_s_memrealtime() - t0 > 10000000ull) {
+                    __hip_atomic_store(ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+            }
+            // the consumer side of the hand-off: one agent-scope acquire
+            // after the poll, waited before the workgroup barrier (the next
+            // layer's activation loads are sc1 loads as well)
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const unsigned e = __hip_atomic_fetch_add(ctl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (e == G - 1) {  // every workgroup is past every barrier
+            __hip_atomic_store(ctl, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(ctl + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 // K splits of a skinny linear: enough workgroups for ~4 per CU over the
 // output column tiles, chunks of 64 kSkW k each, at most 16 splits.  The split
 // (hence every output row's summation order) depends on n and k only, not on
@@ -268,7 +523,7 @@ __global__ __launch_bounds__(256) void traj_mse_kernel(const float *__restrict__
 
 }  // namespace
 
-extern "C" int mmpde_version(void) { return 11400; }
+extern "C" int mmpde_version(void) { return 11500; }
 
 extern "C" int mmpde_traj_mse(const float *pred, const float *labels, int64_t batches, int64_t n_per,
                               float *out, mmpde_stream_t stream) {
@@ -327,6 +582,141 @@ extern "C" int mmpde_linear_skinny_ws(const float *x, int64_t ldx, int64_t m, in
                        n, act, y, ldy, nchz, part, tickets);
     MMPDE_RET_LAUNCH();
     return MMPDE_OK;
+}
+
+// ---- linear chains (linear_chain_kernel) --------------------------------
+namespace mmpde_detail {
+// K split of chain layer (n, k): about two workgroups per CU over the output
+// column tiles; a function of (n, k, CUs) only, so a row's summation order does
+// not depend on the rows launched beside it.
+static void chain_split(int64_t n, int64_t k, int cus, int &z, int &nchz) {
+    const int64_t ctiles = (n + 15) / 16, chunks = (k + 64 * kSkW - 1) / (64 * kSkW);
+    int64_t zz = (2 * (int64_t)cus) / ctiles;
+    zz = zz < chunks ? zz : chunks;
+    zz = zz < kSkMaxZ ? zz : kSkMaxZ;
+    zz = zz > 1 ? zz : 1;
+    nchz = (int)((chunks + zz - 1) / zz);
+    z = (int)((chunks + nchz - 1) / nchz);  // no empty split
+}
+
+// every region of the chain workspace on 128-B lines of its own (a line
+// shared by two regions could be cached by one XCD's L2 before the other
+// region is written)
+static int64_t up32(int64_t v) { return (v + 31) & ~int64_t(31); }
+
+// workspace floats of a chain, and (args non-null) its layout in ws
+static int64_t chain_plan(const float *x, int64_t ldx, int64_t m, int nl, const ChainSpec *sp, int cus,
+                          float *ws, ChainArgs *a) {
+    int64_t off = kChainCtl + kChainMax * kChainTickets;
+    if (a) {
+        *a = ChainArgs{};
+        a->x = x;
+        a->ldx = ldx;
+        a->m = m;
+        a->nl = nl;
+        a->rtiles = (int)((m + 15) / 16);
+        a->ctl = (unsigned *)ws;
+    }
+    for (int l = 0; l < nl; ++l) {
+        int z, nchz;
+        chain_split(sp[l].n, sp[l].k, cus, z, nchz);
+        const int64_t pf = z > 1 ? up32((int64_t)z * m * sp[l].n) : 0;
+        const bool own_y = sp[l].y == nullptr;
+        if (a) {
+            ChainLayer &L = a->L[l];
+            L.w = sp[l].w;
+            L.b = sp[l].b;
+            L.ldw = sp[l].ldw;
+            L.n = sp[l].n;
+            L.k = sp[l].k;
+            L.act = sp[l].act;
+            L.z = z;
+            L.nchz = nchz;
+            L.ctiles = (int)((sp[l].n + 15) / 16);
+            L.items = L.ctiles * a->rtiles * z;
+            L.part = z > 1 ? ws + off : nullptr;
+            L.y = own_y ? ws + off + pf : sp[l].y;
+            L.ldy = own_y ? sp[l].n : sp[l].ldy;
+        }
+        off += pf + (own_y ? up32(m * sp[l].n) : 0);
+    }
+    return off;
+}
+
+bool chain_ok(int64_t m, int nl, const ChainSpec *sp) {
+    if (m <= 0 || m > 64 || nl < 1 || nl > kChainMax) return false;
+    for (int l = 0; l < nl; ++l) {
+        if (!sp[l].w || sp[l].n <= 0 || sp[l].k <= 0 || sp[l].ldw < sp[l].k || sp[l].act < 0 || sp[l].act > 2)
+            return false;
+        if (l && sp[l].k != sp[l - 1].n) return false;
+        if (sp[l].y && sp[l].ldy < sp[l].n) return false;
+        // an intermediate handed to the next layer inside the launch: lines of
+        // its own (128-B aligned, whole lines)
+        if (sp[l].y && l + 1 < nl && ((((uintptr_t)sp[l].y) & 127u) || (m * sp[l].ldy) % 32)) return false;
+        if (((sp[l].n + 15) / 16) * ((m + 15) / 16) > kChainTickets) return false;
+    }
+    return sp[nl - 1].y != nullptr;
+}
+
+int64_t chain_ws_bytes(int64_t m, int nl, const ChainSpec *sp) {
+    return chain_plan(nullptr, 0, m, nl, sp, skinny_cus(), nullptr, nullptr) * (int64_t)sizeof(float);
+}
+
+int linear_chain(const float *x, int64_t ldx, int64_t m, int nl, const ChainSpec *sp, void *workspace,
+                 int64_t workspace_bytes, hipStream_t st) {
+    if (!x || !workspace || ((uintptr_t)workspace & 127u) || !chain_ok(m, nl, sp) || ldx < sp[0].k)
+        return MMPDE_ERR_INVALID_ARG;
+    const int cus = skinny_cus();
+    ChainArgs a;
+    const int64_t need = chain_plan(x, ldx, m, nl, sp, cus, (float *)workspace, &a) * (int64_t)sizeof(float);
+    if (workspace_bytes < need) return MMPDE_ERR_INVALID_ARG;
+    // grid: at most two resident workgroups per CU (every workgroup must be
+    // resident for the grid barrier), no more than the largest layer's items
+    static int occ = -1;
+    if (occ < 0) {
+        int o = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, (const void *)linear_chain_kernel<kSkW>, kSkW * 64,
+                                                         0) != hipSuccess)
+            o = 1;
+        occ = o < 1 ? 1 : (o > 2 ? 2 : o);
+    }
+    int items = 1;
+    for (int l = 0; l < nl; ++l) items = a.L[l].items > items ? a.L[l].items : items;
+    const int grid = items < occ * cus ? items : occ * cus;
+    hipLaunchKernelGGL(linear_chain_kernel<kSkW>, dim3((unsigned)grid), dim3(kSkW * 64), 0, st, a);
+    MMPDE_RET_LAUNCH();
+    return MMPDE_OK;
+}
+}  // namespace mmpde_detail
+
+static int chain_specs(int64_t m, int nl, const int64_t *dims, const float *const *w, const int64_t *ldw,
+                       const float *const *b, const int *act, float *y, int64_t ldy,
+                       mmpde_detail::ChainSpec *sp) {
+    (void)m;
+    if (!dims || !w || !act || nl < 1 || nl > kChainMax) return MMPDE_ERR_INVALID_ARG;
+    for (int l = 0; l < nl; ++l) {
+        sp[l] = mmpde_detail::ChainSpec{w[l], ldw ? ldw[l] : dims[l], b ? b[l] : nullptr, dims[l + 1], dims[l],
+                                        act[l], l + 1 == nl ? y : nullptr, l + 1 == nl ? ldy : 0};
+    }
+    return MMPDE_OK;
+}
+
+extern "C" int64_t mmpde_linear_chain_workspace_bytes(int64_t m, int nl, const int64_t *dims) {
+    if (!dims || nl < 1 || nl > kChainMax || m <= 0) return 0;
+    mmpde_detail::ChainSpec sp[kChainMax];
+    for (int l = 0; l < nl; ++l) sp[l] = mmpde_detail::ChainSpec{nullptr, dims[l], nullptr, dims[l + 1], dims[l], 0,
+                                                               nullptr, 0};
+    sp[nl - 1].y = (float *)16;  // the caller's output: no workspace
+    return mmpde_detail::chain_ws_bytes(m, nl, sp);
+}
+
+extern "C" int mmpde_linear_chain_ws(const float *x, int64_t ldx, int64_t m, int nl, const int64_t *dims,
+                                     const float *const *w, const int64_t *ldw, const float *const *b,
+                                     const int *act, float *y, int64_t ldy, void *workspace,
+                                     int64_t workspace_bytes, mmpde_stream_t stream) {
+    mmpde_detail::ChainSpec sp[kChainMax];
+    MMPDE_REQUIRE(y && chain_specs(m, nl, dims, w, ldw, b, act, y, ldy, sp) == MMPDE_OK);
+    return mmpde_detail::linear_chain(x, ldx, m, nl, sp, workspace, workspace_bytes, as_stream(stream));
 }
 
 extern "C" int mmpde_linear_skinny(const float *x, int64_t ldx, int64_t m, int64_t k,

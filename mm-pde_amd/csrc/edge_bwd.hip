@@ -21,6 +21,9 @@
 // neighbour slot: z2, gm1 and the dW2 outer products); no atomics, so the
 // gradients are deterministic.
 #include "common.hpp"
+#include "f16x3.hpp"
+
+#include <algorithm>
 
 namespace {
 
@@ -197,6 +200,254 @@ __global__ __launch_bounds__(256, 1) void edge_bwd_kernel(EdgeBwdArgs p) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// The same backward with the three GEMMs in the fp16x3 split (every fp32
+// operand scaled by a power of two and split into fp16 hi + lo; products
+// hi.hi + hi.lo + lo.hi on v_mfma_f32_16x16x32_f16, fp32 accumulation: the
+// forward's MMPDE_EDGE_GEMM_F16X3 arithmetic).  Scales are uniform per launch:
+// relu(z1) by split_scale(max|a| + max|b|), gz2 by split_scale(max|g|) (one
+// pre-pass reduction), W2 per output column (packed images, as the forward).
+// One 512-thread workgroup per CU, persistent over 32-target tiles; a slot is
+// one neighbour e of the tile's 32 targets (32 edges = the K of the dW2 GEMM):
+//   P1  z1 = a + b_src (b rows prefetched one slot ahead into registers),
+//       relu(z1) split -> LDS row-major (A of z2) and column-major (B of dW2),
+//       the z1 > 0 bits
+//   P2  z2 = relu(z1) W2^T (wave w: output columns 16w..), gz2 = g/deg
+//       [z2 + b2 > 0][e < deg] split -> LDS row-major (A of gm1) and
+//       column-major (A of dW2); db2 in fp32
+//   P3  gm1 = gz2 W2 (wave w: columns 16w..), gz1 = gm1 [z1 > 0] -> grad_edge
+//       and the dL/da sums; dW2 += gz2^T relu(z1) (wave w: rows 16w..)
+// Deterministic: fixed orders, per-workgroup partials, no atomics in the sums.
+// ---------------------------------------------------------------------------
+constexpr int FT = 32;          // targets per tile
+constexpr int FAW = BH + 4;     // fp32 row stride of the a / g tiles
+constexpr int FAS = BH + 8;     // half row stride, row-major images (272 B: 16-B row skew)
+constexpr int FCS = FT;         // half row stride, column-major images [128][32 edges]
+constexpr int FKMAX = 64;       // neighbour slots per target this kernel takes
+
+struct EdgeBwdF16Args {
+    const float *a, *b;
+    const int32_t *nbr, *deg;
+    int64_t n;
+    int k, ntiles;
+    const char *img1, *img2;  // B images: W2 (z2 = relu(z1) W2^T), W2^T (gm1 = gz2 W2)
+    const float *b2, *gmean;
+    const unsigned *mx;       // max|a|, max|b|, max|g| (float bits)
+    float *ga, *gz1, *pw2, *pb2;
+};
+
+__device__ __forceinline__ void split1(float x, _Float16 &h, _Float16 &l) {
+    h = (_Float16)x;
+    l = (_Float16)(x - (float)h);
+}
+
+__global__ __launch_bounds__(512, 2) void edge_bwd_f16_kernel(EdgeBwdF16Args p) {
+    __shared__ float at[FT * FAW];             // a rows of the tile
+    __shared__ float gms[FT * FAW];            // g / deg rows (0 for rows past n)
+    __shared__ _Float16 za[2][FT * FAS];       // relu(z1) sz: hi, lo, [edge][kk]
+    __shared__ _Float16 zb[2][BH * FCS];       // the same, [kk][edge]
+    __shared__ _Float16 gr[2][FT * FAS];       // gz2 sg, [edge][c]
+    __shared__ _Float16 gt[2][BH * FCS];       // the same, [c][edge]
+    __shared__ uint8_t zm[BH * (FT / 8)];      // z1 > 0, [kk][edge / 8] bits
+    __shared__ int nb[FT * FKMAX];             // the tile's neighbour rows (clamped)
+    __shared__ int dg[FT];                     // degrees (0 past n)
+    const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int r = lane & 15, g = lane >> 4;
+    const int64_t nmax = p.n - 1;
+    const int k = p.k;
+    const float sz = split_scale(__uint_as_float(p.mx[0]) + __uint_as_float(p.mx[1]));
+    const float sg = split_scale(__uint_as_float(p.mx[2]));
+    // B operands of this wave's column tile, for the whole launch
+    half8 w1h[4], w1l[4], w2h[4], w2l[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        w1h[s] = bfrag(p.img1, 4, wave, s, 0, lane);
+        w1l[s] = bfrag(p.img1, 4, wave, s, 1, lane);
+        w2h[s] = bfrag(p.img2, 4, wave, s, 0, lane);
+        w2l[s] = bfrag(p.img2, 4, wave, s, 1, lane);
+    }
+    const int col = 16 * wave + r;  // output column of z2 (c) and of gm1 (kk)
+    const float un1 = pow2_inv(sz) * pow2_inv(((const float *)(p.img1 + 65536))[col]);
+    const float un2 = pow2_inv(sg) * pow2_inv(((const float *)(p.img2 + 65536))[col]);
+    const float bias = p.b2[col];
+    f32x4 dw[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dw[j] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+    float db = 0.0f;
+    // P1 role: column kk1 of edges 8 eg .. 8 eg + 7
+    const int kk1 = tid & (BH - 1), eg = tid >> 7;
+    for (int tile = blockIdx.x; tile < p.ntiles; tile += gridDim.x) {
+        const int64_t row0 = (int64_t)tile * FT;
+        __syncthreads();  // the previous tile's readers are done
+        for (int i = tid; i < FT * BH / 4; i += 512) {
+            const int rr = i >> 5, c4 = i & 31;
+            const int64_t row = min(row0 + rr, nmax);
+            const bool live = row0 + rr < p.n;
+            const int d = p.deg ? p.deg[row] : k;
+            const float inv = live ? 1.0f / (float)max(d, 1) : 0.0f;
+            const float4 av = ((const float4 *)(p.a + row * BH))[c4];
+            const float4 gv = ((const float4 *)(p.gmean + row * BH))[c4];
+            *(float4 *)&at[rr * FAW + 4 * c4] = av;
+            *(float4 *)&gms[rr * FAW + 4 * c4] = make_float4(gv.x * inv, gv.y * inv, gv.z * inv, gv.w * inv);
+        }
+        for (int i = tid; i < FT * k; i += 512) {
+            const int rr = i / k, e = i - rr * k;
+            const int s = p.nbr[min(row0 + rr, nmax) * k + e];
+            nb[rr * FKMAX + e] = (s < 0 || s > nmax) ? 0 : s;  // padded / malformed: masked by e < deg
+        }
+        if (tid < FT) dg[tid] = row0 + tid < p.n ? (p.deg ? p.deg[row0 + tid] : k) : 0;
+        __syncthreads();
+        float bv[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) bv[t] = p.b[(int64_t)nb[(8 * eg + t) * FKMAX] * BH + kk1];
+        f32x4 gacc[2] = {(f32x4){0.0f, 0.0f, 0.0f, 0.0f}, (f32x4){0.0f, 0.0f, 0.0f, 0.0f}};
+        for (int e = 0; e < k; ++e) {
+            // ---- P1
+            {
+                half8 hi, lo;
+                unsigned bits = 0;
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    const int ed = 8 * eg + t;
+                    const float z = at[ed * FAW + kk1] + bv[t];
+                    bits |= (z > 0.0f ? 1u : 0u) << t;
+                    _Float16 h, l;
+                    split1(fmaxf(z, 0.0f) * sz, h, l);
+                    hi[t] = h;
+                    lo[t] = l;
+                    za[0][ed * FAS + kk1] = h;
+                    za[1][ed * FAS + kk1] = l;
+                }
+                *(half8 *)&zb[0][kk1 * FCS + 8 * eg] = hi;
+                *(half8 *)&zb[1][kk1 * FCS + 8 * eg] = lo;
+                zm[kk1 * 4 + eg] = (uint8_t)bits;
+                if (e + 1 < k) {  // next slot's b values, in flight during P2 / P3
+#pragma unroll
+                    for (int t = 0; t < 8; ++t)
+                        bv[t] = p.b[(int64_t)nb[(8 * eg + t) * FKMAX + e + 1] * BH + kk1];
+                }
+            }
+            __syncthreads();
+            // ---- P2: z2 and gz2 (column c = col)
+            {
+                f32x4 acc[2] = {(f32x4){0.0f, 0.0f, 0.0f, 0.0f}, (f32x4){0.0f, 0.0f, 0.0f, 0.0f}};
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+#pragma unroll
+                    for (int rb = 0; rb < 2; ++rb) {
+                        const half8 ah = *(const half8 *)&za[0][(16 * rb + r) * FAS + 32 * s + 8 * g];
+                        const half8 al = *(const half8 *)&za[1][(16 * rb + r) * FAS + 32 * s + 8 * g];
+                        acc[rb] = mfma_f16(ah, w1h[s], acc[rb]);
+                        acc[rb] = mfma_f16(ah, w1l[s], acc[rb]);
+                        acc[rb] = mfma_f16(al, w1h[s], acc[rb]);
+                    }
+                }
+#pragma unroll
+                for (int rb = 0; rb < 2; ++rb) {
+                    _Float16 hv[4], lv[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int rr = 16 * rb + 4 * g + q;
+                        const bool on = e < dg[rr] && acc[rb][q] * un1 + bias > 0.0f;
+                        const float v = on ? gms[rr * FAW + col] : 0.0f;
+                        db += v;
+                        split1(v * sg, hv[q], lv[q]);
+                        gr[0][rr * FAS + col] = hv[q];
+                        gr[1][rr * FAS + col] = lv[q];
+                    }
+                    typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+                    *(half4 *)&gt[0][col * FCS + 16 * rb + 4 * g] = (half4){hv[0], hv[1], hv[2], hv[3]};
+                    *(half4 *)&gt[1][col * FCS + 16 * rb + 4 * g] = (half4){lv[0], lv[1], lv[2], lv[3]};
+                }
+            }
+            __syncthreads();
+            // ---- P3: gm1 -> gz1 (column kk = col); dW2 rows 16 wave ..
+            {
+                f32x4 acc[2] = {(f32x4){0.0f, 0.0f, 0.0f, 0.0f}, (f32x4){0.0f, 0.0f, 0.0f, 0.0f}};
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+#pragma unroll
+                    for (int rb = 0; rb < 2; ++rb) {
+                        const half8 ah = *(const half8 *)&gr[0][(16 * rb + r) * FAS + 32 * s + 8 * g];
+                        const half8 al = *(const half8 *)&gr[1][(16 * rb + r) * FAS + 32 * s + 8 * g];
+                        acc[rb] = mfma_f16(ah, w2h[s], acc[rb]);
+                        acc[rb] = mfma_f16(ah, w2l[s], acc[rb]);
+                        acc[rb] = mfma_f16(al, w2h[s], acc[rb]);
+                    }
+                }
+                const half8 gh = *(const half8 *)&gt[0][col * FCS + 8 * g];
+                const half8 gl = *(const half8 *)&gt[1][col * FCS + 8 * g];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const half8 bh = *(const half8 *)&zb[0][(16 * j + r) * FCS + 8 * g];
+                    const half8 bl = *(const half8 *)&zb[1][(16 * j + r) * FCS + 8 * g];
+                    dw[j] = mfma_f16(gh, bh, dw[j]);
+                    dw[j] = mfma_f16(gh, bl, dw[j]);
+                    dw[j] = mfma_f16(gl, bh, dw[j]);
+                }
+#pragma unroll
+                for (int rb = 0; rb < 2; ++rb) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int rr = 16 * rb + 4 * g + q;
+                        const bool pos = (zm[col * 4 + (rr >> 3)] >> (rr & 7)) & 1u;
+                        const float v = pos ? acc[rb][q] * un2 : 0.0f;
+                        gacc[rb][q] += v;
+                        if (row0 + rr < p.n) p.gz1[((row0 + rr) * k + e) * BH + col] = v;
+                    }
+                }
+            }
+            __syncthreads();  // P1 of the next slot rewrites za / zb / zm; P2 gr / gt
+        }
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int64_t row = row0 + 16 * rb + 4 * g + q;
+                if (row < p.n) p.ga[row * BH + col] = gacc[rb][q];
+            }
+        }
+    }
+    // partials: dW2[c = 16 wave + 4 g + q][kk = 16 j + r], db2[col]
+    const float und = pow2_inv(sg) * pow2_inv(sz);
+    float *pw = p.pw2 + (int64_t)blockIdx.x * BH * BH;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) pw[(16 * wave + 4 * g + q) * BH + 16 * j + r] = dw[j][q] * und;
+    const float v1 = __shfl(db, r + 16, 64), v2 = __shfl(db, r + 32, 64), v3 = __shfl(db, r + 48, 64);
+    if (g == 0) p.pb2[(int64_t)blockIdx.x * BH + col] = ((db + v1) + v2) + v3;
+}
+
+// max|a|, max|b|, max|g| over [n, 128] rows into mx[0..2] (float bits, zeroed
+// before): the fp16x3 backward's split scales.
+__global__ __launch_bounds__(256) void maxabs3_kernel(const float *__restrict__ a, const float *__restrict__ b,
+                                                      const float *__restrict__ gm, int64_t n4,
+                                                      unsigned *__restrict__ mx) {
+    float m[3] = {0.0f, 0.0f, 0.0f};
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+        const float4 x = ((const float4 *)a)[i], y = ((const float4 *)b)[i], z = ((const float4 *)gm)[i];
+        m[0] = fmaxf(m[0], fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
+        m[1] = fmaxf(m[1], fmaxf(fmaxf(fabsf(y.x), fabsf(y.y)), fmaxf(fabsf(y.z), fabsf(y.w))));
+        m[2] = fmaxf(m[2], fmaxf(fmaxf(fabsf(z.x), fabsf(z.y)), fmaxf(fabsf(z.z), fabsf(z.w))));
+    }
+    int vzero;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(vzero));
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        const float w = wave_max(m[q]);
+        // the address through a VGPR: a vector-memory atomic (non-negative
+        // floats order like their bit patterns)
+        if ((threadIdx.x & 63) == 0)
+            __hip_atomic_fetch_max(mx + q + vzero, __float_as_uint(w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+__global__ __launch_bounds__(256) void transpose128_kernel(const float *__restrict__ w, float *__restrict__ wt) {
+    const int i = blockIdx.x * 256 + threadIdx.x;  // 128 x 128
+    wt[(i & 127) * BH + (i >> 7)] = w[i];
+}
+
 // out[j] = sum_{p in [off[j], off[j+1])} rows[edge[p]]: one wave per source
 // row j, two columns per lane, in list order.
 __global__ __launch_bounds__(256) void edge_source_sum_kernel(const float *__restrict__ rows,
@@ -241,13 +492,18 @@ __global__ __launch_bounds__(256) void partial_sum_kernel(const float *__restric
 
 }  // namespace
 
+constexpr int64_t kBwdImg = (BH * BH * 4 + BH * 4) / 4;     // floats of one packed W2 image
+constexpr int64_t kBwdExtra = 2 * kBwdImg + BH * BH + 64;     // images, W2^T, maxima
+
 extern "C" int64_t mmpde_gnn_edge_backward_partials(int *grid) {
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         cus = 256;
     if (grid) *grid = cus > 0 ? cus : 256;
-    return (int64_t)(cus > 0 ? cus : 256) * (BH * BH + BH);
+    // per-workgroup dW2 / db2 partials, then (fp16x3 mode) the two W2 images,
+    // W2^T and the three maxima
+    return (int64_t)(cus > 0 ? cus : 256) * (BH * BH + BH) + kBwdExtra;
 }
 
 extern "C" int mmpde_gnn_edge_backward(const float *a, const float *b, const int32_t *nbr, const int32_t *deg,
@@ -267,6 +523,60 @@ extern "C" int mmpde_gnn_edge_backward(const float *a, const float *b, const int
     EdgeBwdArgs p{a, b, nbr, deg, n, k, (int)ntiles, msg2_w, msg2_b, grad_mean, grad_a, grad_edge, pw2, pb2};
     hipStream_t st = as_stream(stream);
     hipLaunchKernelGGL(edge_bwd_kernel, dim3(grid), dim3(256), 0, st, p);
+    MMPDE_RET_LAUNCH();
+    hipLaunchKernelGGL(partial_sum_kernel, dim3(ceil_div(BH * BH, 256)), dim3(256), 0, st, pw2, grid,
+                       (int64_t)BH * BH, grad_w2);
+    hipLaunchKernelGGL(partial_sum_kernel, dim3(1), dim3(256), 0, st, pb2, grid, (int64_t)BH, grad_b2);
+    MMPDE_RET_LAUNCH();
+    return MMPDE_OK;
+}
+
+extern "C" int mmpde_gnn_edge_backward_ex(const float *a, const float *b, const int32_t *nbr, const int32_t *deg,
+                                          int64_t n, int k, const float *msg2_w, const float *msg2_b,
+                                          const float *grad_mean, float *grad_a, float *grad_edge,
+                                          float *partials, float *grad_w2, float *grad_b2, int edge_gemm,
+                                          mmpde_stream_t stream) {
+    MMPDE_REQUIRE(edge_gemm == MMPDE_EDGE_GEMM_F32 || edge_gemm == MMPDE_EDGE_GEMM_F16X3);
+    if (edge_gemm == MMPDE_EDGE_GEMM_F32 || k > FKMAX)
+        return mmpde_gnn_edge_backward(a, b, nbr, deg, n, k, msg2_w, msg2_b, grad_mean, grad_a, grad_edge,
+                                       partials, grad_w2, grad_b2, stream);
+    MMPDE_REQUIRE(a && b && nbr && msg2_w && msg2_b && grad_mean && grad_a && grad_edge && partials);
+    MMPDE_REQUIRE(grad_w2 && grad_b2 && n > 0 && k > 0 && n <= (int64_t)INT32_MAX);
+    MMPDE_REQUIRE((((uintptr_t)a | (uintptr_t)b | (uintptr_t)msg2_w | (uintptr_t)grad_mean |
+                    (uintptr_t)partials) & 15) == 0);
+    int grid = 256;
+    mmpde_gnn_edge_backward_partials(&grid);
+    const int64_t ntiles = (n + FT - 1) / FT;
+    MMPDE_REQUIRE(ntiles < (int64_t)INT32_MAX && n * 32 < (int64_t)INT32_MAX * 256LL);
+    const int G = grid;
+    if (grid > ntiles) grid = (int)ntiles;
+    float *pw2 = partials, *pb2 = partials + (int64_t)G * BH * BH;
+    float *ex = partials + (int64_t)G * (BH * BH + BH);
+    char *img1 = (char *)ex, *img2 = (char *)(ex + kBwdImg);
+    float *w2t = ex + 2 * kBwdImg;
+    unsigned *mx = (unsigned *)(w2t + BH * BH);
+    hipStream_t st = as_stream(stream);
+    // W2 and W2^T as fp16x3 B images (f16x3.hpp layout), the split maxima
+    PackSrc s1{}, s2{};
+    s1.w[0] = msg2_w;
+    s1.ld[0] = BH;
+    s2.w[0] = w2t;
+    s2.ld[0] = BH;
+    hipLaunchKernelGGL(transpose128_kernel, dim3(BH * BH / 256), dim3(256), 0, st, msg2_w, w2t);
+    hipLaunchKernelGGL((pack_f16x3_kernel<BH>), dim3(BH, 1), dim3(BH), 0, st, s1, 0, (int64_t)0, (int64_t)BH, img1);
+    hipLaunchKernelGGL((pack_f16x3_kernel<BH>), dim3(BH, 1), dim3(BH), 0, st, s2, 0, (int64_t)0, (int64_t)BH, img2);
+    MMPDE_RET_LAUNCH();
+    {
+        const hipError_t me = hipMemsetAsync(mx, 0, 4 * sizeof(unsigned), st);
+        if (me != hipSuccess) return MMPDE_ERR_HIP_BASE - (int)me;
+    }
+    const int64_t n4 = n * BH / 4;
+    hipLaunchKernelGGL(maxabs3_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(n4, 256), 1024)), dim3(256), 0, st,
+                       a, b, grad_mean, n4, mx);
+    MMPDE_RET_LAUNCH();
+    EdgeBwdF16Args p{a, b, nbr, deg, n, k, (int)ntiles, img1, img2, msg2_b, grad_mean, mx, grad_a, grad_edge,
+                     pw2, pb2};
+    hipLaunchKernelGGL(edge_bwd_f16_kernel, dim3(grid), dim3(512), 0, st, p);
     MMPDE_RET_LAUNCH();
     hipLaunchKernelGGL(partial_sum_kernel, dim3(ceil_div(BH * BH, 256)), dim3(256), 0, st, pw2, grid,
                        (int64_t)BH * BH, grad_w2);

@@ -13,7 +13,7 @@ import os
 import torch
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libmmpde_hip.so")
-ABI_VERSION = 11400
+ABI_VERSION = 11500
 
 ACT_NONE, ACT_TANH, ACT_RELU, ACT_ELU = 0, 1, 2, 3
 PAD_ZEROS, PAD_CIRCULAR = 0, 1
@@ -116,6 +116,9 @@ _SIGS = {
     "mmpde_linear_skinny_workspace_bytes": (_I64, [_I64, _I64, _I64]),
     "mmpde_linear_skinny_ws": (_I, [_P, _I64, _I64, _I64, _P, _I64, _P, _I64, _I, _P, _I64, _P, _I64,
                                     _P]),
+    "mmpde_gnn_edge_backward_ex": (_I, [_P, _P, _P, _P, _I64, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
+    "mmpde_linear_chain_workspace_bytes": (_I64, [_I64, _I, _P]),
+    "mmpde_linear_chain_ws": (_I, [_P, _I64, _I64, _I, _P, _P, _P, _P, _P, _P, _I64, _P, _I64, _P]),
     "mmpde_traj_mse": (_I, [_P, _P, _I64, _I64, _P, _P]),
     "mmpde_conv2d": (_I, [_P, _I64, _I, _I, _I, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P]),
     "mmpde_resample_bilinear": (_I, [_P, _I64, _I, _I, _I, _I, _P, _P]),

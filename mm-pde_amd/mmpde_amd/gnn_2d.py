@@ -69,10 +69,12 @@ class EdgeMean(torch.autograd.Function):
     """mean_i = 1/max(deg_i, 1) sum_{e < deg_i} relu(W2 relu(a_i + b_{nbr[i,e]}) + b2):
     message_net_2 over the in-edges and PyG's aggr='mean' (gnn_2d.py:36,59-63),
     with a = the target half and b = the source half of message_net_1's
-    pre-activation.  Gradients for a, b, W2 and b2; exact fp32, deterministic."""
+    pre-activation.  Gradients for a, b, W2 and b2, deterministic; the forward in
+    exact fp32, the backward's three GEMMs in exact fp32 (edge_gemm 'f32') or
+    the fp16x3 split (edge_gemm 'f16x3', mmpde_gnn_edge_backward_ex)."""
 
     @staticmethod
-    def forward(ctx, a, b, w2, b2, graph: EdgeGraph):
+    def forward(ctx, a, b, w2, b2, graph: EdgeGraph, edge_gemm: str = "f32"):
         n, k = graph.nbr.shape
         if a.shape != (n, 128) or b.shape != (n, 128) or w2.shape != (128, 128):
             raise ValueError("EdgeMean takes a, b [n, 128] and W2 [128, 128]")
@@ -85,6 +87,7 @@ class EdgeMean(torch.autograd.Function):
                 "mmpde_gnn_edge_mean_deg")
         ctx.save_for_backward(a, b, w2, b2)
         ctx.graph = graph
+        ctx.edge_gemm = L.EDGE_GEMM[edge_gemm]
         return mean
 
     @staticmethod
@@ -103,14 +106,15 @@ class EdgeMean(torch.autograd.Function):
         gw2 = torch.empty((128, 128), dtype=torch.float32, device=dev)
         gb2 = torch.empty((128,), dtype=torch.float32, device=dev)
         st = L.stream(dev)
-        L.check(lib.mmpde_gnn_edge_backward(L.ptr(a), L.ptr(b), L.ptr(graph.nbr), L.ptr(graph.deg),
-                                            n, k, L.ptr(w2), L.ptr(b2), L.ptr(g), L.ptr(ga),
-                                            L.ptr(gedge), L.ptr(part), L.ptr(gw2), L.ptr(gb2), st),
-                "mmpde_gnn_edge_backward")
+        L.check(lib.mmpde_gnn_edge_backward_ex(L.ptr(a), L.ptr(b), L.ptr(graph.nbr), L.ptr(graph.deg),
+                                               n, k, L.ptr(w2), L.ptr(b2), L.ptr(g), L.ptr(ga),
+                                               L.ptr(gedge), L.ptr(part), L.ptr(gw2), L.ptr(gb2),
+                                               ctx.edge_gemm, st),
+                "mmpde_gnn_edge_backward_ex")
         rev_off, rev_edge = graph.reverse()
         L.check(lib.mmpde_gnn_edge_source_sum(L.ptr(gedge), L.ptr(rev_off), L.ptr(rev_edge), n,
                                               L.ptr(gb), st), "mmpde_gnn_edge_source_sum")
-        return ga, gb, gw2, gb2, None
+        return ga, gb, gw2, gb2, None, None
 
 
 class GNN_Layer_FS_2D(nn.Module):  # noqa: N801 - reference name
@@ -163,7 +167,7 @@ class GNN_Layer_FS_2D(nn.Module):  # noqa: N801 - reference name
             self._pack, self._pack_key = (p, keep), key
         return self._pack[0]
 
-    def train_forward(self, h, u, pos_x, pos_y, variables, graph: EdgeGraph):
+    def train_forward(self, h, u, pos_x, pos_y, variables, graph: EdgeGraph, edge_gemm: str = "f32"):
         """Differentiable layer (gnn_2d.py:53-69).  message_net_1 of the edge (i, j)
         is W1 cat(h_i, h_j, u_i - u_j, dx, dy, t_i) + b1 = a_i + b_j with
         a = [h u x y t] Wa^T + b1 and b = [h u x y] Wb^T (Wb holding -W1 on the
@@ -179,7 +183,7 @@ class GNN_Layer_FS_2D(nn.Module):  # noqa: N801 - reference name
                         torch.cat((w1[:, :f], wdu, wdxy, wt), 1).t())
         b = torch.cat((h, u, pos_x, pos_y), -1) @ torch.cat((w1[:, f:2 * f], -wdu, -wdxy), 1).t()
         m2 = self.message_net_2[0]
-        mean = EdgeMean.apply(a, b, m2.weight, m2.bias, graph)
+        mean = EdgeMean.apply(a, b, m2.weight, m2.bias, graph, edge_gemm)
         upd = self.update_net_2(self.update_net_1(torch.cat((h, mean, variables), -1)))
         return self.norm(h + upd)
 
@@ -380,7 +384,7 @@ class MP_PDE_Solver_2D(nn.Module):  # noqa: N801 - reference name
         variables = pos[:, 0][:, None] / self.pde.tmax
         h = self.embedding_mlp(torch.cat((u, pos_x, pos_y, variables), -1))
         for layer in self.gnn_layers:
-            h = layer.train_forward(h, u, pos_x, pos_y, variables, graph)
+            h = layer.train_forward(h, u, pos_x, pos_y, variables, graph, self.edge_gemm)
         diff = self.output_mlp(h[:, None]).squeeze(1)
         return self.out_scales()[None].to(h.device) * diff
 

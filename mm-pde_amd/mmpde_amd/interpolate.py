@@ -109,8 +109,12 @@ class ItpNet(nn.Module):
                 x = ops.conv2d(x, d[i].weight, d[i].bias, 1, 2, L.ACT_TANH)
             return x
         x = data.reshape(data.shape[0], -1)
-        for i, act in ((0, L.ACT_TANH), (2, L.ACT_TANH), (4, L.ACT_TANH), (6, L.ACT_NONE)):
-            x = ops.linear_skinny(x, d[i].weight, d[i].bias, act)
+        layers = [(d[i].weight, d[i].bias, act)
+                  for i, act in ((0, L.ACT_TANH), (2, L.ACT_TANH), (4, L.ACT_TANH), (6, L.ACT_NONE))]
+        if x.shape[0] <= 64:   # the four layers in one launch (grid barrier between layers)
+            return ops.linear_chain(x, layers)
+        for w, b, act in layers:
+            x = ops.linear_skinny(x, w, b, act)
         return x
 
     def forward(self, neighbors, query_points, mode, data=None):

@@ -57,6 +57,13 @@ def test_null_arguments_are_rejected_before_launch():
     assert lib.mmpde_gnn_edge_backward(None, None, None, None, 10, 35, None, None, None, None,
                                        None, None, None, None, None) == -1
     assert lib.mmpde_gnn_edge_source_sum(None, None, None, 10, None, None) == -1
+    # linear chain: null pointers and m > 64 refused; workspace sizing without a GPU
+    import ctypes
+    dims = (ctypes.c_int64 * 5)(2521, 2048, 512, 2048, 2521)
+    assert lib.mmpde_linear_chain_ws(None, 2521, 16, 4, dims, None, None, None, None, None, 2521, None, 0,
+                                     None) == -1
+    assert lib.mmpde_linear_chain_workspace_bytes(16, 4, dims) >= (4096 + 16 * (2048 + 512 + 2048)) * 4
+    assert lib.mmpde_linear_chain_workspace_bytes(16, 5, dims) == 0
 
 
 def test_edge_backward_partials_sizing_without_gpu():
@@ -64,4 +71,7 @@ def test_edge_backward_partials_sizing_without_gpu():
 
     g = ctypes.c_int(0)
     n = _lib.lib().mmpde_gnn_edge_backward_partials(ctypes.byref(g))
-    assert g.value > 0 and n == g.value * (128 * 128 + 128)
+    # per-workgroup dW2 / db2 partials, then the fp16x3 mode's two W2 images
+    # (128 x 128 fp16 hi / lo + 128 column scales each), W2^T and the maxima
+    extra = 2 * (128 * 128 * 4 + 128 * 4) // 4 + 128 * 128 + 64
+    assert g.value > 0 and n == g.value * (128 * 128 + 128) + extra

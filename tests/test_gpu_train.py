@@ -80,8 +80,9 @@ def _edge_mean_ref(a, b, w2, b2, nbr, deg):
     return m.sum(1) / deg.clamp(min=1).to(a.dtype)[:, None]
 
 
+@pytest.mark.parametrize("edge_gemm", ["f32", "f16x3"])
 @pytest.mark.parametrize("ragged", [False, True])
-def test_edge_mean_forward_backward_vs_autograd(dev, ragged):
+def test_edge_mean_forward_backward_vs_autograd(dev, ragged, edge_gemm):
     from mmpde_amd.gnn_2d import EdgeGraph, EdgeMean
 
     g = torch.Generator().manual_seed(5 + ragged)
@@ -105,10 +106,10 @@ def test_edge_mean_forward_backward_vs_autograd(dev, ragged):
 
     graph = EdgeGraph(nbr.to(dev), deg.to(dev) if ragged else None)
     got_in = [t.to(dev).requires_grad_() for t in (a, b, w2, b2)]
-    out = EdgeMean.apply(*got_in, graph)
+    out = EdgeMean.apply(*got_in, graph, edge_gemm)
     (out * gout.to(dev)).sum().backward()
     torch.cuda.synchronize()
-    tag = "ragged" if ragged else "fixed"
+    tag = ("ragged " if ragged else "fixed ") + edge_gemm
     _close(out, ref, 2e-5, f"{tag} mean")
     for name, t, r in zip(("a", "b", "W2", "b2"), got_in, ref_in):
         _close(t.grad, r.grad, 2e-5, f"{tag} d/d{name}")
@@ -116,7 +117,7 @@ def test_edge_mean_forward_backward_vs_autograd(dev, ragged):
     grads = [t.grad.clone() for t in got_in]
     for t in got_in:
         t.grad = None
-    EdgeMean.apply(*got_in, graph).mul(gout.to(dev)).sum().backward()
+    EdgeMean.apply(*got_in, graph, edge_gemm).mul(gout.to(dev)).sum().backward()
     for t, g0 in zip(got_in, grads):
         assert torch.equal(t.grad, g0)
 
@@ -152,8 +153,9 @@ def _setup(kind, B, seed=0):
     return pde, opde, model, model_b, itp, dmm, gc, u
 
 
+@pytest.mark.parametrize("edge_gemm", ["f32", "f16x3"])
 @pytest.mark.parametrize("kind", ["cy", "burgers"])
-def test_training_step_gradients_vs_oracle(dev, kind):
+def test_training_step_gradients_vs_oracle(dev, kind, edge_gemm):
     torch.set_num_threads(min(16, torch.get_num_threads()))
     B = 2
     pde, opde, model, model_b, itp, dmm, gc, u = _setup(kind, B)
@@ -162,6 +164,7 @@ def test_training_step_gradients_vs_oracle(dev, kind):
     sds32 = _sds(torch.float32, model=model, model_b=model_b, itp=itp)   # the fp32 floor
     for m in (model, model_b, itp, dmm):
         m.to(dev)
+    model.edge_gemm = model_b.edge_gemm = edge_gemm   # the edge backward's GEMM arithmetic
     model.train()
     model_b.train()
     itp.train()

@@ -8,7 +8,10 @@ one JSON line with ms per iteration and node-updates/s (B*N nodes of both
 GNNs' forward + backward per iteration).  The edge-stage backward kernel is
 timed with HIP events around a standalone EdgeMean backward of one layer.
 
-    python tools/train_bench.py [--batch 16] [--iters 10] [--warmup 3]
+    python tools/train_bench.py [--batch 16] [--iters 10] [--warmup 3] [--edge-gemm f32|f16x3]
+
+--edge-gemm sets both GNNs' edge_gemm: the edge-stage backward's three GEMMs
+in exact fp32 or in the fp16x3 split (mmpde_gnn_edge_backward_ex).
 """
 import argparse
 import json
@@ -27,6 +30,7 @@ def main():
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--edge-gemm", default="f32", choices=["f32", "f16x3"])
     args = ap.parse_args()
     from mmpde_amd.gnn_2d import EdgeGraph, EdgeMean
     from mmpde_amd.synth import build_models, fields
@@ -37,6 +41,7 @@ def main():
     u = fields(pde.ori_grid, B, 30, seed=1)
     for m in (model, model_b, itp, dmm):
         m.to(dev)
+    model.edge_gemm = model_b.edge_gemm = args.edge_gemm
     model.train()
     model_b.train()
     itp.train()
@@ -77,10 +82,10 @@ def main():
     graph = EdgeGraph(knn_graph_nbr(gc.uniform_grid(dev).repeat(B, 1), B, 35))
     gout = torch.randn(n, 128, device=dev)
     for _ in range(3):
-        EdgeMean.apply(a, b, lay.weight, lay.bias, graph).backward(gout)
+        EdgeMean.apply(a, b, lay.weight, lay.bias, graph, args.edge_gemm).backward(gout)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     reps = 10
-    out = EdgeMean.apply(a, b, lay.weight, lay.bias, graph)
+    out = EdgeMean.apply(a, b, lay.weight, lay.bias, graph, args.edge_gemm)
     torch.cuda.synchronize()
     e0.record()
     for _ in range(reps):
@@ -92,11 +97,12 @@ def main():
     flops = 3 * 2 * edges * 128 * 128          # z2, gm1 and the dW2 outer products
     print(json.dumps({
         "what": "MM-PDE training iteration (train_helper_2d.py:95-131), cy synthetic",
-        "batch": B, "nodes": n, "ms_per_iter": round(ms, 3),
+        "batch": B, "nodes": n, "edge_gemm": args.edge_gemm, "ms_per_iter": round(ms, 3),
         "train_node_updates_per_s": round(2 * 6 * n / (ms * 1e-3)),
         "loss": float(loss),
         "edge_backward_layer_us": round(bwd_us, 1),
-        "edge_backward_tflops_fp32": round(flops / (bwd_us * 1e-6) / 1e12, 2),
+        "edge_backward_tflops": round(flops / (bwd_us * 1e-6) / 1e12, 2),
+        "edge_backward_peak_tflops": 157.3 if args.edge_gemm == "f32" else round(2516.6 / 3, 1),
     }))
 
 
