@@ -196,6 +196,10 @@ int mmpde_linear_skinny_ws(const float *x, int64_t ldx, int64_t m, int64_t k, co
  * ZEROED before its first use and reused (each call leaves its first 4096
  * words at zero again; the intermediate activations live after them). */
 int64_t mmpde_linear_chain_workspace_bytes(int64_t m, int nl, const int64_t *dims);
+/* Whether the DMM mesh / branch calls run their output MLP as one chain
+ * launch (1, default) or as per-layer mmpde_linear_skinny_ws launches (0);
+ * enable < 0 only queries.  Returns the previous setting.  Process-wide. */
+int mmpde_linear_chain_dmm(int enable);
 int mmpde_linear_chain_ws(const float *x, int64_t ldx, int64_t m, int nl, const int64_t *dims,
                           const float *const *w, const int64_t *ldw, const float *const *b,
                           const int *act, float *y, int64_t ldy, void *workspace,

@@ -155,6 +155,7 @@ struct ChainSpec {
     int64_t ldy;
 };
 __attribute__((visibility("hidden"))) bool chain_ok(int64_t m, int nl, const ChainSpec *sp);
+__attribute__((visibility("hidden"))) bool chain_dmm_enabled();
 __attribute__((visibility("hidden"))) int64_t chain_ws_bytes(int64_t m, int nl, const ChainSpec *sp);
 __attribute__((visibility("hidden"))) int linear_chain(const float *x, int64_t ldx, int64_t m, int nl,
                                                        const ChainSpec *sp, void *workspace,

@@ -167,19 +167,22 @@ __global__ __launch_bounds__(kSkW * 64) void linear_skinny_kernel(const float *_
 // interpolate.py:66-74; the DMM output_mlp + P = Wb . branch,
 // mesh/dmm_model.py:175-181): a persistent grid walks each layer's work items
 // (16 x 16 output tile x K split, the linear_skinny_kernel item above, same
-// per-item arithmetic), then meets at a grid barrier before the next layer.
-// What the fusion buys is the barrier's shadow: before waiting, every
-// workgroup issues the weight loads of its first item of the next layer
-// (weights do not depend on the activations), so a layer's weight stream
-// starts while the previous layer drains.  Activations written inside the
+// per-item arithmetic); an item of layer l + 1 starts once every item of layer
+// l is done.  What the fusion buys is that wait's shadow: a workgroup issues
+// the weight loads of its next item before it waits (weights do not depend on
+// the activations), so a layer's weight stream starts while the previous layer
+// drains.  Activations written inside the
 // launch go through write-through agent-scope stores and are read back with
 // agent-scope loads (no release / acquire fences: the XCD L2s are not
 // coherent, the sc1 path is); every buffer is written once per launch.
-// The barrier counter and exit counter reset themselves: the last workgroup to
-// leave zeroes both, so a zeroed workspace serves every later launch.
+// The control words reset themselves (the last workgroup to leave zeroes
+// them), so a zeroed workspace serves every later launch.
 constexpr int kChainMax = 4;           // layers per launch
-constexpr int kChainTickets = 1008;    // ticket words per layer (output tiles)
-constexpr int kChainCtl = 64;          // control words before the tickets (4096 words in all)
+constexpr int kChainTickets = 960;     // ticket words per layer (output tiles)
+constexpr int kChainCtl = 256;         // control words before the tickets (4096 words in all)
+// control words, each on a 128-B line of its own (the claim counter is not
+// slowed by the polls of the done counters): claims, exits, timeout, done[l]
+constexpr int kCtlClaim = 0, kCtlExit = 32, kCtlTimeout = 64, kCtlDone = 96;  // done[l] at kCtlDone + 32 l
 
 struct ChainLayer {
     const float *w, *b;
@@ -193,7 +196,7 @@ struct ChainArgs {
     const float *x;
     int64_t ldx, m;
     int nl, rtiles;
-    unsigned *ctl;     // [0] barrier arrivals, [1] exits, [2] sticky barrier timeout; tickets from kChainCtl
+    unsigned *ctl;     // control words (kCtl*), tickets from kChainCtl
 };
 
 __device__ __forceinline__ float ld_agent(const float *p) {
@@ -232,187 +235,192 @@ __device__ __forceinline__ void chain_loadw(const ChainLayer &Ly, int64_t col0, 
     }
 }
 
-// one layer's items of this workgroup; lw may already hold the first chunk of
-// the first item's weights (wpre)
-template <int kSkW>
-__device__ __forceinline__ void chain_layer(const ChainArgs &a, const ChainLayer &Ly, const float *x,
-                                            int64_t ldx, bool coh, bool last, unsigned *tickets,
-                                            float (&lw)[16], bool wpre, float *sw, float *sx) {
+__device__ __forceinline__ void chain_wait(const unsigned *ctr, unsigned target, unsigned *timeout) {
+    // bounded spin (100 ms of the 100 MHz real-time clock: a fault cannot
+    // hang the queue; a timeout sets the sticky word), then one agent-scope
+    // acquire waited before the workgroup barrier that follows
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(8);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 10000000ull) {
+            __hip_atomic_store(timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// One item (16 x 16 output tile x K split) of chain layer LI: its weights are
+// issued first, then (LI > 0) the wait for every item of layer LI - 1, then the
+// activations (agent-scope loads) and the item as in linear_skinny_kernel.
+template <int kSkW, int LI>
+__device__ __forceinline__ void chain_item_run(const ChainArgs &a, int it, unsigned *ctl, float *sw, float *sx) {
     constexpr int C = 64 * kSkW, LD = C + 4;
+    const ChainLayer &Ly = a.L[LI];
+    const float *x = LI ? a.L[LI > 0 ? LI - 1 : 0].y : a.x;
+    const int64_t ldx = LI ? a.L[LI > 0 ? LI - 1 : 0].ldy : a.ldx;
+    const bool last = LI + 1 == a.nl;
+    unsigned *tickets = ctl + kChainCtl + LI * kChainTickets;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int r = lane & 15, g = lane >> 4;
     const int K = (int)Ly.k;
     const int64_t m = a.m, n = Ly.n;
-    float lx[16];
-    auto loadx = [&](int64_t row0, int kc) {
+    const ChainItem ci = chain_item(Ly, a.rtiles, it, C);
+    float lw[16], lx[16];
+    chain_loadw<kSkW>(Ly, ci.col0, ci.c0 * C, lw);
+    if (LI > 0) {
+        if (tid == 0)
+            chain_wait(ctl + kCtlDone + 32 * (LI > 0 ? LI - 1 : 0), (unsigned)a.L[LI > 0 ? LI - 1 : 0].items,
+                       ctl + kCtlTimeout);
+        __syncthreads();
+    }
+    auto loadx = [&](int kc) {
         const int kk = kc + tid;
         const bool ok = kk < K;
         const int o = ok ? kk : 0;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-            const float *p = x + min(row0 + i, m - 1) * ldx + o;
-            const float c = coh ? ld_agent(p) : *p;
+            const float *p = x + min(ci.row0 + i, m - 1) * ldx + o;
+            const float c = LI ? ld_agent(p) : *p;
             lx[i] = ok ? c : 0.0f;
         }
     };
-    for (int it = blockIdx.x; it < Ly.items; it += gridDim.x) {
-        const ChainItem ci = chain_item(Ly, a.rtiles, it, C);
-        if (!wpre) chain_loadw<kSkW>(Ly, ci.col0, ci.c0 * C, lw);
-        wpre = false;
-        loadx(ci.row0, ci.c0 * C);
-        f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-        for (int c = 0; c < ci.nch; ++c) {
-            if (c) __syncthreads();  // chunk c - 1 consumed
+    loadx(ci.c0 * C);
+    f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+    for (int c = 0; c < ci.nch; ++c) {
+        if (c) __syncthreads();  // chunk c - 1 consumed
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                sw[i * LD + tid] = lw[i];
-                sx[i * LD + tid] = lx[i];
-            }
-            __syncthreads();
-            if (c + 1 < ci.nch) {
-                chain_loadw<kSkW>(Ly, ci.col0, (ci.c0 + c + 1) * C, lw);
-                loadx(ci.row0, (ci.c0 + c + 1) * C);
-            }
-            const float *aw = sw + r * LD + 64 * wave + 4 * g;
-            const float *ax = sx + r * LD + 64 * wave + 4 * g;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float4 wv = *(const float4 *)(aw + 16 * q);
-                const float4 xv = *(const float4 *)(ax + 16 * q);
-                acc = mfma16(xv.x, wv.x, acc);
-                acc = mfma16(xv.y, wv.y, acc);
-                acc = mfma16(xv.z, wv.z, acc);
-                acc = mfma16(xv.w, wv.w, acc);
-            }
+        for (int i = 0; i < 16; ++i) {
+            sw[i * LD + tid] = lw[i];
+            sx[i * LD + tid] = lx[i];
         }
         __syncthreads();
-        f32x4 *wpart = (f32x4 *)sw;  // [wave][lane]
-        wpart[wave * 64 + lane] = acc;
-        __syncthreads();
-        if (wave == 0) {
-            f32x4 s = wpart[lane];
+        if (c + 1 < ci.nch) {
+            chain_loadw<kSkW>(Ly, ci.col0, (ci.c0 + c + 1) * C, lw);
+            loadx((ci.c0 + c + 1) * C);
+        }
+        const float *aw = sw + r * LD + 64 * wave + 4 * g;
+        const float *ax = sx + r * LD + 64 * wave + 4 * g;
 #pragma unroll
-            for (int v = 1; v < kSkW; ++v) s += wpart[v * 64 + lane];
-            const int64_t col = ci.col0 + r;
-            bool write = true;
-            if (Ly.z > 1) {
-                // split-K hand-off as in linear_skinny_kernel (sc1 partials, a
-                // ticket per tile, the last slice adds the slices in z order)
-                float *pz = Ly.part + (int64_t)ci.zz * m * n;
-                if (col < n) {
+        for (int q = 0; q < 4; ++q) {
+            const float4 wv = *(const float4 *)(aw + 16 * q);
+            const float4 xv = *(const float4 *)(ax + 16 * q);
+            acc = mfma16(xv.x, wv.x, acc);
+            acc = mfma16(xv.y, wv.y, acc);
+            acc = mfma16(xv.z, wv.z, acc);
+            acc = mfma16(xv.w, wv.w, acc);
+        }
+    }
+    __syncthreads();
+    f32x4 *wpart = (f32x4 *)sw;  // [wave][lane]
+    wpart[wave * 64 + lane] = acc;
+    __syncthreads();
+    if (wave == 0) {
+        f32x4 s = wpart[lane];
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const int64_t row = ci.row0 + 4 * g + q;
-                        if (row < m) st_agent(pz + row * n + col, s[q]);
-                    }
-                }
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                const int T = Ly.ctiles * a.rtiles;
-                unsigned *tk = tickets + (it - ci.zz * T);
-                unsigned ticket = 0u;
-                if (lane == 0) ticket = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ticket = __builtin_amdgcn_readfirstlane(ticket);
-                write = ticket == (unsigned)(Ly.z - 1);
-                if (write) {
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    const int64_t cc = min(col, n - 1);
-                    float v[kSkMaxZ][4];
-#pragma unroll
-                    for (int zz = 0; zz < kSkMaxZ; ++zz) {
-                        if (zz < Ly.z) {
-                            const float *pq = Ly.part + (int64_t)zz * m * n + cc;
-#pragma unroll
-                            for (int q = 0; q < 4; ++q) v[zz][q] = ld_agent(pq + min(ci.row0 + 4 * g + q, m - 1) * n);
-                        }
-                    }
-                    f32x4 t = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-                    for (int zz = 0; zz < kSkMaxZ; ++zz) {
-                        if (zz < Ly.z) {
-#pragma unroll
-                            for (int q = 0; q < 4; ++q) t[q] += v[zz][q];
-                        }
-                    }
-                    if (lane == 0) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    s = t;
-                }
-            }
-            if (write && col < n) {
-                const float bb = Ly.b ? Ly.b[col] : 0.0f;
+        for (int v = 1; v < kSkW; ++v) s += wpart[v * 64 + lane];
+        const int64_t col = ci.col0 + r;
+        bool write = true;
+        if (Ly.z > 1) {
+            // split-K hand-off as in linear_skinny_kernel (sc1 partials, a
+            // ticket per tile, the last slice adds the slices in z order)
+            float *pz = Ly.part + (int64_t)ci.zz * m * n;
+            if (col < n) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const int64_t row = ci.row0 + 4 * g + q;
-                    if (row < m) {
-                        const float v = act_apply(s[q] + bb, Ly.act);
-                        if (last) Ly.y[row * Ly.ldy + col] = v;
-                        else st_agent(Ly.y + row * Ly.ldy + col, v);
+                    if (row < m) st_agent(pz + row * n + col, s[q]);
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const int T = Ly.ctiles * a.rtiles;
+            unsigned *tk = tickets + (it - ci.zz * T);
+            unsigned ticket = 0u;
+            if (lane == 0) ticket = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ticket = __builtin_amdgcn_readfirstlane(ticket);
+            write = ticket == (unsigned)(Ly.z - 1);
+            if (write) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const int64_t cc = min(col, n - 1);
+                float v[kSkMaxZ][4];
+#pragma unroll
+                for (int zz = 0; zz < kSkMaxZ; ++zz) {
+                    if (zz < Ly.z) {
+                        const float *pq = Ly.part + (int64_t)zz * m * n + cc;
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) v[zz][q] = ld_agent(pq + min(ci.row0 + 4 * g + q, m - 1) * n);
                     }
+                }
+                f32x4 t = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+                for (int zz = 0; zz < kSkMaxZ; ++zz) {
+                    if (zz < Ly.z) {
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) t[q] += v[zz][q];
+                    }
+                }
+                if (lane == 0) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                s = t;
+            }
+        }
+        if (write && col < n) {
+            const float bb = Ly.b ? Ly.b[col] : 0.0f;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int64_t row = ci.row0 + 4 * g + q;
+                if (row < m) {
+                    const float v = act_apply(s[q] + bb, Ly.act);
+                    if (last) Ly.y[row * Ly.ldy + col] = v;
+                    else st_agent(Ly.y + row * Ly.ldy + col, v);
                 }
             }
         }
-        __syncthreads();  // wpart (sw) read before the next item's chunk store
+        // the item is done once its stores have drained
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_fetch_add(ctl + kCtlDone + 32 * LI, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    __syncthreads();  // wpart (sw) read before the next item's chunk store
 }
 
+// Items are CLAIMED from one counter over the flattened (layer, item) list, so
+// a workgroup waits only for items of the previous layer, which carry smaller
+// indices and were therefore claimed by workgroups already running: the wait
+// cannot depend on a workgroup that is not resident, whatever else shares the
+// GPU (other streams, other processes) and however large the grid.  Control
+// words (kCtl*): the claim counter, exits, a sticky wait timeout, items done
+// per layer; the last workgroup to exit zeroes them.
 template <int kSkW>
 __global__ __launch_bounds__(kSkW * 64, 4) void linear_chain_kernel(ChainArgs a) {
     constexpr int C = 64 * kSkW, LD = C + 4;
     __shared__ float sw[16 * LD], sx[16 * LD];
+    __shared__ int s_it;
     // control words through a VGPR base: vector-memory atomics only
     int vzero;
     asm volatile("v_mov_b32 %0, 0" : "=v"(vzero));
     unsigned *ctl = a.ctl + vzero;
-    float lw[16];
-    bool wpre = false;
-    const unsigned G = gridDim.x;
-#pragma unroll
-    for (int l = 0; l < kChainMax; ++l) {
-        if (l >= a.nl) break;
-        const bool last = l + 1 == a.nl;
-        chain_layer<kSkW>(a, a.L[l], l ? a.L[l - 1].y : a.x, l ? a.L[l - 1].ldy : a.ldx, l > 0, last,
-                          ctl + kChainCtl + l * kChainTickets, lw, wpre, sw, sx);
-        wpre = false;
-        if (last) break;
-        // arrive (this workgroup's stores are all wave 0's, drained in
-        // chain_layer before its tickets or here), then prefetch the next
-        // layer's first weights, then wait for every workgroup
-        if (threadIdx.x < 64) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (threadIdx.x == 0) __hip_atomic_fetch_add(ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        const ChainLayer &nx = a.L[l + 1];
-        if ((int)blockIdx.x < nx.items) {
-            const ChainItem ci = chain_item(nx, a.rtiles, blockIdx.x, C);
-            chain_loadw<kSkW>(nx, ci.col0, ci.c0 * C, lw);
-            wpre = true;
-        }
-        if (threadIdx.x == 0) {
-            const unsigned target = (unsigned)(l + 1) * G;
-            // bounded spin (every workgroup of the grid is resident: G <= the
-            // occupancy-derived capacity; 100 ms of the 100 MHz real-time
-            // clock), so a fault cannot hang the queue: a timeout sets the
-            // sticky word ctl[2]
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            while (__hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-                __builtin_amdgcn_s_sleep(2);
-                if (__builtin_amdgcn_s_memrealtime() - t0 > 10000000ull) {
-                    __hip_atomic_store(ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    break;
-                }
-            }
-            // the consumer side of the hand-off: one agent-scope acquire
-            // after the poll, waited before the workgroup barrier (the next
-            // layer's activation loads are sc1 loads as well)
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
+    const int n0 = a.L[0].items, n1 = a.nl > 1 ? a.L[1].items : 0, n2 = a.nl > 2 ? a.L[2].items : 0,
+              n3 = a.nl > 3 ? a.L[3].items : 0;
+    const int total = n0 + n1 + n2 + n3;
+    for (;;) {
+        if (threadIdx.x == 0)
+            s_it = (int)__hip_atomic_fetch_add(ctl + kCtlClaim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();
+        const int it = s_it;
+        if (it >= total) break;
+        if (it < n0) chain_item_run<kSkW, 0>(a, it, ctl, sw, sx);
+        else if (it < n0 + n1) chain_item_run<kSkW, 1>(a, it - n0, ctl, sw, sx);
+        else if (it < n0 + n1 + n2) chain_item_run<kSkW, 2>(a, it - n0 - n1, ctl, sw, sx);
+        else chain_item_run<kSkW, 3>(a, it - n0 - n1 - n2, ctl, sw, sx);
     }
     if (threadIdx.x == 0) {
-        const unsigned e = __hip_atomic_fetch_add(ctl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (e == G - 1) {  // every workgroup is past every barrier
-            __hip_atomic_store(ctl, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(ctl + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned e = __hip_atomic_fetch_add(ctl + kCtlExit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (e == gridDim.x - 1) {  // every item is done and no workgroup claims or waits any more
+            __hip_atomic_store(ctl + kCtlClaim, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(ctl + kCtlExit, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+            for (int l = 0; l < kChainMax; ++l)
+                __hip_atomic_store(ctl + kCtlDone + 32 * l, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }
@@ -670,8 +678,8 @@ int linear_chain(const float *x, int64_t ldx, int64_t m, int nl, const ChainSpec
     ChainArgs a;
     const int64_t need = chain_plan(x, ldx, m, nl, sp, cus, (float *)workspace, &a) * (int64_t)sizeof(float);
     if (workspace_bytes < need) return MMPDE_ERR_INVALID_ARG;
-    // grid: at most two resident workgroups per CU (every workgroup must be
-    // resident for the grid barrier), no more than the largest layer's items
+    // grid: two workgroups per CU at most (items are claimed, so residency is
+    // a matter of speed only), no more than the largest layer's items
     static int occ = -1;
     if (occ < 0) {
         int o = 0;
@@ -699,6 +707,18 @@ static int chain_specs(int64_t m, int nl, const int64_t *dims, const float *cons
                                         act[l], l + 1 == nl ? y : nullptr, l + 1 == nl ? ldy : 0};
     }
     return MMPDE_OK;
+}
+
+// whether the DMM output MLP runs as one chain launch (dmm.hip) or as per-layer
+// skinny launches; both give the same results to fp32 rounding
+static int g_chain_dmm = 1;
+namespace mmpde_detail {
+bool chain_dmm_enabled() { return g_chain_dmm != 0; }
+}  // namespace mmpde_detail
+extern "C" int mmpde_linear_chain_dmm(int enable) {
+    const int prev = g_chain_dmm;
+    if (enable >= 0) g_chain_dmm = enable ? 1 : 0;
+    return prev;
 }
 
 extern "C" int64_t mmpde_linear_chain_workspace_bytes(int64_t m, int nl, const int64_t *dims) {

@@ -566,7 +566,8 @@ int skinny(const float *x, int64_t ldx, int64_t m, int64_t k, const float *w, in
 float *chain_ws(float *sk) { return (float *)(((uintptr_t)sk + 127) & ~(uintptr_t)127); }
 bool chain_fits(int64_t m, int nl, const mmpde_detail::ChainSpec *sp, float *sk, int64_t skf) {
     const int64_t avail = (skf - (chain_ws(sk) - sk)) * (int64_t)sizeof(float);
-    return mmpde_detail::chain_ok(m, nl, sp) && mmpde_detail::chain_ws_bytes(m, nl, sp) <= avail;
+    return mmpde_detail::chain_dmm_enabled() && mmpde_detail::chain_ok(m, nl, sp) &&
+           mmpde_detail::chain_ws_bytes(m, nl, sp) <= avail;
 }
 int chain_run(const float *x, int64_t ldx, int64_t m, int nl, const mmpde_detail::ChainSpec *sp, float *sk,
               int64_t skf, hipStream_t st) {

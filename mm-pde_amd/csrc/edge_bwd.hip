@@ -211,7 +211,7 @@ __global__ __launch_bounds__(256, 1) void edge_bwd_kernel(EdgeBwdArgs p) {
 // one neighbour e of the tile's 32 targets (32 edges = the K of the dW2 GEMM):
 //   P1  z1 = a + b_src (b rows prefetched one slot ahead into registers),
 //       relu(z1) split -> LDS row-major (A of z2) and column-major (B of dW2),
-//       the z1 > 0 bits
+//       the z1 > 0 bits (double-buffered by slot parity: two barriers a slot)
 //   P2  z2 = relu(z1) W2^T (wave w: output columns 16w..), gz2 = g/deg
 //       [z2 + b2 > 0][e < deg] split -> LDS row-major (A of gm1) and
 //       column-major (A of dW2); db2 in fp32
@@ -244,11 +244,13 @@ __device__ __forceinline__ void split1(float x, _Float16 &h, _Float16 &l) {
 __global__ __launch_bounds__(512, 2) void edge_bwd_f16_kernel(EdgeBwdF16Args p) {
     __shared__ float at[FT * FAW];             // a rows of the tile
     __shared__ float gms[FT * FAW];            // g / deg rows (0 for rows past n)
-    __shared__ _Float16 za[2][FT * FAS];       // relu(z1) sz: hi, lo, [edge][kk]
-    __shared__ _Float16 zb[2][BH * FCS];       // the same, [kk][edge]
+    // relu(z1) images double-buffered by slot parity (no barrier between a
+    // slot's last readers and the next slot's writers)
+    __shared__ _Float16 za[2][2][FT * FAS];    // [slot & 1] relu(z1) sz: hi, lo, [edge][kk]
+    __shared__ _Float16 zb[2][2][BH * FCS];    // the same, [kk][edge]
     __shared__ _Float16 gr[2][FT * FAS];       // gz2 sg, [edge][c]
     __shared__ _Float16 gt[2][BH * FCS];       // the same, [c][edge]
-    __shared__ uint8_t zm[BH * (FT / 8)];      // z1 > 0, [kk][edge / 8] bits
+    __shared__ uint8_t zm[2][BH * (FT / 8)];   // z1 > 0, [kk][edge / 8] bits
     __shared__ int nb[FT * FKMAX];             // the tile's neighbour rows (clamped)
     __shared__ int dg[FT];                     // degrees (0 past n)
     const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -302,6 +304,7 @@ __global__ __launch_bounds__(512, 2) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
         for (int t = 0; t < 8; ++t) bv[t] = p.b[(int64_t)nb[(8 * eg + t) * FKMAX] * BH + kk1];
         f32x4 gacc[2] = {(f32x4){0.0f, 0.0f, 0.0f, 0.0f}, (f32x4){0.0f, 0.0f, 0.0f, 0.0f}};
         for (int e = 0; e < k; ++e) {
+            const int sb = e & 1;
             // ---- P1
             {
                 half8 hi, lo;
@@ -315,12 +318,12 @@ __global__ __launch_bounds__(512, 2) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
                     split1(fmaxf(z, 0.0f) * sz, h, l);
                     hi[t] = h;
                     lo[t] = l;
-                    za[0][ed * FAS + kk1] = h;
-                    za[1][ed * FAS + kk1] = l;
+                    za[sb][0][ed * FAS + kk1] = h;
+                    za[sb][1][ed * FAS + kk1] = l;
                 }
-                *(half8 *)&zb[0][kk1 * FCS + 8 * eg] = hi;
-                *(half8 *)&zb[1][kk1 * FCS + 8 * eg] = lo;
-                zm[kk1 * 4 + eg] = (uint8_t)bits;
+                *(half8 *)&zb[sb][0][kk1 * FCS + 8 * eg] = hi;
+                *(half8 *)&zb[sb][1][kk1 * FCS + 8 * eg] = lo;
+                zm[sb][kk1 * 4 + eg] = (uint8_t)bits;
                 if (e + 1 < k) {  // next slot's b values, in flight during P2 / P3
 #pragma unroll
                     for (int t = 0; t < 8; ++t)
@@ -335,8 +338,8 @@ __global__ __launch_bounds__(512, 2) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
                 for (int s = 0; s < 4; ++s) {
 #pragma unroll
                     for (int rb = 0; rb < 2; ++rb) {
-                        const half8 ah = *(const half8 *)&za[0][(16 * rb + r) * FAS + 32 * s + 8 * g];
-                        const half8 al = *(const half8 *)&za[1][(16 * rb + r) * FAS + 32 * s + 8 * g];
+                        const half8 ah = *(const half8 *)&za[sb][0][(16 * rb + r) * FAS + 32 * s + 8 * g];
+                        const half8 al = *(const half8 *)&za[sb][1][(16 * rb + r) * FAS + 32 * s + 8 * g];
                         acc[rb] = mfma_f16(ah, w1h[s], acc[rb]);
                         acc[rb] = mfma_f16(ah, w1l[s], acc[rb]);
                         acc[rb] = mfma_f16(al, w1h[s], acc[rb]);
@@ -379,8 +382,8 @@ __global__ __launch_bounds__(512, 2) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
                 const half8 gl = *(const half8 *)&gt[1][col * FCS + 8 * g];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    const half8 bh = *(const half8 *)&zb[0][(16 * j + r) * FCS + 8 * g];
-                    const half8 bl = *(const half8 *)&zb[1][(16 * j + r) * FCS + 8 * g];
+                    const half8 bh = *(const half8 *)&zb[sb][0][(16 * j + r) * FCS + 8 * g];
+                    const half8 bl = *(const half8 *)&zb[sb][1][(16 * j + r) * FCS + 8 * g];
                     dw[j] = mfma_f16(gh, bh, dw[j]);
                     dw[j] = mfma_f16(gh, bl, dw[j]);
                     dw[j] = mfma_f16(gl, bh, dw[j]);
@@ -390,14 +393,16 @@ __global__ __launch_bounds__(512, 2) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
                         const int rr = 16 * rb + 4 * g + q;
-                        const bool pos = (zm[col * 4 + (rr >> 3)] >> (rr & 7)) & 1u;
+                        const bool pos = (zm[sb][col * 4 + (rr >> 3)] >> (rr & 7)) & 1u;
                         const float v = pos ? acc[rb][q] * un2 : 0.0f;
                         gacc[rb][q] += v;
                         if (row0 + rr < p.n) p.gz1[((row0 + rr) * k + e) * BH + col] = v;
                     }
                 }
             }
-            __syncthreads();  // P1 of the next slot rewrites za / zb / zm; P2 gr / gt
+            // no barrier here: P1 of the next slot writes the other za / zb / zm
+            // buffer, and its P2 (gr / gt) starts only after the next P1
+            // barrier, which every wave reaches after this P3
         }
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb) {

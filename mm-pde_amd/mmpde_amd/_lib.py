@@ -118,6 +118,7 @@ _SIGS = {
                                     _P]),
     "mmpde_gnn_edge_backward_ex": (_I, [_P, _P, _P, _P, _I64, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
     "mmpde_linear_chain_workspace_bytes": (_I64, [_I64, _I, _P]),
+    "mmpde_linear_chain_dmm": (_I, [_I]),
     "mmpde_linear_chain_ws": (_I, [_P, _I64, _I64, _I, _P, _P, _P, _P, _P, _P, _I64, _P, _I64, _P]),
     "mmpde_traj_mse": (_I, [_P, _P, _I64, _I64, _P, _P]),
     "mmpde_conv2d": (_I, [_P, _I64, _I, _I, _I, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P]),

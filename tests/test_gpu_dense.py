@@ -200,3 +200,35 @@ def test_linear_chain_under_uneven_load(dev):
         assert err <= bound, (it, err, bound)
     for ws in ops._CHAIN_WS.values():
         assert int(ws[:4096].view(torch.int32).abs().sum()) == 0, "control / timeout words left non-zero"
+
+
+def test_linear_chains_concurrent_streams(dev):
+    """Two chains in flight at once on two streams, grids larger than half the
+    chip each: a workgroup only ever waits for items claimed before its own,
+    so concurrent chains cannot starve each other (the failure mode of a grid
+    barrier); every result against float64."""
+    from mmpde_amd import ops
+
+    g = torch.Generator().manual_seed(9)
+    specs = [CHAINS[0], CHAINS[1]]
+    chains = [_chain_layers(d, a, g, dev) for d, a in specs]
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    xs = [(ci, torch.randn(16, specs[ci][0][0], generator=g).to(dev)) for it in range(6) for ci in (0, 1)]
+    for ci in (0, 1):   # workspaces allocated (zeroed) before the concurrent launches
+        with torch.cuda.stream(streams[ci]):
+            ops.linear_chain(xs[ci][1], chains[ci])
+    torch.cuda.synchronize(dev)
+    outs = []
+    for ci, x in xs:   # launched back to back, no synchronisation in between
+        with torch.cuda.stream(streams[ci]):
+            outs.append(ops.linear_chain(x, chains[ci]))
+    torch.cuda.synchronize(dev)
+    for (ci, x), y in zip(xs, outs):
+        r = x.double()
+        for w, b, act in chains[ci]:
+            r = r @ w.double().t() + b.double()
+            r = torch.tanh(r) if act == 1 else r
+        bound = sum(_bound(r, k) for k in specs[ci][0][:-1]) * 4
+        assert (y.double() - r).abs().max().item() <= bound
+    for ws in ops._CHAIN_WS.values():
+        assert int(ws[:4096].view(torch.int32).abs().sum()) == 0, "control / timeout words left non-zero"
