@@ -191,16 +191,16 @@ def main():
     ap.add_argument("--serial", action="store_true",
                     help="one stream in every pass (per-kernel profiles without concurrent "
                          "kernels sharing the GPU)")
-    ap.add_argument("--no-chain", action="store_true",
-                    help="res_cut and the DMM output MLP as per-layer skinny launches instead "
-                         "of one linear-chain launch each (A/B)")
+    ap.add_argument("--chain", action="store_true",
+                    help="res_cut and the DMM output MLP as one linear-chain launch each "
+                         "instead of per-layer skinny launches (A/B: 2.077 vs 2.012 ms/step)")
     args = ap.parse_args()
 
     from mmpde_amd import _lib as L, ops
     from mmpde_amd import dist as D
-    if args.no_chain:
-        ops.CHAIN_RES_CUT = False
-        L.lib().mmpde_linear_chain_dmm(0)
+    if args.chain:
+        ops.CHAIN_RES_CUT = True
+        L.lib().mmpde_linear_chain_dmm(1)
     from mmpde_amd.rollout import MMPDERollout
     from mmpde_amd.synth import build_models, burgers_grid_points, fields
 

@@ -197,7 +197,7 @@ int mmpde_linear_skinny_ws(const float *x, int64_t ldx, int64_t m, int64_t k, co
  * words at zero again; the intermediate activations live after them). */
 int64_t mmpde_linear_chain_workspace_bytes(int64_t m, int nl, const int64_t *dims);
 /* Whether the DMM mesh / branch calls run their output MLP as one chain
- * launch (1, default) or as per-layer mmpde_linear_skinny_ws launches (0);
+ * launch (1) or as per-layer mmpde_linear_skinny_ws launches (0, default);
  * enable < 0 only queries.  Returns the previous setting.  Process-wide. */
 int mmpde_linear_chain_dmm(int enable);
 int mmpde_linear_chain_ws(const float *x, int64_t ldx, int64_t m, int nl, const int64_t *dims,

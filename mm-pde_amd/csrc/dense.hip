@@ -710,8 +710,9 @@ static int chain_specs(int64_t m, int nl, const int64_t *dims, const float *cons
 }
 
 // whether the DMM output MLP runs as one chain launch (dmm.hip) or as per-layer
-// skinny launches; both give the same results to fp32 rounding
-static int g_chain_dmm = 1;
+// skinny launches (the default: measured faster in the rollout step, DESIGN.md
+// §4); both give the same results to fp32 rounding
+static int g_chain_dmm = 0;
 namespace mmpde_detail {
 bool chain_dmm_enabled() { return g_chain_dmm != 0; }
 }  // namespace mmpde_detail

@@ -319,8 +319,9 @@ def linear_skinny(x: torch.Tensor, w: torch.Tensor, b=None, act: int = L.ACT_NON
 
 _CHAIN_WS = {}
 # res_cut's four layers as one chain launch (linear_chain) or four skinny
-# launches; the same results to fp32 rounding (tests/test_gpu_dense.py)
-CHAIN_RES_CUT = True
+# launches (the default: measured faster in the rollout step);
+# the same results to fp32 rounding (tests/test_gpu_dense.py)
+CHAIN_RES_CUT = False
 
 
 def linear_chain(x: torch.Tensor, layers, out: torch.Tensor | None = None) -> torch.Tensor:

@@ -406,7 +406,11 @@ def test_edge_mean_vs_torch_fp32(dev):
 
 
 # ============================================================================ DMM
-def test_dmm_mesh_graph_matches_autograd(dev):
+@pytest.mark.parametrize("chain", [0, 1])
+def test_dmm_mesh_graph_matches_autograd(dev, chain):
+    """chain: the output MLP + P as per-layer skinny launches (0, the default)
+    or one mmpde_linear_chain launch (1)."""
+    from mmpde_amd import _lib as L
     from mmpde_amd.synth import build_models, fields
 
     pde, _, _, _, dmm, _ = build_models("cy")
@@ -417,13 +421,20 @@ def test_dmm_mesh_graph_matches_autograd(dev):
                                          grid[None, :, 1].repeat(B, 1), grid)
     ref = torch.cat((ref_x, ref_y), -1)
     dmm.to(dev)
-    got = dmm.mesh(u.to(dev), grid.to(dev))
+    prev = L.lib().mmpde_linear_chain_dmm(chain)
+    try:
+        got = dmm.mesh(u.to(dev), grid.to(dev))
+        torch.cuda.synchronize()
+    finally:
+        L.lib().mmpde_linear_chain_dmm(prev)
     disp = (ref - grid.repeat(B, 1)).abs().max().item()
     assert disp > 1e-3                                         # the mesh actually moves
     _close(got, ref, 0.0, 2e-6, "dmm graph mesh")              # absolute, coords in [0,1]
 
 
-def test_dmm_mesh_array_matches_autograd(dev):
+@pytest.mark.parametrize("chain", [0, 1])
+def test_dmm_mesh_array_matches_autograd(dev, chain):
+    from mmpde_amd import _lib as L
     from mmpde_amd.synth import build_models, burgers_grid_points, fields
 
     pde, _, _, _, dmm, gc = build_models("burgers")
@@ -433,7 +444,12 @@ def test_dmm_mesh_array_matches_autograd(dev):
                                 48, 48)
     ref = torch.cat((ox, oy), -1)
     dmm.to(dev)
-    got = dmm.mesh(u.to(dev).contiguous(), gc.xi_grid_xy(48, 48, dev))
+    prev = L.lib().mmpde_linear_chain_dmm(chain)
+    try:
+        got = dmm.mesh(u.to(dev).contiguous(), gc.xi_grid_xy(48, 48, dev))
+        torch.cuda.synchronize()
+    finally:
+        L.lib().mmpde_linear_chain_dmm(prev)
     _close(got, ref, 0.0, 2e-6, "dmm array mesh")
 
 
