@@ -3,7 +3,7 @@
 # first, then the full GPU suite, the default bench line and a serial profile.
 set -u
 export TMPDIR=/tmp
-O=gpurun_out/r3q
+O=gpurun_out/${R3Q_OUT:-r3q}
 mkdir -p $O
 timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_dense.py > $O/dense.log 2>&1
 rc=$?; echo "dense rc=$rc"; grep -E "passed|failed" $O/dense.log | tail -2
