@@ -424,11 +424,12 @@ __global__ __launch_bounds__(512, 2) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
     if (g == 0) p.pb2[(int64_t)blockIdx.x * BH + col] = ((db + v1) + v2) + v3;
 }
 
-// max|a|, max|b|, max|g| over [n, 128] rows into mx[0..2] (float bits, zeroed
-// before): the fp16x3 backward's split scales.
+// max|a|, max|b|, max|g| over [n, 128] rows: per-workgroup maxima into
+// part[3][gridDim.x] (no atomics: 3 x 1024 adds on one line serialised at the
+// memory-side atomic unit took 148 us), reduced by maxabs3_final_kernel.
 __global__ __launch_bounds__(256) void maxabs3_kernel(const float *__restrict__ a, const float *__restrict__ b,
                                                       const float *__restrict__ gm, int64_t n4,
-                                                      unsigned *__restrict__ mx) {
+                                                      float *__restrict__ part) {
     float m[3] = {0.0f, 0.0f, 0.0f};
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
         const float4 x = ((const float4 *)a)[i], y = ((const float4 *)b)[i], z = ((const float4 *)gm)[i];
@@ -436,16 +437,29 @@ __global__ __launch_bounds__(256) void maxabs3_kernel(const float *__restrict__ 
         m[1] = fmaxf(m[1], fmaxf(fmaxf(fabsf(y.x), fabsf(y.y)), fmaxf(fabsf(y.z), fabsf(y.w))));
         m[2] = fmaxf(m[2], fmaxf(fmaxf(fabsf(z.x), fabsf(z.y)), fmaxf(fabsf(z.z), fabsf(z.w))));
     }
-    int vzero;
-    asm volatile("v_mov_b32 %0, 0" : "=v"(vzero));
+    __shared__ float red[3][4];
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
         const float w = wave_max(m[q]);
-        // the address through a VGPR: a vector-memory atomic (non-negative
-        // floats order like their bit patterns)
-        if ((threadIdx.x & 63) == 0)
-            __hip_atomic_fetch_max(mx + q + vzero, __float_as_uint(w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((threadIdx.x & 63) == 0) red[q][threadIdx.x >> 6] = w;
     }
+    __syncthreads();
+    if (threadIdx.x < 3)
+        part[threadIdx.x * gridDim.x + blockIdx.x] =
+            fmaxf(fmaxf(red[threadIdx.x][0], red[threadIdx.x][1]), fmaxf(red[threadIdx.x][2], red[threadIdx.x][3]));
+}
+
+// mx[q] = max over the G per-workgroup maxima of quantity q (float bits).
+__global__ __launch_bounds__(256) void maxabs3_final_kernel(const float *__restrict__ part, int G,
+                                                            unsigned *__restrict__ mx) {
+    __shared__ float red[4];
+    const int q = blockIdx.x;
+    float m = 0.0f;
+    for (int i = threadIdx.x; i < G; i += 256) m = fmaxf(m, part[q * G + i]);
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) mx[q] = __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
 }
 
 __global__ __launch_bounds__(256) void transpose128_kernel(const float *__restrict__ w, float *__restrict__ wt) {
@@ -463,7 +477,20 @@ __global__ __launch_bounds__(256) void edge_source_sum_kernel(const float *__res
     const int lane = threadIdx.x & 63;
     if (j >= n) return;
     float2 acc = make_float2(0.0f, 0.0f);
-    for (int64_t q = off[j]; q < off[j + 1]; ++q) {
+    int64_t q = off[j];
+    const int64_t qe = off[j + 1];
+    // eight rows in flight per step, added in list order (the same sums)
+    for (; q + 8 <= qe; q += 8) {
+        float2 v[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v[t] = ((const float2 *)(rows + edge[q + t] * BH))[lane];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            acc.x += v[t].x;
+            acc.y += v[t].y;
+        }
+    }
+    for (; q < qe; ++q) {
         const float2 v = ((const float2 *)(rows + edge[q] * BH))[lane];
         acc.x += v.x;
         acc.y += v.y;
@@ -491,14 +518,22 @@ __global__ __launch_bounds__(256) void partial_sum_kernel(const float *__restric
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= len) return;
     float s = 0.0f;
-    for (int q = 0; q < G; ++q) s += part[(int64_t)q * len + i];
+    int q = 0;
+    for (; q + 8 <= G; q += 8) {  // eight partials in flight, added in g order
+        float v[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v[t] = part[(int64_t)(q + t) * len + i];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) s += v[t];
+    }
+    for (; q < G; ++q) s += part[(int64_t)q * len + i];
     out[i] = s;
 }
 
 }  // namespace
 
 constexpr int64_t kBwdImg = (BH * BH * 4 + BH * 4) / 4;     // floats of one packed W2 image
-constexpr int64_t kBwdExtra = 2 * kBwdImg + BH * BH + 64;     // images, W2^T, maxima
+constexpr int64_t kBwdExtra = 2 * kBwdImg + BH * BH + 64 + 3 * 1024;  // images, W2^T, maxima
 
 extern "C" int64_t mmpde_gnn_edge_backward_partials(int *grid) {
     int dev = 0, cus = 256;
@@ -571,13 +606,11 @@ extern "C" int mmpde_gnn_edge_backward_ex(const float *a, const float *b, const 
     hipLaunchKernelGGL((pack_f16x3_kernel<BH>), dim3(BH, 1), dim3(BH), 0, st, s1, 0, (int64_t)0, (int64_t)BH, img1);
     hipLaunchKernelGGL((pack_f16x3_kernel<BH>), dim3(BH, 1), dim3(BH), 0, st, s2, 0, (int64_t)0, (int64_t)BH, img2);
     MMPDE_RET_LAUNCH();
-    {
-        const hipError_t me = hipMemsetAsync(mx, 0, 4 * sizeof(unsigned), st);
-        if (me != hipSuccess) return MMPDE_ERR_HIP_BASE - (int)me;
-    }
     const int64_t n4 = n * BH / 4;
-    hipLaunchKernelGGL(maxabs3_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(n4, 256), 1024)), dim3(256), 0, st,
-                       a, b, grad_mean, n4, mx);
+    const int mg = (int)std::min<int64_t>(ceil_div(n4, 256), 1024);
+    float *mpart = (float *)(mx + 64);  // 3 x mg per-workgroup maxima
+    hipLaunchKernelGGL(maxabs3_kernel, dim3((unsigned)mg), dim3(256), 0, st, a, b, grad_mean, n4, mpart);
+    hipLaunchKernelGGL(maxabs3_final_kernel, dim3(3), dim3(256), 0, st, mpart, mg, mx);
     MMPDE_RET_LAUNCH();
     EdgeBwdF16Args p{a, b, nbr, deg, n, k, (int)ntiles, img1, img2, msg2_b, grad_mean, mx, grad_a, grad_edge,
                      pw2, pb2};

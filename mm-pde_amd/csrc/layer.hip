@@ -523,6 +523,19 @@ constexpr int NLD = 132;  // fp32 staging row stride (floats)
 #define MMPDE_NODE_WPE 4
 #endif
 constexpr int NODE_WPE = MMPDE_NODE_WPE;  // node / embed launch bounds: waves per SIMD
+// node / embed kernels: issue B operands one phase before their GEMMs instead
+// of just before them.  EARLY_U2: update_net_2's (dead bH / bM registers);
+// EARLY_B: the next projections' b' operands beside a' (measured: node
+// 50.6-51.1 vs 50.0-50.2 us, embed 45.2-45.4 vs 42.8-43.0 us with 4 spills;
+// off).  Same arithmetic either way.
+#ifndef MMPDE_NODE_EARLY_U2
+#define MMPDE_NODE_EARLY_U2 1
+#endif
+#ifndef MMPDE_NODE_EARLY_B
+#define MMPDE_NODE_EARLY_B 0
+#endif
+constexpr bool NODE_EARLY_U2 = MMPDE_NODE_EARLY_U2 != 0;
+constexpr bool NODE_EARLY_B = MMPDE_NODE_EARLY_B != 0;
 
 // Operand images in LDS, per 16-row block rb and K step s (1 KB units of 64
 // lanes x 16 B): F16X3 [rb][s (32-wide)][hi|lo] with lane (r, g) holding
@@ -877,6 +890,9 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs2 pp) {
         gemm_tile<F16X3, RB, S1>(aH, img, 256, 0, bH, lane);
         if (!PRE) bM.load(p.pk + kPkU1, 8, wave, S1, wu1, 128, lane);
         gemm_tile<F16X3, RB, S1>(F16X3 ? aM : aH, img, 256, S1, bM, lane);
+        // update_net_2's operands issued now (bH / bM are dead): in flight over
+        // this epilogue, the operand prep and its two barriers
+        if (!PRE && NODE_EARLY_U2) bU2.load(p.pk + kPkU2, 4, wave, 0, wu2, 0, lane);
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) {
 #pragma unroll
@@ -893,15 +909,17 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs2 pp) {
     __syncthreads();
 
     // ---- update_net_2 + residual + BatchNorm(eval)
-    BOps<F16X3, S1> bA;
+    BOps<F16X3, S1> bA, bB;
     {
         f32x4 acc[RB];
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) acc[rb] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
-        if (!PRE) bU2.load(p.pk + kPkU2, 4, wave, 0, wu2, 0, lane);
+        if (!PRE && !NODE_EARLY_U2) bU2.load(p.pk + kPkU2, 4, wave, 0, wu2, 0, lane);
         gemm_tile<F16X3, RB, S1>(acc, img, 128, 0, bU2, lane);
-        // next layer's message_net_1 operands of a' (column tile wave)
+        // next layer's message_net_1 operands of a' (column tile wave), and of
+        // b' with NODE_EARLY_B (both in flight over the epilogue and the prep)
         if (NEXT) bA.load(p.pkn + kPkW1, 4, wave, 0, w1r, 0, lane);
+        if (NEXT && NODE_EARLY_B) bB.load(p.pkn + kPkW1, 4, 8 + wave, 0, w1r, 128, lane);
         const bool full = row0 + ROWS <= p.n;
         float *hp = p.h_out + (row0 + 4 * g) * LH + col;
 #pragma unroll
@@ -924,7 +942,7 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs2 pp) {
         __syncthreads();
         // ---- next layer's message_net_1 node halves
         proj_phase<F16X3, RB>(bA, img, rs[3], &rowv[0][0], w1c, p.pkn, w1r, tw, row0, p.n, p.seg_n,
-                              p.a_out, p.b_out, p.rng_out, wave, lane);
+                              p.a_out, p.b_out, p.rng_out, wave, lane, NODE_EARLY_B ? &bB : nullptr);
     }
 }
 
@@ -1030,7 +1048,7 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_embed_kernel(EmbedArgs2 pp)
     __syncthreads();
     prep<F16X3, ROWS>(stage, NLD, 0, ROWS, false, img, 128, 0, rsz);
     __syncthreads();
-    BOps<F16X3, S1> bA;
+    BOps<F16X3, S1> bA, bB;
     {
         f32x4 acc[RB];
 #pragma unroll
@@ -1045,6 +1063,7 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_embed_kernel(EmbedArgs2 pp)
             gemm_tile<false, RB, 8>(acc, img, 128, 0, b3, lane);
         }
         bA.load(p.pk + kPkW1, 4, wave, 0, w1r, 0, lane);
+        if (NODE_EARLY_B) bB.load(p.pk + kPkW1, 4, 8 + wave, 0, w1r, 128, lane);
         const bool full = row0 + ROWS <= p.n;
         float *hp = p.h_out + (row0 + 4 * g) * LH + col;
 #pragma unroll
@@ -1062,7 +1081,7 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_embed_kernel(EmbedArgs2 pp)
     prep<F16X3, ROWS>(stage, NLD, 0, ROWS, false, img, 128, 0, rs);
     __syncthreads();
     proj_phase<F16X3, RB>(bA, img, rs, &rowv[0][0], w1c, p.pk, w1r, tw, row0, p.n, p.seg_n,
-                          p.a_out, p.b_out, p.rng_out, wave, lane);
+                          p.a_out, p.b_out, p.rng_out, wave, lane, NODE_EARLY_B ? &bB : nullptr);
 }
 
 inline bool al16(const void *q) { return ((uintptr_t)q & 15u) == 0; }

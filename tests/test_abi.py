@@ -72,6 +72,7 @@ def test_edge_backward_partials_sizing_without_gpu():
     g = ctypes.c_int(0)
     n = _lib.lib().mmpde_gnn_edge_backward_partials(ctypes.byref(g))
     # per-workgroup dW2 / db2 partials, then the fp16x3 mode's two W2 images
-    # (128 x 128 fp16 hi / lo + 128 column scales each), W2^T and the maxima
-    extra = 2 * (128 * 128 * 4 + 128 * 4) // 4 + 128 * 128 + 64
+    # (128 x 128 fp16 hi / lo + 128 column scales each), W2^T, the maxima and
+    # their per-workgroup partials
+    extra = 2 * (128 * 128 * 4 + 128 * 4) // 4 + 128 * 128 + 64 + 3 * 1024
     assert g.value > 0 and n == g.value * (128 * 128 + 128) + extra
