@@ -535,6 +535,12 @@ constexpr int NODE_WPE = MMPDE_NODE_WPE;  // node / embed launch bounds: waves p
 #define MMPDE_NODE_EARLY_B 0
 #endif
 constexpr bool NODE_EARLY_U2 = MMPDE_NODE_EARLY_U2 != 0;
+// EARLY_M: update_net_1's mean-half operands beside the h-half ones at the
+// start, in the last layer's kernel (with the next projections it spills)
+#ifndef MMPDE_NODE_EARLY_M
+#define MMPDE_NODE_EARLY_M 1
+#endif
+constexpr bool NODE_EARLY_M = MMPDE_NODE_EARLY_M != 0;
 constexpr bool NODE_EARLY_B = MMPDE_NODE_EARLY_B != 0;
 
 // Operand images in LDS, per 16-row block rb and K step s (1 KB units of 64
@@ -865,8 +871,8 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs2 pp) {
     constexpr bool PRE = RB >= 4;
     BOps<F16X3, S1> bH, bM, bU2;
     bH.load(p.pk + kPkU1, 8, wave, 0, wu1, 0, lane);
+    if (PRE || (NODE_EARLY_M && !NEXT)) bM.load(p.pk + kPkU1, 8, wave, S1, wu1, 128, lane);
     if (PRE) {
-        bM.load(p.pk + kPkU1, 8, wave, S1, wu1, 128, lane);
         bU2.load(p.pk + kPkU2, 4, wave, 0, wu2, 0, lane);
     }
 
@@ -888,7 +894,7 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs2 pp) {
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) aH[rb] = aM[rb] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
         gemm_tile<F16X3, RB, S1>(aH, img, 256, 0, bH, lane);
-        if (!PRE) bM.load(p.pk + kPkU1, 8, wave, S1, wu1, 128, lane);
+        if (!PRE && !(NODE_EARLY_M && !NEXT)) bM.load(p.pk + kPkU1, 8, wave, S1, wu1, 128, lane);
         gemm_tile<F16X3, RB, S1>(F16X3 ? aM : aH, img, 256, S1, bM, lane);
         // update_net_2's operands issued now (bH / bM are dead): in flight over
         // this epilogue, the operand prep and its two barriers
