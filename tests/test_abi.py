@@ -64,6 +64,14 @@ def test_null_arguments_are_rejected_before_launch():
                                      None) == -1
     assert lib.mmpde_linear_chain_workspace_bytes(16, 4, dims) >= (4096 + 16 * (2048 + 512 + 2048)) * 4
     assert lib.mmpde_linear_chain_workspace_bytes(16, 5, dims) == 0
+    # the DMM chain switch: query (-1) leaves it, set returns the previous value
+    cur = lib.mmpde_linear_chain_dmm(-1)
+    assert lib.mmpde_linear_chain_dmm(1 - cur) == cur and lib.mmpde_linear_chain_dmm(cur) == 1 - cur
+    # fp16x3 edge backward: null pointers and an unknown GEMM mode refused before any launch
+    assert lib.mmpde_gnn_edge_backward_ex(None, None, None, None, 10, 35, None, None, None, None, None,
+                                          None, None, None, 1, None) == -1
+    assert lib.mmpde_gnn_edge_backward_ex(None, None, None, None, 10, 35, None, None, None, None, None,
+                                          None, None, None, 7, None) == -1
 
 
 def test_edge_backward_partials_sizing_without_gpu():
