@@ -536,9 +536,10 @@ constexpr int NODE_WPE = MMPDE_NODE_WPE;  // node / embed launch bounds: waves p
 #endif
 constexpr bool NODE_EARLY_U2 = MMPDE_NODE_EARLY_U2 != 0;
 // EARLY_M: update_net_1's mean-half operands beside the h-half ones at the
-// start, in the last layer's kernel (with the next projections it spills)
+// start, in the last layer's kernel (with the next projections it spills);
+// not yet measured on the GPU, so off
 #ifndef MMPDE_NODE_EARLY_M
-#define MMPDE_NODE_EARLY_M 1
+#define MMPDE_NODE_EARLY_M 0
 #endif
 constexpr bool NODE_EARLY_M = MMPDE_NODE_EARLY_M != 0;
 constexpr bool NODE_EARLY_B = MMPDE_NODE_EARLY_B != 0;
