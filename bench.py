@@ -7,9 +7,11 @@
 A *step* is one full MM-PDE forward step over the rank's trajectories (DMM
 moved mesh, moved-mesh kNN-35 graph, model_b, kNN-30 + ItpNet interpolation +
 res_cut, model on the fixed-grid graph, sum), fed back autoregressively.
-Default workload = BASELINE config 4: cylinder MM-PDE, 16 trajectories of the
-2521-node mesh per GPU (weak scaling: trajectories shard across ranks, no
-data-path collective).  value = node-updates/s of the whole job
+Default workload = BASELINE configs[3]: cylinder MM-PDE, 16 trajectories of
+the 2521-node mesh per GPU (weak scaling: trajectories shard across ranks, no
+data-path collective).  --global-trajectories G fixes the job instead
+(configs[4]'s strong-scaling half: G = 64 split over the ranks, "scaling":
+"strong").  value = node-updates/s of the whole job
 = trajectories_total * 2521 * K / max-over-ranks(time of the K timed steps).
 
 Also reported (rank 0):
@@ -114,20 +116,12 @@ class EdgeTracer:
         self.traces.append((t, arr))
         return t
 
-    def launch_times_ms(self, paired=False):
-        """[(layer index, edge-stage ms, node-stage ms)] for every traced layer.
-        paired: consecutive forwards (model, model_b of one step) shared one
-        node-stage launch per layer (gnn_2d.forward_pair), which starts after
-        model_b's edge stage: each gets half of that launch."""
+    def launch_times_ms(self):
+        """[(layer index, edge-stage ms, node-stage ms)] for every traced layer."""
         out = []
-        for i, (_, (beg, mid, end)) in enumerate(self.traces):
+        for _, (beg, mid, end) in self.traces:
             for l in range(self.L):
-                if paired:
-                    _, (_, mid_b, end_b) = self.traces[i | 1]
-                    node = 0.5 * self.pool.elapsed_ms(mid_b[l], end_b[l])
-                else:
-                    node = self.pool.elapsed_ms(mid[l], end[l])
-                out.append((l, self.pool.elapsed_ms(beg[l], mid[l]), node))
+                out.append((l, self.pool.elapsed_ms(beg[l], mid[l]), self.pool.elapsed_ms(mid[l], end[l])))
         return out
 
 
@@ -177,7 +171,12 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="cy-mmpde", choices=sorted(CONFIGS))
-    ap.add_argument("--batch", type=int, default=None, help="trajectories per GPU")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="trajectories per GPU (weak scaling: the job grows with --gpus)")
+    ap.add_argument("--global-trajectories", type=int, default=None,
+                    help="a FIXED number of trajectories for the whole job, sharded "
+                         "contiguously across the ranks (strong scaling, BASELINE "
+                         "configs[4]: 64 over 1/2/4/8 GPUs)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--edge-gemm", default="f16x3", choices=["f32", "f16x3"],
@@ -191,16 +190,9 @@ def main():
     ap.add_argument("--serial", action="store_true",
                     help="one stream in every pass (per-kernel profiles without concurrent "
                          "kernels sharing the GPU)")
-    ap.add_argument("--chain", action="store_true",
-                    help="res_cut and the DMM output MLP as one linear-chain launch each "
-                         "instead of per-layer skinny launches (A/B: 2.077 vs 2.012 ms/step)")
     args = ap.parse_args()
 
-    from mmpde_amd import _lib as L, ops
     from mmpde_amd import dist as D
-    if args.chain:
-        ops.CHAIN_RES_CUT = True
-        L.lib().mmpde_linear_chain_dmm(1)
     from mmpde_amd.rollout import MMPDERollout
     from mmpde_amd.synth import build_models, burgers_grid_points, fields
 
@@ -210,9 +202,19 @@ def main():
     device = torch.device(f"cuda:{local}")
     torch.cuda.set_device(device)
     kind, moving, b_default, cfg_name, side = CONFIGS[args.config]
-    B = args.batch or b_default
-    total = B * world
+    strong = args.global_trajectories is not None
+    if strong:
+        if args.batch is not None:
+            raise SystemExit("--batch (per GPU) and --global-trajectories (whole job) exclude each other")
+        total = args.global_trajectories
+        if total < world:
+            raise SystemExit("--global-trajectories must give every rank at least one trajectory")
+        cfg_name = ("configs[4]: Cylinder MM-PDE batched rollout, trajectories sharded across GPUs"
+                    if kind == "cy" and moving else cfg_name)
+    else:
+        total = (args.batch or b_default) * world
     lo, hi = D.shard_range(total, rank, world)
+    B = hi - lo
 
     pde, model, model_b, itp, dmm, gc = build_models(kind, moving_mesh=moving)
     if kind == "burgers" and side != 48:
@@ -276,10 +278,10 @@ def main():
     if not args.no_f32_exact and args.edge_gemm != "f32":
         el32, u32 = timed_run("f32", False)
         rel = ((u - u32).abs().max() / u32.abs().max().clamp_min(1e-30)).item()
-        exact = {"value": (hi - lo) * world * n_nodes * args.steps / el32,
+        exact = {"value": total * n_nodes * args.steps / el32,
                  "ms_per_step": 1e3 * el32 / args.steps,
                  "final_state_max_rel_diff_vs_main": rel}
-    launches = tracer.launch_times_ms(paired=moving and eng.pair)
+    launches = tracer.launch_times_ms()
     tracer.pool.close()
 
     if rank != 0:
@@ -316,15 +318,18 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": 1e3 * elapsed / args.steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "f32" if args.edge_gemm == "f32" else "f32 (edge GEMM fp32-emulated by fp16x3 split, fp32 accumulate)",
         "data": "synthetic: seeded cy-synth 2521-node mesh / 48x48 grid, seeded sin-cos+noise "
                 "fields, seeded default-init weights (no dataset or checkpoint offline)",
         "config": {"workload": args.config, "baseline_config": cfg_name,
-                   "trajectories_per_gpu": B, "global_trajectories": total,
+                   "trajectories_per_gpu": B if not strong else total / world,
+                   "global_trajectories": total,
                    "nodes_per_trajectory": n_nodes, "neighbors": gc.n, "time_window": 1,
                    "parallelism": f"trajectory-shard x{world} (no data-path collective)",
+                   "shard": "contiguous trajectory blocks, dist.shard_range; rank 0 holds "
+                            f"{hi - lo}",
                    "rollout": "autoregressive (pred -> next input)",
                    "launch": "hipGraph replay of the step" if args.graph else "eager, three HIP streams"},
         "roofline": {"kernel": ("gnn_edge_wave_kernel" if args.edge_gemm == "f16x3" else "gnn_edge_kernel")

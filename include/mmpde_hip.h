@@ -183,28 +183,6 @@ int mmpde_linear_skinny_ws(const float *x, int64_t ldx, int64_t m, int64_t k, co
                            int64_t ldw, const float *b, int64_t n, int act, float *y, int64_t ldy,
                            float *workspace, int64_t workspace_bytes, mmpde_stream_t stream);
 
-/* A chain of nl <= 4 skinny linears in ONE launch (the res_cut MLP,
- * interpolate.py:66-74 / :95-97; the DMM output_mlp, mesh/dmm_model.py:175-181):
- *   x_0 = x [m, dims[0]],  x_{l+1} = act[l](x_l . w[l]^T + b[l])   (w[l]: [dims[l+1], dims[l]],
- *   row stride ldw[l] or dims[l] when ldw is NULL; b NULL or b[l] NULL: no bias),
- * y = x_nl [m, dims[nl]] (row stride ldy).  m <= 64.  A persistent grid walks
- * each layer's (16 x 16 tile, K split) items and meets at a grid barrier
- * between layers, issuing its next weights before it waits.  Per item the
- * arithmetic is mmpde_linear_skinny_ws's (exact fp32 MFMA products, fixed
- * summation order, a K split that depends on (n, k) only).  workspace: at
- * least mmpde_linear_chain_workspace_bytes(m, nl, dims) bytes, 4-B aligned,
- * ZEROED before its first use and reused (each call leaves its first 4096
- * words at zero again; the intermediate activations live after them). */
-int64_t mmpde_linear_chain_workspace_bytes(int64_t m, int nl, const int64_t *dims);
-/* Whether the DMM mesh / branch calls run their output MLP as one chain
- * launch (1) or as per-layer mmpde_linear_skinny_ws launches (0, default);
- * enable < 0 only queries.  Returns the previous setting.  Process-wide. */
-int mmpde_linear_chain_dmm(int enable);
-int mmpde_linear_chain_ws(const float *x, int64_t ldx, int64_t m, int nl, const int64_t *dims,
-                          const float *const *w, const int64_t *ldw, const float *const *b,
-                          const int *act, float *y, int64_t ldy, void *workspace,
-                          int64_t workspace_bytes, mmpde_stream_t stream);
-
 /* out[b] = mean_i (pred[b, i] - labels[b, i])^2 per trajectory b (n_per values
  * each): the loss of mmpde.py:33-36 (MSELoss) kept per trajectory for the
  * sharded teacher-forced evaluation (train_helper_2d.py:184-185,193-198).
@@ -428,31 +406,6 @@ int mmpde_gnn_forward_ex(const float *u, const float *pos, int64_t n, int k, con
                          const mmpde_gnn_head_params *head, void *workspace, float *out,
                          const mmpde_gnn_exec *exec, mmpde_stream_t stream);
 
-/* One mmpde_gnn_forward_ex call's arguments (mmpde_gnn_forward_pair). */
-typedef struct {
-    const float *u, *pos;
-    int64_t n;
-    int k;
-    const int32_t *nbr;
-    mmpde_gnn_scales sc;
-    const mmpde_gnn_embed_params *emb;
-    const mmpde_gnn_layer_params *layers;
-    int n_layers;
-    const mmpde_gnn_head_params *head;
-    void *workspace; /* mmpde_gnn_workspace_bytes(n), one per call */
-    float *out;
-    const mmpde_gnn_exec *exec;
-} mmpde_gnn_call;
-
-/* Two independent GNN forwards -- the MM-PDE step's `model(graph_uniform)` and
- * `model_b(graph)` (reference train_helper_2d.py:174-185) -- as one sequence of
- * launches: one embedding launch over both problems' rows, per layer the two
- * edge stages then ONE node-stage launch over both, one head launch.  Each
- * output equals mmpde_gnn_forward_ex's for its call, bit for bit.  Both calls:
- * F16X3 with exec->packed images, the same n_layers (>= 1) and time window;
- * their events are recorded around their own edge stages and after the shared
- * node stage. */
-int mmpde_gnn_forward_pair(const mmpde_gnn_call *calls, mmpde_stream_t stream);
 
 /* ------------------------------------------------------------------------
  * DMM mesh mover (reference mesh/dmm_model.py, data_creator_2d.py:88-137)

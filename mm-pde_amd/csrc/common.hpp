@@ -142,22 +142,4 @@ __attribute__((visibility("hidden"))) int conv2d(const float *x, int64_t batches
                                                  const float *residual, int act, float *y,
                                                  hipStream_t st, unsigned *zero, int n_zero,
                                                  int circular = 0, int res_after_act = 0);
-// One layer of a linear chain (dense.hip linear_chain_kernel): y = act(x . w^T
-// + b), x = the previous layer's y (the chain's input for layer 0), k = the
-// previous n.  y == nullptr: the output lives in the chain's workspace.
-struct ChainSpec {
-    const float *w;
-    int64_t ldw;
-    const float *b;
-    int64_t n, k;
-    int act;
-    float *y;
-    int64_t ldy;
-};
-__attribute__((visibility("hidden"))) bool chain_ok(int64_t m, int nl, const ChainSpec *sp);
-__attribute__((visibility("hidden"))) bool chain_dmm_enabled();
-__attribute__((visibility("hidden"))) int64_t chain_ws_bytes(int64_t m, int nl, const ChainSpec *sp);
-__attribute__((visibility("hidden"))) int linear_chain(const float *x, int64_t ldx, int64_t m, int nl,
-                                                       const ChainSpec *sp, void *workspace,
-                                                       int64_t workspace_bytes, hipStream_t st);
 }  // namespace mmpde_detail

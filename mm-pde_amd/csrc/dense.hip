@@ -162,276 +162,15 @@ __global__ __launch_bounds__(kSkW * 64) void linear_skinny_kernel(const float *_
     }
 }
 
-// ---------------------------------------------------------------------------
-// A chain of skinny linears in ONE launch (res_cut's 4-layer MLP,
-// interpolate.py:66-74; the DMM output_mlp + P = Wb . branch,
-// mesh/dmm_model.py:175-181): a persistent grid walks each layer's work items
-// (16 x 16 output tile x K split, the linear_skinny_kernel item above, same
-// per-item arithmetic); an item of layer l + 1 starts once every item of layer
-// l is done.  What the fusion buys is that wait's shadow: a workgroup issues
-// the weight loads of its next item before it waits (weights do not depend on
-// the activations), so a layer's weight stream starts while the previous layer
-// drains.  Activations written inside the
-// launch go through write-through agent-scope stores and are read back with
-// agent-scope loads (no release / acquire fences: the XCD L2s are not
-// coherent, the sc1 path is); every buffer is written once per launch.
-// The control words reset themselves (the last workgroup to leave zeroes
-// them), so a zeroed workspace serves every later launch.
-constexpr int kChainMax = 4;           // layers per launch
-constexpr int kChainTickets = 960;     // ticket words per layer (output tiles)
-constexpr int kChainCtl = 256;         // control words before the tickets (4096 words in all)
-// control words, each on a 128-B line of its own (the claim counter is not
-// slowed by the polls of the done counters): claims, exits, timeout, done[l]
-constexpr int kCtlClaim = 0, kCtlExit = 32, kCtlTimeout = 64, kCtlDone = 96;  // done[l] at kCtlDone + 32 l
-
-struct ChainLayer {
-    const float *w, *b;
-    float *y, *part;   // output (row stride ldy); split-K partials (z > 1)
-    int64_t ldw, ldy, n, k;
-    int act, z, nchz, ctiles, items;
-};
-
-struct ChainArgs {
-    ChainLayer L[kChainMax];
-    const float *x;
-    int64_t ldx, m;
-    int nl, rtiles;
-    unsigned *ctl;     // control words (kCtl*), tickets from kChainCtl
-};
-
-__device__ __forceinline__ float ld_agent(const float *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_agent(float *p, float v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// item -> (column tile, row tile, split): the split is the slowest index
-struct ChainItem {
-    int64_t col0, row0;
-    int zz, c0, nch;
-};
-__device__ __forceinline__ ChainItem chain_item(const ChainLayer &Ly, int rtiles, int it, int C) {
-    ChainItem c;
-    const int T = Ly.ctiles * rtiles;
-    c.zz = it / T;
-    const int t = it - c.zz * T;
-    c.col0 = (int64_t)(t % Ly.ctiles) * 16;
-    c.row0 = (int64_t)(t / Ly.ctiles) * 16;
-    c.c0 = c.zz * Ly.nchz;
-    c.nch = min(((int)Ly.k + C - 1) / C - c.c0, Ly.nchz);
-    return c;
-}
-
-template <int kSkW>
-__device__ __forceinline__ void chain_loadw(const ChainLayer &Ly, int64_t col0, int kc, float (&lw)[16]) {
-    const int kk = kc + (int)threadIdx.x;
-    const bool ok = kk < Ly.k;
-    const int o = ok ? kk : 0;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const float a = Ly.w[min(col0 + i, Ly.n - 1) * Ly.ldw + o];
-        lw[i] = ok ? a : 0.0f;
-    }
-}
-
-__device__ __forceinline__ void chain_wait(const unsigned *ctr, unsigned target, unsigned *timeout) {
-    // bounded spin (100 ms of the 100 MHz real-time clock: a fault cannot
-    // hang the queue; a timeout sets the sticky word), then one agent-scope
-    // acquire waited before the workgroup barrier that follows
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-        __builtin_amdgcn_s_sleep(8);
-        if (__builtin_amdgcn_s_memrealtime() - t0 > 10000000ull) {
-            __hip_atomic_store(timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-// One item (16 x 16 output tile x K split) of chain layer LI: its weights are
-// issued first, then (LI > 0) the wait for every item of layer LI - 1, then the
-// activations (agent-scope loads) and the item as in linear_skinny_kernel.
-template <int kSkW, int LI>
-__device__ __forceinline__ void chain_item_run(const ChainArgs &a, int it, unsigned *ctl, float *sw, float *sx) {
-    constexpr int C = 64 * kSkW, LD = C + 4;
-    const ChainLayer &Ly = a.L[LI];
-    const float *x = LI ? a.L[LI > 0 ? LI - 1 : 0].y : a.x;
-    const int64_t ldx = LI ? a.L[LI > 0 ? LI - 1 : 0].ldy : a.ldx;
-    const bool last = LI + 1 == a.nl;
-    unsigned *tickets = ctl + kChainCtl + LI * kChainTickets;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int r = lane & 15, g = lane >> 4;
-    const int K = (int)Ly.k;
-    const int64_t m = a.m, n = Ly.n;
-    const ChainItem ci = chain_item(Ly, a.rtiles, it, C);
-    float lw[16], lx[16];
-    chain_loadw<kSkW>(Ly, ci.col0, ci.c0 * C, lw);
-    if (LI > 0) {
-        if (tid == 0)
-            chain_wait(ctl + kCtlDone + 32 * (LI > 0 ? LI - 1 : 0), (unsigned)a.L[LI > 0 ? LI - 1 : 0].items,
-                       ctl + kCtlTimeout);
-        __syncthreads();
-    }
-    auto loadx = [&](int kc) {
-        const int kk = kc + tid;
-        const bool ok = kk < K;
-        const int o = ok ? kk : 0;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const float *p = x + min(ci.row0 + i, m - 1) * ldx + o;
-            const float c = LI ? ld_agent(p) : *p;
-            lx[i] = ok ? c : 0.0f;
-        }
-    };
-    loadx(ci.c0 * C);
-    f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-    for (int c = 0; c < ci.nch; ++c) {
-        if (c) __syncthreads();  // chunk c - 1 consumed
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            sw[i * LD + tid] = lw[i];
-            sx[i * LD + tid] = lx[i];
-        }
-        __syncthreads();
-        if (c + 1 < ci.nch) {
-            chain_loadw<kSkW>(Ly, ci.col0, (ci.c0 + c + 1) * C, lw);
-            loadx((ci.c0 + c + 1) * C);
-        }
-        const float *aw = sw + r * LD + 64 * wave + 4 * g;
-        const float *ax = sx + r * LD + 64 * wave + 4 * g;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const float4 wv = *(const float4 *)(aw + 16 * q);
-            const float4 xv = *(const float4 *)(ax + 16 * q);
-            acc = mfma16(xv.x, wv.x, acc);
-            acc = mfma16(xv.y, wv.y, acc);
-            acc = mfma16(xv.z, wv.z, acc);
-            acc = mfma16(xv.w, wv.w, acc);
-        }
-    }
-    __syncthreads();
-    f32x4 *wpart = (f32x4 *)sw;  // [wave][lane]
-    wpart[wave * 64 + lane] = acc;
-    __syncthreads();
-    if (wave == 0) {
-        f32x4 s = wpart[lane];
-#pragma unroll
-        for (int v = 1; v < kSkW; ++v) s += wpart[v * 64 + lane];
-        const int64_t col = ci.col0 + r;
-        bool write = true;
-        if (Ly.z > 1) {
-            // split-K hand-off as in linear_skinny_kernel (sc1 partials, a
-            // ticket per tile, the last slice adds the slices in z order)
-            float *pz = Ly.part + (int64_t)ci.zz * m * n;
-            if (col < n) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int64_t row = ci.row0 + 4 * g + q;
-                    if (row < m) st_agent(pz + row * n + col, s[q]);
-                }
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const int T = Ly.ctiles * a.rtiles;
-            unsigned *tk = tickets + (it - ci.zz * T);
-            unsigned ticket = 0u;
-            if (lane == 0) ticket = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            ticket = __builtin_amdgcn_readfirstlane(ticket);
-            write = ticket == (unsigned)(Ly.z - 1);
-            if (write) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                const int64_t cc = min(col, n - 1);
-                float v[kSkMaxZ][4];
-#pragma unroll
-                for (int zz = 0; zz < kSkMaxZ; ++zz) {
-                    if (zz < Ly.z) {
-                        const float *pq = Ly.part + (int64_t)zz * m * n + cc;
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) v[zz][q] = ld_agent(pq + min(ci.row0 + 4 * g + q, m - 1) * n);
-                    }
-                }
-                f32x4 t = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-                for (int zz = 0; zz < kSkMaxZ; ++zz) {
-                    if (zz < Ly.z) {
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) t[q] += v[zz][q];
-                    }
-                }
-                if (lane == 0) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                s = t;
-            }
-        }
-        if (write && col < n) {
-            const float bb = Ly.b ? Ly.b[col] : 0.0f;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int64_t row = ci.row0 + 4 * g + q;
-                if (row < m) {
-                    const float v = act_apply(s[q] + bb, Ly.act);
-                    if (last) Ly.y[row * Ly.ldy + col] = v;
-                    else st_agent(Ly.y + row * Ly.ldy + col, v);
-                }
-            }
-        }
-        // the item is done once its stores have drained
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0) __hip_atomic_fetch_add(ctl + kCtlDone + 32 * LI, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();  // wpart (sw) read before the next item's chunk store
-}
-
-// Items are CLAIMED from one counter over the flattened (layer, item) list, so
-// a workgroup waits only for items of the previous layer, which carry smaller
-// indices and were therefore claimed by workgroups already running: the wait
-// cannot depend on a workgroup that is not resident, whatever else shares the
-// GPU (other streams, other processes) and however large the grid.  Control
-// words (kCtl*): the claim counter, exits, a sticky wait timeout, items done
-// per layer; the last workgroup to exit zeroes them.
-template <int kSkW>
-__global__ __launch_bounds__(kSkW * 64, 4) void linear_chain_kernel(ChainArgs a) {
-    constexpr int C = 64 * kSkW, LD = C + 4;
-    __shared__ float sw[16 * LD], sx[16 * LD];
-    __shared__ int s_it;
-    // control words through a VGPR base: vector-memory atomics only
-    int vzero;
-    asm volatile("v_mov_b32 %0, 0" : "=v"(vzero));
-    unsigned *ctl = a.ctl + vzero;
-    const int n0 = a.L[0].items, n1 = a.nl > 1 ? a.L[1].items : 0, n2 = a.nl > 2 ? a.L[2].items : 0,
-              n3 = a.nl > 3 ? a.L[3].items : 0;
-    const int total = n0 + n1 + n2 + n3;
-    for (;;) {
-        if (threadIdx.x == 0)
-            s_it = (int)__hip_atomic_fetch_add(ctl + kCtlClaim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();
-        const int it = s_it;
-        if (it >= total) break;
-        if (it < n0) chain_item_run<kSkW, 0>(a, it, ctl, sw, sx);
-        else if (it < n0 + n1) chain_item_run<kSkW, 1>(a, it - n0, ctl, sw, sx);
-        else if (it < n0 + n1 + n2) chain_item_run<kSkW, 2>(a, it - n0 - n1, ctl, sw, sx);
-        else chain_item_run<kSkW, 3>(a, it - n0 - n1 - n2, ctl, sw, sx);
-    }
-    if (threadIdx.x == 0) {
-        const unsigned e = __hip_atomic_fetch_add(ctl + kCtlExit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (e == gridDim.x - 1) {  // every item is done and no workgroup claims or waits any more
-            __hip_atomic_store(ctl + kCtlClaim, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(ctl + kCtlExit, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-            for (int l = 0; l < kChainMax; ++l)
-                __hip_atomic_store(ctl + kCtlDone + 32 * l, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-}
-
 // K splits of a skinny linear: enough workgroups for ~4 per CU over the
 // output column tiles, chunks of 64 kSkW k each, at most 16 splits.  The split
 // (hence every output row's summation order) depends on n and k only, not on
 // the row count m, so a row's result does not depend on the rows beside it.
-inline int skinny_splits(int64_t m, int64_t n, int64_t k, int cus) {
+// The ticket block (kSkTickets words, one per output tile) bounds the tiles of
+// one split launch: mmpde_linear_skinny_ws runs larger m as row blocks with
+// the same split rather than unsplit (which would change a row's rounding).
+inline int skinny_splits(int64_t n, int64_t k, int cus) {
     const int64_t ctiles = (n + 15) / 16;
-    if (ctiles * ((m + 15) / 16) > 4096) return 1;  // = kSkTickets
     const int64_t chunks = (k + 64 * kSkW - 1) / (64 * kSkW);
     int64_t z = (4 * (int64_t)cus + ctiles - 1) / ctiles;
     z = z < chunks ? z : chunks;
@@ -531,7 +270,7 @@ __global__ __launch_bounds__(256) void traj_mse_kernel(const float *__restrict__
 
 }  // namespace
 
-extern "C" int mmpde_version(void) { return 11500; }
+extern "C" int mmpde_version(void) { return 11600; }
 
 extern "C" int mmpde_traj_mse(const float *pred, const float *labels, int64_t batches, int64_t n_per,
                               float *out, mmpde_stream_t stream) {
@@ -569,7 +308,7 @@ static int64_t skinny_ws_bytes(int64_t m, int64_t n, int z) {
 
 extern "C" int64_t mmpde_linear_skinny_workspace_bytes(int64_t m, int64_t n, int64_t k) {
     if (m <= 0 || n <= 0 || k <= 0) return 0;
-    return skinny_ws_bytes(m, n, skinny_splits(m, n, k, skinny_cus()));
+    return skinny_ws_bytes(m, n, skinny_splits(n, k, skinny_cus()));
 }
 
 extern "C" int mmpde_linear_skinny_ws(const float *x, int64_t ldx, int64_t m, int64_t k, const float *w,
@@ -578,166 +317,27 @@ extern "C" int mmpde_linear_skinny_ws(const float *x, int64_t ldx, int64_t m, in
     MMPDE_REQUIRE(x && w && y && m > 0 && k > 0 && n > 0 && m <= 4096);
     MMPDE_REQUIRE(ldx >= k && ldw >= k && ldy >= n && act >= 0 && act <= 2);
     hipStream_t st = as_stream(stream);
-    int z = skinny_splits(m, n, k, skinny_cus());
+    int z = skinny_splits(n, k, skinny_cus());
     if (!workspace || workspace_bytes < skinny_ws_bytes(m, n, z)) z = 1;
     const int chunks = ceil_div(k, 64 * kSkW);
     const int nchz = z > 1 ? ceil_div(chunks, z) : chunks;
     z = z > 1 ? ceil_div(chunks, nchz) : 1;  // no empty split
-    const dim3 grid((unsigned)ceil_div(n, 16), (unsigned)ceil_div(m, 16), (unsigned)z);
+    const int64_t ctiles = ceil_div(n, 16);
+    MMPDE_REQUIRE(z == 1 || ctiles <= kSkTickets);
+    // a split launch holds at most kSkTickets output tiles (one ticket each):
+    // more rows run as row blocks of that many tiles, one launch each, with the
+    // same split (a row's summation order does not depend on m)
+    const int64_t rows_per = z > 1 ? 16 * (kSkTickets / ctiles) : m;
     unsigned *tickets = z > 1 ? (unsigned *)workspace : nullptr;
     float *part = z > 1 ? workspace + kSkTickets : nullptr;
-    hipLaunchKernelGGL(linear_skinny_kernel<kSkW>, grid, dim3(kSkW * 64), 0, st, x, ldx, m, k, w, ldw, b,
-                       n, act, y, ldy, nchz, part, tickets);
-    MMPDE_RET_LAUNCH();
-    return MMPDE_OK;
-}
-
-// ---- linear chains (linear_chain_kernel) --------------------------------
-namespace mmpde_detail {
-// K split of chain layer (n, k): about two workgroups per CU over the output
-// column tiles; a function of (n, k, CUs) only, so a row's summation order does
-// not depend on the rows launched beside it.
-static void chain_split(int64_t n, int64_t k, int cus, int &z, int &nchz) {
-    const int64_t ctiles = (n + 15) / 16, chunks = (k + 64 * kSkW - 1) / (64 * kSkW);
-    int64_t zz = (2 * (int64_t)cus) / ctiles;
-    zz = zz < chunks ? zz : chunks;
-    zz = zz < kSkMaxZ ? zz : kSkMaxZ;
-    zz = zz > 1 ? zz : 1;
-    nchz = (int)((chunks + zz - 1) / zz);
-    z = (int)((chunks + nchz - 1) / nchz);  // no empty split
-}
-
-// every region of the chain workspace on 128-B lines of its own (a line
-// shared by two regions could be cached by one XCD's L2 before the other
-// region is written)
-static int64_t up32(int64_t v) { return (v + 31) & ~int64_t(31); }
-
-// workspace floats of a chain, and (args non-null) its layout in ws
-static int64_t chain_plan(const float *x, int64_t ldx, int64_t m, int nl, const ChainSpec *sp, int cus,
-                          float *ws, ChainArgs *a) {
-    int64_t off = kChainCtl + kChainMax * kChainTickets;
-    if (a) {
-        *a = ChainArgs{};
-        a->x = x;
-        a->ldx = ldx;
-        a->m = m;
-        a->nl = nl;
-        a->rtiles = (int)((m + 15) / 16);
-        a->ctl = (unsigned *)ws;
-    }
-    for (int l = 0; l < nl; ++l) {
-        int z, nchz;
-        chain_split(sp[l].n, sp[l].k, cus, z, nchz);
-        const int64_t pf = z > 1 ? up32((int64_t)z * m * sp[l].n) : 0;
-        const bool own_y = sp[l].y == nullptr;
-        if (a) {
-            ChainLayer &L = a->L[l];
-            L.w = sp[l].w;
-            L.b = sp[l].b;
-            L.ldw = sp[l].ldw;
-            L.n = sp[l].n;
-            L.k = sp[l].k;
-            L.act = sp[l].act;
-            L.z = z;
-            L.nchz = nchz;
-            L.ctiles = (int)((sp[l].n + 15) / 16);
-            L.items = L.ctiles * a->rtiles * z;
-            L.part = z > 1 ? ws + off : nullptr;
-            L.y = own_y ? ws + off + pf : sp[l].y;
-            L.ldy = own_y ? sp[l].n : sp[l].ldy;
-        }
-        off += pf + (own_y ? up32(m * sp[l].n) : 0);
-    }
-    return off;
-}
-
-bool chain_ok(int64_t m, int nl, const ChainSpec *sp) {
-    if (m <= 0 || m > 64 || nl < 1 || nl > kChainMax) return false;
-    for (int l = 0; l < nl; ++l) {
-        if (!sp[l].w || sp[l].n <= 0 || sp[l].k <= 0 || sp[l].ldw < sp[l].k || sp[l].act < 0 || sp[l].act > 2)
-            return false;
-        if (l && sp[l].k != sp[l - 1].n) return false;
-        if (sp[l].y && sp[l].ldy < sp[l].n) return false;
-        // an intermediate handed to the next layer inside the launch: lines of
-        // its own (128-B aligned, whole lines)
-        if (sp[l].y && l + 1 < nl && ((((uintptr_t)sp[l].y) & 127u) || (m * sp[l].ldy) % 32)) return false;
-        if (((sp[l].n + 15) / 16) * ((m + 15) / 16) > kChainTickets) return false;
-    }
-    return sp[nl - 1].y != nullptr;
-}
-
-int64_t chain_ws_bytes(int64_t m, int nl, const ChainSpec *sp) {
-    return chain_plan(nullptr, 0, m, nl, sp, skinny_cus(), nullptr, nullptr) * (int64_t)sizeof(float);
-}
-
-int linear_chain(const float *x, int64_t ldx, int64_t m, int nl, const ChainSpec *sp, void *workspace,
-                 int64_t workspace_bytes, hipStream_t st) {
-    if (!x || !workspace || ((uintptr_t)workspace & 127u) || !chain_ok(m, nl, sp) || ldx < sp[0].k)
-        return MMPDE_ERR_INVALID_ARG;
-    const int cus = skinny_cus();
-    ChainArgs a;
-    const int64_t need = chain_plan(x, ldx, m, nl, sp, cus, (float *)workspace, &a) * (int64_t)sizeof(float);
-    if (workspace_bytes < need) return MMPDE_ERR_INVALID_ARG;
-    // grid: two workgroups per CU at most (items are claimed, so residency is
-    // a matter of speed only), no more than the largest layer's items
-    static int occ = -1;
-    if (occ < 0) {
-        int o = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, (const void *)linear_chain_kernel<kSkW>, kSkW * 64,
-                                                         0) != hipSuccess)
-            o = 1;
-        occ = o < 1 ? 1 : (o > 2 ? 2 : o);
-    }
-    int items = 1;
-    for (int l = 0; l < nl; ++l) items = a.L[l].items > items ? a.L[l].items : items;
-    const int grid = items < occ * cus ? items : occ * cus;
-    hipLaunchKernelGGL(linear_chain_kernel<kSkW>, dim3((unsigned)grid), dim3(kSkW * 64), 0, st, a);
-    MMPDE_RET_LAUNCH();
-    return MMPDE_OK;
-}
-}  // namespace mmpde_detail
-
-static int chain_specs(int64_t m, int nl, const int64_t *dims, const float *const *w, const int64_t *ldw,
-                       const float *const *b, const int *act, float *y, int64_t ldy,
-                       mmpde_detail::ChainSpec *sp) {
-    (void)m;
-    if (!dims || !w || !act || nl < 1 || nl > kChainMax) return MMPDE_ERR_INVALID_ARG;
-    for (int l = 0; l < nl; ++l) {
-        sp[l] = mmpde_detail::ChainSpec{w[l], ldw ? ldw[l] : dims[l], b ? b[l] : nullptr, dims[l + 1], dims[l],
-                                        act[l], l + 1 == nl ? y : nullptr, l + 1 == nl ? ldy : 0};
+    for (int64_t r0 = 0; r0 < m; r0 += rows_per) {
+        const int64_t mr = m - r0 < rows_per ? m - r0 : rows_per;
+        const dim3 grid((unsigned)ctiles, (unsigned)ceil_div(mr, 16), (unsigned)z);
+        hipLaunchKernelGGL(linear_skinny_kernel<kSkW>, grid, dim3(kSkW * 64), 0, st, x + r0 * ldx, ldx, mr, k, w,
+                           ldw, b, n, act, y + r0 * ldy, ldy, nchz, part, tickets);
+        MMPDE_RET_LAUNCH();
     }
     return MMPDE_OK;
-}
-
-// whether the DMM output MLP runs as one chain launch (dmm.hip) or as per-layer
-// skinny launches (the default: measured faster in the rollout step, DESIGN.md
-// §4); both give the same results to fp32 rounding
-static int g_chain_dmm = 0;
-namespace mmpde_detail {
-bool chain_dmm_enabled() { return g_chain_dmm != 0; }
-}  // namespace mmpde_detail
-extern "C" int mmpde_linear_chain_dmm(int enable) {
-    const int prev = g_chain_dmm;
-    if (enable >= 0) g_chain_dmm = enable ? 1 : 0;
-    return prev;
-}
-
-extern "C" int64_t mmpde_linear_chain_workspace_bytes(int64_t m, int nl, const int64_t *dims) {
-    if (!dims || nl < 1 || nl > kChainMax || m <= 0) return 0;
-    mmpde_detail::ChainSpec sp[kChainMax];
-    for (int l = 0; l < nl; ++l) sp[l] = mmpde_detail::ChainSpec{nullptr, dims[l], nullptr, dims[l + 1], dims[l], 0,
-                                                               nullptr, 0};
-    sp[nl - 1].y = (float *)16;  // the caller's output: no workspace
-    return mmpde_detail::chain_ws_bytes(m, nl, sp);
-}
-
-extern "C" int mmpde_linear_chain_ws(const float *x, int64_t ldx, int64_t m, int nl, const int64_t *dims,
-                                     const float *const *w, const int64_t *ldw, const float *const *b,
-                                     const int *act, float *y, int64_t ldy, void *workspace,
-                                     int64_t workspace_bytes, mmpde_stream_t stream) {
-    mmpde_detail::ChainSpec sp[kChainMax];
-    MMPDE_REQUIRE(y && chain_specs(m, nl, dims, w, ldw, b, act, y, ldy, sp) == MMPDE_OK);
-    return mmpde_detail::linear_chain(x, ldx, m, nl, sp, workspace, workspace_bytes, as_stream(stream));
 }
 
 extern "C" int mmpde_linear_skinny(const float *x, int64_t ldx, int64_t m, int64_t k,

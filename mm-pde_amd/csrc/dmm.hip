@@ -497,7 +497,7 @@ int64_t cache_floats(int64_t n_per, int hidden) { return 3 * n_per * hidden; }
 // branch [B, L] -> mesh [B*N, 2]; cache: a prepared grid side (or null: computed here)
 int dmm_head(const float *branch, const float *xi, int64_t batches, int64_t n_per,
              const mmpde_dmm_head *hd, float *ws, const float *cache, float *mesh_out,
-             hipStream_t st, float *sk, int64_t skf, bool p_done = false) {
+             hipStream_t st, float *sk, int64_t skf) {
     const int L = hd->latent, Lp = hd->hidden, th = hd->th;
     if (!head_ok(hd)) return MMPDE_ERR_UNSUPPORTED;
     HeadWs w = carve_head(ws, batches, n_per, L, Lp, th);
@@ -508,13 +508,10 @@ int dmm_head(const float *branch, const float *xi, int64_t batches, int64_t n_pe
         rc = dmm_head_grid(xi, n_per, hd, w, w.q, w.jac, st);
         if (rc) return rc;
     }
-    // P = Wb . branch + b_o1 (Wb = out_nn.layers.0.weight[:, :L], row stride 2L),
-    // unless the branch's output chain already ended with it
-    if (!p_done) {
-        rc = mmpde_linear_skinny_ws(branch, L, batches, L, hd->o0_w, 2 * L, hd->o0_b, Lp, MMPDE_ACT_NONE, w.p,
-                                    Lp, sk, skf * (int64_t)sizeof(float), st);
-        if (rc) return rc;
-    }
+    // P = Wb . branch + b_o1 (Wb = out_nn.layers.0.weight[:, :L], row stride 2L)
+    rc = mmpde_linear_skinny_ws(branch, L, batches, L, hd->o0_w, 2 * L, hd->o0_b, Lp, MMPDE_ACT_NONE, w.p,
+                                Lp, sk, skf * (int64_t)sizeof(float), st);
+    if (rc) return rc;
     const size_t lds = (size_t)batches * Lp * sizeof(float);
     if (Lp == 512 && lds <= 65536) {
         hipLaunchKernelGGL(mesh_vjp_wave_kernel<8>, dim3((unsigned)ceil_div(n_per, 4)), dim3(256),
@@ -544,9 +541,8 @@ int64_t dmm_base_floats(int64_t batches, int64_t n_per, int latent, int hidden) 
                                 8 * batches * n_per + 256;
     return branch_side + head_floats(batches, n_per, latent, hidden, 64) + 256;
 }
-// dense.hip kSkTickets; zeroed by the branch's first kernel on every call
-// 4096 ticket / chain control words from the first 128-B line of the region
-// (+ 32 floats of alignment slack), all zeroed by the branch's first kernel
+// dense.hip kSkTickets (+ 32 floats of slack); zeroed by the branch's first
+// kernel on every call
 int64_t dmm_skinny_ticket_floats(int64_t) { return 4096 + 32; }
 int64_t dmm_skinny_floats(int64_t batches) {
     return dmm_skinny_ticket_floats(batches) + 16 * (batches > 64 ? batches : 64) * 2048;
@@ -560,20 +556,6 @@ int skinny(const float *x, int64_t ldx, int64_t m, int64_t k, const float *w, in
                                   scratch_floats * (int64_t)sizeof(float), st);
 }
 
-// The output MLP as one mmpde_detail::linear_chain launch (dense.hip), its
-// workspace = the split-K region from its first 128-B line; chain_fits says
-// whether the chain applies (else the per-layer skinny launches above).
-float *chain_ws(float *sk) { return (float *)(((uintptr_t)sk + 127) & ~(uintptr_t)127); }
-bool chain_fits(int64_t m, int nl, const mmpde_detail::ChainSpec *sp, float *sk, int64_t skf) {
-    const int64_t avail = (skf - (chain_ws(sk) - sk)) * (int64_t)sizeof(float);
-    return mmpde_detail::chain_dmm_enabled() && mmpde_detail::chain_ok(m, nl, sp) &&
-           mmpde_detail::chain_ws_bytes(m, nl, sp) <= avail;
-}
-int chain_run(const float *x, int64_t ldx, int64_t m, int nl, const mmpde_detail::ChainSpec *sp, float *sk,
-              int64_t skf, hipStream_t st) {
-    const int64_t avail = (skf - (chain_ws(sk) - sk)) * (int64_t)sizeof(float);
-    return mmpde_detail::linear_chain(x, ldx, m, nl, sp, chain_ws(sk), avail, st);
-}
 }  // namespace
 
 extern "C" int64_t mmpde_dmm_workspace_bytes(int64_t batches, int64_t n_per, int latent,
@@ -610,8 +592,7 @@ namespace {
 // activations); *ws_end = the first float after it.
 int graph_branch(const float *u, const float *grid, int64_t batches, int64_t n_per,
                  const int32_t *grid_nbr, int k, const mmpde_dmm_graph_branch *br, int latent, float *ws,
-                 float *sk, int64_t skf, float *branch, float **ws_end, hipStream_t st,
-                 const mmpde_dmm_head *hd_p = nullptr, float *p_out = nullptr, bool *p_done = nullptr) {
+                 float *sk, int64_t skf, float *branch, float **ws_end, hipStream_t st) {
     const int64_t nt = batches * n_per;
     float4 *h0 = (float4 *)ws;
     float4 *h1 = h0 + nt;
@@ -653,21 +634,6 @@ int graph_branch(const float *u, const float *grid, int64_t batches, int64_t n_p
                        br->dec1_w, br->dec1_b, dec);
     MMPDE_RET_LAUNCH();
     // output_mlp: Linear(N,512) tanh Linear(512,256) tanh Linear(256,L) on [B, N]
-    // (then, given hd_p, the head's P = Wb . branch + b_o1): one chain launch
-    {
-        mmpde_detail::ChainSpec sp[4] = {
-            {br->om0_w, n_per, br->om0_b, 512, n_per, MMPDE_ACT_TANH, nullptr, 0},
-            {br->om2_w, 512, br->om2_b, 256, 512, MMPDE_ACT_TANH, nullptr, 0},
-            {br->om4_w, 256, br->om4_b, latent, 256, MMPDE_ACT_NONE, branch, latent},
-            {hd_p ? hd_p->o0_w : nullptr, 2 * (int64_t)latent, hd_p ? hd_p->o0_b : nullptr,
-             hd_p ? hd_p->hidden : 0, latent, MMPDE_ACT_NONE, p_out, hd_p ? hd_p->hidden : 0}};
-        const int nl = hd_p && p_out ? 4 : 3;
-        if (nl == 4) sp[2].y = nullptr;  // branch only feeds P: kept in the chain's workspace
-        if (chain_fits(batches, nl, sp, sk, skf)) {
-            if (p_done) *p_done = nl == 4;
-            return chain_run(dec, n_per, batches, nl, sp, sk, skf, st);
-        }
-    }
     int rc = skinny(dec, n_per, batches, n_per, br->om0_w, n_per, br->om0_b, 512, MMPDE_ACT_TANH, om1, 512,
                     sk, skf, st);
     if (rc) return rc;
@@ -681,8 +647,7 @@ int graph_branch(const float *u, const float *grid, int64_t batches, int64_t n_p
 // Array-mode branch: ConvNet.forward (dmm_model.py:65-81), u [B, s, s] ->
 // branch [B, L].  conv0 also zeroes the skinny linears' tickets.
 int array_branch(const float *u, int64_t batches, const mmpde_dmm_array_branch *br, int latent, float *ws,
-                 float *sk, int64_t skf, float *branch, float **ws_end, hipStream_t st,
-                 const mmpde_dmm_head *hd_p = nullptr, float *p_out = nullptr, bool *p_done = nullptr) {
+                 float *sk, int64_t skf, float *branch, float **ws_end, hipStream_t st) {
     const int s = br->s;
     const int s1 = (s + 4 - 5) / 2 + 1;   // conv0, stride 2, pad 2
     const int s3 = (s1 + 4 - 5) / 2 + 1;  // conv3, stride 2, pad 2
@@ -708,19 +673,6 @@ int array_branch(const float *u, int64_t batches, const mmpde_dmm_array_branch *
     rc = mmpde_conv2d(x3, batches, 8, s1, s1, br->c3_w, br->c3_b, 1, 5, 2, 2, nullptr, MMPDE_ACT_TANH, x4,
                       st);
     if (rc) return rc;
-    {
-        mmpde_detail::ChainSpec sp[3] = {
-            {br->fc2_w, (int64_t)s3 * s3, br->fc2_b, 1024, (int64_t)s3 * s3, MMPDE_ACT_TANH, nullptr, 0},
-            {br->fc3_w, 1024, br->fc3_b, latent, 1024, MMPDE_ACT_NONE, branch, latent},
-            {hd_p ? hd_p->o0_w : nullptr, 2 * (int64_t)latent, hd_p ? hd_p->o0_b : nullptr,
-             hd_p ? hd_p->hidden : 0, latent, MMPDE_ACT_NONE, p_out, hd_p ? hd_p->hidden : 0}};
-        const int nl = hd_p && p_out ? 3 : 2;
-        if (nl == 3) sp[1].y = nullptr;  // branch only feeds P: kept in the chain's workspace
-        if (chain_fits(batches, nl, sp, sk, skf)) {
-            if (p_done) *p_done = nl == 3;
-            return chain_run(x4, (int64_t)s3 * s3, batches, nl, sp, sk, skf, st);
-        }
-    }
     rc = skinny(x4, s3 * s3, batches, s3 * s3, br->fc2_w, s3 * s3, br->fc2_b, 1024, MMPDE_ACT_TANH, f2, 1024,
                 sk, skf, st);
     if (rc) return rc;
@@ -751,13 +703,10 @@ extern "C" int mmpde_dmm_mesh_graph_cached(const float *u, const float *grid, in
     const int64_t nt = batches * n_per;
     float *branch = ws + 8 * nt + ((nt + 3) & ~int64_t(3)) + batches * 768;
     float *head_ws = branch + ((batches * hd->latent + 3) & ~int64_t(3));
-    bool p_done = false;
-    float *p = head_ok(hd) ? carve_head(head_ws, batches, n_per, hd->latent, hd->hidden, hd->th).p : nullptr;
-    int rc = graph_branch(u, grid, batches, n_per, grid_nbr, k, br, hd->latent, ws, sk, skf, branch, &end, st,
-                          p ? hd : nullptr, p, &p_done);
+    int rc = graph_branch(u, grid, batches, n_per, grid_nbr, k, br, hd->latent, ws, sk, skf, branch, &end, st);
     if (rc) return rc;
     return dmm_head(branch, grid, batches, n_per, hd, head_ws, (const float *)head_cache, mesh_out,
-                    st, sk, skf, p_done);
+                    st, sk, skf);
 }
 
 extern "C" int mmpde_dmm_mesh_array(const float *u, const float *xi, int64_t batches,
@@ -786,13 +735,9 @@ extern "C" int mmpde_dmm_mesh_array_cached(const float *u, const float *xi, int6
     float *branch = ws + 2 * up4(batches * 8 * s1 * s1) + up4(batches * 16 * s1 * s1) + up4(batches * s3 * s3) +
                     up4(batches * 1024);
     float *head_ws = branch + up4(batches * hd->latent);
-    bool p_done = false;
-    float *p = head_ok(hd) ? carve_head(head_ws, batches, n_per, hd->latent, hd->hidden, hd->th).p : nullptr;
-    int rc = array_branch(u, batches, br, hd->latent, ws, sk, skf, branch, &end, st, p ? hd : nullptr, p,
-                          &p_done);
+    int rc = array_branch(u, batches, br, hd->latent, ws, sk, skf, branch, &end, st);
     if (rc) return rc;
-    return dmm_head(branch, xi, batches, n_per, hd, head_ws, (const float *)head_cache, mesh_out, st, sk, skf,
-                    p_done);
+    return dmm_head(branch, xi, batches, n_per, hd, head_ws, (const float *)head_cache, mesh_out, st, sk, skf);
 }
 
 // ---------------------------------------------------------------------------

@@ -25,15 +25,14 @@
 // at a unit boundary inside a tile to side[s U + u] (16 x 128), and the node
 // stage adds those side blocks in unit order before dividing by the degree.
 // So a row's sum is a fixed function of (k, U) and the row's tile position.
-// Physical waves: wave j of segment s (XCD-contiguous ranks s * wpsp + j) takes
-// the m = U / wpsp units [j m, (j + 1) m), so every wave of a segment gets the
-// same work to one slot when m = 1.  A wave never leaves its segment, so its
-// split scale comes from its segment's range records alone.  U depends on the
-// segment size and, below 16 segments, on the segment count (layer.hpp
-// edge_wave_plan); a trajectory's result therefore does not depend on the
-// trajectories launched beside it whenever the launches have the same U (every
-// launch of >= 16 cylinder trajectories).  Deterministic: fixed summation
-// order, no atomics.
+// Physical waves: the wpsp waves of segment s (XCD-contiguous ranks s * wpsp
+// + j) split its U units as evenly as whole units allow, wave j taking units
+// [j U / wpsp, (j + 1) U / wpsp).  A wave never leaves its segment, so its
+// split scale comes from its segment's range records alone, and U is a
+// function of the segment alone (layer.hpp edge_wave_plan): a trajectory's
+// result does not depend on how many trajectories are launched beside it
+// (any per-rank shard of a batch sums every row in the same order).
+// Deterministic: fixed summation order, no atomics.
 #include "common.hpp"
 #include "f16x3.hpp"
 #include "layer.hpp"
@@ -66,7 +65,7 @@ struct WaveArgs {
     int tps;                  // 16-row tiles per segment
     int64_t S;                // slots per segment = tps * k
     int U;                    // summation units per segment
-    int m;                    // units per wave (wpsp = U / m waves per segment)
+    int wpsp;                 // waves per segment (<= U)
     const float *b2;          // message_net_2.0 bias
     const char *pk;           // this layer's packed images (W2 at kPkW2)
     const float *rng;         // range records of a, b (layer.hpp)
@@ -132,11 +131,11 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
     const int k = p.k;
     const int64_t nmax = p.n - 1;
     const int rank = wave_rank(blockIdx.x, gridDim.x);
-    const int wpsp = p.U / p.m;
+    const int wpsp = p.wpsp;
     const int seg = rank / wpsp, jw = rank - seg * wpsp;
-    const int u_end = min((jw + 1) * p.m, p.U);
-    int u_next = jw * p.m + 1;  // the next unit to start
-    const int64_t s0 = (int64_t)jw * p.m * p.S / p.U, s1 = (int64_t)u_end * p.S / p.U;
+    const int u_begin = (int)((int64_t)jw * p.U / wpsp), u_end = (int)((int64_t)(jw + 1) * p.U / wpsp);
+    int u_next = u_begin + 1;  // the next unit to start
+    const int64_t s0 = (int64_t)u_begin * p.S / p.U, s1 = (int64_t)u_end * p.S / p.U;
     if (s0 >= s1) return;
     // slot where unit u_next starts (s1 past the wave's last unit)
     int64_t ub = u_next < u_end ? (int64_t)u_next * p.S / p.U : s1;
@@ -145,7 +144,7 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
     const int last = (int)p.seg_n - 1;
     // destination of the run being computed: -1 = out (it starts its tile),
     // else the side block of the unit it starts
-    int run_side = s0 % k ? seg * p.U + jw * p.m : -1;
+    int run_side = s0 % k ? seg * p.U + u_begin : -1;
     // |a + b| <= max|a| + max|b| over the segment, scaled below 2^11 (split8_relu_rtz)
     const float sc = 0.125f * split_scale(segment_range(p.rng, p.seg_n, seg));
     // message_net_2: B operands (AGPRs), accumulator start (bias, scaled), unscale
@@ -414,23 +413,20 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
 // Summation units and waves of one launch (layer.hpp edge_wave_plan).
 EdgePlan edge_wave_plan(int64_t nseg, int64_t S_seg, int cus, int64_t side_cap) {
     EdgePlan pl;
-    // U0: a power of two depending on the segment only, units of 44..88 slots
-    int64_t u0 = 1;
-    while (u0 * 2 * 44 <= S_seg) u0 *= 2;
-    // U1: the waves per segment that fill one wave per SIMD
-    int64_t u1 = 4 * (int64_t)cus / nseg;
-    if (u1 < 1) u1 = 1;
-    const int64_t m = (u0 + u1 - 1) / u1;   // units per wave
-    int64_t U = u1 * m;                      // = u0 when u1 is a power of two <= u0
-    const int64_t cap = S_seg < side_cap / nseg ? S_seg : side_cap / nseg;  // >= 1 slot per unit
-    if (U > cap) {                           // tiny segments: one unit per wave
-        U = cap < 1 ? 1 : cap;
-        pl.m = 1;
-    } else {
-        pl.m = (int)m;
-    }
+    // U: the power of two that makes units of 22..44 slots (cylinder: 128
+    // units of 43 slots), capped by the segment's slots and its share of the
+    // side blocks (3 seg_n / 16 in the standard workspace): a function of the
+    // segment alone
+    int64_t U = 1;
+    while (U * 2 * 22 <= S_seg) U *= 2;
+    const int64_t cap = S_seg < side_cap / nseg ? S_seg : side_cap / nseg;
+    if (U > cap) U = cap < 1 ? 1 : cap;
+    // waves per segment: one wave per SIMD over the launch, at most one per unit
+    int64_t w = 4 * (int64_t)cus / nseg;
+    w = w < 1 ? 1 : (w > U ? U : w);
     pl.U = (int)U;
-    pl.waves = nseg * (U / pl.m);
+    pl.wpsp = (int)w;
+    pl.waves = nseg * w;
     return pl;
 }
 
@@ -443,9 +439,8 @@ int edge_wave_setup(const float *a, const float *b, const int32_t *nbr, const in
     const int64_t nseg = n / seg_n, tps = (seg_n + ET - 1) / ET, S = tps * k;
     if (!(tps < (int64_t)INT32_MAX && S < ((int64_t)1 << 40) && side_cap >= nseg)) return 0;
     const EdgePlan pl = edge_wave_plan(nseg, S, cus, side_cap);
-    // every wave takes m whole units: U must be a multiple of m
-    if (pl.U % pl.m || pl.waves > (int64_t)INT32_MAX || nseg * pl.U > (int64_t)INT32_MAX) return 0;
-    *w = WaveArgs{a, b, nbr, deg, n, k, seg_n, (int)tps, S, pl.U, pl.m, msg2_b, pk, rng, out, side};
+    if (pl.waves > (int64_t)INT32_MAX || nseg * pl.U > (int64_t)INT32_MAX) return 0;
+    *w = WaveArgs{a, b, nbr, deg, n, k, seg_n, (int)tps, S, pl.U, pl.wpsp, msg2_b, pk, rng, out, side};
     *split = EdgeSplit{side, S, pl.U, k, seg_n};
     return (int)pl.waves;
 }

@@ -254,7 +254,7 @@ constexpr int HS = H + 1;        // h row stride (floats)
 constexpr int Y1S = 4 * 38 + 1;  // conv0 output row stride (floats)
 
 // One or two problems per launch: blocks below blocks0 take problem 0's
-// nodes, the rest problem 1's (mmpde_gnn_forward_pair).
+// nodes, the rest problem 1's.
 struct HeadArgs2 {
     const float *h[2];
     int64_t n[2];
@@ -596,86 +596,6 @@ extern "C" int mmpde_gnn_forward_ex(const float *u, const float *pos, int64_t n,
         cur ^= 1;
     }
     return mmpde_gnn_head(hb[cur], n, head, out, stream);
-}
-
-// Two independent forwards in one set of row-stage launches (the MM-PDE
-// step's fixed-grid and moved-mesh GNNs): one embedding launch, per layer the
-// two edge stages then ONE node-stage launch over both problems' row tiles, one
-// head launch.  Every kernel computes exactly what mmpde_gnn_forward_ex does
-// for each problem (same tiles, same per-problem arguments): the outputs are
-// bitwise those of two separate calls.
-extern "C" int mmpde_gnn_forward_pair(const mmpde_gnn_call *calls, mmpde_stream_t stream) {
-    MMPDE_REQUIRE(calls);
-    hipStream_t st = as_stream(stream);
-    const int L = calls[0].n_layers;
-    const int tw = calls[0].sc.tw > 1 ? calls[0].sc.tw : 1;
-    struct Bufs {
-        float *hb[2], *wa, *wb, *wmean, *rng;
-        const char *pack;
-        int64_t seg_n;
-    } bf[2];
-    for (int i = 0; i < 2; ++i) {
-        const mmpde_gnn_call &c = calls[i];
-        MMPDE_REQUIRE(c.u && c.pos && c.nbr && c.emb && c.layers && c.head && c.workspace && c.out && c.exec);
-        MMPDE_REQUIRE(c.n > 0 && c.k > 0 && c.n_layers == L && L >= 1 && L <= MMPDE_GNN_MAX_LAYERS);
-        MMPDE_REQUIRE(aligned16(c.workspace) && (c.sc.tw > 1 ? c.sc.tw : 1) == tw && tw <= 16);
-        MMPDE_REQUIRE((c.head->tw > 1 ? c.head->tw : 1) == tw);
-        for (int l = 0; l < L; ++l) MMPDE_REQUIRE(c.layers[l].msg1_ld >= 259 + tw);
-        MMPDE_REQUIRE(c.exec->edge_gemm == MMPDE_EDGE_GEMM_F16X3 && c.exec->packed && aligned16(c.exec->packed));
-        float *ws = (float *)c.workspace;
-        bf[i].hb[0] = ws;
-        bf[i].hb[1] = ws + c.n * H;
-        bf[i].wa = ws + 2 * c.n * H;
-        bf[i].wb = ws + 3 * c.n * H;
-        bf[i].wmean = ws + 4 * c.n * H;
-        bf[i].rng = ws + kGnnBufs * c.n * H;
-        bf[i].pack = (const char *)c.exec->packed;
-        bf[i].seg_n = c.exec->seg_n;
-    }
-    EmbedStageCall ec[2];
-    for (int i = 0; i < 2; ++i) {
-        const mmpde_gnn_call &c = calls[i];
-        ec[i] = EmbedStageCall{c.u, c.pos, c.n, bf[i].seg_n, c.sc, c.emb, &c.layers[0], bf[i].pack, bf[i].rng,
-                               bf[i].hb[0], bf[i].wa, bf[i].wb};
-    }
-    int rc = launch_embed_stages(ec, 2, st);
-    if (rc) return rc;
-    int cur = 0;
-    for (int l = 0; l < L; ++l) {
-        NodeStageCall nc[2];
-        EdgeSplit split[2];
-        for (int i = 0; i < 2; ++i) {
-            const mmpde_gnn_call &c = calls[i];
-            const mmpde_gnn_exec *ex = c.exec;
-            hipEvent_t eb = ex->edge_begin ? (hipEvent_t)ex->edge_begin[l] : nullptr;
-            hipEvent_t ee = ex->edge_end ? (hipEvent_t)ex->edge_end[l] : nullptr;
-            const mmpde_gnn_layer_params *next = l + 1 < L ? &c.layers[l + 1] : nullptr;
-            const char *pk = bf[i].pack + (int64_t)l * kLayerPack;
-            const char *pkn = next ? bf[i].pack + (int64_t)(l + 1) * kLayerPack : nullptr;
-            if (eb && hipEventRecord(eb, st) != hipSuccess) return MMPDE_ERR_INVALID_ARG;
-            rc = launch_edge_stage(bf[i].wa, bf[i].wb, c.nbr, ex->degree, c.n, c.k, bf[i].seg_n, &c.layers[l], pk,
-                                   bf[i].rng, bf[i].wmean, bf[i].wmean + c.n * H, (kGnnBufs - 5) * c.n * H / (16 * H),
-                                   &split[i], st);
-            if (rc) return rc;
-            if (ee && hipEventRecord(ee, st) != hipSuccess) return MMPDE_ERR_INVALID_ARG;
-            nc[i] = NodeStageCall{bf[i].hb[cur], bf[i].wmean, &split[i], ex->degree, c.u, c.pos, c.n, bf[i].seg_n,
-                                  c.sc, &c.layers[l], next, pk, pkn, next ? bf[i].rng : nullptr,
-                                  bf[i].hb[cur ^ 1], bf[i].wa, bf[i].wb};
-        }
-        rc = launch_node_stages(nc, 2, st);
-        if (rc) return rc;
-        for (int i = 0; i < 2; ++i) {
-            const mmpde_gnn_exec *ex = calls[i].exec;
-            hipEvent_t ne = ex->node_end ? (hipEvent_t)ex->node_end[l] : nullptr;
-            if (ne && hipEventRecord(ne, st) != hipSuccess) return MMPDE_ERR_INVALID_ARG;
-        }
-        cur ^= 1;
-    }
-    const float *hh[2] = {bf[0].hb[cur], bf[1].hb[cur]};
-    const int64_t nn[2] = {calls[0].n, calls[1].n};
-    const mmpde_gnn_head_params *pp[2] = {calls[0].head, calls[1].head};
-    float *oo[2] = {calls[0].out, calls[1].out};
-    return head_launch(hh, nn, pp, oo, 2, st);
 }
 
 extern "C" int mmpde_gnn_forward(const float *u, const float *pos, int64_t n, int k,

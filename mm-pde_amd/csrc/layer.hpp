@@ -66,15 +66,14 @@ inline int64_t effective_seg(int64_t n, int64_t seg_n) {
     return (seg_n >= kRangeRows && seg_n <= n && n % seg_n == 0) ? seg_n : n;
 }
 
-// Summation units per segment U and units per wave m of the wave kernel
-// (waves = nseg * U / m, about one per SIMD).  U = U1 * ceil(U0 / U1) with U0 =
-// the power of two that makes units of 44..88 slots (a function of the
-// segment only) and U1 = floor(4 CUs / nseg): for every power-of-two segment
-// count up to 4 CUs / U0 (16 cylinder trajectories on 256 CUs) U = U0, so
-// those launches sum every row in the same order.  U <= S_seg and nseg * U <=
-// side_cap.
+// Summation units per segment U and waves per segment wpsp of the wave kernel
+// (waves = nseg * wpsp, about one per SIMD).  U = the power of two that makes
+// units of 22..44 slots, a function of the segment alone (capped by S_seg and
+// side_cap / nseg), so every launch sums a row in the same order whatever the
+// segment count; wpsp = floor(4 CUs / nseg) clamped to [1, U], each wave
+// taking a contiguous run of whole units.  nseg * U <= side_cap.
 struct EdgePlan {
-    int U = 1, m = 1;
+    int U = 1, wpsp = 1;
     int64_t waves = 1;
 };
 EdgePlan edge_wave_plan(int64_t nseg, int64_t S_seg, int cus, int64_t side_cap);

@@ -13,7 +13,7 @@ import os
 import torch
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libmmpde_hip.so")
-ABI_VERSION = 11500
+ABI_VERSION = 11600
 
 ACT_NONE, ACT_TANH, ACT_RELU, ACT_ELU = 0, 1, 2, 3
 PAD_ZEROS, PAD_CIRCULAR = 0, 1
@@ -66,13 +66,6 @@ class GnnExec(ctypes.Structure):
                 ("degree", _P), ("seg_n", _I64)]
 
 
-class GnnCall(ctypes.Structure):
-    """mmpde_gnn_call: one mmpde_gnn_forward_ex call's arguments (mmpde_gnn_forward_pair)."""
-    _fields_ = [("u", _P), ("pos", _P), ("n", _I64), ("k", _I), ("nbr", _P), ("sc", GnnScales),
-                ("emb", _P), ("layers", _P), ("n_layers", _I), ("head", _P), ("workspace", _P),
-                ("out", _P), ("exec", _P)]
-
-
 class DmmGraphBranch(ctypes.Structure):
     _fields_ = [(n, _P) for n in ("emb0_w", "emb0_b", "emb1_w", "emb1_b", "emb1_rm", "emb1_rv",
                                   "emb3_w", "emb3_b", "emb4_w", "emb4_b", "emb4_rm", "emb4_rv")] + \
@@ -117,9 +110,6 @@ _SIGS = {
     "mmpde_linear_skinny_ws": (_I, [_P, _I64, _I64, _I64, _P, _I64, _P, _I64, _I, _P, _I64, _P, _I64,
                                     _P]),
     "mmpde_gnn_edge_backward_ex": (_I, [_P, _P, _P, _P, _I64, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
-    "mmpde_linear_chain_workspace_bytes": (_I64, [_I64, _I, _P]),
-    "mmpde_linear_chain_dmm": (_I, [_I]),
-    "mmpde_linear_chain_ws": (_I, [_P, _I64, _I64, _I, _P, _P, _P, _P, _P, _P, _I64, _P, _I64, _P]),
     "mmpde_traj_mse": (_I, [_P, _P, _I64, _I64, _P, _P]),
     "mmpde_conv2d": (_I, [_P, _I64, _I, _I, _I, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P]),
     "mmpde_resample_bilinear": (_I, [_P, _I64, _I, _I, _I, _I, _P, _P]),
@@ -139,7 +129,6 @@ _SIGS = {
     "mmpde_gnn_pack_f16x3": (_I, [_P, _I, _P, _P]),
     "mmpde_gnn_forward_ex": (_I, [_P, _P, _I64, _I, _P, GnnScales, _P, _P, _I, _P, _P, _P, _P,
                                   _P]),
-    "mmpde_gnn_forward_pair": (_I, [_P, _P]),
     "mmpde_dmm_workspace_bytes": (_I64, [_I64, _I64, _I, _I]),
     "mmpde_dmm_mesh_graph": (_I, [_P, _P, _I64, _I64, _P, _I, _P, _P, _P, _P, _P]),
     "mmpde_dmm_mesh_array": (_I, [_P, _P, _I64, _I64, _P, _P, _P, _P, _P]),

@@ -23,11 +23,11 @@ def env_world():
             int(os.environ.get("WORLD_SIZE", "1")))
 
 
-def init(backend: str | None = None):
-    """Initialise the process group when launched under torchrun; returns
-    (rank, local_rank, world)."""
+def init(backend: str | None = None, force: bool = False):
+    """Initialise the process group when launched under torchrun (or, with
+    force, for a one-rank world too); returns (rank, local_rank, world)."""
     rank, local, world = env_world()
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or force) and not dist.is_initialized():
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         if backend == "nccl":
@@ -64,10 +64,14 @@ def per_trajectory_mse(pred: torch.Tensor, labels: torch.Tensor, batches: int) -
     return (d * d).mean(dim=1)
 
 
+def _group():
+    return dist.is_available() and dist.is_initialized()
+
+
 def all_gather_losses(local: torch.Tensor, total: int) -> torch.Tensor:
     """Gather per-trajectory losses of every rank in trajectory order (the one
-    collective of the sharded step)."""
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    collective of the sharded step; runs whenever a process group exists)."""
+    if not _group():
         return local
     world = dist.get_world_size()
     sizes = [shard_range(total, r, world) for r in range(world)]
@@ -80,7 +84,7 @@ def all_gather_losses(local: torch.Tensor, total: int) -> torch.Tensor:
 
 
 def max_over_ranks(value: float, device=None) -> float:
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not _group():
         return value
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -88,7 +92,7 @@ def max_over_ranks(value: float, device=None) -> float:
 
 
 def barrier(device=None):
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if _group():
         if device is not None and device.type == "cuda":
             dist.barrier(device_ids=[device.index])
         else:

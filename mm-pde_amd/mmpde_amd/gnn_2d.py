@@ -19,6 +19,7 @@ device torch ops under autograd.
 from __future__ import annotations
 
 import ctypes
+from types import SimpleNamespace
 
 import torch
 from torch import nn
@@ -322,7 +323,7 @@ class MP_PDE_Solver_2D(nn.Module):  # noqa: N801 - reference name
         return out
 
     def _call(self, data, out, workspace, trace):
-        """(mmpde_gnn_call, out, keep-alive) of one eval forward (see forward)."""
+        """(mmpde_gnn_forward_ex arguments, out, keep-alive) of one eval forward (see forward)."""
         self.check_supported()
         u, pos = data.x, data.pos
         L.require_device(u, pos)
@@ -364,9 +365,10 @@ class MP_PDE_Solver_2D(nn.Module):  # noqa: N801 - reference name
         trace.seg_n = int(seg) if seg else 0
         trace.packed = (L.ptr(self.packed_f16x3(u.device)) if self.edge_gemm == "f16x3"
                         else None)
-        call = L.GnnCall(L.ptr(u), L.ptr(pos), n, nbr.shape[1], L.ptr(nbr), sc,
-                         ctypes.addressof(emb), ctypes.addressof(arr), len(arr),
-                         ctypes.addressof(head), L.ptr(workspace), L.ptr(out), ctypes.addressof(trace))
+        call = SimpleNamespace(u=L.ptr(u), pos=L.ptr(pos), n=n, k=nbr.shape[1], nbr=L.ptr(nbr), sc=sc,
+                               emb=ctypes.addressof(emb), layers=ctypes.addressof(arr), n_layers=len(arr),
+                               head=ctypes.addressof(head), workspace=L.ptr(workspace), out=L.ptr(out),
+                               exec=ctypes.addressof(trace))
         return call, out, (u, pos, nbr, deg, t_slot, workspace, out, trace, emb, arr, head)
 
 
@@ -387,26 +389,3 @@ class MP_PDE_Solver_2D(nn.Module):  # noqa: N801 - reference name
             h = layer.train_forward(h, u, pos_x, pos_y, variables, graph, self.edge_gemm)
         diff = self.output_mlp(h[:, None]).squeeze(1)
         return self.out_scales()[None].to(h.device) * diff
-
-
-def forward_pair(model_a: "MP_PDE_Solver_2D", data_a, model_b: "MP_PDE_Solver_2D", data_b,
-                 out_a=None, out_b=None, workspace_a=None, workspace_b=None, trace_a=None,
-                 trace_b=None):
-    """model_a(data_a), model_b(data_b) -- e.g. the MM-PDE step's model(graph_uniform)
-    and model_b(graph) (train_helper_2d.py:174-185) -- through mmpde_gnn_forward_pair:
-    one embedding, node-stage and head launch for both (bitwise the two separate
-    forwards).  Both in eval mode with edge_gemm 'f16x3' and the same layer count and
-    time window; otherwise the two forwards run one after the other."""
-    paired = (not model_a.training and not model_b.training and
-              model_a.edge_gemm == "f16x3" and model_b.edge_gemm == "f16x3" and
-              len(model_a.gnn_layers) == len(model_b.gnn_layers) >= 1 and
-              model_a.time_window == model_b.time_window)
-    if not paired:
-        return (model_a(data_a, out=out_a, workspace=workspace_a, trace=trace_a),
-                model_b(data_b, out=out_b, workspace=workspace_b, trace=trace_b))
-    ca, oa, ka = model_a._call(data_a, out_a, workspace_a, trace_a)
-    cb, ob, kb = model_b._call(data_b, out_b, workspace_b, trace_b)
-    calls = (L.GnnCall * 2)(ca, cb)
-    L.check(L.lib().mmpde_gnn_forward_pair(calls, L.stream(data_a.x.device)), "mmpde_gnn_forward_pair")
-    del ka, kb
-    return oa, ob

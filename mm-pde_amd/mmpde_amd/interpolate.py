@@ -111,8 +111,6 @@ class ItpNet(nn.Module):
         x = data.reshape(data.shape[0], -1)
         layers = [(d[i].weight, d[i].bias, act)
                   for i, act in ((0, L.ACT_TANH), (2, L.ACT_TANH), (4, L.ACT_TANH), (6, L.ACT_NONE))]
-        if x.shape[0] <= 64 and ops.CHAIN_RES_CUT:   # the four layers in one launch
-            return ops.linear_chain(x, layers)
         for w, b, act in layers:
             x = ops.linear_skinny(x, w, b, act)
         return x

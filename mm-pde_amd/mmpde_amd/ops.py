@@ -317,45 +317,6 @@ def linear_skinny(x: torch.Tensor, w: torch.Tensor, b=None, act: int = L.ACT_NON
     return y
 
 
-_CHAIN_WS = {}
-# res_cut's four layers as one chain launch (linear_chain) or four skinny
-# launches (the default: measured faster in the rollout step);
-# the same results to fp32 rounding (tests/test_gpu_dense.py)
-CHAIN_RES_CUT = False
-
-
-def linear_chain(x: torch.Tensor, layers, out: torch.Tensor | None = None) -> torch.Tensor:
-    """A chain of skinny linears in one launch (mmpde_linear_chain_ws):
-    layers = [(w, b, act), ...] (at most 4), x [m <= 64, k0].  The workspace
-    (counters zero, then the intermediate activations) is kept per device,
-    stream and shape, zeroed once; every call leaves its counters at zero."""
-    L.require_device(x)
-    x = L.f32c(x)
-    m, k0 = x.shape
-    nl = len(layers)
-    dims = [k0] + [int(w.shape[0]) for w, _, _ in layers]
-    ws_ = [L.f32c(w) for w, _, _ in layers]
-    bs_ = [L.f32c(b) if b is not None else None for _, b, _ in layers]
-    for l, w in enumerate(ws_):
-        if w.shape[1] != dims[l]:
-            raise ValueError(f"linear_chain: layer {l} weight {tuple(w.shape)} after width {dims[l]}")
-    y = out if out is not None else torch.empty((m, dims[-1]), dtype=torch.float32, device=x.device)
-    lib = L.lib()
-    cdims = (ctypes.c_int64 * (nl + 1))(*dims)
-    nb = lib.mmpde_linear_chain_workspace_bytes(m, nl, cdims)
-    key = (str(x.device), torch.cuda.current_stream(x.device).cuda_stream, m, tuple(dims))
-    ws = _CHAIN_WS.get(key)
-    if ws is None:
-        ws = torch.zeros((nb // 4 + 4,), dtype=torch.float32, device=x.device)
-        _CHAIN_WS[key] = ws
-    cw = (ctypes.c_void_p * nl)(*[L.ptr(w) for w in ws_])
-    cb = (ctypes.c_void_p * nl)(*[L.ptr(b) if b is not None else None for b in bs_])
-    ca = (ctypes.c_int * nl)(*[int(a) for _, _, a in layers])
-    L.check(lib.mmpde_linear_chain_ws(L.ptr(x), k0, m, nl, cdims, cw, None, cb, ca, L.ptr(y), dims[-1],
-                                      L.ptr(ws), nb, L.stream(x.device)), "mmpde_linear_chain_ws")
-    return y
-
-
 def linear_rows(x: torch.Tensor, w: torch.Tensor, b=None, act: int = L.ACT_NONE) -> torch.Tensor:
     """act(x @ w.T + b) for any number of rows (x [..., k]): linear_skinny on
     blocks of at most 4096 rows (the skinny kernel's row limit)."""

@@ -16,10 +16,7 @@ Burgers (DMM array mode) additionally interpolates u onto the moved mesh first
 moved mesh (data_creator_2d.py:208-209) feeds only graph.y, which no step
 reads, so the rollout (which has no labels) does not compute it.
 
-The fixed-grid GNN runs on a side stream beside the moving-mesh chain; with
-``pair = True`` the two GNNs run as one paired forward instead
-(gnn_2d.forward_pair: per layer the two edge stages, then one node-stage launch
-over both; one embedding and one head launch), bitwise the same.
+The fixed-grid GNN runs on a side stream beside the moving-mesh chain.
 
 Rollout: the prediction becomes the next step's input (u <- pred, t index + 1),
 which the reference itself never does (it only evaluates one-step losses,
@@ -33,7 +30,7 @@ from __future__ import annotations
 import torch
 
 from . import _lib as L
-from . import gnn_2d, ops
+from . import ops
 
 
 class MMPDERollout:
@@ -49,15 +46,6 @@ class MMPDERollout:
         # run the fixed-grid model beside the moving-mesh chain (False: one stream,
         # e.g. to time single kernels without a concurrent neighbour)
         self.overlap = True
-        # True: model and model_b as one paired forward (gnn_2d.forward_pair: one
-        # embedding / node-stage / head launch for both, bitwise the same).
-        # Measured slower at cy B=16 (2.17 vs 2.01 ms/step): the paired node
-        # launch costs what the two did (87.2 vs 2 x 42.4 us: the node kernel's
-        # time follows its rows), and the fixed-grid GNN can no longer run on a
-        # side stream, whose queued launches hide the main stream's launch gaps
-        # (serial wall 2.33 ms against a 2.02 ms kernel sum).  Default: two
-        # forwards, model on a side stream.
-        self.pair = False
         gc = graph_creator
         self.grid = gc.uniform_grid(self.device).contiguous()           # [N, 2]
         self.N = N = self.grid.shape[0]
@@ -180,11 +168,10 @@ class MMPDERollout:
         cur = torch.cuda.current_stream(self.device)
         side = self.side if self.overlap else cur
         nodes_u = self._nodes(u_flat, self.grid_rep, self.nbr_u, step_idx)
-        if not self.pair:
-            side.wait_stream(cur)
-            with torch.cuda.stream(side):
-                u.record_stream(side)
-                out_u = self.model(nodes_u, out=self.out_u, workspace=self.ws_gnn_u, trace=self._trace())
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            u.record_stream(side)
+            out_u = self.model(nodes_u, out=self.out_u, workspace=self.ws_gnn_u, trace=self._trace())
         mesh = self.dmm.mesh(u, self.xi, out=self.mesh, workspace=self.ws_dmm,
                              head_cache=self.dmm_cache)
         cells = ops.knn_moved_cells(mesh, self.xi, B, out=self.knn_cells) \
@@ -214,14 +201,8 @@ class MMPDERollout:
         else:
             u_m = u_flat
         nodes_m = self._nodes(u_m, mesh, nbr_m, step_idx)
-        if self.pair:
-            out_u, out_b = gnn_2d.forward_pair(self.model, nodes_u, self.model_b, nodes_m,
-                                               out_a=self.out_u, out_b=self.out_b,
-                                               workspace_a=self.ws_gnn_u, workspace_b=self.ws_gnn,
-                                               trace_a=self._trace(), trace_b=self._trace())
-        else:
-            out_b = self.model_b(nodes_m, out=self.out_b, workspace=self.ws_gnn, trace=self._trace())
-            cur.wait_stream(side)
+        out_b = self.model_b(nodes_m, out=self.out_b, workspace=self.ws_gnn, trace=self._trace())
+        cur.wait_stream(side)
         cur.wait_stream(side2)
         # interpolate_pred(...) + model(graph_uniform) (train_helper_2d.py:178-185):
         # (interp + res_cut) + out_u in the interpolation kernel's epilogue

@@ -57,16 +57,6 @@ def test_null_arguments_are_rejected_before_launch():
     assert lib.mmpde_gnn_edge_backward(None, None, None, None, 10, 35, None, None, None, None,
                                        None, None, None, None, None) == -1
     assert lib.mmpde_gnn_edge_source_sum(None, None, None, 10, None, None) == -1
-    # linear chain: null pointers and m > 64 refused; workspace sizing without a GPU
-    import ctypes
-    dims = (ctypes.c_int64 * 5)(2521, 2048, 512, 2048, 2521)
-    assert lib.mmpde_linear_chain_ws(None, 2521, 16, 4, dims, None, None, None, None, None, 2521, None, 0,
-                                     None) == -1
-    assert lib.mmpde_linear_chain_workspace_bytes(16, 4, dims) >= (4096 + 16 * (2048 + 512 + 2048)) * 4
-    assert lib.mmpde_linear_chain_workspace_bytes(16, 5, dims) == 0
-    # the DMM chain switch: query (-1) leaves it, set returns the previous value
-    cur = lib.mmpde_linear_chain_dmm(-1)
-    assert lib.mmpde_linear_chain_dmm(1 - cur) == cur and lib.mmpde_linear_chain_dmm(cur) == 1 - cur
     # fp16x3 edge backward: null pointers and an unknown GEMM mode refused before any launch
     assert lib.mmpde_gnn_edge_backward_ex(None, None, None, None, 10, 35, None, None, None, None, None,
                                           None, None, None, 1, None) == -1

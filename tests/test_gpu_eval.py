@@ -7,9 +7,12 @@ Bars: losses 1e-4 relative to the oracle (an MSE of fp32 predictions that
 agree to ~1e-6 relative); sharded vs single process: bit for bit in both edge
 GEMM modes (every kernel computes a trajectory's rows independently of the
 others: the f16x3 split scale is taken per trajectory, and the edge kernel's
-summation units and the skinny linears' K splits do not depend on the batch --
-for the edge kernel, for any power-of-two batch of >= 16 cylinder
-trajectories).
+summation units and the skinny linears' K splits depend on the trajectory and
+the layer shapes alone, never on how many trajectories share a launch), for
+shards of 16, 8 and 12 trajectories per rank -- configs[4]'s strong-scaling
+shards of 64 trajectories over 4 and 8 GPUs are 16 and 8 per rank.
+The RCCL path of dist.py (backend "nccl") runs in a one-rank process group on
+the box's one GPU: the collectives the bench and the sharded evaluation call.
 """
 import os
 import socket
@@ -115,15 +118,17 @@ def _run_shard(kind, total, mode, steps, n_roll, dev, D, EV, MMPDERollout):
     return res["per_trajectory"].cpu(), res["mean"].cpu(), fin
 
 
+@pytest.mark.parametrize("total", [32, 16, 24])
 @pytest.mark.parametrize("mode", ["f32", "f16x3"])
-def test_sharded_eval_matches_single_process(dev, mode):
+def test_sharded_eval_matches_single_process(dev, mode, total):
     from mmpde_amd import dist as D
     from mmpde_amd import evaluate as EV
     from mmpde_amd.rollout import MMPDERollout
 
-    # 32 trajectories, shards of 16: the edge kernel sums every row in the same
-    # order at 16 and at 32 trajectories (csrc/edge_wave.hip, summation units)
-    kind, total, world, steps, n_roll = "cy", 32, 2, [1, 7, 20], 4
+    # shards of 16, 8 and 12 trajectories against one launch of all of them:
+    # the edge kernel's summation units depend on the trajectory alone
+    # (csrc/edge_wave.hip, edge_wave_plan)
+    kind, world, steps, n_roll = "cy", 2, [1, 7, 20], 4
     single = _run_shard(kind, total, mode, steps, n_roll, dev, D, EV, MMPDERollout)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -151,3 +156,41 @@ def test_sharded_eval_matches_single_process(dev, mode):
             if not torch.equal(a, b):
                 bad.append((rank, name, rel))
     assert not bad, bad
+
+
+def _rccl_worker(port, q):
+    import sys
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "mm-pde_amd")]
+    os.environ.update(RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    try:
+        import torch.distributed as dist
+        from mmpde_amd import dist as D
+
+        rank, local, world = D.init(backend="nccl", force=True)
+        dev = torch.device(f"cuda:{local}")
+        assert dist.get_backend() == "nccl"
+        losses = torch.arange(5, dtype=torch.float32, device=dev) * 0.25
+        got = D.all_gather_losses(losses, 5)
+        mx = D.max_over_ranks(1.5, dev)
+        D.barrier(dev)
+        torch.cuda.synchronize(dev)
+        dist.destroy_process_group()
+        q.put((got.cpu().numpy(), mx, None))
+    except Exception as e:
+        q.put((None, None, repr(e)))
+
+
+def test_rccl_collectives_one_rank(dev):
+    """dist.py over RCCL (torch backend "nccl"): init, the loss all-gather, the
+    max-over-ranks all-reduce and the device barrier, as the bench and the
+    sharded evaluation call them, in a one-rank group on this box's GPU."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), q))
+    p.start()
+    got, mx, err = q.get(timeout=180)
+    p.join(timeout=60)
+    assert err is None, err
+    assert p.exitcode == 0
+    assert got.tolist() == [0.0, 0.25, 0.5, 0.75, 1.0] and mx == 1.5

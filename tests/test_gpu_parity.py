@@ -406,11 +406,7 @@ def test_edge_mean_vs_torch_fp32(dev):
 
 
 # ============================================================================ DMM
-@pytest.mark.parametrize("chain", [0, 1])
-def test_dmm_mesh_graph_matches_autograd(dev, chain):
-    """chain: the output MLP + P as per-layer skinny launches (0, the default)
-    or one mmpde_linear_chain launch (1)."""
-    from mmpde_amd import _lib as L
+def test_dmm_mesh_graph_matches_autograd(dev):
     from mmpde_amd.synth import build_models, fields
 
     pde, _, _, _, dmm, _ = build_models("cy")
@@ -421,20 +417,14 @@ def test_dmm_mesh_graph_matches_autograd(dev, chain):
                                          grid[None, :, 1].repeat(B, 1), grid)
     ref = torch.cat((ref_x, ref_y), -1)
     dmm.to(dev)
-    prev = L.lib().mmpde_linear_chain_dmm(chain)
-    try:
-        got = dmm.mesh(u.to(dev), grid.to(dev))
-        torch.cuda.synchronize()
-    finally:
-        L.lib().mmpde_linear_chain_dmm(prev)
+    got = dmm.mesh(u.to(dev), grid.to(dev))
+    torch.cuda.synchronize()
     disp = (ref - grid.repeat(B, 1)).abs().max().item()
     assert disp > 1e-3                                         # the mesh actually moves
     _close(got, ref, 0.0, 2e-6, "dmm graph mesh")              # absolute, coords in [0,1]
 
 
-@pytest.mark.parametrize("chain", [0, 1])
-def test_dmm_mesh_array_matches_autograd(dev, chain):
-    from mmpde_amd import _lib as L
+def test_dmm_mesh_array_matches_autograd(dev):
     from mmpde_amd.synth import build_models, burgers_grid_points, fields
 
     pde, _, _, _, dmm, gc = build_models("burgers")
@@ -444,12 +434,8 @@ def test_dmm_mesh_array_matches_autograd(dev, chain):
                                 48, 48)
     ref = torch.cat((ox, oy), -1)
     dmm.to(dev)
-    prev = L.lib().mmpde_linear_chain_dmm(chain)
-    try:
-        got = dmm.mesh(u.to(dev).contiguous(), gc.xi_grid_xy(48, 48, dev))
-        torch.cuda.synchronize()
-    finally:
-        L.lib().mmpde_linear_chain_dmm(prev)
+    got = dmm.mesh(u.to(dev).contiguous(), gc.xi_grid_xy(48, 48, dev))
+    torch.cuda.synchronize()
     _close(got, ref, 0.0, 2e-6, "dmm array mesh")
 
 
@@ -590,35 +576,6 @@ def test_graph_creator_api_equals_engine(dev):
     ei = graph.edge_index
     assert ei.dtype == torch.int64 and ei.shape == (2, B * 2521 * 35)
     assert torch.equal(ei[0].reshape(-1, 35).int(), graph.nbr)
-
-
-@pytest.mark.parametrize("edge_gemm", ["f16x3", "f32"])
-def test_paired_gnn_forward_equals_separate(dev, edge_gemm):
-    """The rollout's paired GNN forward (MMPDERollout.pair: gnn_2d.forward_pair ->
-    mmpde_gnn_forward_pair, one embedding / node-stage / head launch over
-    model's and model_b's rows) against the two separate forwards, bit for bit,
-    over two autoregressive steps at the bench geometry (16 cylinder
-    trajectories).  In f32 mode forward_pair falls back to two forwards."""
-    from mmpde_amd.rollout import MMPDERollout
-    from mmpde_amd.synth import build_models, fields
-
-    pde, model, model_b, itp, dmm, gc = build_models("cy")
-    for m in (model, model_b, itp, dmm):
-        m.to(dev)
-    for m in (model, model_b):
-        m.edge_gemm = edge_gemm
-    B = 16
-    u0 = fields(pde.ori_grid, B, 30)[:, 0].to(dev)
-    outs = []
-    for pair in (True, False):
-        eng = MMPDERollout("cy", model, model_b, itp, dmm, gc, B, dev)
-        eng.pair = pair
-        p1 = eng.step(u0, 1).clone()
-        o = (eng.out_u.clone(), eng.out_b.clone())
-        p2 = eng.step(p1, 2).clone()
-        outs.append((p1, p2) + o)
-    for a, b in zip(outs[0], outs[1]):
-        assert torch.equal(a, b)
 
 
 # ============================================================================ full size

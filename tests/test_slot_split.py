@@ -1,14 +1,16 @@
 """Host check of the wave edge kernel's work split (csrc/edge_wave.hip,
 csrc/layer.hip prep, layer.hpp EdgeSplit / edge_wave_plan), restated in Python:
 a segment's S = ntiles * k neighbour slots are cut into U summation units
-(unit u = slots [u S / U, (u + 1) S / U)); wave j walks units [j m, (j + 1) m);
+(unit u = slots [u S / U, (u + 1) S / U)); wave j of the w waves of a segment
+walks units [j U / w, (j + 1) U / w);
 a run (the part of a unit inside one tile) closes at its tile's end, at a unit
 boundary and at the wave's end; a run that starts a tile goes to out, a run
 that starts at a unit boundary inside a tile to side[u]; the node stage adds,
 for tile t, the side blocks of the units lo..hi given in closed form.  Brute
-force over many (ntiles, k, U, m): every slot of every tile is summed exactly
+force over many (ntiles, k, U, w): every slot of every tile is summed exactly
 once, in slot order, and the runs -- hence the summation order -- depend on
-(S, U) only, not on how many units a wave takes."""
+(S, U) only, not on how many units a wave takes; U depends on the segment
+alone, so any shard of a batch sums every row in the same order."""
 import pytest
 
 
@@ -19,30 +21,30 @@ def closed_form(t, k, U, S):
 
 
 def plan(nseg, S_seg, cus=256, side_cap=1 << 40):
-    """edge_wave_plan (edge_wave.hip): (U, m, waves)."""
-    u0 = 1
-    while u0 * 2 * 44 <= S_seg:
-        u0 *= 2
-    u1 = max(4 * cus // nseg, 1)
-    m = -(-u0 // u1)
-    U = u1 * m
+    """edge_wave_plan (edge_wave.hip): (U, waves per segment, waves)."""
+    U = 1
+    while U * 2 * 22 <= S_seg:
+        U *= 2
     cap = min(S_seg, side_cap // nseg)
     if U > cap:
-        U, m = max(cap, 1), 1
-    return U, m, nseg * (U // m)
+        U = max(cap, 1)
+    w = min(max(4 * cus // nseg, 1), U)
+    return U, w, nseg * w
 
 
-def runs(ntiles, k, U, m):
+def runs(ntiles, k, U, w):
     """(tile, first slot, last slot + 1, destination) of every run, as the
-    kernel's slot stream produces them, wave by wave."""
+    kernel's slot stream produces them, wave by wave (w waves)."""
     S = ntiles * k
     out = []
-    for j in range(-(-U // m)):
-        u_end = min((j + 1) * m, U)
-        s0, s1 = j * m * S // U, u_end * S // U
-        u_next = j * m + 1
+    for j in range(w):
+        u_begin, u_end = j * U // w, (j + 1) * U // w
+        s0, s1 = u_begin * S // U, u_end * S // U
+        if s0 >= s1:
+            continue
+        u_next = u_begin + 1
         ub = u_next * S // U if u_next < u_end else s1
-        run_side = j * m if s0 % k else -1
+        run_side = u_begin if s0 % k else -1
         s, start = s0, s0
         while s < s1:
             new_unit = s + 1 == ub
@@ -59,16 +61,16 @@ def runs(ntiles, k, U, m):
     return out
 
 
-@pytest.mark.parametrize("ntiles,k,U,m", [(158, 35, 64, 1), (158, 35, 64, 2), (158, 35, 128, 4),
-                                          (7, 35, 20, 1), (7, 1, 7, 1), (7, 3, 20, 3),
-                                          (316, 35, 945, 1), (1, 35, 35, 5), (3, 35, 6, 2),
-                                          (576, 35, 1024, 1), (100, 8, 512, 8), (5, 4, 19, 1)])
-def test_runs_cover_every_slot_once(ntiles, k, U, m):
+@pytest.mark.parametrize("ntiles,k,U,w", [(158, 35, 64, 64), (158, 35, 128, 64), (158, 35, 128, 85),
+                                          (158, 35, 128, 42), (7, 35, 20, 20), (7, 1, 7, 7), (7, 3, 20, 7),
+                                          (316, 35, 945, 945), (1, 35, 35, 7), (3, 35, 6, 3),
+                                          (576, 35, 1024, 1024), (100, 8, 512, 64), (5, 4, 19, 19),
+                                          (144, 35, 128, 32), (158, 35, 128, 1)])
+def test_runs_cover_every_slot_once(ntiles, k, U, w):
     S = ntiles * k
     U = min(U, S)
-    if U % m:
-        pytest.skip("U must be a multiple of m")
-    rs = runs(ntiles, k, U, m)
+    w = min(w, U)
+    rs = runs(ntiles, k, U, w)
     per_tile = {}
     for t, s, e, dest in rs:
         per_tile.setdefault(t, []).append((s, e, dest))
@@ -85,23 +87,24 @@ def test_runs_cover_every_slot_once(ntiles, k, U, m):
         assert [p[2][1] for p in parts[1:]] == list(range(lo, hi + 1))
 
 
-@pytest.mark.parametrize("ntiles,k,U", [(158, 35, 64), (144, 35, 64), (100, 8, 256)])
-def test_runs_do_not_depend_on_units_per_wave(ntiles, k, U):
-    base = sorted(runs(ntiles, k, U, 1))
-    for m in (2, 4, 8):
-        if U % m == 0:
-            assert sorted(runs(ntiles, k, U, m)) == base
+@pytest.mark.parametrize("ntiles,k,U", [(158, 35, 128), (144, 35, 128), (100, 8, 256)])
+def test_runs_do_not_depend_on_waves_per_segment(ntiles, k, U):
+    base = sorted(runs(ntiles, k, U, U))
+    for w in (1, 3, 16, 42, 64, 85, U // 2):
+        assert sorted(runs(ntiles, k, U, w)) == base
 
 
-def test_plan_fills_the_chip_and_is_shared_by_power_of_two_batches():
+def test_plan_is_segment_only_and_fills_the_chip():
     S_cy = 158 * 35                       # cylinder: 2521 nodes, k = 35
-    for nseg in (1, 2, 4, 8, 16, 32, 64, 128):
-        U, m, waves = plan(nseg, S_cy)
-        assert U % m == 0 and waves == nseg * U // m
-        assert waves == 1024                # one wave per SIMD on 256 CUs
-    # 16 and more trajectories share U (the same summation order for every row)
-    assert len({plan(nseg, S_cy)[0] for nseg in (16, 32, 64, 128)}) == 1
-    # other counts still fill the chip to within one unit
-    for nseg in (3, 5, 12, 24):
-        U, m, waves = plan(nseg, S_cy)
-        assert waves <= 1024 and U % m == 0
+    S_bu = 144 * 35                       # Burgers 48 x 48: 2304 nodes
+    for S in (S_cy, S_bu):
+        # every segment count sums a row in the same order (U from the segment alone)
+        assert len({plan(nseg, S)[0] for nseg in range(1, 129)}) == 1
+    assert plan(16, S_cy)[0] == 128 and plan(32, S_bu)[0] == 128
+    for nseg in (8, 16, 32, 64, 128):      # power-of-two shards: one wave per SIMD
+        assert plan(nseg, S_cy)[2] == 1024
+    for nseg in (3, 5, 12, 24):            # others: never more waves than SIMDs
+        U, w, waves = plan(nseg, S_cy)
+        assert waves <= 1024 and w <= U
+    # the side-block cap (3 seg_n / 16 blocks per segment) is a function of the segment
+    assert plan(16, 5530, side_cap=16 * (3 * 2521 // 16))[0] == 128
