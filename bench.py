@@ -282,6 +282,7 @@ def main():
                  "ms_per_step": 1e3 * el32 / args.steps,
                  "final_state_max_rel_diff_vs_main": rel}
     launches = tracer.launch_times_ms()
+    ties = eng.knn_query_ties() if moving else 0
     tracer.pool.close()
 
     if rank != 0:
@@ -347,6 +348,10 @@ def main():
         "node_stage_ms": node_ms / nl,
         "finite": finite,
     }
+    if moving:
+        # kNN-30 queries with an exact fp64 distance tie (sklearn's order
+        # unpinned there), over every step this process ran
+        line["knn_query_ties"] = ties
     if not moving:
         # configs[2] is quoted against the scatter-add / HBM roofline: SURVEY.md
         # §8(d)'s fused minimum of ~18.7 KB of HBM traffic per GNN node-update

@@ -122,9 +122,14 @@ int mmpde_knn_graph_cand(const float *pos, const float *xi, const float *cells, 
  * (dx*dx + dy*dy), ascending, ties by index.
  * src [batches*n_src, 2], qry [batches*n_qry, 2] fp32
  * idx_out [batches*n_qry, k] int32 LOCAL source index (0..n_src-1).
+ * ties (nullable, one int32 the caller zeroes): += the number of queries
+ * whose sorted fp64 distances hold an exact tie inside the first k or
+ * between ranks k-1 and k -- the only inputs on which sklearn's own order (its
+ * KD-tree traversal) may differ from (distance, index); parity with sklearn is
+ * unpinned for those queries.
  * Requires k <= n_src <= 16384, k <= 63. */
 int mmpde_knn_query(const float *src, const float *qry, int64_t batches, int64_t n_src,
-                    int64_t n_qry, int k, int32_t *idx_out, mmpde_stream_t stream);
+                    int64_t n_qry, int k, int32_t *idx_out, int32_t *ties, mmpde_stream_t stream);
 
 /* mmpde_knn_query of qry [batches * n_per, 2] onto moved points src = xi +
  * displacement [batches * n_per, 2] (reference data_creator_2d.py:66-78, the
@@ -134,11 +139,12 @@ int mmpde_knn_query(const float *src, const float *qry, int64_t batches, int64_t
  * complete, by the full search elsewhere.  ref [n_per, 2]: the reference
  * points the table was built for (NULL: xi); cells from
  * mmpde_knn_moved_cells(src, xi).  n_src = n_qry = n_per; scratch as for
- * mmpde_knn_graph_cand.  k <= 64 and 128 <= n_per <= 4096, else it is
- * mmpde_knn_query. */
+ * mmpde_knn_graph_cand; ties as for mmpde_knn_query (each query counted
+ * once, by whichever kernel answered it).  k <= 64 and 128 <= n_per <= 4096,
+ * else it is mmpde_knn_query. */
 int mmpde_knn_query_cand(const float *src, const float *qry, const float *xi, const float *ref,
                          const float *cells, float skip_above, int64_t batches, int64_t n_per, int k,
-                         const int32_t *cand, int32_t *idx_out, void *scratch,
+                         const int32_t *cand, int32_t *idx_out, int32_t *ties, void *scratch,
                          mmpde_stream_t stream);
 
 /* torch_cluster.radius_graph(pos, r, batch, loop=False, max_num_neighbors)

@@ -232,12 +232,17 @@ template <bool QUERY>
 __device__ __forceinline__ void knn_finish(const float2 *sP, typename KeyTraits<QUERY>::key_t *sKey,
                                            int *sIdx, int *sSel, int m, float2 q, int kk, int k, int qi,
                                            int b, int n_src, int n_q, int cpl, int lane, uint64_t below,
-                                           int32_t *__restrict__ out, int32_t *__restrict__ degenerate) {
+                                           int32_t *__restrict__ out, int32_t *__restrict__ degenerate,
+                                           bool count_tie = true) {
     typedef KeyTraits<QUERY> KT;
     typedef typename KT::key_t key_t;
     key_t mk = ~key_t(0);
     int mi = 0x7fffffff;
     int rank = lane;
+    // QUERY: an exact fp64 distance tie inside the first kk (order) or between
+    // ranks kk - 1 and kk (set): the inputs on which sklearn's order is its
+    // KD-tree's traversal, not (distance, index) -- counted in *degenerate
+    bool tie = false;
     if (m <= 64) {
         // The common case (a mesh point's list holds ~1.5 kk): one pair per
         // lane, one 64-wide bitonic sort.
@@ -250,6 +255,10 @@ __device__ __forceinline__ void knn_finish(const float2 *sP, typename KeyTraits<
         }
         wave_sort64_ki(k0, i0, lane);
         if (lane < kk) mi = i0;
+        if (QUERY) {
+            const key_t kn = (key_t)__shfl((unsigned long long)k0, (lane + 1) & 63, 64);
+            tie = __ballot(lane < kk && lane + 1 < m && k0 == kn) != 0ull;
+        }
     } else if (m <= 128) {
         // Two pairs per lane, one 128-wide bitonic sort.
         wave_lds_sync();
@@ -265,6 +274,11 @@ __device__ __forceinline__ void knn_finish(const float2 *sP, typename KeyTraits<
         }
         wave_sort128(k0, i0, k1, i1, lane);
         if (lane < kk) mi = i0;
+        if (QUERY) {  // element lane + 1: lane 63's is element 64 (k1 of lane 0)
+            const key_t n0 = (key_t)__shfl((unsigned long long)k0, (lane + 1) & 63, 64);
+            const key_t n1 = (key_t)__shfl((unsigned long long)k1, 0, 64);
+            tie = __ballot(lane < kk && k0 == (lane == 63 ? n1 : n0)) != 0ull;
+        }
     } else if (m <= kCap) {
         wave_lds_sync();
         for (int i = lane; i < m; i += 64) sKey[i] = KT::key(sP[sIdx[i]], q);
@@ -272,14 +286,17 @@ __device__ __forceinline__ void knn_finish(const float2 *sP, typename KeyTraits<
         for (int i = lane; i < m; i += 64) {
             const key_t ki = sKey[i];
             const int ii = sIdx[i];
-            int rk = 0;
+            int rk = 0, eq_after = 0;
             for (int f = 0; f < m; ++f) {
                 const key_t fk = sKey[f];
                 const int fi = sIdx[f];
                 rk += (fk < ki) || (fk == ki && fi < ii);
+                eq_after += fk == ki && fi > ii;
             }
             if (rk < kk) sSel[rk] = ii;
+            tie = tie || (QUERY && rk < kk && eq_after > 0);
         }
+        tie = __ballot(tie) != 0ull;
         wave_lds_sync();
         if (lane < kk) mi = sSel[lane];
     } else {
@@ -326,16 +343,21 @@ __device__ __forceinline__ void knn_finish(const float2 *sP, typename KeyTraits<
             mi = sIdx[lane];
         }
         rank = 0;
+        int dup = 0;
         for (int f = 0; f < kk; ++f) {
             const key_t fk = sKey[f];
             const int fi = sIdx[f];
             rank += (fk < mk) || (fk == mk && fi < mi);
+            dup += fk == mk && fi != mi;
         }
+        // ties inside the first kk, or more points at the kk-th key than taken
+        tie = __ballot(lane < kk && dup > 0) != 0ull || eq_taken > need;
     }
     wave_lds_sync();  // the next query overwrites sKey / sIdx / sSel
     const int64_t row = ((int64_t)b * n_q + qi) * k;
     if (QUERY) {
         if (lane < kk) out[row + rank] = mi;
+        if (tie && count_tie && lane == 0 && degenerate) atomicAdd(degenerate, 1);
     } else {
         const uint64_t smask = __ballot(lane < kk && mi == qi);
         const bool has_self = smask != 0ull;
@@ -373,7 +395,11 @@ __global__ __launch_bounds__(256) void knn_kernel(const float2 *__restrict__ pts
     const int b = blockIdx.y;
     int q_count = n_q;  // queries of this trajectory to answer
     __shared__ int sList[QPB];
+    // QUERY ties are counted for the queries the candidate kernel did not
+    // answer (its miss flags, valid unless the trajectory skipped the table)
+    const uint8_t *miss_cnt = miss;
     if (miss && cell_skipped(cells, b)[role]) {  // workgroup-uniform: the plain search
+        miss_cnt = nullptr;
         if (blockIdx.x == 0 && threadIdx.x == 0) cell_last_miss(cells, b)[role] = n_q;
         miss = nullptr;
     }
@@ -465,7 +491,7 @@ __global__ __launch_bounds__(256) void knn_kernel(const float2 *__restrict__ pts
             ++pidx;
         }
         knn_finish<QUERY>(sP, sKey[wave], sIdx[wave], sSel[wave], m, q, kk, k, qi, b, n_src, n_q, CPL, lane,
-                          below, out, degenerate);
+                          below, out, degenerate, !miss_cnt || miss_cnt[(int64_t)b * n_q + qi] != 0);
     }
 }
 
@@ -844,7 +870,7 @@ __global__ __launch_bounds__(256) void knn_cand_kernel(const float2 *__restrict_
     }
     int i0 = min(max(cr[lane], 0), n_per - 1), i1 = min(max(cr[64 + lane], 0), n_per - 1);
     key_t k0 = 0, k1 = 0;
-    bool sorted = false;
+    bool sorted = false, tie = false;  // tie: as knn_finish's (QUERY)
     if constexpr (QUERY) if (kk < 64) {
         // sklearn's fp64 order, found by the cheaper fp32 (key, index) sort and
         // checked exactly: ranks 0 .. kk-1 must be in fp64 (key, index) order
@@ -865,12 +891,19 @@ __global__ __launch_bounds__(256) void knn_cand_kernel(const float2 *__restrict_
             k0 = e0;
             i0 = j0;
             sorted = true;
+            // rank kk's fp64 key exceeds rank kk - 1's (the margin): ties only inside
+            tie = __ballot(lane < kk - 1 && e0 == en) != 0ull;
         }
     }
     if (!sorted) {
         k0 = KT::key(X[i0], q);
         k1 = KT::key(X[i1], q);
         wave_sort128(k0, i0, k1, i1, lane);
+        if (QUERY) {  // element lane + 1 (lane 63: element 64, k1 of lane 0)
+            const key_t n0 = (key_t)__shfl((unsigned long long)k0, (lane + 1) & 63, 64);
+            const key_t n1 = (key_t)__shfl((unsigned long long)k1, 0, 64);
+            tie = __ballot(lane < kk && k0 == (lane == 63 ? n1 : n0)) != 0ull;
+        }
     }
     const key_t key_kk = __shfl(k0, kk - 1, 64);
     float d_kk;
@@ -887,6 +920,7 @@ __global__ __launch_bounds__(256) void knn_cand_kernel(const float2 *__restrict_
     const int mi = i0, rank = lane;
     if (QUERY) {
         if (lane < kk) out[p * k + rank] = mi;
+        if (tie && lane == 0 && degenerate) atomicAdd(degenerate, 1);
     } else {
         const uint64_t smask = __ballot(lane < kk && mi == pl);
         const bool has_self = smask != 0ull;
@@ -1093,22 +1127,21 @@ extern "C" int mmpde_knn_graph_cand(const float *pos, const float *xi, const flo
 
 extern "C" int mmpde_knn_query_cand(const float *src, const float *qry, const float *xi, const float *ref,
                                     const float *cells, float skip_above, int64_t batches, int64_t n_per, int k,
-                                    const int32_t *cand, int32_t *idx_out, void *scratch,
+                                    const int32_t *cand, int32_t *idx_out, int32_t *ties, void *scratch,
                                     mmpde_stream_t stream) {
     MMPDE_REQUIRE(src && qry && xi && cells && cand && idx_out && scratch);
     hipStream_t st = as_stream(stream);
     if (!cand_path_applies(batches, n_per, k))
-        return launch_knn<true>(src, qry, batches, n_per, n_per, k, idx_out, nullptr, st);
+        return launch_knn<true>(src, qry, batches, n_per, n_per, k, idx_out, ties, st);
     return knn_cand_launch<true>(src, qry, xi, ref ? ref : xi, cells, skip_above, batches, n_per, k, cand,
-                                 idx_out, nullptr, scratch, st);
+                                 idx_out, ties, scratch, st);
 }
 
 extern "C" int mmpde_knn_query(const float *src, const float *qry, int64_t batches,
-                               int64_t n_src, int64_t n_qry, int k, int32_t *idx_out,
+                               int64_t n_src, int64_t n_qry, int k, int32_t *idx_out, int32_t *ties,
                                mmpde_stream_t stream) {
     MMPDE_REQUIRE(src && qry && idx_out);
-    return launch_knn<true>(src, qry, batches, n_src, n_qry, k, idx_out, nullptr,
-                            as_stream(stream));
+    return launch_knn<true>(src, qry, batches, n_src, n_qry, k, idx_out, ties, as_stream(stream));
 }
 
 extern "C" int mmpde_radius_graph(const float *pos, int64_t batches, int64_t n_per, float r,

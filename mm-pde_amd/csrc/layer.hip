@@ -829,8 +829,24 @@ struct NodeArgs2 {
     int64_t tiles0;
 };
 
+// Profiling builds only (tools/ubench/node_ubench with -DMMPDE_NODE_STAMPS):
+// wave 0 of every workgroup records the shader clock at the phase boundaries
+// into g_node_stamps[block][8] (vector stores).
+#ifdef MMPDE_NODE_STAMPS
+__device__ uint64_t *g_node_stamps;
+#define NODE_STAMP(i)                                                                       \
+    do {                                                                                   \
+        if (threadIdx.x == 0) g_node_stamps[(int64_t)blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define NODE_STAMP(i) \
+    do {              \
+    } while (0)
+#endif
+
 template <bool NEXT, bool F16X3, int RB>
 __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs2 pp) {
+    NODE_STAMP(0);
     constexpr int ROWS = 16 * RB;
     const bool second = (int64_t)blockIdx.x >= pp.tiles0;  // workgroup-uniform
     const NodeArgs &p = pp.a[second ? 1 : 0];
@@ -877,6 +893,7 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs2 pp) {
         bU2.load(p.pk + kPkU2, 4, wave, 0, wu2, 0, lane);
     }
 
+    NODE_STAMP(1);
     // ---- [h | mean] -> image (K = 256)
     if constexpr (ROWS * 8 <= 256) {  // h on waves 0-3, mean on waves 4-7 at once
         if (tid < 256) prep<F16X3, ROWS>(p.h, LH, row0, p.n, true, img, 256, 0, rs[0], hres, 0, 256);
@@ -911,9 +928,11 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs2 pp) {
             }
         }
     }
+    NODE_STAMP(3);
     __syncthreads();
     prep<F16X3, ROWS>(stage, NLD, 0, ROWS, false, img, 128, 0, rs[2]);
     __syncthreads();
+    NODE_STAMP(4);
 
     // ---- update_net_2 + residual + BatchNorm(eval)
     BOps<F16X3, S1> bA, bB;
@@ -943,14 +962,17 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs2 pp) {
             }
         }
     }
+    NODE_STAMP(5);
     if constexpr (NEXT) {
         __syncthreads();
         prep<F16X3, ROWS>(stage, NLD, 0, ROWS, false, img, 128, 0, rs[3]);
         __syncthreads();
+        NODE_STAMP(6);
         // ---- next layer's message_net_1 node halves
         proj_phase<F16X3, RB>(bA, img, rs[3], &rowv[0][0], w1c, p.pkn, w1r, tw, row0, p.n, p.seg_n,
                               p.a_out, p.b_out, p.rng_out, wave, lane, NODE_EARLY_B ? &bB : nullptr);
     }
+    NODE_STAMP(7);
 }
 
 // ---------------------------------------------------------------------------

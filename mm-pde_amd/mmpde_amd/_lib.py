@@ -102,8 +102,8 @@ _SIGS = {
     "mmpde_knn_graph_cand_scratch_bytes": (_I64, [_I64, _I64]),
     "mmpde_knn_skip_threshold": (_I, [_P, _P, _I64, _P, _I, _I, _P, _P]),
     "mmpde_knn_graph_cand": (_I, [_P, _P, _P, _F, _I64, _I64, _I, _P, _P, _P, _P, _P]),
-    "mmpde_knn_query_cand": (_I, [_P, _P, _P, _P, _P, _F, _I64, _I64, _I, _P, _P, _P, _P]),
-    "mmpde_knn_query": (_I, [_P, _P, _I64, _I64, _I64, _I, _P, _P]),
+    "mmpde_knn_query_cand": (_I, [_P, _P, _P, _P, _P, _F, _I64, _I64, _I, _P, _P, _P, _P, _P]),
+    "mmpde_knn_query": (_I, [_P, _P, _I64, _I64, _I64, _I, _P, _P, _P]),
     "mmpde_edge_index_from_nbr": (_I, [_P, _I64, _I, _P, _P]),
     "mmpde_linear_skinny": (_I, [_P, _I64, _I64, _I64, _P, _I64, _P, _I64, _I, _P, _I64, _P]),
     "mmpde_linear_skinny_workspace_bytes": (_I64, [_I64, _I64, _I64]),

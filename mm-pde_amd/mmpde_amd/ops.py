@@ -119,6 +119,67 @@ def knn_table_share(cells: torch.Tensor, batches: int, n_per: int) -> torch.Tens
     return 1.0 - miss.float() / n_per
 
 
+class KnnTablePolicy:
+    """Per-role choice between the candidate table (knn_graph_moved /
+    knn_query_moved) and the plain full search for a rollout, from a cost model
+    and the share f of lookups the table answered at an earlier step.
+
+    Cost model (tools/knn_cand_time.py, cy B=16 on MI355X): the table path costs
+    about T_cand + (1 - f) T_full -- the candidate kernel (38-42 us when every
+    lookup passes) plus the full search of the lookups it could not answer --
+    against T_full (59-74 us) for the full search, so it pays only while f >
+    T_cand / T_full ~ 0.6; MIN_SHARE = 0.7 leaves room for the sorts the failed
+    lookups also pay.  f is read back without a sync: after a table step the
+    per-trajectory miss counters are copied to pinned host memory behind an
+    event and consumed at a later step.  Below MIN_SHARE the role runs the full
+    search -- no table, candidate or cell kernels -- for PROBE_EVERY steps, then
+    probes the table again.  Either path gives the same indices bit for bit."""
+
+    MIN_SHARE = 0.7
+    PROBE_EVERY = 16
+    CHECK_EVERY = 4
+
+    def __init__(self, device, batches: int, n_per: int, roles):
+        self.device = torch.device(device)
+        self.B, self.N = batches, n_per
+        self.state = {r: {"table": True, "wait": 0, "since": 0, "pending": None} for r in roles}
+        self.enabled = True
+
+    def use_table(self, role) -> bool:
+        st = self.state[role]
+        pend = st["pending"]
+        if pend is not None and pend[0].query():
+            st["pending"] = None
+            share = 1.0 - float(pend[1].sum()) / (self.B * self.N)
+            st["last_share"] = share
+            if share < self.MIN_SHARE:
+                st["table"], st["wait"] = False, self.PROBE_EVERY
+        if not st["table"]:
+            st["wait"] -= 1
+            if st["wait"] < 0:
+                st["table"], st["since"] = True, 0       # probe the table again
+        return st["table"] or not self.enabled
+
+    def after_table(self, role, cells: torch.Tensor, column: int) -> None:
+        """Queue the read-back of the miss counters of the call just made with
+        `cells` (on the current stream, after that call) every CHECK_EVERY table
+        steps and at a probe."""
+        st = self.state[role]
+        st["since"] += 1
+        if st["pending"] is not None or (st["since"] - 1) % self.CHECK_EVERY:
+            return
+        if torch.cuda.is_current_stream_capturing():
+            return
+        miss = torch.empty((self.B, 2), dtype=torch.int32, device=self.device)
+        L.check(L.lib().mmpde_knn_table_misses(L.ptr(cells), self.B, L.ptr(miss), L.stream(self.device)),
+                "mmpde_knn_table_misses")
+        host = torch.empty((self.B,), dtype=torch.int32, pin_memory=True)
+        host.copy_(miss[:, column], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        st["pending"] = (ev, host)
+
+
 def _cand_scratch(scratch, batches, N, device):
     need = L.lib().mmpde_knn_graph_cand_scratch_bytes(batches, N)
     if scratch is None or scratch.numel() * scratch.element_size() < need:
@@ -231,10 +292,19 @@ def nbr_table_from_edge_index(edge_index: torch.Tensor, n: int):
     return nbr, deg.to(torch.int32)
 
 
-def knn_query(src: torch.Tensor, qry: torch.Tensor, batches: int, k: int) -> torch.Tensor:
+def _ties(ties):
+    if ties is not None and (ties.dtype != torch.int32 or ties.numel() < 1 or not ties.is_cuda):
+        raise ValueError("ties must be an int32 device counter")
+    return ties
+
+
+def knn_query(src: torch.Tensor, qry: torch.Tensor, batches: int, k: int,
+              ties: torch.Tensor | None = None) -> torch.Tensor:
     """Per-trajectory sklearn NearestNeighbors(k).fit(src_b).kneighbors(qry_b):
     LOCAL indices int32 [batches * n_qry, k], fp64-distance order
-    (reference data_creator_2d.py:66-78)."""
+    (reference data_creator_2d.py:66-78).  ties: optional int32 [1] device
+    counter, += the queries with an exact fp64 distance tie among their first
+    k (or at rank k): where sklearn's order is its KD-tree's, parity unpinned."""
     L.require_device(src, qry)
     src = L.f32c(src).reshape(-1, 2)
     qry = L.f32c(qry).reshape(-1, 2)
@@ -242,22 +312,23 @@ def knn_query(src: torch.Tensor, qry: torch.Tensor, batches: int, k: int) -> tor
     _knn_points_check(ns, k, "knn_query")
     idx = torch.empty((batches * nq, k), dtype=torch.int32, device=src.device)
     L.check(L.lib().mmpde_knn_query(L.ptr(src), L.ptr(qry), batches, ns, nq, k, L.ptr(idx),
-                                    L.stream(src.device)), "mmpde_knn_query")
+                                    L.ptr(_ties(ties)), L.stream(src.device)), "mmpde_knn_query")
     return idx
 
 
 def knn_query_moved(src: torch.Tensor, qry: torch.Tensor, xi: torch.Tensor, cand, batches: int,
                     k: int, scratch: torch.Tensor | None = None, ref: torch.Tensor | None = None,
-                    cells: torch.Tensor | None = None, skip_above: float = 0.0) -> torch.Tensor:
+                    cells: torch.Tensor | None = None, skip_above: float = 0.0,
+                    ties: torch.Tensor | None = None) -> torch.Tensor:
     """knn_query of qry onto moved points src (every trajectory's mesh moved
     from the same xi [N, 2]; n_src = n_qry = N), bit for bit, answered from the
     candidate table `cand` = knn_candidates(xi, ref) (ref: the fixed points the
     queries sit at or near, default xi) where a distance bound proves it
     complete and by the full search elsewhere (reference data_creator_2d.py:66-78
     onto the DMM's moved mesh).  cells: knn_moved_cells(src, xi, batches) if
-    already computed; skip_above as for knn_graph_moved."""
+    already computed; skip_above as for knn_graph_moved; ties as for knn_query."""
     if cand is None:
-        return knn_query(src, qry, batches, k)
+        return knn_query(src, qry, batches, k, ties)
     L.require_device(src, qry, ref)
     src = L.f32c(src).reshape(-1, 2)
     qry = L.f32c(qry).reshape(-1, 2)
@@ -277,7 +348,7 @@ def knn_query_moved(src: torch.Tensor, qry: torch.Tensor, xi: torch.Tensor, cand
     idx = torch.empty((batches * N, k), dtype=torch.int32, device=src.device)
     L.check(L.lib().mmpde_knn_query_cand(L.ptr(src), L.ptr(qry), L.ptr(xi), L.ptr(ref),
                                          L.ptr(cells), float(skip_above), batches, N, k,
-                                         L.ptr(cand), L.ptr(idx),
+                                         L.ptr(cand), L.ptr(idx), L.ptr(_ties(ties)),
                                          L.ptr(scratch), L.stream(src.device)),
             "mmpde_knn_query_cand")
     return idx

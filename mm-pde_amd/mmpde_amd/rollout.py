@@ -88,6 +88,10 @@ class MMPDERollout:
             self.knn_scratch = torch.empty((nb,), dtype=torch.uint8, device=self.device)
             # the kNN-30 query runs on side2 beside the graph: its own scratch
             self.knn_scratch_q = torch.empty((nb,), dtype=torch.uint8, device=self.device)
+            # queries of the kNN-30 searches whose sorted fp64 distances hold an
+            # exact tie (sklearn's order unpinned there): cumulative, read by
+            # knn_query_ties()
+            self.knn_ties = torch.zeros((1,), dtype=torch.int32, device=self.device)
             # per-step displacement record shared by both (ops.knn_moved_cells)
             self.knn_cells = torch.empty((L.lib().mmpde_knn_moved_cells_bytes(batches) // 4,),
                                          dtype=torch.float32, device=self.device)
@@ -101,6 +105,10 @@ class MMPDERollout:
                                                          moved_queries=True)
                 self.knn_cells_1 = torch.empty_like(self.knn_cells)
                 self.knn_scratch_1 = torch.empty((nb,), dtype=torch.uint8, device=self.device)
+            # table vs full search per role, from the share the table answered at
+            # an earlier step (ops.KnnTablePolicy: the cost model, no sync)
+            self.knn_policy = ops.KnnTablePolicy(
+                self.device, batches, N, ("graph", "query") + (("query1",) if kind == "burgers" else ()))
             # the fixed-grid model depends on u only: it runs on a side stream,
             # with its own workspace, beside the moving-mesh chain
             self.side = torch.cuda.Stream(self.device)
@@ -174,29 +182,48 @@ class MMPDERollout:
             out_u = self.model(nodes_u, out=self.out_u, workspace=self.ws_gnn_u, trace=self._trace())
         mesh = self.dmm.mesh(u, self.xi, out=self.mesh, workspace=self.ws_dmm,
                              head_cache=self.dmm_cache)
+        pol = self.knn_policy
+        use_g, use_q = pol.use_table("graph"), pol.use_table("query")
         cells = ops.knn_moved_cells(mesh, self.xi, B, out=self.knn_cells) \
-            if self.knn_cand is not None else None
+            if self.knn_cand is not None and (use_g or use_q) else None
         side2 = self.side2 if self.overlap else cur
         side2.wait_stream(cur)
         with torch.cuda.stream(side2):
             u.record_stream(side2)
-            self.idx2 = idx2 = ops.knn_query_moved(mesh, self.grid_rep, self.xi, self.knn_cand_q, B,
-                                                   30, self.knn_scratch_q, ref=self.grid,
-                                                   cells=cells, skip_above=self.knn_skip_q)
+            if use_q:
+                idx2 = ops.knn_query_moved(mesh, self.grid_rep, self.xi, self.knn_cand_q, B, 30,
+                                           self.knn_scratch_q, ref=self.grid, cells=cells,
+                                           skip_above=self.knn_skip_q, ties=self.knn_ties)
+                if cells is not None:
+                    pol.after_table("query", cells, 1)
+            else:
+                idx2 = ops.knn_query(mesh, self.grid_rep, B, 30, ties=self.knn_ties)
+            self.idx2 = idx2
             if self.kind == "burgers":
                 res = self.itp.res_cut(u.reshape(B, 1, self.s, self.s)).reshape(-1)
             else:
                 res = self.itp.res_cut(u.reshape(B, N)).reshape(-1)
             idx2.record_stream(cur)
             res.record_stream(cur)
-        self.nbr_m = nbr_m = ops.knn_graph_moved(mesh, self.xi, self.knn_cand, B, self.gc.n,
-                                                 self.knn_scratch, cells=cells,
-                                                 skip_above=self.knn_skip)
+        if use_g:
+            nbr_m = ops.knn_graph_moved(mesh, self.xi, self.knn_cand, B, self.gc.n, self.knn_scratch,
+                                        cells=cells, skip_above=self.knn_skip)
+            if cells is not None:
+                pol.after_table("graph", cells, 0)
+        else:
+            nbr_m = ops.knn_graph_nbr(mesh, B, self.gc.n)
+        self.nbr_m = nbr_m
         if self.kind == "burgers":
-            cells1 = ops.knn_moved_cells(self.grid_rep, self.grid, B, out=self.knn_cells_1)
-            self.idx1 = idx1 = ops.knn_query_moved(self.grid_rep, mesh, self.grid, self.knn_cand_1, B,
-                                                   30, self.knn_scratch_1, ref=self.xi, cells=cells1,
-                                                   skip_above=self.knn_skip_1)
+            if pol.use_table("query1"):
+                cells1 = ops.knn_moved_cells(self.grid_rep, self.grid, B, out=self.knn_cells_1)
+                idx1 = ops.knn_query_moved(self.grid_rep, mesh, self.grid, self.knn_cand_1, B, 30,
+                                           self.knn_scratch_1, ref=self.xi, cells=cells1,
+                                           skip_above=self.knn_skip_1, ties=self.knn_ties)
+                if self.knn_cand_1 is not None:
+                    pol.after_table("query1", cells1, 1)
+            else:
+                idx1 = ops.knn_query(self.grid_rep, mesh, B, 30, ties=self.knn_ties)
+            self.idx1 = idx1
             u_m = ops.itp_interp(self.grid_rep, u_flat, mesh, idx1, B, self.itp.packed("1"))
         else:
             u_m = u_flat
@@ -221,6 +248,17 @@ class MMPDERollout:
         if self.kind == "burgers":
             s.append(ops.knn_table_share(self.knn_cells_1, self.B, self.N)[:, 1].mean().item())
         return tuple(s)
+
+    def knn_query_ties(self) -> int:
+        """Queries of the kNN-30 searches (reference data_creator_2d.py:75-76)
+        since construction whose sorted fp64 distances held an exact tie inside
+        the first 30 or at rank 30: the only inputs on which sklearn's order (its
+        KD-tree traversal) may differ from the engine's (distance, index) order,
+        i.e. where parity with the reference is unpinned.  Synchronises."""
+        if not self.moving_mesh:
+            return 0
+        torch.cuda.synchronize(self.device)
+        return int(self.knn_ties.item())
 
     def rollout(self, u0: torch.Tensor, start_step: int, n_steps: int):
         """Feed each prediction back as the next input; returns the final state."""

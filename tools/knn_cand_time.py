@@ -74,6 +74,27 @@ for disp in disps:
                                                     skip_above=thr_q))
         print(f"  query k=30: full {t_fq:.1f} us, candidates {t_cq:.1f} us, answered by table "
               f"{100 * done:.1f}%, equal {same}; with the skip threshold {t_qskip:.1f} us")
+        # the rollout's policy (ops.KnnTablePolicy): per role, table or full
+        # search from the share read back at an earlier call, probes included
+        pol = ops.KnnTablePolicy(dev, B, N, ("graph", "query"))
+
+        def policy_step():
+            ug, uq = pol.use_table("graph"), pol.use_table("query")
+            c = ops.knn_moved_cells(pos, xi, B, out=cells) if (ug or uq) else None
+            if ug:
+                ops.knn_graph_moved(pos, xi, cand, B, 35, scr, cells=c, skip_above=thr_g)
+                pol.after_table("graph", c, 0)
+            else:
+                ops.knn_graph_nbr(pos, B, 35)
+            if uq:
+                ops.knn_query_moved(pos, qry, xi, cand, B, 30, scr, cells=c, skip_above=thr_q)
+                pol.after_table("query", c, 1)
+            else:
+                ops.knn_query(pos, qry, B, 30)
+        t_pol = timed(policy_step, reps=96)
+        modes = {r: ("table" if st["table"] else "full") for r, st in pol.state.items()}
+        print(f"  policy (graph + query + cells, probes every {pol.PROBE_EVERY}): {t_pol:.1f} us per call "
+              f"against full {t_full + t_fq:.1f} / table {t_cand + t_cq + t_cells:.1f}; modes {modes}")
 
 # the bench's own moved meshes: share of queries the tables answer over a rollout
 from mmpde_amd.rollout import MMPDERollout  # noqa: E402
@@ -93,7 +114,8 @@ for kind, bk in (("cy", B), ("burgers", 2 * B)):
         for i in range(10):
             u = eng.step(u, 1 + i)
             shares.append(eng.knn_table_share())
+        modes = {r: ("table" if st["table"] else "full") for r, st in eng.knn_policy.state.items()}
             dmax.append((eng.mesh.reshape(bk, -1, 2) - eng.xi).norm(dim=-1).max().item())
     print(f"{kind} bench rollout (B={bk}): table share (graph, query[, mode-1 query]) per step",
           [tuple(round(a, 4) for a in sh) for sh in shares],
-          "max displacement", [round(x, 4) for x in dmax])
+          "max displacement", [round(x, 4) for x in dmax], "policy after 10 steps", modes)
