@@ -299,6 +299,18 @@ int mmpde_gnn_edge_mean_deg(const float *a, const float *b, const int32_t *nbr, 
                             int64_t n, int k, const float *msg2_w, const float *msg2_b,
                             float *mean_out, mmpde_stream_t stream);
 
+/* mmpde_gnn_edge_mean_deg in a chosen arithmetic: edge_gemm
+ * MMPDE_EDGE_GEMM_F32 is mmpde_gnn_edge_mean_deg; MMPDE_EDGE_GEMM_F16X3 runs
+ * message_net_2 in the fp16x3 split (the eval path's arithmetic), packing
+ * W2 and the split scale (max|a| + max|b| over all n rows) into workspace
+ * (>= mmpde_gnn_edge_mean_workspace_bytes(n, edge_gemm) bytes, 16-B aligned)
+ * on every call: the forward of the f16x3 training path, whose weights
+ * change every iteration. */
+int64_t mmpde_gnn_edge_mean_workspace_bytes(int64_t n, int edge_gemm);
+int mmpde_gnn_edge_mean_ex(const float *a, const float *b, const int32_t *nbr, const int32_t *deg,
+                           int64_t n, int k, const float *msg2_w, const float *msg2_b, float *mean_out,
+                           int edge_gemm, void *workspace, int64_t workspace_bytes, mmpde_stream_t stream);
+
 /* ---------------------------------------------------------------- training
  * Backward of the edge stage (reference: loss.backward() at
  * train_helper_2d.py:126 through GNN_Layer_FS_2D.message / aggr='mean',

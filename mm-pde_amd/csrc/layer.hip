@@ -516,6 +516,7 @@ struct NodeArgs {
     const int32_t *div_deg = nullptr;
     int div_k = 0;
     EdgeSplit split;       // units > 0: add the wave kernel's side blocks first
+    int side32 = 0;        // the side-block index arithmetic fits 32 bits (side_fetch)
 };
 
 constexpr int NLD = 132;  // fp32 staging row stride (floats)
@@ -554,6 +555,36 @@ constexpr bool NODE_EARLY_B = MMPDE_NODE_EARLY_B != 0;
 // buffer order (the edge stage's per-part sums); div_k > 0: the total is then
 // divided by the row's degree max(div_deg[row], 1), or by div_k (IEEE division:
 // torch_scatter's mean = sum / count).
+// Node / embed kernel variants (tools/ubench/node_phases A/B builds):
+// LDSBAR: LDS hand-offs wait for the wave's own LDS operations only (a
+// __syncthreads also drains its outstanding global stores); EARLY_ROWS: the
+// [h | mean] rows issued first, every use of a constant deferred to after the
+// rows' arrival (loads complete in issue order); PROJ2: the b' operands issued
+// after a's GEMM, in flight over a's epilogue.  Measured (r04, node_phases):
+// EARLY_ROWS with the constants' arithmetic before the rows' use and PROJ2
+// together 60-61 us against 53-54 (legacy), so all default off.
+#ifndef MMPDE_NODE_LDSBAR
+#define MMPDE_NODE_LDSBAR 0
+#endif
+#ifndef MMPDE_NODE_EARLY_ROWS
+#define MMPDE_NODE_EARLY_ROWS 0
+#endif
+#ifndef MMPDE_NODE_PROJ2
+#define MMPDE_NODE_PROJ2 0
+#endif
+
+// Hand-off of LDS data between the waves of a workgroup: wait for this wave's
+// own LDS operations, then the barrier.  A __syncthreads would also drain the
+// wave's outstanding GLOBAL stores (its release fence waits vmcnt(0)), which
+// nothing here needs: no wave reads another's global stores in these kernels.
+__device__ __forceinline__ void lds_barrier() {
+    if (!MMPDE_NODE_LDSBAR) {
+        __syncthreads();
+    } else {
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+}
+
 // The (row, part) item of prep's work index idx: a wave takes 8 rows x 8 parts,
 // lane = 8 part + row: the 8 lanes of one ds_write_b128 group write 8
 // consecutive image rows (conflict-free).
@@ -572,10 +603,29 @@ __device__ __forceinline__ void prep_fetch(const float *src, int64_t lds, int64_
     for (int q = 0; q < 4; ++q) x[q] = *(const float4 *)(sp + 4 * q);
 }
 
+// The first side block of item (row, part) of global row srow (see
+// prep_finish), loaded ahead with the row itself (unconditionally: the
+// address is clamped to a valid block); returns whether the row's tile has
+// one.
+__device__ __forceinline__ bool side_fetch(EdgeSplit split, int64_t srow, int part, float4 (&y)[4]) {
+    // 32-bit index arithmetic (node_args sets side32 when (S + k) U + S and the
+    // row count fit; 64-bit divisions here also tripped a gfx950 code-generation
+    // error, "Operand has incorrect register class")
+    const uint32_t seg_n = (uint32_t)split.seg_n, r = (uint32_t)srow;
+    const uint32_t sg = r / seg_n, q = r - sg * seg_n, t = q / 16;
+    const uint32_t S = (uint32_t)split.S, G = (uint32_t)split.units, kk = (uint32_t)split.k;
+    const uint32_t lo = max((((t * kk + 1) * G) + S - 1) / S, 1u);
+    const uint32_t hi = min(((t + 1) * kk * G + S - 1) / S - 1, G - 1);
+    const float *q4 = split.side + ((int64_t)(sg * G + min(lo, G - 1)) * 16 + (q & 15)) * 128 + 16 * part;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) y[i] = *(const float4 *)(q4 + 4 * i);
+    return lo <= hi;
+}
+
 // prep, second half: the fetched values x of item (row, part) (global row srow
 // when global) -> the image (and copy, rs), after the optional side-block sums
 // and degree division (see prep).
-template <bool F16X3>
+template <bool F16X3, bool PRE = false>
 __device__ __forceinline__ void prep_finish(float4 (&x)[4], const float *src, int64_t srow, int row, int part,
                                             float4 *img, int KT, int kofs, float *rs, float *copy, int nsum,
                                             int64_t sum_stride, const int32_t *div_deg, int div_k,
@@ -591,12 +641,13 @@ __device__ __forceinline__ void prep_finish(float4 (&x)[4], const float *src, in
     if (split && split->units > 0) {
         // side blocks of the units u of this row's segment whose first slot
         // s0(u) = floor(u S / U) lies strictly inside the row's 16-row tile
-        // t (local): t k < s0(u) < (t + 1) k
+        // t (local): t k < s0(u) < (t + 1) k; PRE: the caller has added the
+        // first of them already (side_fetch, fetched with the row)
         const int64_t sg = srow / split->seg_n, q = srow - sg * split->seg_n, t = q / 16;
         const int64_t S = split->S, G = split->units, kk = split->k;
         const int64_t lo = max(((t * kk + 1) * G + S - 1) / S, (int64_t)1);
         const int64_t hi = min(((t + 1) * kk * G + S - 1) / S - 1, G - 1);
-        for (int64_t w = lo; w <= hi; ++w) {
+        for (int64_t w = PRE ? lo + 1 : lo; w <= hi; ++w) {
             const float *q4 = split->side + ((sg * G + w) * 16 + (q & 15)) * 128 + 16 * part;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -751,14 +802,6 @@ __device__ __forceinline__ void proj_phase(const BOps<F16X3, F16X3 ? 4 : 8> &bA,
     f32x4 aA[RB], aB[RB];
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) aA[rb] = aB[rb] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
-    gemm_tile<F16X3, RB, S1>(aA, img, 128, 0, bA, lane);
-    if (bBpre) {  // operands of b preloaded (the weight-stationary node kernel)
-        gemm_tile<F16X3, RB, S1>(aB, img, 128, 0, *bBpre, lane);
-    } else {
-        BOps<F16X3, S1> bB;
-        bB.load(pk + kPkW1, 4, 8 + wave, 0, w1r, 128, lane);
-        gemm_tile<F16X3, RB, S1>(aB, img, 128, 0, bB, lane);
-    }
     // |a|, |b| maxima of each 16-row block's rows in the block's first segment
     // (0) and in the next one (1), for the block's range record (layer.hpp:
     // kRangeRows = 16; seg_n >= 16: a block touches at most two segments)
@@ -769,30 +812,81 @@ __device__ __forceinline__ void proj_phase(const BOps<F16X3, F16X3 ? 4 : 8> &bA,
     // for a tile that runs past n (wave-uniform)
     const bool full = row0 + ROWS <= n;
     float *ap = a_out + (row0 + 4 * g) * LH + col, *bp = b_out + (row0 + 4 * g) * LH + col;
+    // the node term w.(u, x, y) of row lr (shared by a and b)
+    auto node_term = [&](int lr) {
+        float node = w.du * rowv[3 * ROWS + lr];
+        for (int c = 1; c < tw; ++c) node += w1r[256 + c] * rowv[(3 + c) * ROWS + lr];
+        return node + w.dx * rowv[ROWS + lr] + w.dy * rowv[2 * ROWS + lr];
+    };
+    auto seg_of = [&](int rb, int lr) { return (int)(row0 + lr >= ((row0 + 16 * rb) / seg_n + 1) * seg_n); };
+    gemm_tile<F16X3, RB, S1>(aA, img, 128, 0, bA, lane);
+    if (MMPDE_NODE_PROJ2 && !bBpre) {
+        // b's operands issued after a's GEMM, in flight over a's epilogue
+        BOps<F16X3, S1> bB;
+        bB.load(pk + kPkW1, 4, 8 + wave, 0, w1r, 128, lane);
 #pragma unroll
-    for (int rb = 0; rb < RB; ++rb) {
-        const int64_t rb0 = row0 + 16 * rb;
-        const int64_t seg1 = (rb0 / seg_n + 1) * seg_n;  // first row of the next segment
+        for (int rb = 0; rb < RB; ++rb) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int lr = 16 * rb + 4 * g + q;
-            if (full || row0 + lr < n) {
-                float za = aA[rb][q], zb = aB[rb][q];
-                if (F16X3) {
-                    const float ir = pow2_inv(rs[lr]);
-                    za = za * ir * w.isa;
-                    zb = zb * ir * w.isb;
+            for (int q = 0; q < 4; ++q) {
+                const int lr = 16 * rb + 4 * g + q;
+                if (full || row0 + lr < n) {
+                    float za = aA[rb][q];
+                    if (F16X3) za = za * pow2_inv(rs[lr]) * w.isa;
+                    const float va = za + node_term(lr) + w.t * rowv[lr] + w.b;
+                    ap[(16 * rb + q) * LH] = va;
+                    const int sx = seg_of(rb, lr);
+                    amx[rb][sx] = fmaxf(amx[rb][sx], fabsf(va));
                 }
-                float node = w.du * rowv[3 * ROWS + lr];
-                for (int c = 1; c < tw; ++c) node += w1r[256 + c] * rowv[(3 + c) * ROWS + lr];
-                node = node + w.dx * rowv[ROWS + lr] + w.dy * rowv[2 * ROWS + lr];
-                const float va = za + node + w.t * rowv[lr] + w.b;
-                const float vb = zb - node;
-                ap[(16 * rb + q) * LH] = va;
-                bp[(16 * rb + q) * LH] = vb;
-                const int sx = row0 + lr >= seg1;
-                amx[rb][sx] = fmaxf(amx[rb][sx], fabsf(va));
-                bmx[rb][sx] = fmaxf(bmx[rb][sx], fabsf(vb));
+            }
+        }
+        // b's GEMM re-reads its A operands from LDS: a's operands kept in
+        // registers across a's epilogue (what the compiler would do) spill
+        asm volatile("" ::: "memory");
+        gemm_tile<F16X3, RB, S1>(aB, img, 128, 0, bB, lane);
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int lr = 16 * rb + 4 * g + q;
+                if (full || row0 + lr < n) {
+                    float zb = aB[rb][q];
+                    if (F16X3) zb = zb * pow2_inv(rs[lr]) * w.isb;
+                    const float vb = zb - node_term(lr);
+                    bp[(16 * rb + q) * LH] = vb;
+                    const int sx = seg_of(rb, lr);
+                    bmx[rb][sx] = fmaxf(bmx[rb][sx], fabsf(vb));
+                }
+            }
+        }
+    } else {
+        if (bBpre) {  // operands of b preloaded (the weight-stationary node kernel)
+            gemm_tile<F16X3, RB, S1>(aB, img, 128, 0, *bBpre, lane);
+        } else {
+            BOps<F16X3, S1> bB;
+            bB.load(pk + kPkW1, 4, 8 + wave, 0, w1r, 128, lane);
+            gemm_tile<F16X3, RB, S1>(aB, img, 128, 0, bB, lane);
+        }
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int lr = 16 * rb + 4 * g + q;
+                if (full || row0 + lr < n) {
+                    float za = aA[rb][q], zb = aB[rb][q];
+                    if (F16X3) {
+                        const float ir = pow2_inv(rs[lr]);
+                        za = za * ir * w.isa;
+                        zb = zb * ir * w.isb;
+                    }
+                    const float node = node_term(lr);
+                    const float va = za + node + w.t * rowv[lr] + w.b;
+                    const float vb = zb - node;
+                    ap[(16 * rb + q) * LH] = va;
+                    bp[(16 * rb + q) * LH] = vb;
+                    const int sx = seg_of(rb, lr);
+                    amx[rb][sx] = fmaxf(amx[rb][sx], fabsf(va));
+                    bmx[rb][sx] = fmaxf(bmx[rb][sx], fabsf(vb));
+                }
             }
         }
     }
@@ -811,7 +905,7 @@ __device__ __forceinline__ void proj_phase(const BOps<F16X3, F16X3 ? 4 : 8> &bA,
                 red[wave][rb][3] = m3;
             }
         }
-        __syncthreads();
+        lds_barrier();
         if (wave == 0 && lane < 4 * RB) {
             const int rb = lane >> 2, e = lane & 3;
             float m = red[0][rb][e];
@@ -822,21 +916,15 @@ __device__ __forceinline__ void proj_phase(const BOps<F16X3, F16X3 ? 4 : 8> &bA,
     }
 }
 
-// One or two problems per launch (launch_node_stages): workgroups below
-// tiles0 take problem 0's row tiles, the rest problem 1's.
-struct NodeArgs2 {
-    NodeArgs a[2];
-    int64_t tiles0;
-};
-
 // Profiling builds only (tools/ubench/node_ubench with -DMMPDE_NODE_STAMPS):
-// wave 0 of every workgroup records the shader clock at the phase boundaries
-// into g_node_stamps[block][8] (vector stores).
+// thread 0 of every workgroup records the 100 MHz real-time clock (one clock
+// for the whole chip) at the phase boundaries into g_node_stamps[block][8]
+// (vector stores).
 #ifdef MMPDE_NODE_STAMPS
 __device__ uint64_t *g_node_stamps;
 #define NODE_STAMP(i)                                                                       \
     do {                                                                                   \
-        if (threadIdx.x == 0) g_node_stamps[(int64_t)blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
+        if (threadIdx.x == 0) g_node_stamps[(int64_t)blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 #else
 #define NODE_STAMP(i) \
@@ -845,11 +933,9 @@ __device__ uint64_t *g_node_stamps;
 #endif
 
 template <bool NEXT, bool F16X3, int RB>
-__global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs2 pp) {
+__global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs p) {
     NODE_STAMP(0);
     constexpr int ROWS = 16 * RB;
-    const bool second = (int64_t)blockIdx.x >= pp.tiles0;  // workgroup-uniform
-    const NodeArgs &p = pp.a[second ? 1 : 0];
     __shared__ float4 img[RB * 16 * 64];        // operand image, K = 256 (h | mean), then 128
     __shared__ float stage[ROWS * NLD];         // fp32 v, then h'
     __shared__ float hres[ROWS * NLD];          // fp32 h (residual)
@@ -857,27 +943,46 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs2 pp) {
     __shared__ float rowv[3 + MAX_TW][ROWS];    // per row: t / tmax, x / Lx, y / Ly, u_0 .. u_{tw-1}
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int r = lane & 15, g = lane >> 4;
-    const int64_t row0 = ((int64_t)blockIdx.x - (second ? pp.tiles0 : 0)) * ROWS;
+    const int64_t row0 = (int64_t)blockIdx.x * ROWS;
     const int col = 16 * wave + r;  // this lane's output column (tile = wave)
     const int tw = p.sc.tw > 1 ? p.sc.tw : 1;
     constexpr int S1 = F16X3 ? 4 : 8;    // K steps per 128 columns of K
     const float *wu1 = p.u1 + (int64_t)col * p.ld_u1, *wu2 = p.u2 + (int64_t)col * LH;
+    // The loads issue in the order their data is needed last: the [h | mean]
+    // rows first (HBM; one item of 16 values per thread when the tile has 256
+    // items per half, with the row's first side block), then the per-row
+    // node values, the per-column constants and update_net_1's operands.  A
+    // wave issues in order and stalls at its first use of a load, so any
+    // arithmetic on a constant placed before a load would hold that load back.
+    constexpr bool EARLY_ROWS = ROWS * 8 == 256 && MMPDE_NODE_EARLY_ROWS;
+    const bool hhalf = tid < 256;   // wave-uniform: waves 0-3 the h rows, 4-7 the mean rows
+    int irow = 0, ipart = 0;
+    float4 xr[4], ys[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) xr[q] = ys[q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    const bool side = !hhalf && p.split.units > 0 && p.side32;  // wave-uniform
+    bool has_side = false;
+    if constexpr (EARLY_ROWS) {
+        prep_item(tid & 255, irow, ipart);
+        prep_fetch(hhalf ? p.h : p.mean, LH, row0, p.n, true, irow, ipart, xr);
+        if (side) has_side = side_fetch(p.split, min(row0 + irow, p.n - 1), ipart, ys);
+    }
     // everything the epilogues read from global memory is fetched up front
     // (per-row node values to LDS, per-column constants to registers), so no
     // epilogue waits on a memory round trip
+    float rv[3] = {0.0f, 0.0f, 0.0f}, ru0 = 0.0f;
     if (tid < ROWS) {
         const int64_t row = min(row0 + tid, p.n - 1);
-        rowv[0][tid] = node_t(p.sc, p.pos, row) * p.sc.inv_tmax;
-        rowv[1][tid] = node_x(p.sc, p.pos, row) * p.sc.inv_lx;
-        rowv[2][tid] = node_y(p.sc, p.pos, row) * p.sc.inv_ly;
-        for (int c = 0; c < tw; ++c) rowv[3 + c][tid] = p.u[row * tw + c];
+        rv[0] = node_t(p.sc, p.pos, row);
+        rv[1] = node_x(p.sc, p.pos, row);
+        rv[2] = node_y(p.sc, p.pos, row);
+        ru0 = p.u[row * tw];
     }
     const float u1_wt = wu1[256], u1_b = p.c1[col];
-    const float u1_is = F16X3 ? pow2_inv(((const float *)(p.pk + kPkU1 + 131072))[col]) : 1.0f;
+    const float u1_sw = F16X3 ? ((const float *)(p.pk + kPkU1 + 131072))[col] : 1.0f;
     const float u2_b = p.c2[col];
-    BnAffine bn;
-    bn.set(p.bn_rm[col], p.bn_rv[col], p.bn_w[col], p.bn_b[col], p.eps);
-    const float u2_is = F16X3 ? pow2_inv(((const float *)(p.pk + kPkU2 + 65536))[col]) : 1.0f;
+    const float bn_rm = p.bn_rm[col], bn_rv = p.bn_rv[col], bn_w = p.bn_w[col], bn_bb = p.bn_b[col];
+    const float u2_sw = F16X3 ? ((const float *)(p.pk + kPkU2 + 65536))[col] : 1.0f;
     const float *w1r = NEXT ? p.w1n + (int64_t)col * p.ld_w1n : nullptr;
     W1C w1c;
     if (NEXT) w1c.load<F16X3>(w1r, p.b1n, p.pkn, col, tw);
@@ -892,10 +997,47 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs2 pp) {
     if (PRE) {
         bU2.load(p.pk + kPkU2, 4, wave, 0, wu2, 0, lane);
     }
+    // the arithmetic on what was loaded (EARLY_ROWS: after the rows' use, as
+    // a load completes only after every load issued before it)
+    float u1_is = 1.0f, u2_is = 1.0f;
+    BnAffine bn;
+    auto consume = [&]() {
+        if (tid < ROWS) {
+            const int64_t row = min(row0 + tid, p.n - 1);
+            rowv[0][tid] = rv[0] * p.sc.inv_tmax;
+            rowv[1][tid] = rv[1] * p.sc.inv_lx;
+            rowv[2][tid] = rv[2] * p.sc.inv_ly;
+            rowv[3][tid] = ru0;
+            for (int c = 1; c < tw; ++c) rowv[3 + c][tid] = p.u[row * tw + c];
+        }
+        u1_is = F16X3 ? pow2_inv(u1_sw) : 1.0f;
+        u2_is = F16X3 ? pow2_inv(u2_sw) : 1.0f;
+        bn.set(bn_rm, bn_rv, bn_w, bn_bb, p.eps);
+    };
+    if constexpr (!EARLY_ROWS) consume();
 
     NODE_STAMP(1);
     // ---- [h | mean] -> image (K = 256)
-    if constexpr (ROWS * 8 <= 256) {  // h on waves 0-3, mean on waves 4-7 at once
+    if constexpr (EARLY_ROWS) {
+        const int64_t srow = min(row0 + irow, p.n - 1);
+        if (hhalf)
+            prep_finish<F16X3>(xr, p.h, srow, irow, ipart, img, 256, 0, rs[0], hres, 1, 0, nullptr, 0, nullptr);
+        else if (side) {
+            // the row's first side block, the rest in prep_finish: the same
+            // order of additions as prep's
+            if (has_side) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    xr[q] = make_float4(xr[q].x + ys[q].x, xr[q].y + ys[q].y, xr[q].z + ys[q].z,
+                                        xr[q].w + ys[q].w);
+            }
+            prep_finish<F16X3, true>(xr, p.mean, srow, irow, ipart, img, 256, 128, rs[1], nullptr, p.parts,
+                                     p.part_stride, p.div_deg, p.div_k, &p.split);
+        }
+        else
+            prep_finish<F16X3>(xr, p.mean, srow, irow, ipart, img, 256, 128, rs[1], nullptr, p.parts,
+                               p.part_stride, p.div_deg, p.div_k, &p.split);
+    } else if constexpr (ROWS * 8 <= 256) {  // h on waves 0-3, mean on waves 4-7 at once
         if (tid < 256) prep<F16X3, ROWS>(p.h, LH, row0, p.n, true, img, 256, 0, rs[0], hres, 0, 256);
         else prep<F16X3, ROWS>(p.mean, LH, row0, p.n, true, img, 256, 128, rs[1], nullptr, 256, 256, p.parts,
                                p.part_stride, p.div_deg, p.div_k, &p.split);
@@ -904,7 +1046,9 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs2 pp) {
         prep<F16X3, ROWS>(p.mean, LH, row0, p.n, true, img, 256, 128, rs[1], nullptr, -1, 512, p.parts,
                           p.part_stride, p.div_deg, p.div_k, &p.split);
     }
-    __syncthreads();
+    if constexpr (EARLY_ROWS) consume();
+    lds_barrier();
+    NODE_STAMP(2);
 
     // ---- update_net_1: v = relu(U1 [h | mean | t] + c1)
     {
@@ -929,9 +1073,9 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs2 pp) {
         }
     }
     NODE_STAMP(3);
-    __syncthreads();
+    lds_barrier();
     prep<F16X3, ROWS>(stage, NLD, 0, ROWS, false, img, 128, 0, rs[2]);
-    __syncthreads();
+    lds_barrier();
     NODE_STAMP(4);
 
     // ---- update_net_2 + residual + BatchNorm(eval)
@@ -964,9 +1108,9 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs2 pp) {
     }
     NODE_STAMP(5);
     if constexpr (NEXT) {
-        __syncthreads();
+        lds_barrier();
         prep<F16X3, ROWS>(stage, NLD, 0, ROWS, false, img, 128, 0, rs[3]);
-        __syncthreads();
+        lds_barrier();
         NODE_STAMP(6);
         // ---- next layer's message_net_1 node halves
         proj_phase<F16X3, RB>(bA, img, rs[3], &rowv[0][0], w1c, p.pkn, w1r, tw, row0, p.n, p.seg_n,
@@ -996,16 +1140,9 @@ struct EmbedArgs {
     int64_t seg_n;         // rows per trajectory segment (range records)
 };
 
-struct EmbedArgs2 {
-    EmbedArgs a[2];
-    int64_t tiles0;
-};
-
 template <bool F16X3, int RB>
-__global__ __launch_bounds__(512, NODE_WPE) void gnn_embed_kernel(EmbedArgs2 pp) {
+__global__ __launch_bounds__(512, NODE_WPE) void gnn_embed_kernel(EmbedArgs p) {
     constexpr int ROWS = 16 * RB;
-    const bool second = (int64_t)blockIdx.x >= pp.tiles0;  // workgroup-uniform
-    const EmbedArgs &p = pp.a[second ? 1 : 0];
     constexpr int S1 = F16X3 ? 4 : 8;
     __shared__ float4 img[RB * 8 * 64];   // K = 128 operand image
     __shared__ float stage[ROWS * NLD];   // fp32 z, then h0
@@ -1014,7 +1151,7 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_embed_kernel(EmbedArgs2 pp)
     __shared__ float rowv[3 + MAX_TW][ROWS];  // per row: t / tmax, x / Lx, y / Ly, u_0 .. u_{tw-1}
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int g = lane >> 4;
-    const int64_t row0 = ((int64_t)blockIdx.x - (second ? pp.tiles0 : 0)) * ROWS;
+    const int64_t row0 = (int64_t)blockIdx.x * ROWS;
     const int col = 16 * wave + (lane & 15);
     const int tw = p.sc.tw > 1 ? p.sc.tw : 1;
     if (tid < ROWS) {
@@ -1067,16 +1204,16 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_embed_kernel(EmbedArgs2 pp)
     const float zb = e.b0[c];
     BnAffine bn1;
     bn1.set(e.bn1_rm[c], e.bn1_rv[c], e.bn1_w[c], e.bn1_b[c], e.eps);
-    __syncthreads();
+    lds_barrier();
     for (int row = tid >> 7; row < ROWS; row += 4) {
         float v = zb + zw0 * rowv[3][row];
         for (int ch = 1; ch < tw; ++ch) v += zwr[ch] * rowv[3 + ch][row];
         v = v + zw1 * rowv[1][row] + zw2 * rowv[2][row] + zw3 * rowv[0][row];
         stage[row * NLD + c] = fmaxf(bn1(v), 0.0f);
     }
-    __syncthreads();
+    lds_barrier();
     prep<F16X3, ROWS>(stage, NLD, 0, ROWS, false, img, 128, 0, rsz);
-    __syncthreads();
+    lds_barrier();
     BOps<F16X3, S1> bA, bB;
     {
         f32x4 acc[RB];
@@ -1106,9 +1243,9 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_embed_kernel(EmbedArgs2 pp)
             }
         }
     }
-    __syncthreads();
+    lds_barrier();
     prep<F16X3, ROWS>(stage, NLD, 0, ROWS, false, img, 128, 0, rs);
-    __syncthreads();
+    lds_barrier();
     proj_phase<F16X3, RB>(bA, img, rs, &rowv[0][0], w1c, p.pk, w1r, tw, row0, p.n, p.seg_n,
                           p.a_out, p.b_out, p.rng_out, wave, lane, NODE_EARLY_B ? &bB : nullptr);
 }
@@ -1165,8 +1302,59 @@ int launch_edge_stage(const float *a, const float *b, const int32_t *nbr, const 
     return MMPDE_OK;
 }
 
-// The kernel arguments of one node-stage call (validated); *next_out / *f16
-// select the kernel instance.
+// Range records (layer.hpp) of a, b over ONE segment of all n rows: per
+// 16-row block {max|a|, max|b|, 0, 0}.  One wave per block.
+__global__ __launch_bounds__(256) void range_records_kernel(const float *__restrict__ a, const float *__restrict__ b,
+                                                            int64_t n, float *__restrict__ rng) {
+    const int64_t blk = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (blk >= range_tiles(n)) return;  // wave-uniform
+    float ma = 0.0f, mb = 0.0f;
+    const int64_t r0 = blk * kRangeRows;
+    for (int i = lane; i < kRangeRows * (LH / 4); i += 64) {
+        const int64_t row = min(r0 + i / (LH / 4), n - 1);
+        const int c4 = i % (LH / 4);
+        ma = absmax4(ma, *(const float4 *)(a + row * LH + 4 * c4));
+        mb = absmax4(mb, *(const float4 *)(b + row * LH + 4 * c4));
+    }
+    ma = wave_max(ma);
+    mb = wave_max(mb);
+    if (lane == 0) *(float4 *)(rng + 4 * blk) = make_float4(ma, mb, 0.0f, 0.0f);
+}
+
+int64_t edge_mean_f16x3_ws_bytes(int64_t n) { return kLayerPack + range_tiles(n) * 16; }
+
+// The edge stage writing the mean itself (the persistent ring kernel), F16X3
+// with this call's own W2 image and range records (one segment of n rows):
+// the training forward (mmpde_gnn_edge_mean_ex), where the weights change every
+// iteration.
+int launch_edge_mean_f16x3(const float *a, const float *b, const int32_t *nbr, const int32_t *deg, int64_t n,
+                           int k, const float *w2, const float *b2, float *mean, void *ws, hipStream_t st) {
+    MMPDE_REQUIRE(a && b && nbr && w2 && b2 && mean && ws && n > 0 && k > 0 && n <= (int64_t)INT32_MAX);
+    MMPDE_REQUIRE(al16(a) && al16(b) && al16(w2) && al16(mean) && al16(ws));
+    const int64_t ntiles = (n + ET - 1) / ET;
+    MMPDE_REQUIRE(ntiles * ((k + ESL - 1) / ESL) < (int64_t)INT32_MAX);
+    char *pk = (char *)ws;
+    float *rng = (float *)(pk + kLayerPack);
+    PackSrc src{};
+    src.w[0] = w2;
+    src.ld[0] = LH;
+    hipLaunchKernelGGL(pack_f16x3_kernel<128>, dim3(128, 1), dim3(128), 0, st, src, 0, kPkW2, (int64_t)128, pk);
+    MMPDE_RET_LAUNCH();
+    hipLaunchKernelGGL(range_records_kernel, dim3((unsigned)ceil_div(range_tiles(n), 4)), dim3(256), 0, st, a, b, n,
+                       rng);
+    MMPDE_RET_LAUNCH();
+    EdgeArgs e{a, b, nbr, n, k, (int)ntiles, w2, b2, pk, rng, mean, nullptr, deg};
+    const int cus = device_cus();
+    const int grid = ntiles < cus ? (int)ntiles : cus;
+    const dim3 block(64 * (4 * EDGE_NC + 4 * EDGE_NP));
+    if (deg) hipLaunchKernelGGL((gnn_edge_kernel<true, EDGE_PH, EDGE_NC, EDGE_NP, true>), dim3(grid), block, 0, st, e);
+    else hipLaunchKernelGGL(gnn_edge_kernel<true>, dim3(grid), block, 0, st, e);
+    MMPDE_RET_LAUNCH();
+    return MMPDE_OK;
+}
+
+// The kernel arguments of one node-stage call (validated).
 static int node_args(const NodeStageCall &c, NodeArgs *out) {
     const bool sums = c.split && c.split->units > 0;
     MMPDE_REQUIRE(!sums || (c.split->side && c.split->S > 0 && c.split->k > 0 && c.split->seg_n > 0 &&
@@ -1181,7 +1369,11 @@ static int node_args(const NodeStageCall &c, NodeArgs *out) {
                p->bn_rm, p->bn_rv, p->eps, c.h_out, nullptr, nullptr, 0, c.a_out, c.b_out, c.u, c.pos, c.sc,
                c.pk, c.pkn, c.rng_out, effective_seg(c.n, c.seg_n), 1, 0, sums ? c.deg : nullptr,
                sums ? c.split->k : 0};
-    if (sums) a.split = *c.split;
+    if (sums) {
+        a.split = *c.split;
+        const int64_t S = c.split->S, U = c.split->units, k = c.split->k;
+        a.side32 = (S + k) * U + S < ((int64_t)1 << 32) && c.n < ((int64_t)1 << 31);
+    }
     if (c.next) {
         MMPDE_REQUIRE(c.a_out && c.b_out && c.next->msg1_ld >= 260 && (c.next->msg1_ld & 3) == 0 &&
                       al16(c.next->msg1_w));
@@ -1193,27 +1385,17 @@ static int node_args(const NodeStageCall &c, NodeArgs *out) {
     return MMPDE_OK;
 }
 
-int launch_node_stages(const NodeStageCall *calls, int count, hipStream_t st) {
-    MMPDE_REQUIRE(calls && (count == 1 || count == 2));
+static int launch_node_stage(const NodeStageCall &c, hipStream_t st) {
     constexpr int RB = MMPDE_NODE_RB;
-    NodeArgs2 pp;
-    int rc = node_args(calls[0], &pp.a[0]);
+    NodeArgs a;
+    int rc = node_args(c, &a);
     if (rc) return rc;
-    const bool next = calls[0].next != nullptr, f16 = calls[0].pk != nullptr;
-    pp.tiles0 = ceil_div(calls[0].n, 16 * RB);
-    int64_t tiles = pp.tiles0;
-    if (count == 2) {
-        MMPDE_REQUIRE((calls[1].next != nullptr) == next && (calls[1].pk != nullptr) == f16);
-        rc = node_args(calls[1], &pp.a[1]);
-        if (rc) return rc;
-        tiles += ceil_div(calls[1].n, 16 * RB);
-    } else {
-        pp.a[1] = pp.a[0];
-    }
+    const bool next = c.next != nullptr, f16 = c.pk != nullptr;
+    const int64_t tiles = ceil_div(c.n, 16 * RB);
     MMPDE_REQUIRE(tiles < (int64_t)INT32_MAX);
     const dim3 grid((unsigned)tiles);
 #define MMPDE_NODE(NX, SPLIT) \
-    hipLaunchKernelGGL((gnn_node_kernel<NX, SPLIT, RB>), grid, dim3(512), 0, st, pp)
+    hipLaunchKernelGGL((gnn_node_kernel<NX, SPLIT, RB>), grid, dim3(512), 0, st, a)
     if (next && f16) MMPDE_NODE(true, true);
     else if (next) MMPDE_NODE(true, false);
     else if (f16) MMPDE_NODE(false, true);
@@ -1230,7 +1412,7 @@ int launch_node_stage(const float *h, const float *mean, const EdgeSplit *split,
                       float *b_out, hipStream_t st) {
     const NodeStageCall c{h, mean, split, deg, u, pos, n, seg_n, sc, p, next, pk, pkn, rng_out, h_out, a_out,
                           b_out};
-    return launch_node_stages(&c, 1, st);
+    return launch_node_stage(c, st);
 }
 
 static int embed_args(const EmbedStageCall &c, EmbedArgs *out) {
@@ -1243,27 +1425,16 @@ static int embed_args(const EmbedStageCall &c, EmbedArgs *out) {
     return MMPDE_OK;
 }
 
-int launch_embed_stages(const EmbedStageCall *calls, int count, hipStream_t st) {
-    MMPDE_REQUIRE(calls && (count == 1 || count == 2));
+static int launch_embed_stage(const EmbedStageCall &c, hipStream_t st) {
     constexpr int RB = MMPDE_NODE_RB;
-    EmbedArgs2 pp;
-    int rc = embed_args(calls[0], &pp.a[0]);
+    EmbedArgs a;
+    int rc = embed_args(c, &a);
     if (rc) return rc;
-    const bool f16 = calls[0].pk0 != nullptr;
-    pp.tiles0 = ceil_div(calls[0].n, 16 * RB);
-    int64_t tiles = pp.tiles0;
-    if (count == 2) {
-        MMPDE_REQUIRE((calls[1].pk0 != nullptr) == f16);
-        rc = embed_args(calls[1], &pp.a[1]);
-        if (rc) return rc;
-        tiles += ceil_div(calls[1].n, 16 * RB);
-    } else {
-        pp.a[1] = pp.a[0];
-    }
+    const int64_t tiles = ceil_div(c.n, 16 * RB);
     MMPDE_REQUIRE(tiles < (int64_t)INT32_MAX);
     const dim3 grid((unsigned)tiles);
-    if (f16) hipLaunchKernelGGL((gnn_embed_kernel<true, RB>), grid, dim3(512), 0, st, pp);
-    else hipLaunchKernelGGL((gnn_embed_kernel<false, RB>), grid, dim3(512), 0, st, pp);
+    if (c.pk0) hipLaunchKernelGGL((gnn_embed_kernel<true, RB>), grid, dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((gnn_embed_kernel<false, RB>), grid, dim3(512), 0, st, a);
     MMPDE_RET_LAUNCH();
     return MMPDE_OK;
 }
@@ -1273,5 +1444,5 @@ int launch_embed_stage(const float *u, const float *pos, int64_t n, int64_t seg_
                        const char *pk0, float *rng_out, float *h_out, float *a_out,
                        float *b_out, hipStream_t st) {
     const EmbedStageCall c{u, pos, n, seg_n, sc, e, l0, pk0, rng_out, h_out, a_out, b_out};
-    return launch_embed_stages(&c, 1, st);
+    return launch_embed_stage(c, st);
 }

@@ -12,7 +12,7 @@
 // its own segment only, so a trajectory's f16x3 result does not depend on the
 // trajectories launched beside it.  Plain stores, no atomics, no zeroing.
 constexpr int kRangeRows = 16;
-inline int64_t range_tiles(int64_t n) { return (n + kRangeRows - 1) / kRangeRows; }
+__host__ __device__ inline int64_t range_tiles(int64_t n) { return (n + kRangeRows - 1) / kRangeRows; }
 
 // max |a| + max |b| over segment s from the range records of the node tiles
 // that hold its rows (layer.hpp kRangeRows): a block whose first row lies in s
@@ -60,6 +60,12 @@ int launch_edge_stage(const float *a, const float *b, const int32_t *nbr, const 
                       const float *rng, float *mean, float *side, int64_t side_cap,
                       EdgeSplit *split, hipStream_t st);
 
+// The training forward's F16X3 edge stage (writes the mean; packs W2 and
+// computes the range records of a, b itself in ws, edge_mean_f16x3_ws_bytes).
+int64_t edge_mean_f16x3_ws_bytes(int64_t n);
+int launch_edge_mean_f16x3(const float *a, const float *b, const int32_t *nbr, const int32_t *deg, int64_t n,
+                           int k, const float *w2, const float *b2, float *mean, void *ws, hipStream_t st);
+
 // Segment size the kernels use for a requested seg_n (n when seg_n is 0, does
 // not divide n or is below kRangeRows).
 inline int64_t effective_seg(int64_t n, int64_t seg_n) {
@@ -97,11 +103,7 @@ int launch_node_stage(const float *h, const float *mean, const EdgeSplit *split,
                       const char *pk, const char *pkn, float *rng_out, float *h_out, float *a_out,
                       float *b_out, hipStream_t st);
 
-// The arguments of one launch_node_stage call; launch_node_stages runs one or
-// two of them (two independent problems, e.g. the MM-PDE step's two GNNs) in
-// ONE launch: problem 0's row tiles, then problem 1's, each workgroup reading
-// its own problem's arguments.  Both must take the same kernel (next and pk
-// both set or both null).
+// The arguments of one launch_node_stage call.
 struct NodeStageCall {
     const float *h, *mean;
     const EdgeSplit *split;
@@ -113,7 +115,6 @@ struct NodeStageCall {
     const char *pk, *pkn;
     float *rng_out, *h_out, *a_out, *b_out;
 };
-int launch_node_stages(const NodeStageCall *calls, int count, hipStream_t st);
 
 // Embedding (gnn_2d.py:99-106) + layer 0's message_net_1 node halves in one
 // launch: h_out = embedding_mlp(cat(u, x/Lx, y/Ly, t/tmax)), a_out / b_out as
@@ -123,8 +124,7 @@ int launch_embed_stage(const float *u, const float *pos, int64_t n, int64_t seg_
                        const char *pk0, float *rng_out, float *h_out, float *a_out,
                        float *b_out, hipStream_t st);
 
-// launch_embed_stage's arguments; launch_embed_stages: one or two problems in
-// one launch, as launch_node_stages (pk0 both set or both null).
+// launch_embed_stage's arguments.
 struct EmbedStageCall {
     const float *u, *pos;
     int64_t n, seg_n;
@@ -134,4 +134,3 @@ struct EmbedStageCall {
     const char *pk0;
     float *rng_out, *h_out, *a_out, *b_out;
 };
-int launch_embed_stages(const EmbedStageCall *calls, int count, hipStream_t st);

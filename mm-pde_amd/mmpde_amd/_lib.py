@@ -119,6 +119,8 @@ _SIGS = {
     "mmpde_gnn_layer": (_I, [_P, _P, _P, _I64, _I, _P, GnnScales, _P, _P, _P, _P]),
     "mmpde_gnn_edge_mean": (_I, [_P, _P, _P, _I64, _I, _P, _P, _P, _P]),
     "mmpde_gnn_edge_mean_deg": (_I, [_P, _P, _P, _P, _I64, _I, _P, _P, _P, _P]),
+    "mmpde_gnn_edge_mean_workspace_bytes": (_I64, [_I64, _I]),
+    "mmpde_gnn_edge_mean_ex": (_I, [_P, _P, _P, _P, _I64, _I, _P, _P, _P, _I, _P, _I64, _P]),
     "mmpde_gnn_edge_backward_partials": (_I64, [ctypes.POINTER(_I)]),
     "mmpde_gnn_edge_backward": (_I, [_P, _P, _P, _P, _I64, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "mmpde_gnn_edge_source_sum": (_I, [_P, _P, _P, _I64, _P, _P]),

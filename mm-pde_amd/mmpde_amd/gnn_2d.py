@@ -70,9 +70,9 @@ class EdgeMean(torch.autograd.Function):
     """mean_i = 1/max(deg_i, 1) sum_{e < deg_i} relu(W2 relu(a_i + b_{nbr[i,e]}) + b2):
     message_net_2 over the in-edges and PyG's aggr='mean' (gnn_2d.py:36,59-63),
     with a = the target half and b = the source half of message_net_1's
-    pre-activation.  Gradients for a, b, W2 and b2, deterministic; the forward in
-    exact fp32, the backward's three GEMMs in exact fp32 (edge_gemm 'f32') or
-    the fp16x3 split (edge_gemm 'f16x3', mmpde_gnn_edge_backward_ex)."""
+    pre-activation.  Gradients for a, b, W2 and b2, deterministic; forward and
+    backward GEMMs in exact fp32 (edge_gemm 'f32') or the fp16x3 split
+    (edge_gemm 'f16x3': mmpde_gnn_edge_mean_ex, mmpde_gnn_edge_backward_ex)."""
 
     @staticmethod
     def forward(ctx, a, b, w2, b2, graph: EdgeGraph, edge_gemm: str = "f32"):
@@ -82,10 +82,14 @@ class EdgeMean(torch.autograd.Function):
         L.require_device(a, b, w2, b2, graph.nbr, graph.deg)
         a, b, w2, b2 = L.f32c(a), L.f32c(b), L.f32c(w2), L.f32c(b2)
         mean = torch.empty((n, 128), dtype=torch.float32, device=a.device)
-        L.check(L.lib().mmpde_gnn_edge_mean_deg(L.ptr(a), L.ptr(b), L.ptr(graph.nbr),
-                                                L.ptr(graph.deg), n, k, L.ptr(w2), L.ptr(b2),
-                                                L.ptr(mean), L.stream(a.device)),
-                "mmpde_gnn_edge_mean_deg")
+        mode = L.EDGE_GEMM[edge_gemm]
+        lib = L.lib()
+        wsb = lib.mmpde_gnn_edge_mean_workspace_bytes(n, mode)
+        ws = torch.empty((max(wsb, 16) // 4,), dtype=torch.float32, device=a.device) if wsb else None
+        L.check(lib.mmpde_gnn_edge_mean_ex(L.ptr(a), L.ptr(b), L.ptr(graph.nbr), L.ptr(graph.deg), n, k,
+                                           L.ptr(w2), L.ptr(b2), L.ptr(mean), mode, L.ptr(ws), wsb,
+                                           L.stream(a.device)),
+                "mmpde_gnn_edge_mean_ex")
         ctx.save_for_backward(a, b, w2, b2)
         ctx.graph = graph
         ctx.edge_gemm = L.EDGE_GEMM[edge_gemm]

@@ -125,48 +125,67 @@ class KnnTablePolicy:
     and the share f of lookups the table answered at an earlier step.
 
     Cost model (tools/knn_cand_time.py, cy B=16 on MI355X): the table path costs
-    about T_cand + (1 - f) T_full -- the candidate kernel (38-42 us when every
+    about T_cand + (1 - f) T_full -- the candidate kernel (37-44 us when every
     lookup passes) plus the full search of the lookups it could not answer --
-    against T_full (59-74 us) for the full search, so it pays only while f >
+    against T_full (61-80 us) for the full search, so it pays only while f >
     T_cand / T_full ~ 0.6; MIN_SHARE = 0.7 leaves room for the sorts the failed
-    lookups also pay.  f is read back without a sync: after a table step the
-    per-trajectory miss counters are copied to pinned host memory behind an
-    event and consumed at a later step.  Below MIN_SHARE the role runs the full
-    search -- no table, candidate or cell kernels -- for PROBE_EVERY steps, then
-    probes the table again.  Either path gives the same indices bit for bit."""
+    lookups also pay.  f is read back without a sync: the per-trajectory miss
+    counters are copied to pinned host memory behind an event after a table
+    call and consumed at a later step.  A role starts on the table (checked
+    every CHECK_EVERY calls); below MIN_SHARE it runs the full search -- no
+    candidate or cell kernels -- and after PROBE_EVERY calls makes ONE table
+    call (a probe), staying on the full search until the probe's share is
+    known.  Either path gives the same indices bit for bit."""
 
     MIN_SHARE = 0.7
-    PROBE_EVERY = 16
+    PROBE_EVERY = 64
     CHECK_EVERY = 4
 
     def __init__(self, device, batches: int, n_per: int, roles):
         self.device = torch.device(device)
         self.B, self.N = batches, n_per
-        self.state = {r: {"table": True, "wait": 0, "since": 0, "pending": None} for r in roles}
+        self.state = {r: {"mode": "table", "wait": 0, "since": 0, "pending": None, "share": None}
+                      for r in roles}
         self.enabled = True
 
-    def use_table(self, role) -> bool:
-        st = self.state[role]
+    def _resolve(self, st):
         pend = st["pending"]
-        if pend is not None and pend[0].query():
-            st["pending"] = None
-            share = 1.0 - float(pend[1].sum()) / (self.B * self.N)
-            st["last_share"] = share
-            if share < self.MIN_SHARE:
-                st["table"], st["wait"] = False, self.PROBE_EVERY
-        if not st["table"]:
+        if pend is None or not pend[0].query():
+            return
+        st["pending"] = None
+        share = 1.0 - float(pend[1].sum()) / (self.B * self.N)
+        st["share"] = share
+        if share >= self.MIN_SHARE:
+            if st["mode"] != "table":
+                st["mode"], st["since"] = "table", 0
+        else:
+            st["mode"], st["wait"] = "full", self.PROBE_EVERY
+
+    def use_table(self, role) -> bool:
+        if not self.enabled:
+            return True
+        st = self.state[role]
+        self._resolve(st)
+        if st["mode"] == "full":
             st["wait"] -= 1
             if st["wait"] < 0:
-                st["table"], st["since"] = True, 0       # probe the table again
-        return st["table"] or not self.enabled
+                st["mode"], st["since"] = "probe", 0
+                return True                          # the probe call
+            return False
+        if st["mode"] == "probe":                    # probe made, its share not known yet
+            return False
+        return True
+
+    def mode(self, role) -> str:
+        return self.state[role]["mode"]
 
     def after_table(self, role, cells: torch.Tensor, column: int) -> None:
-        """Queue the read-back of the miss counters of the call just made with
-        `cells` (on the current stream, after that call) every CHECK_EVERY table
-        steps and at a probe."""
+        """Queue the read-back of the miss counters of the table call just made
+        with `cells` (on the current stream, after that call): at a probe and
+        every CHECK_EVERY table calls."""
         st = self.state[role]
         st["since"] += 1
-        if st["pending"] is not None or (st["since"] - 1) % self.CHECK_EVERY:
+        if st["pending"] is not None or (st["mode"] == "table" and (st["since"] - 1) % self.CHECK_EVERY):
             return
         if torch.cuda.is_current_stream_capturing():
             return

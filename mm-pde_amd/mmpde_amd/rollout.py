@@ -43,6 +43,7 @@ class MMPDERollout:
         self.device = torch.device(device)
         self.moving_mesh = moving_mesh
         self.trace_hook = None   # callable() -> _lib.GnnTrace | None, one per GNN forward
+        self._knn_used = {}      # kNN searches that used the candidate table in the last step
         # run the fixed-grid model beside the moving-mesh chain (False: one stream,
         # e.g. to time single kernels without a concurrent neighbour)
         self.overlap = True
@@ -184,6 +185,7 @@ class MMPDERollout:
                              head_cache=self.dmm_cache)
         pol = self.knn_policy
         use_g, use_q = pol.use_table("graph"), pol.use_table("query")
+        self._knn_used = {"graph": use_g, "query": use_q}
         cells = ops.knn_moved_cells(mesh, self.xi, B, out=self.knn_cells) \
             if self.knn_cand is not None and (use_g or use_q) else None
         side2 = self.side2 if self.overlap else cur
@@ -214,7 +216,8 @@ class MMPDERollout:
             nbr_m = ops.knn_graph_nbr(mesh, B, self.gc.n)
         self.nbr_m = nbr_m
         if self.kind == "burgers":
-            if pol.use_table("query1"):
+            self._knn_used["query1"] = pol.use_table("query1")
+            if self._knn_used["query1"]:
                 cells1 = ops.knn_moved_cells(self.grid_rep, self.grid, B, out=self.knn_cells_1)
                 idx1 = ops.knn_query_moved(self.grid_rep, mesh, self.grid, self.knn_cand_1, B, 30,
                                            self.knn_scratch_1, ref=self.xi, cells=cells1,
@@ -240,14 +243,24 @@ class MMPDERollout:
     def knn_table_share(self):
         """(graph, query[, burgers mode-'1' query]): the share of the last step's
         moved-mesh kNN lookups the candidate tables answered (the rest went to
-        the full search).  Diagnostics: synchronises the device."""
+        the full search); None for a search the policy ran without the table
+        that step (ops.KnnTablePolicy).  Diagnostics: synchronises the device."""
         if not self.moving_mesh or self.knn_cand is None:
             return None
         torch.cuda.synchronize(self.device)
+        used = self._knn_used
         s = ops.knn_table_share(self.knn_cells, self.B, self.N).mean(0).tolist()
+        s = [s[0] if used.get("graph") else None, s[1] if used.get("query") else None]
         if self.kind == "burgers":
-            s.append(ops.knn_table_share(self.knn_cells_1, self.B, self.N)[:, 1].mean().item())
+            s.append(ops.knn_table_share(self.knn_cells_1, self.B, self.N)[:, 1].mean().item()
+                     if used.get("query1") else None)
         return tuple(s)
+
+    def knn_modes(self):
+        """Per kNN search of the step: 'table', 'full' or 'probe' (ops.KnnTablePolicy)."""
+        if not self.moving_mesh:
+            return {}
+        return {r: self.knn_policy.mode(r) for r in self.knn_policy.state}
 
     def knn_query_ties(self) -> int:
         """Queries of the kNN-30 searches (reference data_creator_2d.py:75-76)

@@ -91,8 +91,11 @@ for disp in disps:
                 pol.after_table("query", c, 1)
             else:
                 ops.knn_query(pos, qry, B, 30)
-        t_pol = timed(policy_step, reps=96)
-        modes = {r: ("table" if st["table"] else "full") for r, st in pol.state.items()}
+        for _ in range(8):   # the first read-backs resolve (the host runs ahead of the GPU)
+            policy_step()
+        torch.cuda.synchronize()
+        t_pol = timed(policy_step, reps=128)
+        modes = {r: pol.mode(r) for r in pol.state}
         print(f"  policy (graph + query + cells, probes every {pol.PROBE_EVERY}): {t_pol:.1f} us per call "
               f"against full {t_full + t_fq:.1f} / table {t_cand + t_cq + t_cells:.1f}; modes {modes}")
 
@@ -114,8 +117,8 @@ for kind, bk in (("cy", B), ("burgers", 2 * B)):
         for i in range(10):
             u = eng.step(u, 1 + i)
             shares.append(eng.knn_table_share())
-        modes = {r: ("table" if st["table"] else "full") for r, st in eng.knn_policy.state.items()}
             dmax.append((eng.mesh.reshape(bk, -1, 2) - eng.xi).norm(dim=-1).max().item())
+        modes = eng.knn_modes()
     print(f"{kind} bench rollout (B={bk}): table share (graph, query[, mode-1 query]) per step",
-          [tuple(round(a, 4) for a in sh) for sh in shares],
+          [tuple(None if a is None else round(a, 4) for a in sh) for sh in shares],
           "max displacement", [round(x, 4) for x in dmax], "policy after 10 steps", modes)

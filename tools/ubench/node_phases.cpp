@@ -115,16 +115,16 @@ int main(int argc, char **argv) {
             }
             ph[0] += (double)(s[7] - s[0]);
         }
-        const double clk = (double)(t1 - t0) / (1e-3 * ms / it);  // shader clocks per second (approx)
-        printf("%s node kernel: %.2f us per launch; one stamped launch spans %.0f clocks (~%.2f GHz)\n",
-               next ? "NEXT" : "last", 1e3 * ms / it, (double)(t1 - t0), clk / 1e9);
+        // stamps: the 100 MHz real-time clock (10 ns ticks)
+        printf("%s node kernel: %.2f us per launch; the stamped launch spans %.2f us\n",
+               next ? "NEXT" : "last", 1e3 * ms / it, 0.01 * (double)(t1 - t0));
         static const char *names[8] = {"whole workgroup", "constants + operand issue", "prep [h|mean] + barrier",
                                        "GEMM1 + epilogue", "barrier + prep v + barrier",
                                        "GEMM2 + epilogue (h')", "barrier + prep h' + barrier",
                                        "GEMM3 projections + stores"};
         for (int i = 0; i < 8; ++i) {
             if (!next && i == 6) continue;
-            printf("  %-30s %8.0f clocks mean\n", names[i], ph[i] / nblk);
+            printf("  %-30s %8.2f us mean\n", names[i], 0.01 * ph[i] / nblk);
         }
         // concurrency: workgroups alive at the midpoint of every workgroup's life
         std::vector<std::pair<uint64_t, int>> ev;
@@ -141,6 +141,21 @@ int main(int argc, char **argv) {
             area += (double)live * (double)(ev[i + 1].first - ev[i].first);
         }
         printf("  workgroups alive: peak %d, mean %.0f\n", peak, area / (double)(t1 - t0));
+        // output hash (FNV-1a over h', a', b' and the range records): builds
+        // of the kernel that must be bitwise equal print the same value
+        uint64_t hsh = 1469598103934665603ull;
+        auto fold = [&](const float *d, size_t cnt) {
+            std::vector<uint32_t> v(cnt);
+            hipMemcpy(v.data(), d, cnt * 4, hipMemcpyDeviceToHost);
+            for (uint32_t w : v) hsh = (hsh ^ w) * 1099511628211ull;
+        };
+        fold(h1, n * H);
+        if (next) {
+            fold(ao, n * H);
+            fold(bo, n * H);
+            fold(rout, 4 * range_tiles(n));
+        }
+        printf("  output hash %016llx\n", (unsigned long long)hsh);
     }
     CK(hipGetLastError());
     return 0;
