@@ -218,6 +218,18 @@ int mmpde_conv2d_ex(const float *x, int64_t batches, int cin, int h, int w, cons
                     const float *residual, int res_after_act, int act, float *y,
                     mmpde_stream_t stream);
 
+/* Weight and bias gradients of a stride-1 mmpde_conv2d_ex convolution (output
+ * size = input size, pad = ks / 2 for odd ks) -- the training backward of
+ * BaseCNN (models_cnn.py:66-83 through loss.backward(), train_helper_2d.py:
+ * 121-126): dw [cout, cin, ks, ks] = sum over batches and pixels of
+ * dy[b, co, y, x] * x[b, ci, y - pad + ky, x - pad + kx] (wrapped or zero
+ * padded), db [cout] = sum of dy (nullable).  ks * ks <= 256.  Fixed summation
+ * order: deterministic.  (The input gradient is mmpde_conv2d_ex of dy with
+ * the flipped, transposed kernel.) */
+int mmpde_conv2d_grad_weight(const float *x, int64_t batches, int cin, int h, int w, const float *dy,
+                             int cout, int ks, int pad, int pad_mode, float *dw_out, float *db_out,
+                             mmpde_stream_t stream);
+
 /* ------------------------------------------------------------------------
  * MP_PDE_Solver_2D (reference gnn_2d.py:19-141), hidden width 128.
  * Node inputs: u [n, tw] fp32 (data.x), pos [n, 3] fp32 = (t, x, y) (data.pos).

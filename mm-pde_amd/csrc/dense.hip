@@ -244,6 +244,80 @@ __global__ __launch_bounds__(256) void conv2d_kernel(const float *__restrict__ x
     y[e] = act_apply(acc, act);
 }
 
+// Weight / bias gradient of a stride-1 convolution (the backward of
+// conv2d_kernel; BaseCNN training, models_cnn.py:66-83 under
+// train_helper_2d.py:121-126):
+//   dw[co, ci, ky, kx] = sum_{b, y, x} dy[b, co, y, x] * x[b, ci, y - pad + ky, x - pad + kx]
+//   db[co]             = sum_{b, y, x} dy[b, co, y, x]        (ci == 0 workgroups)
+// with circular (wrapped) or zero (skipped) padding.  One workgroup per
+// (co, ci): thread t takes tap t % T (T = ks * ks) and pixel slice t / T; the
+// (x, dy) planes of each batch are staged in LDS when they fit.  Every sum runs
+// in a fixed order (batches, then the slice's pixels, then the slices):
+// deterministic, no atomics.
+constexpr int kGwThreads = 256;
+template <bool LDS>
+__global__ __launch_bounds__(kGwThreads) void conv2d_grad_weight_kernel(const float *__restrict__ x,
+                                                                       const float *__restrict__ dy, int batches,
+                                                                       int cin, int cout, int h, int w, int ks,
+                                                                       int pad, int circular,
+                                                                       float *__restrict__ dw,
+                                                                       float *__restrict__ db) {
+    extern __shared__ float sm[];  // LDS: x plane [h * w], dy plane [h * w]; then the slice sums
+    const int co = (int)blockIdx.x / cin, ci = (int)blockIdx.x % cin;
+    const int T = ks * ks, S = kGwThreads / T;
+    const int t = threadIdx.x, tap = t % T, sl = t / T;
+    const bool act = sl < S;
+    const int ky = tap / ks, kx = tap % ks;
+    const int hw = h * w;
+    float acc = 0.0f, accb = 0.0f;
+    for (int b = 0; b < batches; ++b) {
+        const float *xp = x + ((int64_t)b * cin + ci) * hw;
+        const float *dp = dy + ((int64_t)b * cout + co) * hw;
+        const float *X = xp, *D = dp;
+        if (LDS) {
+            __syncthreads();  // the previous batch's planes are consumed
+            for (int i = t; i < hw; i += kGwThreads) {
+                sm[i] = xp[i];
+                sm[hw + i] = dp[i];
+            }
+            __syncthreads();
+            X = sm;
+            D = sm + hw;
+        }
+        if (act) {
+            for (int p = sl; p < hw; p += S) {
+                const int oy = p / w, ox = p - oy * w;
+                const float g = D[p];
+                if (ci == 0 && tap == 0) accb += g;  // the bias sums every pixel
+                int iy = oy - pad + ky, ix = ox - pad + kx;
+                if (circular) {
+                    iy = iy < 0 ? iy + h : (iy >= h ? iy - h : iy);
+                    ix = ix < 0 ? ix + w : (ix >= w ? ix - w : ix);
+                } else if (iy < 0 || iy >= h || ix < 0 || ix >= w) {
+                    continue;
+                }
+                acc = fmaf(g, X[iy * w + ix], acc);
+            }
+        }
+    }
+    // the slices of each tap, added in slice order
+    __syncthreads();
+    float *part = sm;  // [S][T] (+ bias partials after)
+    if (act) part[sl * T + tap] = acc;
+    if (act && tap == 0) part[S * T + sl] = accb;
+    __syncthreads();
+    if (t < T) {
+        float v = 0.0f;
+        for (int q = 0; q < S; ++q) v += part[q * T + t];
+        dw[(((int64_t)co * cin + ci) * ks + t / ks) * ks + t % ks] = v;
+    }
+    if (ci == 0 && t == 0 && db) {
+        float v = 0.0f;
+        for (int q = 0; q < S; ++q) v += part[S * T + q];
+        db[co] = v;
+    }
+}
+
 // Per-trajectory mean squared error: one workgroup per trajectory, every thread
 // sums a fixed strided subset in index order, then a fixed LDS tree: the
 // result depends only on that trajectory's values (not on how many
@@ -389,6 +463,32 @@ int conv2d(const float *x, int64_t batches, int cin, int h, int w, const float *
     return MMPDE_OK;
 }
 }  // namespace mmpde_detail
+
+extern "C" int mmpde_conv2d_grad_weight(const float *x, int64_t batches, int cin, int h, int w, const float *dy,
+                                        int cout, int ks, int pad, int pad_mode, float *dw_out, float *db_out,
+                                        mmpde_stream_t stream) {
+    MMPDE_REQUIRE(x && dy && dw_out && batches > 0 && batches <= INT32_MAX && cin > 0 && cout > 0);
+    MMPDE_REQUIRE(ks > 0 && ks * ks <= kGwThreads && pad >= 0 && h > 0 && w > 0);
+    MMPDE_REQUIRE(h + 2 * pad - ks + 1 == h && w + 2 * pad - ks + 1 == w);  // stride 1, output size = input size
+    MMPDE_REQUIRE(pad_mode == MMPDE_PAD_ZEROS || (pad_mode == MMPDE_PAD_CIRCULAR && pad <= h && pad <= w));
+    MMPDE_REQUIRE((int64_t)cin * cout < INT32_MAX && (int64_t)h * w < INT32_MAX / 2);
+    const int T = ks * ks, S = kGwThreads / T;
+    const size_t part = (size_t)(S * T + S) * sizeof(float);
+    const size_t planes = (size_t)2 * h * w * sizeof(float);
+    const bool lds = planes <= 64 * 1024;
+    const size_t shm = lds ? (planes > part ? planes : part) : part;
+    const dim3 grid((unsigned)(cin * cout));
+    if (lds)
+        hipLaunchKernelGGL(conv2d_grad_weight_kernel<true>, grid, dim3(kGwThreads), shm, as_stream(stream), x, dy,
+                           (int)batches, cin, cout, h, w, ks, pad, pad_mode == MMPDE_PAD_CIRCULAR ? 1 : 0, dw_out,
+                           db_out);
+    else
+        hipLaunchKernelGGL(conv2d_grad_weight_kernel<false>, grid, dim3(kGwThreads), shm, as_stream(stream), x, dy,
+                           (int)batches, cin, cout, h, w, ks, pad, pad_mode == MMPDE_PAD_CIRCULAR ? 1 : 0, dw_out,
+                           db_out);
+    MMPDE_RET_LAUNCH();
+    return MMPDE_OK;
+}
 
 extern "C" int mmpde_resample_bilinear(const float *x, int64_t planes, int h, int w, int oh, int ow, float *y,
                                        mmpde_stream_t stream) {

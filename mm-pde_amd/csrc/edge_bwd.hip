@@ -241,7 +241,16 @@ __device__ __forceinline__ void split1(float x, _Float16 &h, _Float16 &l) {
     l = (_Float16)(x - (float)h);
 }
 
-__global__ __launch_bounds__(512, 2) void edge_bwd_f16_kernel(EdgeBwdF16Args p) {
+// Static LDS of edge_bwd_f16_kernel (the arrays below): ~141 KiB, which only
+// gfx950's 160 KiB per CU holds, one workgroup per CU -- hence the launch
+// bound of one 512-thread workgroup and the size check.
+constexpr size_t kEdgeBwdF16Lds = sizeof(float) * 2 * FT * FAW + sizeof(_Float16) * 2 * 2 * FT * FAS +
+                                  sizeof(_Float16) * 2 * 2 * BH * FCS + sizeof(_Float16) * 2 * FT * FAS +
+                                  sizeof(_Float16) * 2 * BH * FCS + 2 * BH * (FT / 8) + sizeof(int) * FT * FKMAX +
+                                  sizeof(int) * FT;
+static_assert(kEdgeBwdF16Lds <= 160 * 1024, "edge_bwd_f16_kernel: LDS beyond gfx950's 160 KiB per CU");
+
+__global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) {
     __shared__ float at[FT * FAW];             // a rows of the tile
     __shared__ float gms[FT * FAW];            // g / deg rows (0 for rows past n)
     // relu(z1) images double-buffered by slot parity (no barrier between a

@@ -114,6 +114,7 @@ _SIGS = {
     "mmpde_conv2d": (_I, [_P, _I64, _I, _I, _I, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P]),
     "mmpde_resample_bilinear": (_I, [_P, _I64, _I, _I, _I, _I, _P, _P]),
     "mmpde_conv2d_ex": (_I, [_P, _I64, _I, _I, _I, _P, _P, _I, _I, _I, _I, _I, _P, _I, _I, _P, _P]),
+    "mmpde_conv2d_grad_weight": (_I, [_P, _I64, _I, _I, _I, _P, _I, _I, _I, _I, _P, _P, _P]),
     "mmpde_gnn_workspace_bytes": (_I64, [_I64]),
     "mmpde_gnn_embed": (_I, [_P, _P, _I64, GnnScales, _P, _P, _P, _P]),
     "mmpde_gnn_layer": (_I, [_P, _P, _P, _I64, _I, _P, GnnScales, _P, _P, _P, _P]),

@@ -318,7 +318,7 @@ def objective(model, args, sample, nx, init_mesh, device):
 
 # --------------------------------------------------------------------------- training
 def train_MA_res(ori_u, all_u, test_u, args, model, init_mesh, n_epoch_adam, n_epoch_lbfgs, device,
-                 save_dir=None, evaluate_every=1):  # noqa: N802 - reference name
+                 save_dir=None, evaluate_every=1, reference_save_path=False):  # noqa: N802 - reference name
     """dmm_utils.py:391-1095 without the random-feature branch: n_epoch_adam
     epochs of Adam then n_epoch_lbfgs of LBFGS, each epoch max(1, train_sample_grid
     T / (bx bu)) draws of fresh samples; per epoch the equation residual of the
@@ -328,7 +328,21 @@ def train_MA_res(ori_u, all_u, test_u, args, model, init_mesh, n_epoch_adam, n_e
     reference's 15-tuple (dmm_utils.py:1094-1095): model, loss_in, loss_bound,
     loss_convex, test_equ_loss / max / min / mid, train_std, train_minmax,
     test_std, test_minmax, itp_list1, itp_list2 (empty: filled only by the
-    random-feature branch), logs_txt."""
+    random-feature branch), logs_txt.
+
+    Checkpoint file: 'dmm_{experiment}_epoch{N}.pt' in save_dir, one per epoch;
+    reference_save_path=True writes the reference's name instead,
+    '{experiment}/{datetime}_{rf}_bound{loss_bound_rf}_..._{gamma_adam}'
+    (dmm_utils.py:768-770), so scripts that look checkpoints up by that name
+    find them.  The dict holds the reference's keys plus test_equ_loss and logs.
+
+    Deliberate difference: with init_mesh=True the reference's LBFGS closure
+    (dmm_utils.py:659-662) never calls backward -- LBFGS then steps on zeroed
+    gradients -- and its logging (:691-696) reads loss_convex and LHS, which
+    that branch never assigns (a NameError on the first logged draw).  Here the
+    init_mesh LBFGS phase runs backward like every other phase and logs 0 for
+    the convexity loss and None for LHS (tests/test_gpu_dmm_train.py
+    ::test_init_mesh_lbfgs_phase_trains)."""
     model.train()
     opt_adam = torch.optim.Adam(model.parameters(), lr=args.lr_adam, betas=(0.9, 0.999), eps=1e-8,
                                 weight_decay=args.weight_decay)
@@ -409,7 +423,15 @@ def train_MA_res(ori_u, all_u, test_u, args, model, init_mesh, n_epoch_adam, n_e
         if save_dir is not False:
             d = save_dir if save_dir is not None else args.experiment
             os.makedirs(d, exist_ok=True)
-            torch.save(ckpt, os.path.join(d, f"dmm_{args.experiment}_epoch{epoch}.pt"))
+            if reference_save_path:
+                name = "{}_{}_bound{}_{}_{}_{}_{}_{}_{}_{}_{}_{}_{}_{}_{}".format(
+                    datetime.now(), args.rf, args.loss_bound_rf, args.epochs_rf, args.max_iter, args.sub_u,
+                    args.epochs_lbfgs, args.batch_size_u_adam, args.batch_size_x_adam, args.loss_weight1,
+                    args.train_sample_grid, args.branch_layers, args.lr_adam, args.trunk_layers,
+                    args.gamma_adam)
+            else:
+                name = f"dmm_{args.experiment}_epoch{epoch}.pt"
+            torch.save(ckpt, os.path.join(d, name))
     return (model, log["loss_in"], log["loss_bound"], log["loss_convex"], log["test_equ_loss"],
             log["test_equ_max"], log["test_equ_min"], log["test_equ_mid"], log["train_std"],
             log["train_minmax"], log["test_std"], log["test_minmax"], [], [], log["logs_txt"])

@@ -25,7 +25,7 @@ import torch
 from torch import nn
 
 from . import _lib as L
-from .ops import nbr_table_from_edge_index, reverse_adjacency
+from .ops import LinearRows, linear_train, nbr_table_from_edge_index, reverse_adjacency
 
 
 class BatchNorm(nn.Module):
@@ -184,12 +184,14 @@ class GNN_Layer_FS_2D(nn.Module):  # noqa: N801 - reference name
         wdu = w1[:, 2 * f:2 * f + tw]
         wdxy = w1[:, 2 * f + tw:2 * f + tw + 2]
         wt = w1[:, 2 * f + tw + 2:]
-        a = torch.addmm(b1, torch.cat((h, u, pos_x, pos_y, variables), -1),
-                        torch.cat((w1[:, :f], wdu, wdxy, wt), 1).t())
-        b = torch.cat((h, u, pos_x, pos_y), -1) @ torch.cat((w1[:, f:2 * f], -wdu, -wdxy), 1).t()
+        a = LinearRows.apply(torch.cat((h, u, pos_x, pos_y, variables), -1),
+                             torch.cat((w1[:, :f], wdu, wdxy, wt), 1), b1)
+        b = LinearRows.apply(torch.cat((h, u, pos_x, pos_y), -1),
+                             torch.cat((w1[:, f:2 * f], -wdu, -wdxy), 1), None)
         m2 = self.message_net_2[0]
         mean = EdgeMean.apply(a, b, m2.weight, m2.bias, graph, edge_gemm)
-        upd = self.update_net_2(self.update_net_1(torch.cat((h, mean, variables), -1)))
+        v = torch.relu(linear_train(torch.cat((h, mean, variables), -1), self.update_net_1[0]))
+        upd = torch.relu(linear_train(v, self.update_net_2[0]))
         return self.norm(h + upd)
 
     def forward(self, x, u, pos_x, pos_y, variables, edge_index, batch):
@@ -388,8 +390,35 @@ class MP_PDE_Solver_2D(nn.Module):  # noqa: N801 - reference name
         pos_x = pos[:, 1][:, None] / self.pde.Lx
         pos_y = pos[:, 2][:, None] / self.pde.Ly
         variables = pos[:, 0][:, None] / self.pde.tmax
-        h = self.embedding_mlp(torch.cat((u, pos_x, pos_y, variables), -1))
+        e = self.embedding_mlp
+        z = torch.relu(e[1](linear_train(torch.cat((u, pos_x, pos_y, variables), -1), e[0])))
+        h = e[4](linear_train(z, e[3]))
         for layer in self.gnn_layers:
             h = layer.train_forward(h, u, pos_x, pos_y, variables, graph, self.edge_gemm)
-        diff = self.output_mlp(h[:, None]).squeeze(1)
+        diff = self._head_train(h)
         return self.out_scales()[None].to(h.device) * diff
+
+    def _head_train(self, h: torch.Tensor) -> torch.Tensor:
+        """output_mlp(h[:, None]).squeeze(1) (gnn_2d.py:108-114,136), as the
+        same three strided Conv1d written as unfold + GEMM (per node: 128 -> 38
+        x 4 -> 9 x 8 -> 1): autograd through batched GEMMs and unfold's
+        gather-form backward instead of MIOpen's convolution search and
+        kernels (which cost ~1 ms per training iteration and a multi-second
+        search on first use)."""
+        o = self.output_mlp
+        n = h.shape[0]
+        x = h
+        y = None
+        for i, idx in enumerate((0, 2, 4)):
+            c = o[idx]
+            cout, cin, ks = c.weight.shape
+            st = c.stride[0]
+            if i == 0:
+                win = x.unfold(1, ks, st)                               # [n, L, ks]   (cin = 1)
+            else:
+                win = y.transpose(1, 2).unfold(2, ks, st)               # [n, cin, L, ks]
+                win = win.permute(0, 2, 1, 3).reshape(n, win.shape[2], cin * ks)
+            y = win @ c.weight.reshape(cout, cin * ks).t() + c.bias    # [n, L, cout]
+            if idx != 4:
+                y = torch.relu(y)
+        return y.transpose(1, 2).squeeze(1)                             # [n, L_last]

@@ -90,11 +90,15 @@ class ItpNet(nn.Module):
         mods = self.layers if mode == "1" else self.layers2
         x = torch.cat((neighbors, query_points), dim=-2).reshape(
             neighbors.shape[0], neighbors.shape[1], -1)
+        lead = x.shape[:-1]
+        x = x.reshape(-1, x.shape[-1])
         for i, lin in enumerate(mods):
-            x = lin(x)
+            # rows of every trajectory's queries: the row-chunked weight
+            # gradient of ops.LinearRows (the library's K = rows GEMM is slow)
+            x = ops.linear_train(x, lin) if x.requires_grad or lin.weight.requires_grad else lin(x)
             if i != len(mods) - 1:
                 x = torch.tanh(x)
-        return x
+        return x.reshape(*lead, x.shape[-1])
 
     def res_cut(self, data: torch.Tensor) -> torch.Tensor:
         """``down`` network (interpolate.py:95-97): data [B, N] (cylinder) or

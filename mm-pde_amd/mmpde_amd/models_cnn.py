@@ -7,9 +7,12 @@ residual connections on the time window stacked as channels, then
 initialisation order match the reference, so its checkpoints load and a
 seeded construction gives the same weights.  The convolutions run on
 ``mmpde_conv2d_ex`` (circular indices, ELU and the post-activation residual
-fused); the output combine is two small elementwise ops.  Eval-mode forward
-(inference / ``test_timestep_losses``); training the CNN baseline is outside
-the hot path and raises.
+fused); the output combine is two small elementwise ops.  In train() mode
+(the reference's ``training_loop_branch`` non-GNN branch,
+train_helper_2d.py:107-125) every convolution is ops.Conv2dSame -- forward on
+the same kernel, backward on HIP (input gradient as the convolution of dy with
+the flipped kernel, weight / bias gradients by mmpde_conv2d_grad_weight) --
+and ELU, the residuals and the output combine are autograd torch ops.
 """
 from __future__ import annotations
 
@@ -44,13 +47,12 @@ class BaseCNN(nn.Module):
 
     def forward(self, u: torch.Tensor) -> torch.Tensor:
         """u [B, tw, X, Y] -> squeeze([B, 1, tw, X, Y]) (models_cnn.py:66-83)."""
-        if self.training:
-            raise NotImplementedError("training the BaseCNN baseline is out of scope "
-                                      "(SURVEY.md §8(f) row 4); call .eval()")
         L.require_device(u)
         circ = self.padding_mode == "circular"
         if not circ and self.padding_mode != "zeros":
             raise NotImplementedError(f"padding_mode {self.padding_mode!r}")
+        if self.training:
+            return self._train_forward(u, circ)
         u = L.f32c(u)
 
         def conv(i, x, act, residual=None):
@@ -65,5 +67,23 @@ class BaseCNN(nn.Module):
         x = conv(8, x, L.ACT_NONE)
         tw = self.time_window
         dt = torch.cumsum(torch.full((1, tw), float(self.pde.dt), device=u.device), dim=1)[None, :, :, None, None]
+        out = u[:, -1][:, None, None].repeat(1, 1, tw, 1, 1) + dt * x[:, None]
+        return out.squeeze()
+
+    def _train_forward(self, u: torch.Tensor, circ: bool) -> torch.Tensor:
+        """models_cnn.py:66-83, differentiable (ops.Conv2dSame + torch ELU)."""
+        import torch.nn.functional as F
+
+        def conv(i, x):
+            c = getattr(self, f"conv{i}")
+            return ops.Conv2dSame.apply(x, c.weight, c.bias, circ)
+
+        u = u.float()
+        x = F.elu(conv(1, u))
+        for i in range(2, 8):
+            x = x + F.elu(conv(i, x))
+        x = conv(8, x)
+        tw = self.time_window
+        dt = torch.cumsum(torch.ones(1, tw, device=u.device) * float(self.pde.dt), dim=1)[None, :, :, None, None]
         out = u[:, -1][:, None, None].repeat(1, 1, tw, 1, 1) + dt * x[:, None]
         return out.squeeze()

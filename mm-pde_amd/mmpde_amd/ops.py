@@ -450,6 +450,104 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, b, stride: int, pad: int, act: int,
     return y
 
 
+def conv2d_grad_weight(x: torch.Tensor, dy: torch.Tensor, ks: int, pad: int, circular: bool,
+                       bias: bool = True):
+    """(dw [cout, cin, ks, ks], db [cout] or None) of a stride-1 conv2d with
+    output size = input size (mmpde_conv2d_grad_weight; deterministic)."""
+    L.require_device(x, dy)
+    x, dy = L.f32c(x), L.f32c(dy)
+    bt, cin, h, wd = x.shape
+    cout = dy.shape[1]
+    if dy.shape != (bt, cout, h, wd):
+        raise ValueError("dy must be [batches, cout, h, w] of x's batches and plane")
+    dw = torch.empty((cout, cin, ks, ks), dtype=torch.float32, device=x.device)
+    db = torch.empty((cout,), dtype=torch.float32, device=x.device) if bias else None
+    L.check(L.lib().mmpde_conv2d_grad_weight(L.ptr(x), bt, cin, h, wd, L.ptr(dy), cout, ks, pad,
+                                             L.PAD_CIRCULAR if circular else L.PAD_ZEROS, L.ptr(dw), L.ptr(db),
+                                             L.stream(x.device)), "mmpde_conv2d_grad_weight")
+    return dw, db
+
+
+class LinearRows(torch.autograd.Function):
+    """y = x W^T + b over many rows (the train-mode node GEMMs of
+    GNN_Layer_FS_2D / MP_PDE_Solver_2D, gnn_2d.py:53-69,99-106), with a
+    weight gradient that reduces over the rows in chunks: dW = sum_c dY_c^T X_c
+    as one batched GEMM over C equal row chunks plus the remainder rows,
+    summed in chunk order.  The library's single GEMM with K = n rows
+    (hipBLASLt picks 32 x 32 tiles and a serial K loop) takes 105-247 us per
+    layer GEMM at n = 40336; the batched form 26-53 us (tools/gemm_shapes.py,
+    profiles/r04_gemm_shapes.log).  dX = dY W and the forward stay single GEMMs.
+    Deterministic for a given shape (fixed chunking, fixed reduction order)."""
+
+    @staticmethod
+    def chunks(n: int, k: int) -> int:
+        return 0 if n < 4096 else (64 if k > 160 else 16)
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.has_bias = b is not None
+        y = x @ w.t()
+        return y + b if b is not None else y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = dy @ w
+        if ctx.needs_input_grad[1]:
+            n, k = x.shape
+            C = LinearRows.chunks(n, k)
+            if C:
+                R = n // C
+                xs, dys = x[:C * R].reshape(C, R, k), dy[:C * R].reshape(C, R, dy.shape[1])
+                gw = torch.bmm(dys.transpose(1, 2), xs).sum(0)
+                if C * R < n:
+                    gw = gw + dy[C * R:].t() @ x[C * R:]
+            else:
+                gw = dy.t() @ x
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            gb = dy.sum(0)
+        return gx, gw, gb
+
+
+def linear_train(x: torch.Tensor, lin: torch.nn.Linear) -> torch.Tensor:
+    """lin(x) for [n, k] rows in train mode through LinearRows."""
+    return LinearRows.apply(x.contiguous(), lin.weight, lin.bias)
+
+
+class Conv2dSame(torch.autograd.Function):
+    """Differentiable stride-1 conv2d with output size = input size (odd ks,
+    pad = ks // 2), zero or circular padding, on the HIP kernels: forward
+    mmpde_conv2d_ex; backward dx = the same convolution of dy with the flipped,
+    transposed kernel (circular indices wrap the same way), dw / db
+    mmpde_conv2d_grad_weight.  Deterministic."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, circular: bool):
+        ks = w.shape[-1]
+        if w.shape[-2] != ks or ks % 2 != 1:
+            raise ValueError("Conv2dSame takes square odd kernels")
+        ctx.save_for_backward(x, w)
+        ctx.circular = circular
+        ctx.has_bias = b is not None
+        return conv2d(x, w, b, 1, ks // 2, L.ACT_NONE, circular=circular)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        ks = w.shape[-1]
+        dy = L.f32c(dy)
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            wt = w.flip(2, 3).transpose(0, 1).contiguous()
+            gx = conv2d(dy, wt, None, 1, ks // 2, L.ACT_NONE, circular=ctx.circular)
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            gw, gb = conv2d_grad_weight(x, dy, ks, ks // 2, ctx.circular, bias=ctx.has_bias)
+        return gx, gw, gb, None
+
+
 def itp_interp(src, vals, qry, idx, batches: int, packed: torch.Tensor, addend=None, addend2=None):
     """ItpNet weights + weighted neighbour sum (interpolate.py:77-93,
     data_creator_2d.py:80-83), + addend, then + addend2 (both optional).

@@ -55,8 +55,9 @@ def training_itp(itp_model, mesh_model, unrolling, batch_size, optimizer, optimi
 def training_loop_branch(model, model_b, itp_model, mesh_model, unrolling, batch_size, optimizer,
                          optimizer2, loader, graph_creator, criterion,
                          device="cpu") -> torch.Tensor:
-    """train_helper_2d.py:65-134 (GNN branch): pred = interpolate_pred(itp,
-    model_b(graph), graph, data) + model(graph_uni), MSE against the labels,
+    """train_helper_2d.py:65-134: GNN branch pred = interpolate_pred(itp,
+    model_b(graph), graph, data) + model(graph_uni), MSE against the labels;
+    CNN branch (BaseCNN) pred = model(data), MSE against labels.squeeze();
     backward, AdamW step."""
     losses = []
     for idx, (_u_base, u_super) in enumerate(loader):
@@ -66,7 +67,16 @@ def training_loop_branch(model, model_b, itp_model, mesh_model, unrolling, batch
         random_steps = _draw_steps(graph_creator, unrolling, batch_size)
         data, labels = graph_creator.create_data(u_super, random_steps)
         if f"{model}" != "GNN":
-            raise NotImplementedError("the BaseCNN baseline (models_cnn.py) is out of scope")
+            # the CNN baseline (train_helper_2d.py:116-117,124-125)
+            data, labels = data.to(device), labels.to(device)
+            pred = model(data)
+            loss = criterion(pred, labels.squeeze())
+            loss.backward()
+            losses.append(loss.detach())
+            optimizer.step()
+            if optimizer2 is not None and idx % 1 == 0:
+                optimizer2.step()
+            continue
         graph_uni = graph_creator.create_graph(itp_model, data, labels, random_steps, device, None)
         if mesh_model is not None:
             graph = graph_creator.create_graph(itp_model, data, labels, random_steps, device,

@@ -286,6 +286,31 @@ def test_train_MA_res_lbfgs_epoch_runs(dev):  # noqa: N802
     assert all(torch.isfinite(p).all() for p in dmm.parameters())
 
 
+def test_init_mesh_lbfgs_phase_trains(dev, tmp_path):  # noqa: N802
+    """The deliberate difference of the init_mesh LBFGS phase (dmm_train.py
+    docstring; reference dmm_utils.py:659-662,691-696, whose closure skips
+    backward and then reads unassigned names): here it runs backward, moves the
+    parameters, logs 0 for the convexity loss and None for LHS; the checkpoint
+    goes to the reference's file name with reference_save_path."""
+    from mmpde_amd import dmm_train as T
+
+    pde, dmm = _models("burgers")
+    all_u = _data("burgers", pde, 6)
+    args = _args("burgers", 8, 4, rf=False, loss_bound_rf=1.0, epochs_rf=0, max_iter=20, sub_u=1,
+                 epochs_lbfgs=1, branch_layers=[4, 3], trunk_layers=[32, 512])
+    dmm.to(dev)
+    p0 = [p.detach().clone() for p in dmm.parameters()]
+    np.random.seed(3)
+    out = T.train_MA_res(all_u, all_u, all_u[:2], args, dmm, True, 0, 1, dev, save_dir=str(tmp_path),
+                         evaluate_every=0, reference_save_path=True)
+    assert out[3] == [0.0] and np.isfinite(out[1][0]) and np.isfinite(out[2][0])
+    assert out[4] == []                      # no LHS: no equation residual
+    assert any(not torch.equal(a, b.detach()) for a, b in zip(p0, dmm.parameters()))
+    assert all(torch.isfinite(p).all() for p in dmm.parameters())
+    names = [f.name for f in tmp_path.iterdir()]
+    assert len(names) == 1 and "_False_bound1.0_0_20_1_1_4_8_1000.0_0_[4, 3]_0.0002_[32, 512]_0.2" in names[0]
+
+
 # ----------------------------------------------------------------------------- evaluation
 def test_evaluate_tri_vs_oracle(dev):
     from scipy.spatial import Delaunay
