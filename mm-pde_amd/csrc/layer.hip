@@ -516,7 +516,6 @@ struct NodeArgs {
     const int32_t *div_deg = nullptr;
     int div_k = 0;
     EdgeSplit split;       // units > 0: add the wave kernel's side blocks first
-    int side32 = 0;        // the side-block index arithmetic fits 32 bits (side_fetch)
 };
 
 constexpr int NLD = 132;  // fp32 staging row stride (floats)
@@ -555,36 +554,6 @@ constexpr bool NODE_EARLY_B = MMPDE_NODE_EARLY_B != 0;
 // buffer order (the edge stage's per-part sums); div_k > 0: the total is then
 // divided by the row's degree max(div_deg[row], 1), or by div_k (IEEE division:
 // torch_scatter's mean = sum / count).
-// Node / embed kernel variants (tools/ubench/node_phases A/B builds):
-// LDSBAR: LDS hand-offs wait for the wave's own LDS operations only (a
-// __syncthreads also drains its outstanding global stores); EARLY_ROWS: the
-// [h | mean] rows issued first, every use of a constant deferred to after the
-// rows' arrival (loads complete in issue order); PROJ2: the b' operands issued
-// after a's GEMM, in flight over a's epilogue.  Measured (r04, node_phases):
-// EARLY_ROWS with the constants' arithmetic before the rows' use and PROJ2
-// together 60-61 us against 53-54 (legacy), so all default off.
-#ifndef MMPDE_NODE_LDSBAR
-#define MMPDE_NODE_LDSBAR 0
-#endif
-#ifndef MMPDE_NODE_EARLY_ROWS
-#define MMPDE_NODE_EARLY_ROWS 0
-#endif
-#ifndef MMPDE_NODE_PROJ2
-#define MMPDE_NODE_PROJ2 0
-#endif
-
-// Hand-off of LDS data between the waves of a workgroup: wait for this wave's
-// own LDS operations, then the barrier.  A __syncthreads would also drain the
-// wave's outstanding GLOBAL stores (its release fence waits vmcnt(0)), which
-// nothing here needs: no wave reads another's global stores in these kernels.
-__device__ __forceinline__ void lds_barrier() {
-    if (!MMPDE_NODE_LDSBAR) {
-        __syncthreads();
-    } else {
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    }
-}
-
 // The (row, part) item of prep's work index idx: a wave takes 8 rows x 8 parts,
 // lane = 8 part + row: the 8 lanes of one ds_write_b128 group write 8
 // consecutive image rows (conflict-free).
@@ -603,29 +572,10 @@ __device__ __forceinline__ void prep_fetch(const float *src, int64_t lds, int64_
     for (int q = 0; q < 4; ++q) x[q] = *(const float4 *)(sp + 4 * q);
 }
 
-// The first side block of item (row, part) of global row srow (see
-// prep_finish), loaded ahead with the row itself (unconditionally: the
-// address is clamped to a valid block); returns whether the row's tile has
-// one.
-__device__ __forceinline__ bool side_fetch(EdgeSplit split, int64_t srow, int part, float4 (&y)[4]) {
-    // 32-bit index arithmetic (node_args sets side32 when (S + k) U + S and the
-    // row count fit; 64-bit divisions here also tripped a gfx950 code-generation
-    // error, "Operand has incorrect register class")
-    const uint32_t seg_n = (uint32_t)split.seg_n, r = (uint32_t)srow;
-    const uint32_t sg = r / seg_n, q = r - sg * seg_n, t = q / 16;
-    const uint32_t S = (uint32_t)split.S, G = (uint32_t)split.units, kk = (uint32_t)split.k;
-    const uint32_t lo = max((((t * kk + 1) * G) + S - 1) / S, 1u);
-    const uint32_t hi = min(((t + 1) * kk * G + S - 1) / S - 1, G - 1);
-    const float *q4 = split.side + ((int64_t)(sg * G + min(lo, G - 1)) * 16 + (q & 15)) * 128 + 16 * part;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) y[i] = *(const float4 *)(q4 + 4 * i);
-    return lo <= hi;
-}
-
 // prep, second half: the fetched values x of item (row, part) (global row srow
 // when global) -> the image (and copy, rs), after the optional side-block sums
 // and degree division (see prep).
-template <bool F16X3, bool PRE = false>
+template <bool F16X3>
 __device__ __forceinline__ void prep_finish(float4 (&x)[4], const float *src, int64_t srow, int row, int part,
                                             float4 *img, int KT, int kofs, float *rs, float *copy, int nsum,
                                             int64_t sum_stride, const int32_t *div_deg, int div_k,
@@ -641,13 +591,12 @@ __device__ __forceinline__ void prep_finish(float4 (&x)[4], const float *src, in
     if (split && split->units > 0) {
         // side blocks of the units u of this row's segment whose first slot
         // s0(u) = floor(u S / U) lies strictly inside the row's 16-row tile
-        // t (local): t k < s0(u) < (t + 1) k; PRE: the caller has added the
-        // first of them already (side_fetch, fetched with the row)
+        // t (local): t k < s0(u) < (t + 1) k
         const int64_t sg = srow / split->seg_n, q = srow - sg * split->seg_n, t = q / 16;
         const int64_t S = split->S, G = split->units, kk = split->k;
         const int64_t lo = max(((t * kk + 1) * G + S - 1) / S, (int64_t)1);
         const int64_t hi = min(((t + 1) * kk * G + S - 1) / S - 1, G - 1);
-        for (int64_t w = PRE ? lo + 1 : lo; w <= hi; ++w) {
+        for (int64_t w = lo; w <= hi; ++w) {
             const float *q4 = split->side + ((sg * G + w) * 16 + (q & 15)) * 128 + 16 * part;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -820,45 +769,7 @@ __device__ __forceinline__ void proj_phase(const BOps<F16X3, F16X3 ? 4 : 8> &bA,
     };
     auto seg_of = [&](int rb, int lr) { return (int)(row0 + lr >= ((row0 + 16 * rb) / seg_n + 1) * seg_n); };
     gemm_tile<F16X3, RB, S1>(aA, img, 128, 0, bA, lane);
-    if (MMPDE_NODE_PROJ2 && !bBpre) {
-        // b's operands issued after a's GEMM, in flight over a's epilogue
-        BOps<F16X3, S1> bB;
-        bB.load(pk + kPkW1, 4, 8 + wave, 0, w1r, 128, lane);
-#pragma unroll
-        for (int rb = 0; rb < RB; ++rb) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int lr = 16 * rb + 4 * g + q;
-                if (full || row0 + lr < n) {
-                    float za = aA[rb][q];
-                    if (F16X3) za = za * pow2_inv(rs[lr]) * w.isa;
-                    const float va = za + node_term(lr) + w.t * rowv[lr] + w.b;
-                    ap[(16 * rb + q) * LH] = va;
-                    const int sx = seg_of(rb, lr);
-                    amx[rb][sx] = fmaxf(amx[rb][sx], fabsf(va));
-                }
-            }
-        }
-        // b's GEMM re-reads its A operands from LDS: a's operands kept in
-        // registers across a's epilogue (what the compiler would do) spill
-        asm volatile("" ::: "memory");
-        gemm_tile<F16X3, RB, S1>(aB, img, 128, 0, bB, lane);
-#pragma unroll
-        for (int rb = 0; rb < RB; ++rb) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int lr = 16 * rb + 4 * g + q;
-                if (full || row0 + lr < n) {
-                    float zb = aB[rb][q];
-                    if (F16X3) zb = zb * pow2_inv(rs[lr]) * w.isb;
-                    const float vb = zb - node_term(lr);
-                    bp[(16 * rb + q) * LH] = vb;
-                    const int sx = seg_of(rb, lr);
-                    bmx[rb][sx] = fmaxf(bmx[rb][sx], fabsf(vb));
-                }
-            }
-        }
-    } else {
+    {
         if (bBpre) {  // operands of b preloaded (the weight-stationary node kernel)
             gemm_tile<F16X3, RB, S1>(aB, img, 128, 0, *bBpre, lane);
         } else {
@@ -905,7 +816,7 @@ __device__ __forceinline__ void proj_phase(const BOps<F16X3, F16X3 ? 4 : 8> &bA,
                 red[wave][rb][3] = m3;
             }
         }
-        lds_barrier();
+        __syncthreads();
         if (wave == 0 && lane < 4 * RB) {
             const int rb = lane >> 2, e = lane & 3;
             float m = red[0][rb][e];
@@ -943,46 +854,27 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs p) {
     __shared__ float rowv[3 + MAX_TW][ROWS];    // per row: t / tmax, x / Lx, y / Ly, u_0 .. u_{tw-1}
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int r = lane & 15, g = lane >> 4;
-    const int64_t row0 = (int64_t)blockIdx.x * ROWS;
     const int col = 16 * wave + r;  // this lane's output column (tile = wave)
     const int tw = p.sc.tw > 1 ? p.sc.tw : 1;
     constexpr int S1 = F16X3 ? 4 : 8;    // K steps per 128 columns of K
     const float *wu1 = p.u1 + (int64_t)col * p.ld_u1, *wu2 = p.u2 + (int64_t)col * LH;
-    // The loads issue in the order their data is needed last: the [h | mean]
-    // rows first (HBM; one item of 16 values per thread when the tile has 256
-    // items per half, with the row's first side block), then the per-row
-    // node values, the per-column constants and update_net_1's operands.  A
-    // wave issues in order and stalls at its first use of a load, so any
-    // arithmetic on a constant placed before a load would hold that load back.
-    constexpr bool EARLY_ROWS = ROWS * 8 == 256 && MMPDE_NODE_EARLY_ROWS;
-    const bool hhalf = tid < 256;   // wave-uniform: waves 0-3 the h rows, 4-7 the mean rows
-    int irow = 0, ipart = 0;
-    float4 xr[4], ys[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) xr[q] = ys[q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    const bool side = !hhalf && p.split.units > 0 && p.side32;  // wave-uniform
-    bool has_side = false;
-    if constexpr (EARLY_ROWS) {
-        prep_item(tid & 255, irow, ipart);
-        prep_fetch(hhalf ? p.h : p.mean, LH, row0, p.n, true, irow, ipart, xr);
-        if (side) has_side = side_fetch(p.split, min(row0 + irow, p.n - 1), ipart, ys);
-    }
+    const int64_t row0 = (int64_t)blockIdx.x * ROWS;
     // everything the epilogues read from global memory is fetched up front
     // (per-row node values to LDS, per-column constants to registers), so no
     // epilogue waits on a memory round trip
-    float rv[3] = {0.0f, 0.0f, 0.0f}, ru0 = 0.0f;
     if (tid < ROWS) {
         const int64_t row = min(row0 + tid, p.n - 1);
-        rv[0] = node_t(p.sc, p.pos, row);
-        rv[1] = node_x(p.sc, p.pos, row);
-        rv[2] = node_y(p.sc, p.pos, row);
-        ru0 = p.u[row * tw];
+        rowv[0][tid] = node_t(p.sc, p.pos, row) * p.sc.inv_tmax;
+        rowv[1][tid] = node_x(p.sc, p.pos, row) * p.sc.inv_lx;
+        rowv[2][tid] = node_y(p.sc, p.pos, row) * p.sc.inv_ly;
+        for (int c = 0; c < tw; ++c) rowv[3 + c][tid] = p.u[row * tw + c];
     }
     const float u1_wt = wu1[256], u1_b = p.c1[col];
-    const float u1_sw = F16X3 ? ((const float *)(p.pk + kPkU1 + 131072))[col] : 1.0f;
+    const float u1_is = F16X3 ? pow2_inv(((const float *)(p.pk + kPkU1 + 131072))[col]) : 1.0f;
     const float u2_b = p.c2[col];
-    const float bn_rm = p.bn_rm[col], bn_rv = p.bn_rv[col], bn_w = p.bn_w[col], bn_bb = p.bn_b[col];
-    const float u2_sw = F16X3 ? ((const float *)(p.pk + kPkU2 + 65536))[col] : 1.0f;
+    BnAffine bn;
+    bn.set(p.bn_rm[col], p.bn_rv[col], p.bn_w[col], p.bn_b[col], p.eps);
+    const float u2_is = F16X3 ? pow2_inv(((const float *)(p.pk + kPkU2 + 65536))[col]) : 1.0f;
     const float *w1r = NEXT ? p.w1n + (int64_t)col * p.ld_w1n : nullptr;
     W1C w1c;
     if (NEXT) w1c.load<F16X3>(w1r, p.b1n, p.pkn, col, tw);
@@ -997,47 +889,10 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs p) {
     if (PRE) {
         bU2.load(p.pk + kPkU2, 4, wave, 0, wu2, 0, lane);
     }
-    // the arithmetic on what was loaded (EARLY_ROWS: after the rows' use, as
-    // a load completes only after every load issued before it)
-    float u1_is = 1.0f, u2_is = 1.0f;
-    BnAffine bn;
-    auto consume = [&]() {
-        if (tid < ROWS) {
-            const int64_t row = min(row0 + tid, p.n - 1);
-            rowv[0][tid] = rv[0] * p.sc.inv_tmax;
-            rowv[1][tid] = rv[1] * p.sc.inv_lx;
-            rowv[2][tid] = rv[2] * p.sc.inv_ly;
-            rowv[3][tid] = ru0;
-            for (int c = 1; c < tw; ++c) rowv[3 + c][tid] = p.u[row * tw + c];
-        }
-        u1_is = F16X3 ? pow2_inv(u1_sw) : 1.0f;
-        u2_is = F16X3 ? pow2_inv(u2_sw) : 1.0f;
-        bn.set(bn_rm, bn_rv, bn_w, bn_bb, p.eps);
-    };
-    if constexpr (!EARLY_ROWS) consume();
 
     NODE_STAMP(1);
     // ---- [h | mean] -> image (K = 256)
-    if constexpr (EARLY_ROWS) {
-        const int64_t srow = min(row0 + irow, p.n - 1);
-        if (hhalf)
-            prep_finish<F16X3>(xr, p.h, srow, irow, ipart, img, 256, 0, rs[0], hres, 1, 0, nullptr, 0, nullptr);
-        else if (side) {
-            // the row's first side block, the rest in prep_finish: the same
-            // order of additions as prep's
-            if (has_side) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    xr[q] = make_float4(xr[q].x + ys[q].x, xr[q].y + ys[q].y, xr[q].z + ys[q].z,
-                                        xr[q].w + ys[q].w);
-            }
-            prep_finish<F16X3, true>(xr, p.mean, srow, irow, ipart, img, 256, 128, rs[1], nullptr, p.parts,
-                                     p.part_stride, p.div_deg, p.div_k, &p.split);
-        }
-        else
-            prep_finish<F16X3>(xr, p.mean, srow, irow, ipart, img, 256, 128, rs[1], nullptr, p.parts,
-                               p.part_stride, p.div_deg, p.div_k, &p.split);
-    } else if constexpr (ROWS * 8 <= 256) {  // h on waves 0-3, mean on waves 4-7 at once
+    if constexpr (ROWS * 8 <= 256) {  // h on waves 0-3, mean on waves 4-7 at once
         if (tid < 256) prep<F16X3, ROWS>(p.h, LH, row0, p.n, true, img, 256, 0, rs[0], hres, 0, 256);
         else prep<F16X3, ROWS>(p.mean, LH, row0, p.n, true, img, 256, 128, rs[1], nullptr, 256, 256, p.parts,
                                p.part_stride, p.div_deg, p.div_k, &p.split);
@@ -1046,8 +901,7 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs p) {
         prep<F16X3, ROWS>(p.mean, LH, row0, p.n, true, img, 256, 128, rs[1], nullptr, -1, 512, p.parts,
                           p.part_stride, p.div_deg, p.div_k, &p.split);
     }
-    if constexpr (EARLY_ROWS) consume();
-    lds_barrier();
+    __syncthreads();
     NODE_STAMP(2);
 
     // ---- update_net_1: v = relu(U1 [h | mean | t] + c1)
@@ -1073,9 +927,9 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs p) {
         }
     }
     NODE_STAMP(3);
-    lds_barrier();
+    __syncthreads();
     prep<F16X3, ROWS>(stage, NLD, 0, ROWS, false, img, 128, 0, rs[2]);
-    lds_barrier();
+    __syncthreads();
     NODE_STAMP(4);
 
     // ---- update_net_2 + residual + BatchNorm(eval)
@@ -1108,9 +962,9 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs p) {
     }
     NODE_STAMP(5);
     if constexpr (NEXT) {
-        lds_barrier();
+        __syncthreads();
         prep<F16X3, ROWS>(stage, NLD, 0, ROWS, false, img, 128, 0, rs[3]);
-        lds_barrier();
+        __syncthreads();
         NODE_STAMP(6);
         // ---- next layer's message_net_1 node halves
         proj_phase<F16X3, RB>(bA, img, rs[3], &rowv[0][0], w1c, p.pkn, w1r, tw, row0, p.n, p.seg_n,
@@ -1204,16 +1058,16 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_embed_kernel(EmbedArgs p) {
     const float zb = e.b0[c];
     BnAffine bn1;
     bn1.set(e.bn1_rm[c], e.bn1_rv[c], e.bn1_w[c], e.bn1_b[c], e.eps);
-    lds_barrier();
+    __syncthreads();
     for (int row = tid >> 7; row < ROWS; row += 4) {
         float v = zb + zw0 * rowv[3][row];
         for (int ch = 1; ch < tw; ++ch) v += zwr[ch] * rowv[3 + ch][row];
         v = v + zw1 * rowv[1][row] + zw2 * rowv[2][row] + zw3 * rowv[0][row];
         stage[row * NLD + c] = fmaxf(bn1(v), 0.0f);
     }
-    lds_barrier();
+    __syncthreads();
     prep<F16X3, ROWS>(stage, NLD, 0, ROWS, false, img, 128, 0, rsz);
-    lds_barrier();
+    __syncthreads();
     BOps<F16X3, S1> bA, bB;
     {
         f32x4 acc[RB];
@@ -1243,9 +1097,9 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_embed_kernel(EmbedArgs p) {
             }
         }
     }
-    lds_barrier();
+    __syncthreads();
     prep<F16X3, ROWS>(stage, NLD, 0, ROWS, false, img, 128, 0, rs);
-    lds_barrier();
+    __syncthreads();
     proj_phase<F16X3, RB>(bA, img, rs, &rowv[0][0], w1c, p.pk, w1r, tw, row0, p.n, p.seg_n,
                           p.a_out, p.b_out, p.rng_out, wave, lane, NODE_EARLY_B ? &bB : nullptr);
 }
@@ -1369,11 +1223,7 @@ static int node_args(const NodeStageCall &c, NodeArgs *out) {
                p->bn_rm, p->bn_rv, p->eps, c.h_out, nullptr, nullptr, 0, c.a_out, c.b_out, c.u, c.pos, c.sc,
                c.pk, c.pkn, c.rng_out, effective_seg(c.n, c.seg_n), 1, 0, sums ? c.deg : nullptr,
                sums ? c.split->k : 0};
-    if (sums) {
-        a.split = *c.split;
-        const int64_t S = c.split->S, U = c.split->units, k = c.split->k;
-        a.side32 = (S + k) * U + S < ((int64_t)1 << 32) && c.n < ((int64_t)1 << 31);
-    }
+    if (sums) a.split = *c.split;
     if (c.next) {
         MMPDE_REQUIRE(c.a_out && c.b_out && c.next->msg1_ld >= 260 && (c.next->msg1_ld & 3) == 0 &&
                       al16(c.next->msg1_w));
