@@ -356,12 +356,71 @@ int mmpde_gnn_edge_backward_ex(const float *a, const float *b, const int32_t *nb
  * order given: deterministic). */
 int mmpde_gnn_edge_source_sum(const float *grad_edge, const int64_t *rev_off, const int64_t *rev_edge,
                               int64_t n, float *grad_b, mmpde_stream_t stream);
+/* The backward with grad_edge in source-major order: the row of slot q is
+ * slot_pos[q] (mmpde_reverse_adjacency's slot_pos, a permutation of 0 ..
+ * n*k-1), so that dL/db is the contiguous segmented sum
+ * mmpde_gnn_edge_source_sum_sorted over rev_off: the same sums in the same
+ * order as mmpde_gnn_edge_backward_ex + mmpde_gnn_edge_source_sum, read as a
+ * stream instead of a gather.  n * k < 2^31. */
+int mmpde_gnn_edge_backward_sorted(const float *a, const float *b, const int32_t *nbr, const int32_t *deg,
+                                   int64_t n, int k, const float *msg2_w, const float *msg2_b,
+                                   const float *grad_mean, const int32_t *slot_pos, float *grad_a,
+                                   float *grad_edge, float *partials, float *grad_w2, float *grad_b2,
+                                   int edge_gemm, mmpde_stream_t stream);
+int mmpde_gnn_edge_source_sum_sorted(const float *grad_edge, const int64_t *rev_off, int64_t n, float *grad_b,
+                                     mmpde_stream_t stream);
 /* The same segmented sum for rows of any width: out[j, :] = sum over q in
  * [rev_off[j], rev_off[j+1]) of rows[rev_edge[q], :] (n output rows), in list
  * order.  The deterministic backward of a row gather (the kNN-30 neighbour
  * values of the training-mode interpolation, data_creator_2d.py:77-83). */
 int mmpde_segment_sum(const float *rows, int64_t width, const int64_t *rev_off, const int64_t *rev_edge,
                       int64_t n, float *out, mmpde_stream_t stream);
+/* The reverse adjacency those two take, built on the device: rev_edge [n_tgt *
+ * k capacity] = the live slot ids q = i*k + e (e < deg[i] when deg is given)
+ * grouped by source j = nbr[i, e], ascending q within a source; rev_off
+ * [n_src + 1] the group offsets (rev_off[n_src] = live slots).  Sources
+ * outside [0, n_src) are skipped and counted in *bad (device int32, zeroed
+ * first).  slot_pos (nullable) [n_tgt * k]: the inverse permutation, the
+ * position of slot q in the sorted order (dead slots after rev_off[n_src]).  Deterministic (a stable radix sort by source).  scratch:
+ * mmpde_reverse_adjacency_scratch_bytes(n_tgt, k, n_src), 256-byte aligned. */
+int64_t mmpde_reverse_adjacency_scratch_bytes(int64_t n_tgt, int k, int64_t n_src);
+int mmpde_reverse_adjacency(const int32_t *nbr, int64_t n_tgt, int k, const int32_t *deg, int64_t n_src,
+                            int64_t *rev_off, int64_t *rev_edge, int32_t *slot_pos, void *scratch,
+                            int64_t scratch_bytes, int32_t *bad, mmpde_stream_t stream);
+
+/* Weight / bias gradient of a skinny linear map over many rows (the training
+ * backward of the Conv1d head as unfold + GEMM, gnn_2d.py:108-114, and of the
+ * embedding's first Linear, gnn_2d.py:99-106; train_helper_2d.py:126):
+ * dw [n_out, k] = dy^T x, db [n_out] = sum over rows of dy (nullable; k = 0
+ * computes db alone).  x [rows, k] (row stride ldx), dy [rows, n_out] (row
+ * stride ldy); k <= 64, n_out <= 128, k * n_out + n_out <= 1280.  Fixed
+ * summation order: deterministic.  workspace: ..._workspace_bytes. */
+int64_t mmpde_rows_grad_weight_workspace_bytes(int64_t rows, int k, int n_out);
+int mmpde_rows_grad_weight(const float *x, int64_t ldx, int64_t rows, int k, const float *dy, int64_t ldy,
+                           int n_out, float *dw, float *db, float *workspace, int64_t workspace_bytes,
+                           mmpde_stream_t stream);
+
+/* BatchNorm1d in training mode over rows [n, C] of x + res (res nullable; the
+ * residual add of GNN_Layer_FS_2D, norm(h + update), gnn_2d.py:69; the
+ * embedding's BatchNorm1d, gnn_2d.py:101,105): batch mean and biased variance
+ * (Welford per thread, Chan merges in a fixed order), y = (x + res - mean) /
+ * sqrt(var + eps) * weight + bias (weight / bias nullable), running_mean /
+ * running_var (nullable) <- factor * (mean, unbiased var) + (1 - factor) * old.
+ * stats [4 C] receives mean, invstd and the per-channel affine (kept for the
+ * backward).  C % 4 == 0, C <= 1024; 16-byte aligned pointers.  workspace:
+ * mmpde_batch_norm_rows_workspace_bytes(n, C) (+ 3 C floats for the backward). */
+int64_t mmpde_batch_norm_rows_workspace_bytes(int64_t n, int C);
+int mmpde_batch_norm_rows_train(const float *x, const float *res, int64_t n, int C, const float *weight,
+                                const float *bias, float eps, float factor, float *running_mean,
+                                float *running_var, float *y, float *stats, float *workspace,
+                                int64_t workspace_bytes, mmpde_stream_t stream);
+/* Its backward: dx = w invstd (dy - mean(dy) - xhat mean(dy xhat)) (the input
+ * gradient of x and of res alike), dweight = sum dy xhat, dbias = sum dy
+ * (both nullable), from the forward's stats. */
+int mmpde_batch_norm_rows_backward(const float *x, const float *res, const float *dy, int64_t n, int C,
+                                   const float *weight, const float *stats, float *dx, float *dweight,
+                                   float *dbias, float *workspace, int64_t workspace_bytes,
+                                   mmpde_stream_t stream);
 
 /* out[n] = out_scale * output_mlp(h[:, None]) */
 int mmpde_gnn_head(const float *h, int64_t n, const mmpde_gnn_head_params *p, float *out,

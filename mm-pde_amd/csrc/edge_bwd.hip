@@ -40,8 +40,9 @@ struct EdgeBwdArgs {
     const float *w2, *b2;  // message_net_2.0 weight [128 out][128 in], bias
     const float *gmean;    // [n, 128]
     float *ga;             // [n, 128]
-    float *gz1;            // [n * k, 128] per edge (target-major, as nbr)
+    float *gz1;            // [n * k, 128] per edge (row q = i k + e, or pos[q])
     float *pw2, *pb2;      // [grid][128][128], [grid][128] partials
+    const int32_t *pos;    // nullable: the gz1 row of slot q (source-major order)
 };
 
 __global__ __launch_bounds__(256, 1) void edge_bwd_kernel(EdgeBwdArgs p) {
@@ -150,7 +151,10 @@ __global__ __launch_bounds__(256, 1) void edge_bwd_kernel(EdgeBwdArgs p) {
                     const int rr = 4 * g + t;
                     const float v = z1s[rr * BWS + kk] > 0.0f ? acc[t] : 0.0f;
                     gacc[ci][t] += v;
-                    if (row0 + rr < p.n) p.gz1[((row0 + rr) * k + e) * BH + kk] = v;
+                    if (row0 + rr < p.n) {
+                        const int64_t q = (row0 + rr) * k + e;
+                        p.gz1[(p.pos ? (int64_t)p.pos[q] : q) * BH + kk] = v;
+                    }
                 }
             }
             // dW2[c][kk] += sum_rows gz2[row][c] relu(z1)[row][kk]  (K = the 16 rows)
@@ -234,6 +238,7 @@ struct EdgeBwdF16Args {
     const float *b2, *gmean;
     const unsigned *mx;       // max|a|, max|b|, max|g| (float bits)
     float *ga, *gz1, *pw2, *pb2;
+    const int32_t *pos;       // nullable: the gz1 row of slot q (source-major order)
 };
 
 __device__ __forceinline__ void split1(float x, _Float16 &h, _Float16 &l) {
@@ -246,9 +251,14 @@ __device__ __forceinline__ void split1(float x, _Float16 &h, _Float16 &l) {
 // bound of one 512-thread workgroup and the size check.
 constexpr size_t kEdgeBwdF16Lds = sizeof(float) * 2 * FT * FAW + sizeof(_Float16) * 2 * 2 * FT * FAS +
                                   sizeof(_Float16) * 2 * 2 * BH * FCS + sizeof(_Float16) * 2 * FT * FAS +
-                                  sizeof(_Float16) * 2 * BH * FCS + 2 * BH * (FT / 8) + sizeof(int) * FT * FKMAX +
+                                  sizeof(_Float16) * 2 * BH * FCS + 2 * BH * (FT / 8) + 2 * sizeof(int) * FT * FKMAX +
                                   sizeof(int) * FT;
 static_assert(kEdgeBwdF16Lds <= 160 * 1024, "edge_bwd_f16_kernel: LDS beyond gfx950's 160 KiB per CU");
+
+#ifndef MMPDE_BWD_P1_FIRST
+#define MMPDE_BWD_P1_FIRST 1
+#endif
+constexpr bool kBwdP1First = MMPDE_BWD_P1_FIRST != 0;
 
 __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) {
     __shared__ float at[FT * FAW];             // a rows of the tile
@@ -261,6 +271,7 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
     __shared__ _Float16 gt[2][BH * FCS];       // the same, [c][edge]
     __shared__ uint8_t zm[2][BH * (FT / 8)];   // z1 > 0, [kk][edge / 8] bits
     __shared__ int nb[FT * FKMAX];             // the tile's neighbour rows (clamped)
+    __shared__ int gzr[FT * FKMAX];            // the gz1 rows of the tile's slots
     __shared__ int dg[FT];                     // degrees (0 past n)
     const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int r = lane & 15, g = lane >> 4;
@@ -303,8 +314,10 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
         }
         for (int i = tid; i < FT * k; i += 512) {
             const int rr = i / k, e = i - rr * k;
-            const int s = p.nbr[min(row0 + rr, nmax) * k + e];
+            const int64_t q = min(row0 + rr, nmax) * k + e;
+            const int s = p.nbr[q];
             nb[rr * FKMAX + e] = (s < 0 || s > nmax) ? 0 : s;  // padded / malformed: masked by e < deg
+            gzr[rr * FKMAX + e] = p.pos ? p.pos[q] : (int)q;
         }
         if (tid < FT) dg[tid] = row0 + tid < p.n ? (p.deg ? p.deg[row0 + tid] : k) : 0;
         __syncthreads();
@@ -312,107 +325,127 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
 #pragma unroll
         for (int t = 0; t < 8; ++t) bv[t] = p.b[(int64_t)nb[(8 * eg + t) * FKMAX] * BH + kk1];
         f32x4 gacc[2] = {(f32x4){0.0f, 0.0f, 0.0f, 0.0f}, (f32x4){0.0f, 0.0f, 0.0f, 0.0f}};
-        for (int e = 0; e < k; ++e) {
+        // ---- P1 of slot e into buffer e & 1; issues the b loads of slot e + 1
+        // (clamped at the last slot: a harmless reload)
+        auto p1 = [&](int e) {
             const int sb = e & 1;
-            // ---- P1
-            {
-                half8 hi, lo;
-                unsigned bits = 0;
+            half8 hi, lo;
+            unsigned bits = 0;
 #pragma unroll
-                for (int t = 0; t < 8; ++t) {
-                    const int ed = 8 * eg + t;
-                    const float z = at[ed * FAW + kk1] + bv[t];
-                    bits |= (z > 0.0f ? 1u : 0u) << t;
-                    _Float16 h, l;
-                    split1(fmaxf(z, 0.0f) * sz, h, l);
-                    hi[t] = h;
-                    lo[t] = l;
-                    za[sb][0][ed * FAS + kk1] = h;
-                    za[sb][1][ed * FAS + kk1] = l;
-                }
-                *(half8 *)&zb[sb][0][kk1 * FCS + 8 * eg] = hi;
-                *(half8 *)&zb[sb][1][kk1 * FCS + 8 * eg] = lo;
-                zm[sb][kk1 * 4 + eg] = (uint8_t)bits;
-                if (e + 1 < k) {  // next slot's b values, in flight during P2 / P3
-#pragma unroll
-                    for (int t = 0; t < 8; ++t)
-                        bv[t] = p.b[(int64_t)nb[(8 * eg + t) * FKMAX + e + 1] * BH + kk1];
-                }
+            for (int t = 0; t < 8; ++t) {
+                const int ed = 8 * eg + t;
+                const float z = at[ed * FAW + kk1] + bv[t];
+                bits |= (z > 0.0f ? 1u : 0u) << t;
+                _Float16 h, l;
+                split1(fmaxf(z, 0.0f) * sz, h, l);
+                hi[t] = h;
+                lo[t] = l;
+                za[sb][0][ed * FAS + kk1] = h;
+                za[sb][1][ed * FAS + kk1] = l;
             }
-            __syncthreads();
-            // ---- P2: z2 and gz2 (column c = col)
-            {
-                f32x4 acc[2] = {(f32x4){0.0f, 0.0f, 0.0f, 0.0f}, (f32x4){0.0f, 0.0f, 0.0f, 0.0f}};
+            *(half8 *)&zb[sb][0][kk1 * FCS + 8 * eg] = hi;
+            *(half8 *)&zb[sb][1][kk1 * FCS + 8 * eg] = lo;
+            zm[sb][kk1 * 4 + eg] = (uint8_t)bits;
+            const int en = min(e + 1, k - 1);
 #pragma unroll
-                for (int s = 0; s < 4; ++s) {
+            for (int t = 0; t < 8; ++t) bv[t] = p.b[(int64_t)nb[(8 * eg + t) * FKMAX + en] * BH + kk1];
+        };
+        // ---- P2: z2 and gz2 (column c = col) of slot e
+        auto p2 = [&](int e) {
+            const int sb = e & 1;
+            f32x4 acc[2] = {(f32x4){0.0f, 0.0f, 0.0f, 0.0f}, (f32x4){0.0f, 0.0f, 0.0f, 0.0f}};
 #pragma unroll
-                    for (int rb = 0; rb < 2; ++rb) {
-                        const half8 ah = *(const half8 *)&za[sb][0][(16 * rb + r) * FAS + 32 * s + 8 * g];
-                        const half8 al = *(const half8 *)&za[sb][1][(16 * rb + r) * FAS + 32 * s + 8 * g];
-                        acc[rb] = mfma_f16(ah, w1h[s], acc[rb]);
-                        acc[rb] = mfma_f16(ah, w1l[s], acc[rb]);
-                        acc[rb] = mfma_f16(al, w1h[s], acc[rb]);
-                    }
-                }
+            for (int s = 0; s < 4; ++s) {
 #pragma unroll
                 for (int rb = 0; rb < 2; ++rb) {
-                    _Float16 hv[4], lv[4];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const int rr = 16 * rb + 4 * g + q;
-                        const bool on = e < dg[rr] && acc[rb][q] * un1 + bias > 0.0f;
-                        const float v = on ? gms[rr * FAW + col] : 0.0f;
-                        db += v;
-                        split1(v * sg, hv[q], lv[q]);
-                        gr[0][rr * FAS + col] = hv[q];
-                        gr[1][rr * FAS + col] = lv[q];
-                    }
-                    typedef _Float16 half4 __attribute__((ext_vector_type(4)));
-                    *(half4 *)&gt[0][col * FCS + 16 * rb + 4 * g] = (half4){hv[0], hv[1], hv[2], hv[3]};
-                    *(half4 *)&gt[1][col * FCS + 16 * rb + 4 * g] = (half4){lv[0], lv[1], lv[2], lv[3]};
+                    const half8 ah = *(const half8 *)&za[sb][0][(16 * rb + r) * FAS + 32 * s + 8 * g];
+                    const half8 al = *(const half8 *)&za[sb][1][(16 * rb + r) * FAS + 32 * s + 8 * g];
+                    acc[rb] = mfma_f16(ah, w1h[s], acc[rb]);
+                    acc[rb] = mfma_f16(ah, w1l[s], acc[rb]);
+                    acc[rb] = mfma_f16(al, w1h[s], acc[rb]);
                 }
             }
-            __syncthreads();
-            // ---- P3: gm1 -> gz1 (column kk = col); dW2 rows 16 wave ..
-            {
-                f32x4 acc[2] = {(f32x4){0.0f, 0.0f, 0.0f, 0.0f}, (f32x4){0.0f, 0.0f, 0.0f, 0.0f}};
 #pragma unroll
-                for (int s = 0; s < 4; ++s) {
+            for (int rb = 0; rb < 2; ++rb) {
+                _Float16 hv[4], lv[4];
 #pragma unroll
-                    for (int rb = 0; rb < 2; ++rb) {
-                        const half8 ah = *(const half8 *)&gr[0][(16 * rb + r) * FAS + 32 * s + 8 * g];
-                        const half8 al = *(const half8 *)&gr[1][(16 * rb + r) * FAS + 32 * s + 8 * g];
-                        acc[rb] = mfma_f16(ah, w2h[s], acc[rb]);
-                        acc[rb] = mfma_f16(ah, w2l[s], acc[rb]);
-                        acc[rb] = mfma_f16(al, w2h[s], acc[rb]);
-                    }
+                for (int q = 0; q < 4; ++q) {
+                    const int rr = 16 * rb + 4 * g + q;
+                    const bool on = e < dg[rr] && acc[rb][q] * un1 + bias > 0.0f;
+                    const float v = on ? gms[rr * FAW + col] : 0.0f;
+                    db += v;
+                    split1(v * sg, hv[q], lv[q]);
+                    gr[0][rr * FAS + col] = hv[q];
+                    gr[1][rr * FAS + col] = lv[q];
                 }
-                const half8 gh = *(const half8 *)&gt[0][col * FCS + 8 * g];
-                const half8 gl = *(const half8 *)&gt[1][col * FCS + 8 * g];
+                typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+                *(half4 *)&gt[0][col * FCS + 16 * rb + 4 * g] = (half4){hv[0], hv[1], hv[2], hv[3]};
+                *(half4 *)&gt[1][col * FCS + 16 * rb + 4 * g] = (half4){lv[0], lv[1], lv[2], lv[3]};
+            }
+        };
+        // ---- P3 of slot e: gm1 -> gz1 (column kk = col); dW2 rows 16 wave ..
+        // With `next`, P1 of slot e + 1 (the other buffer) goes in front of
+        // P3's MFMAs in the same straight-line block (its b prefetch is
+        // clamped, not branched), so that the scheduler can issue its LDS
+        // writes and VALU work in the MFMAs' shadow.
+        auto p3 = [&](int e, bool next) {
+            const int sb = e & 1;
+            if (next) p1(e + 1);
+            f32x4 acc[2] = {(f32x4){0.0f, 0.0f, 0.0f, 0.0f}, (f32x4){0.0f, 0.0f, 0.0f, 0.0f}};
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const half8 bh = *(const half8 *)&zb[sb][0][(16 * j + r) * FCS + 8 * g];
-                    const half8 bl = *(const half8 *)&zb[sb][1][(16 * j + r) * FCS + 8 * g];
-                    dw[j] = mfma_f16(gh, bh, dw[j]);
-                    dw[j] = mfma_f16(gh, bl, dw[j]);
-                    dw[j] = mfma_f16(gl, bh, dw[j]);
-                }
+            for (int s = 0; s < 4; ++s) {
 #pragma unroll
                 for (int rb = 0; rb < 2; ++rb) {
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const int rr = 16 * rb + 4 * g + q;
-                        const bool pos = (zm[sb][col * 4 + (rr >> 3)] >> (rr & 7)) & 1u;
-                        const float v = pos ? acc[rb][q] * un2 : 0.0f;
-                        gacc[rb][q] += v;
-                        if (row0 + rr < p.n) p.gz1[((row0 + rr) * k + e) * BH + col] = v;
-                    }
+                    const half8 ah = *(const half8 *)&gr[0][(16 * rb + r) * FAS + 32 * s + 8 * g];
+                    const half8 al = *(const half8 *)&gr[1][(16 * rb + r) * FAS + 32 * s + 8 * g];
+                    acc[rb] = mfma_f16(ah, w2h[s], acc[rb]);
+                    acc[rb] = mfma_f16(ah, w2l[s], acc[rb]);
+                    acc[rb] = mfma_f16(al, w2h[s], acc[rb]);
                 }
             }
-            // no barrier here: P1 of the next slot writes the other za / zb / zm
-            // buffer, and its P2 (gr / gt) starts only after the next P1
-            // barrier, which every wave reaches after this P3
+            const half8 gh = *(const half8 *)&gt[0][col * FCS + 8 * g];
+            const half8 gl = *(const half8 *)&gt[1][col * FCS + 8 * g];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const half8 bh = *(const half8 *)&zb[sb][0][(16 * j + r) * FCS + 8 * g];
+                const half8 bl = *(const half8 *)&zb[sb][1][(16 * j + r) * FCS + 8 * g];
+                dw[j] = mfma_f16(gh, bh, dw[j]);
+                dw[j] = mfma_f16(gh, bl, dw[j]);
+                dw[j] = mfma_f16(gl, bh, dw[j]);
+            }
+#pragma unroll
+            for (int rb = 0; rb < 2; ++rb) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int rr = 16 * rb + 4 * g + q;
+                    const bool pos = (zm[sb][col * 4 + (rr >> 3)] >> (rr & 7)) & 1u;
+                    const float v = pos ? acc[rb][q] * un2 : 0.0f;
+                    gacc[rb][q] += v;
+                    if (row0 + rr < p.n) p.gz1[(int64_t)gzr[rr * FKMAX + e] * BH + col] = v;
+                }
+            }
+        };
+        // Per slot: P2(e) | barrier | P3(e) + P1(e + 1) | barrier.  Buffers:
+        // P1(e + 1) writes za / zb / zm[(e + 1) & 1], last read by P2(e - 1)
+        // and P3(e - 1), both before the previous barrier; P2(e + 1) reads
+        // them after the barrier that ends P1(e + 1), and rewrites gr / gt
+        // only after every wave's P3(e) (the same barrier).
+        p1(0);
+        __syncthreads();
+        for (int e = 0; e + 1 < k; ++e) {
+            p2(e);
+            __syncthreads();
+            if (kBwdP1First) {
+                p3(e, true);
+            } else {
+                p3(e, false);
+                p1(e + 1);
+            }
+            __syncthreads();
         }
+        p2(k - 1);
+        __syncthreads();
+        p3(k - 1, false);
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb) {
 #pragma unroll
@@ -507,6 +540,36 @@ __global__ __launch_bounds__(256) void edge_source_sum_kernel(const float *__res
     ((float2 *)(out + j * BH))[lane] = acc;
 }
 
+// out[j] = sum_{p in [off[j], off[j+1])} rows[p]: the rows of source j stored
+// contiguously (mmpde_gnn_edge_backward_sorted); one wave per source, two
+// columns per lane, eight rows in flight, added in list order.
+__global__ __launch_bounds__(256) void edge_source_sum_sorted_kernel(const float *__restrict__ rows,
+                                                                     const int64_t *__restrict__ off, int64_t n,
+                                                                     float *__restrict__ out) {
+    const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (j >= n) return;
+    float2 acc = make_float2(0.0f, 0.0f);
+    int64_t q = off[j];
+    const int64_t qe = off[j + 1];
+    for (; q + 8 <= qe; q += 8) {
+        float2 v[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v[t] = ((const float2 *)(rows + (q + t) * BH))[lane];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            acc.x += v[t].x;
+            acc.y += v[t].y;
+        }
+    }
+    for (; q < qe; ++q) {
+        const float2 v = ((const float2 *)(rows + q * BH))[lane];
+        acc.x += v.x;
+        acc.y += v.y;
+    }
+    ((float2 *)(out + j * BH))[lane] = acc;
+}
+
 // out[j][c] = sum_{p in [off[j], off[j+1])} rows[edge[p]][c] for any row width:
 // one thread per (j, c), in list order.
 __global__ __launch_bounds__(256) void segment_sum_kernel(const float *__restrict__ rows, int64_t width,
@@ -555,11 +618,10 @@ extern "C" int64_t mmpde_gnn_edge_backward_partials(int *grid) {
     return (int64_t)(cus > 0 ? cus : 256) * (BH * BH + BH) + kBwdExtra;
 }
 
-extern "C" int mmpde_gnn_edge_backward(const float *a, const float *b, const int32_t *nbr, const int32_t *deg,
-                                       int64_t n, int k, const float *msg2_w, const float *msg2_b,
-                                       const float *grad_mean, float *grad_a, float *grad_edge,
-                                       float *partials, float *grad_w2, float *grad_b2,
-                                       mmpde_stream_t stream) {
+static int edge_backward_f32(const float *a, const float *b, const int32_t *nbr, const int32_t *deg, int64_t n,
+                             int k, const float *msg2_w, const float *msg2_b, const float *grad_mean,
+                             const int32_t *pos, float *grad_a, float *grad_edge, float *partials, float *grad_w2,
+                             float *grad_b2, mmpde_stream_t stream) {
     MMPDE_REQUIRE(a && b && nbr && msg2_w && msg2_b && grad_mean && grad_a && grad_edge && partials);
     MMPDE_REQUIRE(grad_w2 && grad_b2 && n > 0 && k > 0 && n <= (int64_t)INT32_MAX);
     MMPDE_REQUIRE((((uintptr_t)a | (uintptr_t)b | (uintptr_t)msg2_w | (uintptr_t)grad_mean) & 15) == 0);
@@ -569,7 +631,7 @@ extern "C" int mmpde_gnn_edge_backward(const float *a, const float *b, const int
     MMPDE_REQUIRE(ntiles < (int64_t)INT32_MAX);
     if (grid > ntiles) grid = (int)ntiles;
     float *pw2 = partials, *pb2 = partials + (int64_t)grid * BH * BH;
-    EdgeBwdArgs p{a, b, nbr, deg, n, k, (int)ntiles, msg2_w, msg2_b, grad_mean, grad_a, grad_edge, pw2, pb2};
+    EdgeBwdArgs p{a, b, nbr, deg, n, k, (int)ntiles, msg2_w, msg2_b, grad_mean, grad_a, grad_edge, pw2, pb2, pos};
     hipStream_t st = as_stream(stream);
     hipLaunchKernelGGL(edge_bwd_kernel, dim3(grid), dim3(256), 0, st, p);
     MMPDE_RET_LAUNCH();
@@ -580,15 +642,14 @@ extern "C" int mmpde_gnn_edge_backward(const float *a, const float *b, const int
     return MMPDE_OK;
 }
 
-extern "C" int mmpde_gnn_edge_backward_ex(const float *a, const float *b, const int32_t *nbr, const int32_t *deg,
-                                          int64_t n, int k, const float *msg2_w, const float *msg2_b,
-                                          const float *grad_mean, float *grad_a, float *grad_edge,
-                                          float *partials, float *grad_w2, float *grad_b2, int edge_gemm,
-                                          mmpde_stream_t stream) {
+static int edge_backward(const float *a, const float *b, const int32_t *nbr, const int32_t *deg, int64_t n, int k,
+                         const float *msg2_w, const float *msg2_b, const float *grad_mean, const int32_t *pos,
+                         float *grad_a, float *grad_edge, float *partials, float *grad_w2, float *grad_b2,
+                         int edge_gemm, mmpde_stream_t stream) {
     MMPDE_REQUIRE(edge_gemm == MMPDE_EDGE_GEMM_F32 || edge_gemm == MMPDE_EDGE_GEMM_F16X3);
     if (edge_gemm == MMPDE_EDGE_GEMM_F32 || k > FKMAX)
-        return mmpde_gnn_edge_backward(a, b, nbr, deg, n, k, msg2_w, msg2_b, grad_mean, grad_a, grad_edge,
-                                       partials, grad_w2, grad_b2, stream);
+        return edge_backward_f32(a, b, nbr, deg, n, k, msg2_w, msg2_b, grad_mean, pos, grad_a, grad_edge, partials,
+                                 grad_w2, grad_b2, stream);
     MMPDE_REQUIRE(a && b && nbr && msg2_w && msg2_b && grad_mean && grad_a && grad_edge && partials);
     MMPDE_REQUIRE(grad_w2 && grad_b2 && n > 0 && k > 0 && n <= (int64_t)INT32_MAX);
     MMPDE_REQUIRE((((uintptr_t)a | (uintptr_t)b | (uintptr_t)msg2_w | (uintptr_t)grad_mean |
@@ -596,7 +657,7 @@ extern "C" int mmpde_gnn_edge_backward_ex(const float *a, const float *b, const 
     int grid = 256;
     mmpde_gnn_edge_backward_partials(&grid);
     const int64_t ntiles = (n + FT - 1) / FT;
-    MMPDE_REQUIRE(ntiles < (int64_t)INT32_MAX && n * 32 < (int64_t)INT32_MAX * 256LL);
+    MMPDE_REQUIRE(ntiles < (int64_t)INT32_MAX && n * k < (int64_t)INT32_MAX);
     const int G = grid;
     if (grid > ntiles) grid = (int)ntiles;
     float *pw2 = partials, *pb2 = partials + (int64_t)G * BH * BH;
@@ -622,12 +683,49 @@ extern "C" int mmpde_gnn_edge_backward_ex(const float *a, const float *b, const 
     hipLaunchKernelGGL(maxabs3_final_kernel, dim3(3), dim3(256), 0, st, mpart, mg, mx);
     MMPDE_RET_LAUNCH();
     EdgeBwdF16Args p{a, b, nbr, deg, n, k, (int)ntiles, img1, img2, msg2_b, grad_mean, mx, grad_a, grad_edge,
-                     pw2, pb2};
+                     pw2, pb2, pos};
     hipLaunchKernelGGL(edge_bwd_f16_kernel, dim3(grid), dim3(512), 0, st, p);
     MMPDE_RET_LAUNCH();
     hipLaunchKernelGGL(partial_sum_kernel, dim3(ceil_div(BH * BH, 256)), dim3(256), 0, st, pw2, grid,
                        (int64_t)BH * BH, grad_w2);
     hipLaunchKernelGGL(partial_sum_kernel, dim3(1), dim3(256), 0, st, pb2, grid, (int64_t)BH, grad_b2);
+    MMPDE_RET_LAUNCH();
+    return MMPDE_OK;
+}
+
+extern "C" int mmpde_gnn_edge_backward(const float *a, const float *b, const int32_t *nbr, const int32_t *deg,
+                                       int64_t n, int k, const float *msg2_w, const float *msg2_b,
+                                       const float *grad_mean, float *grad_a, float *grad_edge,
+                                       float *partials, float *grad_w2, float *grad_b2,
+                                       mmpde_stream_t stream) {
+    return edge_backward_f32(a, b, nbr, deg, n, k, msg2_w, msg2_b, grad_mean, nullptr, grad_a, grad_edge, partials,
+                             grad_w2, grad_b2, stream);
+}
+
+extern "C" int mmpde_gnn_edge_backward_ex(const float *a, const float *b, const int32_t *nbr, const int32_t *deg,
+                                          int64_t n, int k, const float *msg2_w, const float *msg2_b,
+                                          const float *grad_mean, float *grad_a, float *grad_edge,
+                                          float *partials, float *grad_w2, float *grad_b2, int edge_gemm,
+                                          mmpde_stream_t stream) {
+    return edge_backward(a, b, nbr, deg, n, k, msg2_w, msg2_b, grad_mean, nullptr, grad_a, grad_edge, partials,
+                         grad_w2, grad_b2, edge_gemm, stream);
+}
+
+extern "C" int mmpde_gnn_edge_backward_sorted(const float *a, const float *b, const int32_t *nbr,
+                                              const int32_t *deg, int64_t n, int k, const float *msg2_w,
+                                              const float *msg2_b, const float *grad_mean, const int32_t *slot_pos,
+                                              float *grad_a, float *grad_edge, float *partials, float *grad_w2,
+                                              float *grad_b2, int edge_gemm, mmpde_stream_t stream) {
+    MMPDE_REQUIRE(slot_pos);
+    return edge_backward(a, b, nbr, deg, n, k, msg2_w, msg2_b, grad_mean, slot_pos, grad_a, grad_edge, partials,
+                         grad_w2, grad_b2, edge_gemm, stream);
+}
+
+extern "C" int mmpde_gnn_edge_source_sum_sorted(const float *grad_edge, const int64_t *rev_off, int64_t n,
+                                                float *grad_b, mmpde_stream_t stream) {
+    MMPDE_REQUIRE(grad_edge && rev_off && grad_b && n > 0);
+    hipLaunchKernelGGL(edge_source_sum_sorted_kernel, dim3((unsigned)ceil_div(n, 4)), dim3(256), 0,
+                       as_stream(stream), grad_edge, rev_off, n, grad_b);
     MMPDE_RET_LAUNCH();
     return MMPDE_OK;
 }

@@ -13,7 +13,7 @@ import os
 import torch
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libmmpde_hip.so")
-ABI_VERSION = 11600
+ABI_VERSION = 11700
 
 ACT_NONE, ACT_TANH, ACT_RELU, ACT_ELU = 0, 1, 2, 3
 PAD_ZEROS, PAD_CIRCULAR = 0, 1
@@ -115,6 +115,16 @@ _SIGS = {
     "mmpde_resample_bilinear": (_I, [_P, _I64, _I, _I, _I, _I, _P, _P]),
     "mmpde_conv2d_ex": (_I, [_P, _I64, _I, _I, _I, _P, _P, _I, _I, _I, _I, _I, _P, _I, _I, _P, _P]),
     "mmpde_conv2d_grad_weight": (_I, [_P, _I64, _I, _I, _I, _P, _I, _I, _I, _I, _P, _P, _P]),
+    "mmpde_rows_grad_weight_workspace_bytes": (_I64, [_I64, _I, _I]),
+    "mmpde_reverse_adjacency_scratch_bytes": (_I64, [_I64, _I, _I64]),
+    "mmpde_reverse_adjacency": (_I, [_P, _I64, _I, _P, _I64, _P, _P, _P, _P, _I64, _P, _P]),
+    "mmpde_gnn_edge_backward_sorted": (_I, [_P, _P, _P, _P, _I64, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I,
+                                           _P]),
+    "mmpde_gnn_edge_source_sum_sorted": (_I, [_P, _P, _I64, _P, _P]),
+    "mmpde_rows_grad_weight": (_I, [_P, _I64, _I64, _I, _P, _I64, _I, _P, _P, _P, _I64, _P]),
+    "mmpde_batch_norm_rows_workspace_bytes": (_I64, [_I64, _I]),
+    "mmpde_batch_norm_rows_train": (_I, [_P, _P, _I64, _I, _P, _P, _F, _F, _P, _P, _P, _P, _P, _I64, _P]),
+    "mmpde_batch_norm_rows_backward": (_I, [_P, _P, _P, _I64, _I, _P, _P, _P, _P, _P, _P, _I64, _P]),
     "mmpde_gnn_workspace_bytes": (_I64, [_I64]),
     "mmpde_gnn_embed": (_I, [_P, _P, _I64, GnnScales, _P, _P, _P, _P]),
     "mmpde_gnn_layer": (_I, [_P, _P, _P, _I64, _I, _P, GnnScales, _P, _P, _P, _P]),

@@ -10,11 +10,15 @@ running statistics), fp32 throughout.  There is no CPU / eager fallback.
 In ``train()`` mode (train_helper_2d.py:107-128) the forward is differentiable:
 the edge stage -- message_net_2 over every in-edge and the mean
 (gnn_2d.py:59-63, aggr='mean') -- runs as the ``EdgeMean`` autograd.Function on
-HIP kernels (mmpde_gnn_edge_mean_deg forward, mmpde_gnn_edge_backward +
-mmpde_gnn_edge_source_sum backward: no per-edge activation is stored); the
-per-node work (message_net_1 factored into its target and source halves,
-update MLPs, BatchNorm with batch statistics, embedding, Conv1d head) runs as
-device torch ops under autograd.
+HIP kernels (mmpde_gnn_edge_mean_ex forward, mmpde_gnn_edge_backward_sorted
++ mmpde_gnn_edge_source_sum_sorted backward: no per-edge activation is
+stored); the
+per-node work runs as autograd Functions over HIP kernels and library GEMMs:
+message_net_1 factored into its target and source halves and the update MLPs
+as ops.LinearRows (row-chunked weight gradients), every BatchNorm1d -- with the
+layer's residual add fused in -- as ops.BatchNormRows
+(mmpde_batch_norm_rows_train / _backward), the Conv1d head as unfold +
+LinearRows (skinny weight gradients on mmpde_rows_grad_weight).
 """
 from __future__ import annotations
 
@@ -25,7 +29,7 @@ import torch
 from torch import nn
 
 from . import _lib as L
-from .ops import LinearRows, linear_train, nbr_table_from_edge_index, reverse_adjacency
+from .ops import LinearRows, batch_norm_rows, linear_train, nbr_table_from_edge_index, reverse_adjacency
 
 
 class BatchNorm(nn.Module):
@@ -40,6 +44,10 @@ class BatchNorm(nn.Module):
 
     def forward(self, x):
         return self.module(x)
+
+    def forward_res(self, x, res):
+        """module(x + res), the add fused into the HIP BatchNorm in train mode."""
+        return batch_norm_rows(self.module, x, res)
 
 
 class EdgeGraph:
@@ -62,7 +70,10 @@ class EdgeGraph:
 
     def reverse(self):
         if self._rev is None:
-            self._rev = reverse_adjacency(self.nbr, self.deg)
+            # tables from the engine's kNN / radius kernels or from
+            # nbr_table_from_edge_index (range-checked there); with the slot
+            # positions of the source-major backward
+            self._rev = reverse_adjacency(self.nbr, self.deg, check=False, slot_pos=True)
         return self._rev
 
 
@@ -111,14 +122,16 @@ class EdgeMean(torch.autograd.Function):
         gw2 = torch.empty((128, 128), dtype=torch.float32, device=dev)
         gb2 = torch.empty((128,), dtype=torch.float32, device=dev)
         st = L.stream(dev)
-        L.check(lib.mmpde_gnn_edge_backward_ex(L.ptr(a), L.ptr(b), L.ptr(graph.nbr), L.ptr(graph.deg),
-                                               n, k, L.ptr(w2), L.ptr(b2), L.ptr(g), L.ptr(ga),
-                                               L.ptr(gedge), L.ptr(part), L.ptr(gw2), L.ptr(gb2),
-                                               ctx.edge_gemm, st),
-                "mmpde_gnn_edge_backward_ex")
-        rev_off, rev_edge = graph.reverse()
-        L.check(lib.mmpde_gnn_edge_source_sum(L.ptr(gedge), L.ptr(rev_off), L.ptr(rev_edge), n,
-                                              L.ptr(gb), st), "mmpde_gnn_edge_source_sum")
+        # per-edge dL/dz1 written source-major (slot_pos), then summed per
+        # source as contiguous runs
+        rev_off, _, slot_pos = graph.reverse()
+        L.check(lib.mmpde_gnn_edge_backward_sorted(L.ptr(a), L.ptr(b), L.ptr(graph.nbr), L.ptr(graph.deg),
+                                                   n, k, L.ptr(w2), L.ptr(b2), L.ptr(g), L.ptr(slot_pos),
+                                                   L.ptr(ga), L.ptr(gedge), L.ptr(part), L.ptr(gw2),
+                                                   L.ptr(gb2), ctx.edge_gemm, st),
+                "mmpde_gnn_edge_backward_sorted")
+        L.check(lib.mmpde_gnn_edge_source_sum_sorted(L.ptr(gedge), L.ptr(rev_off), n, L.ptr(gb), st),
+                "mmpde_gnn_edge_source_sum_sorted")
         return ga, gb, gw2, gb2, None, None
 
 
@@ -192,7 +205,7 @@ class GNN_Layer_FS_2D(nn.Module):  # noqa: N801 - reference name
         mean = EdgeMean.apply(a, b, m2.weight, m2.bias, graph, edge_gemm)
         v = torch.relu(linear_train(torch.cat((h, mean, variables), -1), self.update_net_1[0]))
         upd = torch.relu(linear_train(v, self.update_net_2[0]))
-        return self.norm(h + upd)
+        return self.norm.forward_res(h, upd)
 
     def forward(self, x, u, pos_x, pos_y, variables, edge_index, batch):
         """Layer-level API of the reference (gnn_2d.py:53-57), any edge_index.
@@ -391,8 +404,8 @@ class MP_PDE_Solver_2D(nn.Module):  # noqa: N801 - reference name
         pos_y = pos[:, 2][:, None] / self.pde.Ly
         variables = pos[:, 0][:, None] / self.pde.tmax
         e = self.embedding_mlp
-        z = torch.relu(e[1](linear_train(torch.cat((u, pos_x, pos_y, variables), -1), e[0])))
-        h = e[4](linear_train(z, e[3]))
+        z = torch.relu(batch_norm_rows(e[1], linear_train(torch.cat((u, pos_x, pos_y, variables), -1), e[0])))
+        h = batch_norm_rows(e[4], linear_train(z, e[3]))
         for layer in self.gnn_layers:
             h = layer.train_forward(h, u, pos_x, pos_y, variables, graph, self.edge_gemm)
         diff = self._head_train(h)
@@ -401,10 +414,11 @@ class MP_PDE_Solver_2D(nn.Module):  # noqa: N801 - reference name
     def _head_train(self, h: torch.Tensor) -> torch.Tensor:
         """output_mlp(h[:, None]).squeeze(1) (gnn_2d.py:108-114,136), as the
         same three strided Conv1d written as unfold + GEMM (per node: 128 -> 38
-        x 4 -> 9 x 8 -> 1): autograd through batched GEMMs and unfold's
-        gather-form backward instead of MIOpen's convolution search and
-        kernels (which cost ~1 ms per training iteration and a multi-second
-        search on first use)."""
+        x 4 -> 9 x 8 -> 1): LinearRows over the window rows (weight and bias
+        gradients on mmpde_rows_grad_weight) and unfold's gather-form
+        backward instead of MIOpen's convolution search and kernels (which
+        cost ~1 ms per training iteration and a multi-second search on first
+        use)."""
         o = self.output_mlp
         n = h.shape[0]
         x = h
@@ -418,7 +432,9 @@ class MP_PDE_Solver_2D(nn.Module):  # noqa: N801 - reference name
             else:
                 win = y.transpose(1, 2).unfold(2, ks, st)               # [n, cin, L, ks]
                 win = win.permute(0, 2, 1, 3).reshape(n, win.shape[2], cin * ks)
-            y = win @ c.weight.reshape(cout, cin * ks).t() + c.bias    # [n, L, cout]
+            L_ = win.shape[1]
+            y = LinearRows.apply(win.reshape(n * L_, cin * ks), c.weight.reshape(cout, cin * ks),
+                                 c.bias).reshape(n, L_, cout)           # [n, L, cout]
             if idx != 4:
                 y = torch.relu(y)
         return y.transpose(1, 2).squeeze(1)                             # [n, L_last]

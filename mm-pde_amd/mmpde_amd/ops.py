@@ -298,8 +298,13 @@ def nbr_table_from_edge_index(edge_index: torch.Tensor, n: int):
         k = e // n
         tgt = torch.arange(n, device=edge_index.device).repeat_interleave(k)
         if bool(torch.equal(edge_index[1], tgt)):
-            return edge_index[0].reshape(n, k).to(torch.int32).contiguous(), None
+            src = edge_index[0]
+            if e and (int(src.min()) < 0 or int(src.max()) >= n):
+                raise ValueError("edge_index holds nodes outside [0, n)")
+            return src.reshape(n, k).to(torch.int32).contiguous(), None
     src, tgt = edge_index[0].long(), edge_index[1].long()
+    if e and (int(src.min()) < 0 or int(src.max()) >= n or int(tgt.min()) < 0 or int(tgt.max()) >= n):
+        raise ValueError("edge_index holds nodes outside [0, n)")
     order = torch.argsort(tgt, stable=True)
     src, tgt = src[order], tgt[order]
     deg = torch.bincount(tgt, minlength=n)
@@ -496,8 +501,16 @@ class LinearRows(torch.autograd.Function):
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
             gx = dy @ w
+        n, k = x.shape
+        nout = w.shape[0]
+        want_b = ctx.has_bias and ctx.needs_input_grad[2]
+        if n >= 4096 and rows_grad_fits(k, nout):
+            # skinny map (head windows, embedding): dW and db in one row pass
+            gw, gb = rows_grad_weight(x, dy, k if ctx.needs_input_grad[1] else 0, want_b)
+            return gx, gw, gb
+        if want_b:
+            gb = rows_grad_weight(x, dy, 0, True)[1] if n >= 4096 and nout <= 128 else dy.sum(0)
         if ctx.needs_input_grad[1]:
-            n, k = x.shape
             C = LinearRows.chunks(n, k)
             if C:
                 R = n // C
@@ -507,9 +520,88 @@ class LinearRows(torch.autograd.Function):
                     gw = gw + dy[C * R:].t() @ x[C * R:]
             else:
                 gw = dy.t() @ x
-        if ctx.has_bias and ctx.needs_input_grad[2]:
-            gb = dy.sum(0)
         return gx, gw, gb
+
+
+def rows_grad_fits(k: int, nout: int) -> bool:
+    """Shapes mmpde_rows_grad_weight takes with the weight gradient."""
+    return 0 < k <= 64 and nout <= 128 and k * nout + nout <= 1280
+
+
+def rows_grad_weight(x: torch.Tensor, dy: torch.Tensor, k: int, bias: bool):
+    """(dW = dy^T x [nout, k] or None when k = 0, db = sum_rows dy or None) on
+    mmpde_rows_grad_weight (fixed summation order)."""
+    rows, nout = dy.shape
+    dy = L.f32c(dy)
+    x = L.f32c(x) if k else None
+    dev = dy.device
+    gw = torch.empty((nout, k), dtype=torch.float32, device=dev) if k else None
+    gb = torch.empty((nout,), dtype=torch.float32, device=dev) if bias else None
+    nb = L.lib().mmpde_rows_grad_weight_workspace_bytes(rows, k, nout)
+    ws = torch.empty((nb // 4,), dtype=torch.float32, device=dev)
+    L.check(L.lib().mmpde_rows_grad_weight(L.ptr(x), x.stride(0) if k else 0, rows, k, L.ptr(dy), dy.stride(0),
+                                           nout, L.ptr(gw), L.ptr(gb), L.ptr(ws), nb, L.stream(dev)),
+            "mmpde_rows_grad_weight")
+    return gw, gb
+
+
+class BatchNormRows(torch.autograd.Function):
+    """nn.BatchNorm1d in train mode over [n, C] rows of x + res (the residual
+    add of GNN_Layer_FS_2D, norm(h + update), gnn_2d.py:69, and the
+    embedding's BatchNorm1d, gnn_2d.py:101,105) on
+    mmpde_batch_norm_rows_train / _backward: batch statistics, running
+    statistics update in place, normalisation; gradients for x, res, weight
+    and bias.  Deterministic."""
+
+    @staticmethod
+    def forward(ctx, x, res, weight, bias, eps, factor, running_mean, running_var):
+        n, C = x.shape
+        dev = x.device
+        y = torch.empty_like(x)
+        stats = torch.empty((4 * C,), dtype=torch.float32, device=dev)
+        nb = L.lib().mmpde_batch_norm_rows_workspace_bytes(n, C) + 12 * C
+        ws = torch.empty((nb // 4,), dtype=torch.float32, device=dev)
+        L.check(L.lib().mmpde_batch_norm_rows_train(
+            L.ptr(x), L.ptr(res), n, C, L.ptr(weight), L.ptr(bias), float(eps), float(factor),
+            L.ptr(running_mean), L.ptr(running_var), L.ptr(y), L.ptr(stats), L.ptr(ws), nb, L.stream(dev)),
+            "mmpde_batch_norm_rows_train")
+        ctx.save_for_backward(x, res, weight, stats)
+        ctx.ws = nb
+        ctx.has = (res is not None, weight is not None, bias is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, res, weight, stats = ctx.saved_tensors
+        has_res, has_w, has_b = ctx.has
+        n, C = x.shape
+        dev = x.device
+        dy = L.f32c(dy)
+        dx = torch.empty_like(x)
+        dw = torch.empty((C,), dtype=torch.float32, device=dev) if has_w else None
+        db = torch.empty((C,), dtype=torch.float32, device=dev) if has_b else None
+        ws = torch.empty((ctx.ws // 4,), dtype=torch.float32, device=dev)
+        L.check(L.lib().mmpde_batch_norm_rows_backward(
+            L.ptr(x), L.ptr(res), L.ptr(dy), n, C, L.ptr(weight), L.ptr(stats), L.ptr(dx), L.ptr(dw), L.ptr(db),
+            L.ptr(ws), ctx.ws, L.stream(dev)), "mmpde_batch_norm_rows_backward")
+        return dx, (dx if has_res else None), dw, db, None, None, None, None
+
+
+def batch_norm_rows(bn: torch.nn.BatchNorm1d, x: torch.Tensor, res: torch.Tensor | None = None) -> torch.Tensor:
+    """bn(x + res) for [n, C] rows: the HIP kernels in train mode (running
+    statistics and num_batches_tracked advanced as nn.BatchNorm1d does), the
+    module itself in eval mode."""
+    if not bn.training or x.dim() != 2 or x.shape[1] % 4 or x.shape[1] > 1024 or x.shape[0] < 2:
+        return bn(x if res is None else x + res)
+    factor = 0.0
+    if bn.track_running_stats and bn.num_batches_tracked is not None:
+        bn.num_batches_tracked.add_(1)
+        factor = 1.0 / float(bn.num_batches_tracked) if bn.momentum is None else bn.momentum
+    rm = bn.running_mean if bn.track_running_stats else None
+    rv = bn.running_var if bn.track_running_stats else None
+    x = x.float().contiguous()                  # no detach: autograd inputs
+    res = res.float().contiguous() if res is not None else None
+    return BatchNormRows.apply(x, res, bn.weight, bn.bias, bn.eps, factor, rm, rv)
 
 
 def linear_train(x: torch.Tensor, lin: torch.nn.Linear) -> torch.Tensor:
@@ -567,14 +659,37 @@ def itp_interp(src, vals, qry, idx, batches: int, packed: torch.Tensor, addend=N
 
 
 def reverse_adjacency(nbr: torch.Tensor, degree: torch.Tensor | None = None,
-                      n_src: int | None = None):
+                      n_src: int | None = None, check: bool = True, slot_pos: bool = False):
     """Source-major view of a target-major table, for the source-side gradient of
     the edge stage (mmpde_gnn_edge_source_sum): rev_edge int64 = the live slot
     ids i*k+e grouped by source j (stable: target order within a source),
     rev_off int64 [n_src+1] = the group offsets (n_src defaults to the number of
-    targets).  Index plumbing only."""
+    targets).  Device tables: mmpde_reverse_adjacency (no host round trip
+    unless `check`, which reads back the count of sources outside [0, n_src)
+    and raises on any; the engine's own kNN tables pass check=False;
+    slot_pos=True adds the int32 [nt*k] position of every slot in that order,
+    for mmpde_gnn_edge_backward_sorted).  Host tables (tests): the same lists
+    from a stable argsort."""
     nt, k = nbr.shape
     n = nt if n_src is None else n_src
+    if nbr.is_cuda:
+        dev = nbr.device
+        nbr = nbr.to(torch.int32).contiguous()
+        deg = degree.to(torch.int32).contiguous() if degree is not None else None
+        rev_off = torch.empty((n + 1,), dtype=torch.int64, device=dev)
+        rev_edge = torch.empty((max(nt * k, 1),), dtype=torch.int64, device=dev)
+        sb = L.lib().mmpde_reverse_adjacency_scratch_bytes(nt, k, n)
+        scratch = torch.empty(((sb + 255) // 256 * 64,), dtype=torch.float32, device=dev).view(torch.uint8)
+        bad = torch.empty((1,), dtype=torch.int32, device=dev)
+        pos = torch.empty((max(nt * k, 1),), dtype=torch.int32, device=dev) if slot_pos else None
+        L.check(L.lib().mmpde_reverse_adjacency(L.ptr(nbr), nt, k, L.ptr(deg), n, L.ptr(rev_off),
+                                                L.ptr(rev_edge), L.ptr(pos), L.ptr(scratch), scratch.numel(),
+                                                L.ptr(bad), L.stream(dev)), "mmpde_reverse_adjacency")
+        if check and int(bad.item()):
+            raise ValueError("neighbour table holds sources outside [0, n)")
+        return (rev_off, rev_edge, pos) if slot_pos else (rev_off, rev_edge)
+    if slot_pos:
+        raise ValueError("slot_pos: device tables only")
     src = nbr.reshape(-1).long()
     slot = torch.arange(nt * k, device=nbr.device)
     if degree is not None:
@@ -596,18 +711,19 @@ class GatherRows(torch.autograd.Function):
     order).  rows [n, w] fp32, idx int [m] -> [m, w]."""
 
     @staticmethod
-    def forward(ctx, rows, idx):
+    def forward(ctx, rows, idx, check=False):
         L.require_device(rows, idx)
         ctx.n = rows.shape[0]
         ctx.idx = idx
+        ctx.check = check      # idx from the engine's kNN kernels: in range
         return rows[idx.long()]
 
     @staticmethod
     def backward(ctx, g):
         g = L.f32c(g)
         n, w = ctx.n, g.shape[1]
-        rev_off, rev_edge = reverse_adjacency(ctx.idx.reshape(-1, 1), n_src=n)
+        rev_off, rev_edge = reverse_adjacency(ctx.idx.reshape(-1, 1), n_src=n, check=ctx.check)
         out = torch.empty((n, w), dtype=torch.float32, device=g.device)
         L.check(L.lib().mmpde_segment_sum(L.ptr(g), w, L.ptr(rev_off), L.ptr(rev_edge), n,
                                           L.ptr(out), L.stream(g.device)), "mmpde_segment_sum")
-        return out, None
+        return out, None, None

@@ -1,0 +1,93 @@
+// Edge-stage backward timing (profiling aid, not shipped): the fp16x3
+// backward (edge_bwd_f16_kernel) at cy B=16 size (40336 targets, k = 35 random
+// in-trajectory neighbours), target-major (mmpde_gnn_edge_backward_ex) and
+// source-major (mmpde_gnn_edge_backward_sorted, slot positions from
+// mmpde_reverse_adjacency), plus the two source sums.  Built per variant of
+// the kernel's compile-time placement flags (Makefile bwd_ab_%).
+//   make -C tools/ubench bwd_ab_base && tools/ubench/bwd_ab_base
+#include "../../mm-pde_amd/csrc/edge_bwd.hip"
+#include "../../mm-pde_amd/csrc/train_rows.hip"
+#include <cstdio>
+#include <random>
+#include <vector>
+
+#define CK(x)                                                                         \
+    do {                                                                              \
+        auto e_ = (x);                                                                \
+        if (e_ != 0) {                                                                \
+            fprintf(stderr, "%s:%d status %d\n", __FILE__, __LINE__, (int)e_);        \
+            return 1;                                                                 \
+        }                                                                             \
+    } while (0)
+
+template <class T>
+static T *dev_copy(const std::vector<T> &h) {
+    T *p = nullptr;
+    if (hipMalloc(&p, h.size() * sizeof(T)) != hipSuccess) return nullptr;
+    hipMemcpy(p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice);
+    return p;
+}
+
+int main() {
+    const int B = 16, N = 2521, K = 35;
+    const int64_t n = (int64_t)B * N;
+    std::mt19937 rng(7);
+    std::normal_distribution<float> nd(0.0f, 1.0f);
+    std::vector<float> a(n * 128), b(n * 128), g(n * 128), w2(128 * 128), b2(128);
+    for (auto &v : a) v = 0.5f * nd(rng);
+    for (auto &v : b) v = 0.5f * nd(rng);
+    for (auto &v : g) v = nd(rng);
+    for (auto &v : w2) v = nd(rng) / 11.3f;
+    for (auto &v : b2) v = 0.1f * nd(rng);
+    std::vector<int32_t> nb(n * K);
+    for (int64_t i = 0; i < n; ++i)
+        for (int e = 0; e < K; ++e) nb[i * K + e] = (int32_t)(i / N * N + rng() % N);
+    float *da = dev_copy(a), *db = dev_copy(b), *dg = dev_copy(g), *dw2 = dev_copy(w2), *db2 = dev_copy(b2);
+    int32_t *dnb = dev_copy(nb);
+    float *ga, *gb, *ge, *part, *gw2, *gb2;
+    CK(hipMalloc(&ga, n * 512));
+    CK(hipMalloc(&gb, n * 512));
+    CK(hipMalloc(&ge, n * K * 512));
+    CK(hipMalloc(&part, mmpde_gnn_edge_backward_partials(nullptr) * 4));
+    CK(hipMalloc(&gw2, 128 * 128 * 4));
+    CK(hipMalloc(&gb2, 128 * 4));
+    int64_t *off, *edge;
+    int32_t *pos, *bad;
+    CK(hipMalloc(&off, (n + 1) * 8));
+    CK(hipMalloc(&edge, n * K * 8));
+    CK(hipMalloc(&pos, n * K * 4));
+    CK(hipMalloc(&bad, 4));
+    const int64_t sb = mmpde_reverse_adjacency_scratch_bytes(n, K, n);
+    void *scratch;
+    CK(hipMalloc(&scratch, sb));
+    CK(mmpde_reverse_adjacency(dnb, n, K, nullptr, n, off, edge, pos, scratch, sb, bad, nullptr));
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    auto timed = [&](const char *what, auto fn) {
+        for (int i = 0; i < 3; ++i) fn();
+        hipEventRecord(e0, 0);
+        const int it = 10;
+        for (int i = 0; i < it; ++i) fn();
+        hipEventRecord(e1, 0);
+        hipEventSynchronize(e1);
+        float ms = 0;
+        hipEventElapsedTime(&ms, e0, e1);
+        printf("  %-44s %8.1f us\n", what, 1e3 * ms / it);
+    };
+    printf("edge backward, n=%lld k=%d, P1_FIRST=%d\n", (long long)n, K, (int)kBwdP1First);
+    timed("backward_ex f16x3 (target-major rows)", [&] {
+        mmpde_gnn_edge_backward_ex(da, db, dnb, nullptr, n, K, dw2, db2, dg, ga, ge, part, gw2, gb2, 1, nullptr);
+    });
+    timed("source_sum (gather)", [&] { mmpde_gnn_edge_source_sum(ge, off, edge, n, gb, nullptr); });
+    timed("backward_sorted f16x3 (source-major rows)", [&] {
+        mmpde_gnn_edge_backward_sorted(da, db, dnb, nullptr, n, K, dw2, db2, dg, pos, ga, ge, part, gw2, gb2, 1,
+                                       nullptr);
+    });
+    timed("source_sum_sorted (contiguous)", [&] { mmpde_gnn_edge_source_sum_sorted(ge, off, n, gb, nullptr); });
+    timed("reverse_adjacency (+ slot positions)", [&] {
+        mmpde_reverse_adjacency(dnb, n, K, nullptr, n, off, edge, pos, scratch, sb, bad, nullptr);
+    });
+    CK(hipDeviceSynchronize());
+    return 0;
+}
