@@ -255,8 +255,13 @@ constexpr size_t kEdgeBwdF16Lds = sizeof(float) * 2 * FT * FAW + sizeof(_Float16
                                   sizeof(int) * FT;
 static_assert(kEdgeBwdF16Lds <= 160 * 1024, "edge_bwd_f16_kernel: LDS beyond gfx950's 160 KiB per CU");
 
+// P1 of slot e + 1 in front of P3(e)'s MFMAs in one straight-line block (1),
+// or after P3(e)'s epilogue (0, the round-3 order): 807-817 vs 784-795 us per
+// sorted backward at cy B=16 (tools/ubench/bwd_ab.cpp, profiles/
+// r04_bwd_ab.log) -- the compiler waits on every LDS operand read in the MFMA
+// stream either way, so the placement buys nothing; 0.
 #ifndef MMPDE_BWD_P1_FIRST
-#define MMPDE_BWD_P1_FIRST 1
+#define MMPDE_BWD_P1_FIRST 0
 #endif
 constexpr bool kBwdP1First = MMPDE_BWD_P1_FIRST != 0;
 
