@@ -317,11 +317,15 @@ int mmpde_gnn_edge_mean_deg(const float *a, const float *b, const int32_t *nbr, 
  * W2 and the split scale (max|a| + max|b| over all n rows) into workspace
  * (>= mmpde_gnn_edge_mean_workspace_bytes(n, edge_gemm) bytes, 16-B aligned)
  * on every call: the forward of the f16x3 training path, whose weights
- * change every iteration. */
+ * change every iteration.  relu_mask (nullable, F16X3 only, 16-B aligned):
+ * [n * k][4] uint32, bit c % 32 of word c / 32 of slot q = i*k + e set where
+ * message_net_2's pre-activation z2[c] > 0 for that edge -- the ReLU pattern
+ * mmpde_gnn_edge_backward_sorted then reuses instead of recomputing z2. */
 int64_t mmpde_gnn_edge_mean_workspace_bytes(int64_t n, int edge_gemm);
 int mmpde_gnn_edge_mean_ex(const float *a, const float *b, const int32_t *nbr, const int32_t *deg,
                            int64_t n, int k, const float *msg2_w, const float *msg2_b, float *mean_out,
-                           int edge_gemm, void *workspace, int64_t workspace_bytes, mmpde_stream_t stream);
+                           uint32_t *relu_mask, int edge_gemm, void *workspace, int64_t workspace_bytes,
+                           mmpde_stream_t stream);
 
 /* ---------------------------------------------------------------- training
  * Backward of the edge stage (reference: loss.backward() at
@@ -361,12 +365,15 @@ int mmpde_gnn_edge_source_sum(const float *grad_edge, const int64_t *rev_off, co
  * n*k-1), so that dL/db is the contiguous segmented sum
  * mmpde_gnn_edge_source_sum_sorted over rev_off: the same sums in the same
  * order as mmpde_gnn_edge_backward_ex + mmpde_gnn_edge_source_sum, read as a
- * stream instead of a gather.  n * k < 2^31. */
+ * stream instead of a gather.  n * k < 2^31.  relu_mask (nullable; F16X3,
+ * k <= 64): the forward's z2 > 0 bits (mmpde_gnn_edge_mean_ex): the ReLU
+ * pattern of message_net_2 is taken from it and z2 is not recomputed (one of
+ * the three per-edge GEMMs dropped). */
 int mmpde_gnn_edge_backward_sorted(const float *a, const float *b, const int32_t *nbr, const int32_t *deg,
                                    int64_t n, int k, const float *msg2_w, const float *msg2_b,
-                                   const float *grad_mean, const int32_t *slot_pos, float *grad_a,
-                                   float *grad_edge, float *partials, float *grad_w2, float *grad_b2,
-                                   int edge_gemm, mmpde_stream_t stream);
+                                   const float *grad_mean, const int32_t *slot_pos, const uint32_t *relu_mask,
+                                   float *grad_a, float *grad_edge, float *partials, float *grad_w2,
+                                   float *grad_b2, int edge_gemm, mmpde_stream_t stream);
 int mmpde_gnn_edge_source_sum_sorted(const float *grad_edge, const int64_t *rev_off, int64_t n, float *grad_b,
                                      mmpde_stream_t stream);
 /* The same segmented sum for rows of any width: out[j, :] = sum over q in

@@ -239,6 +239,7 @@ struct EdgeBwdF16Args {
     const unsigned *mx;       // max|a|, max|b|, max|g| (float bits)
     float *ga, *gz1, *pw2, *pb2;
     const int32_t *pos;       // nullable: the gz1 row of slot q (source-major order)
+    const uint32_t *mask;     // MASK: the forward's z2 > 0 bits, [n * k][4] (mmpde_gnn_edge_mean_ex)
 };
 
 __device__ __forceinline__ void split1(float x, _Float16 &h, _Float16 &l) {
@@ -265,6 +266,9 @@ static_assert(kEdgeBwdF16Lds <= 160 * 1024, "edge_bwd_f16_kernel: LDS beyond gfx
 #endif
 constexpr bool kBwdP1First = MMPDE_BWD_P1_FIRST != 0;
 
+// MASK: message_net_2's ReLU pattern comes from the forward's bits instead of
+// recomputing z2 (P2 without its MFMAs; no row-major relu(z1) image).
+template <bool MASK>
 __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) {
     __shared__ float at[FT * FAW];             // a rows of the tile
     __shared__ float gms[FT * FAW];            // g / deg rows (0 for rows past n)
@@ -329,6 +333,14 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
         float bv[8];
 #pragma unroll
         for (int t = 0; t < 8; ++t) bv[t] = p.b[(int64_t)nb[(8 * eg + t) * FKMAX] * BH + kk1];
+        uint32_t mnext[8];  // MASK: the z2 > 0 bits of the slot P2 runs next
+        if (MASK) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int rr = 16 * (i >> 2) + 4 * g + (i & 3);
+                mnext[i] = p.mask[(min(row0 + rr, nmax) * k) * 4 + (wave >> 1)];
+            }
+        }
         f32x4 gacc[2] = {(f32x4){0.0f, 0.0f, 0.0f, 0.0f}, (f32x4){0.0f, 0.0f, 0.0f, 0.0f}};
         // ---- P1 of slot e into buffer e & 1; issues the b loads of slot e + 1
         // (clamped at the last slot: a harmless reload)
@@ -345,8 +357,10 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
                 split1(fmaxf(z, 0.0f) * sz, h, l);
                 hi[t] = h;
                 lo[t] = l;
-                za[sb][0][ed * FAS + kk1] = h;
-                za[sb][1][ed * FAS + kk1] = l;
+                if (!MASK) {
+                    za[sb][0][ed * FAS + kk1] = h;
+                    za[sb][1][ed * FAS + kk1] = l;
+                }
             }
             *(half8 *)&zb[sb][0][kk1 * FCS + 8 * eg] = hi;
             *(half8 *)&zb[sb][1][kk1 * FCS + 8 * eg] = lo;
@@ -359,15 +373,30 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
         auto p2 = [&](int e) {
             const int sb = e & 1;
             f32x4 acc[2] = {(f32x4){0.0f, 0.0f, 0.0f, 0.0f}, (f32x4){0.0f, 0.0f, 0.0f, 0.0f}};
+            if (!MASK) {
 #pragma unroll
-            for (int s = 0; s < 4; ++s) {
+                for (int s = 0; s < 4; ++s) {
 #pragma unroll
-                for (int rb = 0; rb < 2; ++rb) {
-                    const half8 ah = *(const half8 *)&za[sb][0][(16 * rb + r) * FAS + 32 * s + 8 * g];
-                    const half8 al = *(const half8 *)&za[sb][1][(16 * rb + r) * FAS + 32 * s + 8 * g];
-                    acc[rb] = mfma_f16(ah, w1h[s], acc[rb]);
-                    acc[rb] = mfma_f16(ah, w1l[s], acc[rb]);
-                    acc[rb] = mfma_f16(al, w1h[s], acc[rb]);
+                    for (int rb = 0; rb < 2; ++rb) {
+                        const half8 ah = *(const half8 *)&za[sb][0][(16 * rb + r) * FAS + 32 * s + 8 * g];
+                        const half8 al = *(const half8 *)&za[sb][1][(16 * rb + r) * FAS + 32 * s + 8 * g];
+                        acc[rb] = mfma_f16(ah, w1h[s], acc[rb]);
+                        acc[rb] = mfma_f16(ah, w1l[s], acc[rb]);
+                        acc[rb] = mfma_f16(al, w1h[s], acc[rb]);
+                    }
+                }
+            }
+            uint32_t mk[8];
+            if (MASK) {
+                // this slot's bits (column tile = wave, bit r) of the 8 rows of
+                // this lane, then the next slot's issued (in flight over P3)
+#pragma unroll
+                for (int i = 0; i < 8; ++i) mk[i] = mnext[i];
+                const int en = min(e + 1, k - 1);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const int rr = 16 * (i >> 2) + 4 * g + (i & 3);
+                    mnext[i] = p.mask[(min(row0 + rr, nmax) * k + en) * 4 + (wave >> 1)];
                 }
             }
 #pragma unroll
@@ -376,7 +405,9 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const int rr = 16 * rb + 4 * g + q;
-                    const bool on = e < dg[rr] && acc[rb][q] * un1 + bias > 0.0f;
+                    const bool z2pos = MASK ? ((mk[4 * rb + q] >> (16 * (wave & 1) + r)) & 1u) != 0
+                                             : acc[rb][q] * un1 + bias > 0.0f;
+                    const bool on = e < dg[rr] && z2pos;
                     const float v = on ? gms[rr * FAW + col] : 0.0f;
                     db += v;
                     split1(v * sg, hv[q], lv[q]);
@@ -649,8 +680,8 @@ static int edge_backward_f32(const float *a, const float *b, const int32_t *nbr,
 
 static int edge_backward(const float *a, const float *b, const int32_t *nbr, const int32_t *deg, int64_t n, int k,
                          const float *msg2_w, const float *msg2_b, const float *grad_mean, const int32_t *pos,
-                         float *grad_a, float *grad_edge, float *partials, float *grad_w2, float *grad_b2,
-                         int edge_gemm, mmpde_stream_t stream) {
+                         const uint32_t *mask, float *grad_a, float *grad_edge, float *partials, float *grad_w2,
+                         float *grad_b2, int edge_gemm, mmpde_stream_t stream) {
     MMPDE_REQUIRE(edge_gemm == MMPDE_EDGE_GEMM_F32 || edge_gemm == MMPDE_EDGE_GEMM_F16X3);
     if (edge_gemm == MMPDE_EDGE_GEMM_F32 || k > FKMAX)
         return edge_backward_f32(a, b, nbr, deg, n, k, msg2_w, msg2_b, grad_mean, pos, grad_a, grad_edge, partials,
@@ -688,8 +719,9 @@ static int edge_backward(const float *a, const float *b, const int32_t *nbr, con
     hipLaunchKernelGGL(maxabs3_final_kernel, dim3(3), dim3(256), 0, st, mpart, mg, mx);
     MMPDE_RET_LAUNCH();
     EdgeBwdF16Args p{a, b, nbr, deg, n, k, (int)ntiles, img1, img2, msg2_b, grad_mean, mx, grad_a, grad_edge,
-                     pw2, pb2, pos};
-    hipLaunchKernelGGL(edge_bwd_f16_kernel, dim3(grid), dim3(512), 0, st, p);
+                     pw2, pb2, pos, mask};
+    if (mask) hipLaunchKernelGGL(edge_bwd_f16_kernel<true>, dim3(grid), dim3(512), 0, st, p);
+    else hipLaunchKernelGGL(edge_bwd_f16_kernel<false>, dim3(grid), dim3(512), 0, st, p);
     MMPDE_RET_LAUNCH();
     hipLaunchKernelGGL(partial_sum_kernel, dim3(ceil_div(BH * BH, 256)), dim3(256), 0, st, pw2, grid,
                        (int64_t)BH * BH, grad_w2);
@@ -712,18 +744,20 @@ extern "C" int mmpde_gnn_edge_backward_ex(const float *a, const float *b, const 
                                           const float *grad_mean, float *grad_a, float *grad_edge,
                                           float *partials, float *grad_w2, float *grad_b2, int edge_gemm,
                                           mmpde_stream_t stream) {
-    return edge_backward(a, b, nbr, deg, n, k, msg2_w, msg2_b, grad_mean, nullptr, grad_a, grad_edge, partials,
-                         grad_w2, grad_b2, edge_gemm, stream);
+    return edge_backward(a, b, nbr, deg, n, k, msg2_w, msg2_b, grad_mean, nullptr, nullptr, grad_a, grad_edge,
+                         partials, grad_w2, grad_b2, edge_gemm, stream);
 }
 
 extern "C" int mmpde_gnn_edge_backward_sorted(const float *a, const float *b, const int32_t *nbr,
                                               const int32_t *deg, int64_t n, int k, const float *msg2_w,
                                               const float *msg2_b, const float *grad_mean, const int32_t *slot_pos,
-                                              float *grad_a, float *grad_edge, float *partials, float *grad_w2,
-                                              float *grad_b2, int edge_gemm, mmpde_stream_t stream) {
+                                              const uint32_t *relu_mask, float *grad_a, float *grad_edge,
+                                              float *partials, float *grad_w2, float *grad_b2, int edge_gemm,
+                                              mmpde_stream_t stream) {
     MMPDE_REQUIRE(slot_pos);
-    return edge_backward(a, b, nbr, deg, n, k, msg2_w, msg2_b, grad_mean, slot_pos, grad_a, grad_edge, partials,
-                         grad_w2, grad_b2, edge_gemm, stream);
+    MMPDE_REQUIRE(!relu_mask || (edge_gemm == MMPDE_EDGE_GEMM_F16X3 && k <= FKMAX));
+    return edge_backward(a, b, nbr, deg, n, k, msg2_w, msg2_b, grad_mean, slot_pos, relu_mask, grad_a, grad_edge,
+                         partials, grad_w2, grad_b2, edge_gemm, stream);
 }
 
 extern "C" int mmpde_gnn_edge_source_sum_sorted(const float *grad_edge, const int64_t *rev_off, int64_t n,

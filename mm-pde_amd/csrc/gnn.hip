@@ -410,13 +410,16 @@ extern "C" int64_t mmpde_gnn_edge_mean_workspace_bytes(int64_t n, int edge_gemm)
 
 extern "C" int mmpde_gnn_edge_mean_ex(const float *a, const float *b, const int32_t *nbr, const int32_t *deg,
                                       int64_t n, int k, const float *msg2_w, const float *msg2_b, float *mean_out,
-                                      int edge_gemm, void *workspace, int64_t workspace_bytes,
+                                      uint32_t *relu_mask, int edge_gemm, void *workspace, int64_t workspace_bytes,
                                       mmpde_stream_t stream) {
     MMPDE_REQUIRE(edge_gemm == MMPDE_EDGE_GEMM_F32 || edge_gemm == MMPDE_EDGE_GEMM_F16X3);
+    MMPDE_REQUIRE(!relu_mask || edge_gemm == MMPDE_EDGE_GEMM_F16X3);
     if (edge_gemm == MMPDE_EDGE_GEMM_F32)
         return mmpde_gnn_edge_mean_deg(a, b, nbr, deg, n, k, msg2_w, msg2_b, mean_out, stream);
     MMPDE_REQUIRE(n > 0 && workspace && workspace_bytes >= edge_mean_f16x3_ws_bytes(n));
-    return launch_edge_mean_f16x3(a, b, nbr, deg, n, k, msg2_w, msg2_b, mean_out, workspace, as_stream(stream));
+    MMPDE_REQUIRE(!relu_mask || (n * k < (int64_t)INT32_MAX && ((uintptr_t)relu_mask & 15) == 0));
+    return launch_edge_mean_f16x3(a, b, nbr, deg, n, k, msg2_w, msg2_b, mean_out, relu_mask, workspace,
+                                  as_stream(stream));
 }
 
 static int gnn_layer_impl(const float *h_in, const float *u, const float *pos, int64_t n, int k,

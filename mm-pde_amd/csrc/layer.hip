@@ -76,6 +76,7 @@ struct EdgeArgs {
     float *mean;               // [n, 128]
     uint64_t *stamps;          // profiling builds (PH bit 10): per-round s_memtime of block 0
     const int32_t *deg;        // RAGGED: in-degree of every target (nbr row entries past it are ignored)
+    uint32_t *relu_mask;       // nullable: [n * k][4] bits z2 > 0 of every slot (training forward)
 };
 
 struct RoundCtr {  // (tile j, round rd) of a running round index
@@ -414,6 +415,29 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
                     if (RAGGED) v = e < dg[t] ? v : 0.0f;
                     S[cc][t] += v;
                 }
+            }
+            if (p.relu_mask) {
+                // the z2 > 0 bits the backward reuses (mmpde_gnn_edge_backward_sorted):
+                // ballots per (column tile cc, row t) cover rows 4 g + t, g < 4,
+                // 16 columns each; lane l < 16 stores row 4 (l >> 2) + (l & 3)'s
+                // word of this wave's 32 columns (CT = 2 tiles): one store per slot
+                static_assert(!F16X3 || CT == 2, "relu mask words take two column tiles per wave");
+                uint64_t bal[CT][4];
+#pragma unroll
+                for (int cc = 0; cc < CT; ++cc)
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) bal[cc][t] = __ballot(acc[cc][t] > 0.0f);
+                const int tl = lane & 3, gl = (lane >> 2) & 3;
+                uint64_t b0 = bal[0][0], b1 = bal[CT - 1][0];
+#pragma unroll
+                for (int t = 1; t < 4; ++t) {
+                    b0 = tl == t ? bal[0][t] : b0;
+                    b1 = tl == t ? bal[CT - 1][t] : b1;
+                }
+                const uint32_t word = (uint32_t)((b0 >> (16 * gl)) & 0xffffu) |
+                                      ((uint32_t)((b1 >> (16 * gl)) & 0xffffu) << 16);
+                const int64_t row = (int64_t)(first + cC.j * stride) * ET + 4 * gl + tl;
+                if (lane < 16 && row < p.n) p.relu_mask[(row * k + e) * 4 + cg] = word;
             }
         };
         float4 xa[4], xb[4], an[2 / NC];
@@ -1181,9 +1205,11 @@ int64_t edge_mean_f16x3_ws_bytes(int64_t n) { return kLayerPack + range_tiles(n)
 // The edge stage writing the mean itself (the persistent ring kernel), F16X3
 // with this call's own W2 image and range records (one segment of n rows):
 // the training forward (mmpde_gnn_edge_mean_ex), where the weights change every
-// iteration.
+// iteration; relu_mask (nullable) receives every slot's z2 > 0 bits for the
+// backward.
 int launch_edge_mean_f16x3(const float *a, const float *b, const int32_t *nbr, const int32_t *deg, int64_t n,
-                           int k, const float *w2, const float *b2, float *mean, void *ws, hipStream_t st) {
+                           int k, const float *w2, const float *b2, float *mean, uint32_t *relu_mask, void *ws,
+                           hipStream_t st) {
     MMPDE_REQUIRE(a && b && nbr && w2 && b2 && mean && ws && n > 0 && k > 0 && n <= (int64_t)INT32_MAX);
     MMPDE_REQUIRE(al16(a) && al16(b) && al16(w2) && al16(mean) && al16(ws));
     const int64_t ntiles = (n + ET - 1) / ET;
@@ -1198,7 +1224,7 @@ int launch_edge_mean_f16x3(const float *a, const float *b, const int32_t *nbr, c
     hipLaunchKernelGGL(range_records_kernel, dim3((unsigned)ceil_div(range_tiles(n), 4)), dim3(256), 0, st, a, b, n,
                        rng);
     MMPDE_RET_LAUNCH();
-    EdgeArgs e{a, b, nbr, n, k, (int)ntiles, w2, b2, pk, rng, mean, nullptr, deg};
+    EdgeArgs e{a, b, nbr, n, k, (int)ntiles, w2, b2, pk, rng, mean, nullptr, deg, relu_mask};
     const int cus = device_cus();
     const int grid = ntiles < cus ? (int)ntiles : cus;
     const dim3 block(64 * (4 * EDGE_NC + 4 * EDGE_NP));

@@ -64,7 +64,8 @@ int launch_edge_stage(const float *a, const float *b, const int32_t *nbr, const 
 // computes the range records of a, b itself in ws, edge_mean_f16x3_ws_bytes).
 int64_t edge_mean_f16x3_ws_bytes(int64_t n);
 int launch_edge_mean_f16x3(const float *a, const float *b, const int32_t *nbr, const int32_t *deg, int64_t n,
-                           int k, const float *w2, const float *b2, float *mean, void *ws, hipStream_t st);
+                           int k, const float *w2, const float *b2, float *mean, uint32_t *relu_mask, void *ws,
+                           hipStream_t st);
 
 // Segment size the kernels use for a requested seg_n (n when seg_n is 0, does
 // not divide n or is below kRangeRows).

@@ -118,8 +118,8 @@ _SIGS = {
     "mmpde_rows_grad_weight_workspace_bytes": (_I64, [_I64, _I, _I]),
     "mmpde_reverse_adjacency_scratch_bytes": (_I64, [_I64, _I, _I64]),
     "mmpde_reverse_adjacency": (_I, [_P, _I64, _I, _P, _I64, _P, _P, _P, _P, _I64, _P, _P]),
-    "mmpde_gnn_edge_backward_sorted": (_I, [_P, _P, _P, _P, _I64, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I,
-                                           _P]),
+    "mmpde_gnn_edge_backward_sorted": (_I, [_P, _P, _P, _P, _I64, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                                           _I, _P]),
     "mmpde_gnn_edge_source_sum_sorted": (_I, [_P, _P, _I64, _P, _P]),
     "mmpde_rows_grad_weight": (_I, [_P, _I64, _I64, _I, _P, _I64, _I, _P, _P, _P, _I64, _P]),
     "mmpde_batch_norm_rows_workspace_bytes": (_I64, [_I64, _I]),
@@ -131,7 +131,7 @@ _SIGS = {
     "mmpde_gnn_edge_mean": (_I, [_P, _P, _P, _I64, _I, _P, _P, _P, _P]),
     "mmpde_gnn_edge_mean_deg": (_I, [_P, _P, _P, _P, _I64, _I, _P, _P, _P, _P]),
     "mmpde_gnn_edge_mean_workspace_bytes": (_I64, [_I64, _I]),
-    "mmpde_gnn_edge_mean_ex": (_I, [_P, _P, _P, _P, _I64, _I, _P, _P, _P, _I, _P, _I64, _P]),
+    "mmpde_gnn_edge_mean_ex": (_I, [_P, _P, _P, _P, _I64, _I, _P, _P, _P, _P, _I, _P, _I64, _P]),
     "mmpde_gnn_edge_backward_partials": (_I64, [ctypes.POINTER(_I)]),
     "mmpde_gnn_edge_backward": (_I, [_P, _P, _P, _P, _I64, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "mmpde_gnn_edge_source_sum": (_I, [_P, _P, _P, _I64, _P, _P]),

@@ -83,7 +83,9 @@ class EdgeMean(torch.autograd.Function):
     with a = the target half and b = the source half of message_net_1's
     pre-activation.  Gradients for a, b, W2 and b2, deterministic; forward and
     backward GEMMs in exact fp32 (edge_gemm 'f32') or the fp16x3 split
-    (edge_gemm 'f16x3': mmpde_gnn_edge_mean_ex, mmpde_gnn_edge_backward_ex)."""
+    (edge_gemm 'f16x3': mmpde_gnn_edge_mean_ex keeps message_net_2's ReLU
+    pattern, 16 B per edge, which mmpde_gnn_edge_backward_sorted reuses instead
+    of recomputing z2)."""
 
     @staticmethod
     def forward(ctx, a, b, w2, b2, graph: EdgeGraph, edge_gemm: str = "f32"):
@@ -97,12 +99,17 @@ class EdgeMean(torch.autograd.Function):
         lib = L.lib()
         wsb = lib.mmpde_gnn_edge_mean_workspace_bytes(n, mode)
         ws = torch.empty((max(wsb, 16) // 4,), dtype=torch.float32, device=a.device) if wsb else None
+        # f16x3: the forward keeps message_net_2's ReLU pattern (16 B per edge)
+        # for the backward, which then skips recomputing z2
+        mask = (torch.empty((n * k, 4), dtype=torch.int32, device=a.device)
+                if edge_gemm == "f16x3" and k <= 64 else None)
         L.check(lib.mmpde_gnn_edge_mean_ex(L.ptr(a), L.ptr(b), L.ptr(graph.nbr), L.ptr(graph.deg), n, k,
-                                           L.ptr(w2), L.ptr(b2), L.ptr(mean), mode, L.ptr(ws), wsb,
+                                           L.ptr(w2), L.ptr(b2), L.ptr(mean), L.ptr(mask), mode, L.ptr(ws), wsb,
                                            L.stream(a.device)),
                 "mmpde_gnn_edge_mean_ex")
         ctx.save_for_backward(a, b, w2, b2)
         ctx.graph = graph
+        ctx.mask = mask
         ctx.edge_gemm = L.EDGE_GEMM[edge_gemm]
         return mean
 
@@ -127,8 +134,8 @@ class EdgeMean(torch.autograd.Function):
         rev_off, _, slot_pos = graph.reverse()
         L.check(lib.mmpde_gnn_edge_backward_sorted(L.ptr(a), L.ptr(b), L.ptr(graph.nbr), L.ptr(graph.deg),
                                                    n, k, L.ptr(w2), L.ptr(b2), L.ptr(g), L.ptr(slot_pos),
-                                                   L.ptr(ga), L.ptr(gedge), L.ptr(part), L.ptr(gw2),
-                                                   L.ptr(gb2), ctx.edge_gemm, st),
+                                                   L.ptr(ctx.mask), L.ptr(ga), L.ptr(gedge), L.ptr(part),
+                                                   L.ptr(gw2), L.ptr(gb2), ctx.edge_gemm, st),
                 "mmpde_gnn_edge_backward_sorted")
         L.check(lib.mmpde_gnn_edge_source_sum_sorted(L.ptr(gedge), L.ptr(rev_off), n, L.ptr(gb), st),
                 "mmpde_gnn_edge_source_sum_sorted")

@@ -63,7 +63,7 @@ def test_null_arguments_are_rejected_before_launch():
     assert lib.mmpde_gnn_edge_backward_ex(None, None, None, None, 10, 35, None, None, None, None, None,
                                           None, None, None, 7, None) == -1
     assert lib.mmpde_gnn_edge_backward_sorted(None, None, None, None, 10, 35, None, None, None, None, None,
-                                              None, None, None, None, 1, None) == -1
+                                              None, None, None, None, None, 1, None) == -1
     assert lib.mmpde_gnn_edge_source_sum_sorted(None, None, 10, None, None) == -1
     assert lib.mmpde_rows_grad_weight(None, 1, 10, 4, None, 1, 4, None, None, None, 0, None) == -1
     assert lib.mmpde_batch_norm_rows_train(None, None, 10, 128, None, None, 1e-5, 0.1, None, None, None, None,

@@ -204,7 +204,7 @@ def test_edge_backward_sorted_equals_gather_path(dev, edge_gemm, ragged):
         off, edge, pos = reverse_adjacency(nbr, deg, check=True, slot_pos=True)
         if sorted_:
             L.check(lib.mmpde_gnn_edge_backward_sorted(L.ptr(a), L.ptr(b), L.ptr(nbr), L.ptr(deg), n, k, L.ptr(w2),
-                                                       L.ptr(b2), L.ptr(gm), L.ptr(pos), L.ptr(ga), L.ptr(ge),
+                                                       L.ptr(b2), L.ptr(gm), L.ptr(pos), None, L.ptr(ga), L.ptr(ge),
                                                        L.ptr(part), L.ptr(gw2), L.ptr(gb2), mode, st), "sorted")
             L.check(lib.mmpde_gnn_edge_source_sum_sorted(L.ptr(ge), L.ptr(off), n, L.ptr(gb), st), "sum")
         else:

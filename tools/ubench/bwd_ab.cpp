@@ -60,6 +60,10 @@ int main() {
     const int64_t sb = mmpde_reverse_adjacency_scratch_bytes(n, K, n);
     void *scratch;
     CK(hipMalloc(&scratch, sb));
+    // relu mask (timing only: a fixed pattern, about half the bits set)
+    uint32_t *mask;
+    CK(hipMalloc(&mask, n * K * 16));
+    CK(hipMemset(mask, 0x5a, n * K * 16));
     CK(mmpde_reverse_adjacency(dnb, n, K, nullptr, n, off, edge, pos, scratch, sb, bad, nullptr));
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
@@ -81,8 +85,12 @@ int main() {
     });
     timed("source_sum (gather)", [&] { mmpde_gnn_edge_source_sum(ge, off, edge, n, gb, nullptr); });
     timed("backward_sorted f16x3 (source-major rows)", [&] {
-        mmpde_gnn_edge_backward_sorted(da, db, dnb, nullptr, n, K, dw2, db2, dg, pos, ga, ge, part, gw2, gb2, 1,
-                                       nullptr);
+        mmpde_gnn_edge_backward_sorted(da, db, dnb, nullptr, n, K, dw2, db2, dg, pos, nullptr, ga, ge, part, gw2,
+                                       gb2, 1, nullptr);
+    });
+    timed("backward_sorted f16x3 + forward relu mask", [&] {
+        mmpde_gnn_edge_backward_sorted(da, db, dnb, nullptr, n, K, dw2, db2, dg, pos, mask, ga, ge, part, gw2, gb2,
+                                       1, nullptr);
     });
     timed("source_sum_sorted (contiguous)", [&] { mmpde_gnn_edge_source_sum_sorted(ge, off, n, gb, nullptr); });
     timed("reverse_adjacency (+ slot positions)", [&] {
