@@ -274,11 +274,14 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
     __shared__ float gms[FT * FAW];            // g / deg rows (0 for rows past n)
     // relu(z1) images double-buffered by slot parity (no barrier between a
     // slot's last readers and the next slot's writers)
-    __shared__ _Float16 za[2][2][FT * FAS];    // [slot & 1] relu(z1) sz: hi, lo, [edge][kk]
+    // MASK: no z2 GEMM, so no row-major relu(z1) image; gz2 double-buffered by
+    // slot parity instead (one barrier per slot)
+    constexpr int NZA = MASK ? 1 : 2, NGB = MASK ? 2 : 1;
+    __shared__ _Float16 za[NZA][2][MASK ? 8 : FT * FAS];  // [slot & 1] relu(z1) sz: hi, lo, [edge][kk]
     __shared__ _Float16 zb[2][2][BH * FCS];    // the same, [kk][edge]
-    __shared__ _Float16 gr[2][FT * FAS];       // gz2 sg, [edge][c]
-    __shared__ _Float16 gt[2][BH * FCS];       // the same, [c][edge]
-    __shared__ uint8_t zm[2][BH * (FT / 8)];   // z1 > 0, [kk][edge / 8] bits
+    __shared__ _Float16 grb[NGB][2][FT * FAS];  // gz2 sg, [edge][c] ([slot & 1] with MASK)
+    __shared__ _Float16 gtb[NGB][2][BH * FCS];  // the same, [c][edge]
+    __shared__ __attribute__((aligned(16))) uint8_t zm[2][BH * (FT / 8)];  // z1 > 0, [kk][edge / 8] bits
     __shared__ int nb[FT * FKMAX];             // the tile's neighbour rows (clamped)
     __shared__ int gzr[FT * FKMAX];            // the gz1 rows of the tile's slots
     __shared__ int dg[FT];                     // degrees (0 past n)
@@ -341,6 +344,19 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
                 mnext[i] = p.mask[(min(row0 + rr, nmax) * k) * 4 + (wave >> 1)];
             }
         }
+        // MASK (registers to spare without the z2 operands): the tile's a values
+        // of P1, and g / deg and the degrees of P2, in registers for the tile
+        float atv[MASK ? 8 : 1], gmv[MASK ? 8 : 1];
+        int dgv[MASK ? 8 : 1];
+        if (MASK) {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                atv[t] = at[(8 * eg + t) * FAW + kk1];
+                const int rr = 16 * (t >> 2) + 4 * g + (t & 3);
+                gmv[t] = gms[rr * FAW + col];
+                dgv[t] = dg[rr];
+            }
+        }
         f32x4 gacc[2] = {(f32x4){0.0f, 0.0f, 0.0f, 0.0f}, (f32x4){0.0f, 0.0f, 0.0f, 0.0f}};
         // ---- P1 of slot e into buffer e & 1; issues the b loads of slot e + 1
         // (clamped at the last slot: a harmless reload)
@@ -351,15 +367,15 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
 #pragma unroll
             for (int t = 0; t < 8; ++t) {
                 const int ed = 8 * eg + t;
-                const float z = at[ed * FAW + kk1] + bv[t];
+                const float z = (MASK ? atv[MASK ? t : 0] : at[ed * FAW + kk1]) + bv[t];
                 bits |= (z > 0.0f ? 1u : 0u) << t;
                 _Float16 h, l;
                 split1(fmaxf(z, 0.0f) * sz, h, l);
                 hi[t] = h;
                 lo[t] = l;
                 if (!MASK) {
-                    za[sb][0][ed * FAS + kk1] = h;
-                    za[sb][1][ed * FAS + kk1] = l;
+                    za[MASK ? 0 : sb][0][ed * FAS + kk1] = h;
+                    za[MASK ? 0 : sb][1][ed * FAS + kk1] = l;
                 }
             }
             *(half8 *)&zb[sb][0][kk1 * FCS + 8 * eg] = hi;
@@ -372,14 +388,16 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
         // ---- P2: z2 and gz2 (column c = col) of slot e
         auto p2 = [&](int e) {
             const int sb = e & 1;
+            _Float16(*gr)[FT * FAS] = grb[MASK ? sb : 0];
+            _Float16(*gt)[BH * FCS] = gtb[MASK ? sb : 0];
             f32x4 acc[2] = {(f32x4){0.0f, 0.0f, 0.0f, 0.0f}, (f32x4){0.0f, 0.0f, 0.0f, 0.0f}};
             if (!MASK) {
 #pragma unroll
                 for (int s = 0; s < 4; ++s) {
 #pragma unroll
                     for (int rb = 0; rb < 2; ++rb) {
-                        const half8 ah = *(const half8 *)&za[sb][0][(16 * rb + r) * FAS + 32 * s + 8 * g];
-                        const half8 al = *(const half8 *)&za[sb][1][(16 * rb + r) * FAS + 32 * s + 8 * g];
+                        const half8 ah = *(const half8 *)&za[MASK ? 0 : sb][0][(16 * rb + r) * FAS + 32 * s + 8 * g];
+                        const half8 al = *(const half8 *)&za[MASK ? 0 : sb][1][(16 * rb + r) * FAS + 32 * s + 8 * g];
                         acc[rb] = mfma_f16(ah, w1h[s], acc[rb]);
                         acc[rb] = mfma_f16(ah, w1l[s], acc[rb]);
                         acc[rb] = mfma_f16(al, w1h[s], acc[rb]);
@@ -407,8 +425,8 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
                     const int rr = 16 * rb + 4 * g + q;
                     const bool z2pos = MASK ? ((mk[4 * rb + q] >> (16 * (wave & 1) + r)) & 1u) != 0
                                              : acc[rb][q] * un1 + bias > 0.0f;
-                    const bool on = e < dg[rr] && z2pos;
-                    const float v = on ? gms[rr * FAW + col] : 0.0f;
+                    const bool on = e < (MASK ? dgv[MASK ? 4 * rb + q : 0] : dg[rr]) && z2pos;
+                    const float v = on ? (MASK ? gmv[MASK ? 4 * rb + q : 0] : gms[rr * FAW + col]) : 0.0f;
                     db += v;
                     split1(v * sg, hv[q], lv[q]);
                     gr[0][rr * FAS + col] = hv[q];
@@ -426,6 +444,8 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
         // writes and VALU work in the MFMAs' shadow.
         auto p3 = [&](int e, bool next) {
             const int sb = e & 1;
+            const _Float16(*gr)[FT * FAS] = grb[MASK ? sb : 0];
+            const _Float16(*gt)[BH * FCS] = gtb[MASK ? sb : 0];
             if (next) p1(e + 1);
             f32x4 acc[2] = {(f32x4){0.0f, 0.0f, 0.0f, 0.0f}, (f32x4){0.0f, 0.0f, 0.0f, 0.0f}};
 #pragma unroll
@@ -441,6 +461,15 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
             }
             const half8 gh = *(const half8 *)&gt[0][col * FCS + 8 * g];
             const half8 gl = *(const half8 *)&gt[1][col * FCS + 8 * g];
+            // the epilogue's LDS values, read ahead of the dW2 MFMAs: the z1 > 0
+            // bits of column col (bit rr of the 4 bytes), and (MASK, registers
+            // to spare) the gz1 rows of the lane's 8 slots
+            const uint32_t zbits = *(const uint32_t *)&zm[sb][col * 4];
+            int gzrow[MASK ? 8 : 1];
+            if (MASK) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) gzrow[i] = gzr[(16 * (i >> 2) + 4 * g + (i & 3)) * FKMAX + e];
+            }
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const half8 bh = *(const half8 *)&zb[sb][0][(16 * j + r) * FCS + 8 * g];
@@ -454,10 +483,11 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const int rr = 16 * rb + 4 * g + q;
-                    const bool pos = (zm[sb][col * 4 + (rr >> 3)] >> (rr & 7)) & 1u;
+                    const bool pos = (zbits >> rr) & 1u;
                     const float v = pos ? acc[rb][q] * un2 : 0.0f;
                     gacc[rb][q] += v;
-                    if (row0 + rr < p.n) p.gz1[(int64_t)gzr[rr * FKMAX + e] * BH + col] = v;
+                    const int grow = MASK ? gzrow[MASK ? 4 * rb + q : 0] : gzr[rr * FKMAX + e];
+                    if (row0 + rr < p.n) p.gz1[(int64_t)grow * BH + col] = v;
                 }
             }
         };
@@ -466,22 +496,41 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
         // and P3(e - 1), both before the previous barrier; P2(e + 1) reads
         // them after the barrier that ends P1(e + 1), and rewrites gr / gt
         // only after every wave's P3(e) (the same barrier).
-        p1(0);
-        __syncthreads();
-        for (int e = 0; e + 1 < k; ++e) {
-            p2(e);
+        if (MASK) {
+            // P2 reads no LDS image (the bits and g / deg only): P1 + P2 of a slot
+            // form one phase, and with every buffer a P3 reads held by slot
+            // parity, one barrier per slot -- a wave done with P3(e) builds slot
+            // e + 1 while the others still multiply.  P1 / P2(e + 1) write the
+            // (e + 1) & 1 buffers, last read by P3(e - 1), which every wave left
+            // before the previous barrier.
+            p1(0);
+            p2(0);
             __syncthreads();
-            if (kBwdP1First) {
-                p3(e, true);
-            } else {
+            for (int e = 0; e + 1 < k; ++e) {
                 p3(e, false);
                 p1(e + 1);
+                p2(e + 1);
+                __syncthreads();
             }
+            p3(k - 1, false);
+        } else {
+            p1(0);
             __syncthreads();
+            for (int e = 0; e + 1 < k; ++e) {
+                p2(e);
+                __syncthreads();
+                if (kBwdP1First) {
+                    p3(e, true);
+                } else {
+                    p3(e, false);
+                    p1(e + 1);
+                }
+                __syncthreads();
+            }
+            p2(k - 1);
+            __syncthreads();
+            p3(k - 1, false);
         }
-        p2(k - 1);
-        __syncthreads();
-        p3(k - 1, false);
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb) {
 #pragma unroll
