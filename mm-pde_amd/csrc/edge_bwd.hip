@@ -220,7 +220,7 @@ __global__ __launch_bounds__(256, 1) void edge_bwd_kernel(EdgeBwdArgs p) {
 //       [z2 + b2 > 0][e < deg] split -> LDS row-major (A of gm1) and
 //       column-major (A of dW2); db2 in fp32
 //   P3  gm1 = gz2 W2 (wave w: columns 16w..), gz1 = gm1 [z1 > 0] -> grad_edge
-//       and the dL/da sums; dW2 += gz2^T relu(z1) (wave w: rows 16w..)
+//       and the dL/da sums; dW2 += gz2^T relu(z1) (wave w: a 2 x 4 block of tiles)
 // Deterministic: fixed orders, per-workgroup partials, no atomics in the sums.
 // ---------------------------------------------------------------------------
 constexpr int FT = 32;          // targets per tile
@@ -437,7 +437,7 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
                 *(half4 *)&gt[1][col * FCS + 16 * rb + 4 * g] = (half4){lv[0], lv[1], lv[2], lv[3]};
             }
         };
-        // ---- P3 of slot e: gm1 -> gz1 (column kk = col); dW2 rows 16 wave ..
+        // ---- P3 of slot e: gm1 -> gz1 (column kk = col); this wave's dW2 tiles
         // With `next`, P1 of slot e + 1 (the other buffer) goes in front of
         // P3's MFMAs in the same straight-line block (its b prefetch is
         // clamped, not branched), so that the scheduler can issue its LDS
@@ -459,8 +459,14 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
                     acc[rb] = mfma_f16(al, w2h[s], acc[rb]);
                 }
             }
-            const half8 gh = *(const half8 *)&gt[0][col * FCS + 8 * g];
-            const half8 gl = *(const half8 *)&gt[1][col * FCS + 8 * g];
+            // dW2 tiles of this wave: c tiles 2 (wave & 3) + i (i < 2) x kk tiles
+            // 4 (wave >> 2) + jj (jj < 4): 4 A and 8 B fragment reads per slot
+            // (a c-row of tiles would read 2 A and all 16 B fragments)
+            const int cw = 32 * (wave & 3) + r;
+            const half8 gh0 = *(const half8 *)&gt[0][cw * FCS + 8 * g];
+            const half8 gl0 = *(const half8 *)&gt[1][cw * FCS + 8 * g];
+            const half8 gh1 = *(const half8 *)&gt[0][(cw + 16) * FCS + 8 * g];
+            const half8 gl1 = *(const half8 *)&gt[1][(cw + 16) * FCS + 8 * g];
             // the epilogue's LDS values, read ahead of the dW2 MFMAs: the z1 > 0
             // bits of column col (bit rr of the 4 bytes), and (MASK, registers
             // to spare) the gz1 rows of the lane's 8 slots
@@ -471,12 +477,16 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
                 for (int i = 0; i < 8; ++i) gzrow[i] = gzr[(16 * (i >> 2) + 4 * g + (i & 3)) * FKMAX + e];
             }
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
+            for (int jj = 0; jj < 4; ++jj) {
+                const int j = 4 * (wave >> 2) + jj;
                 const half8 bh = *(const half8 *)&zb[sb][0][(16 * j + r) * FCS + 8 * g];
                 const half8 bl = *(const half8 *)&zb[sb][1][(16 * j + r) * FCS + 8 * g];
-                dw[j] = mfma_f16(gh, bh, dw[j]);
-                dw[j] = mfma_f16(gh, bl, dw[j]);
-                dw[j] = mfma_f16(gl, bh, dw[j]);
+                dw[2 * jj] = mfma_f16(gh0, bh, dw[2 * jj]);
+                dw[2 * jj] = mfma_f16(gh0, bl, dw[2 * jj]);
+                dw[2 * jj] = mfma_f16(gl0, bh, dw[2 * jj]);
+                dw[2 * jj + 1] = mfma_f16(gh1, bh, dw[2 * jj + 1]);
+                dw[2 * jj + 1] = mfma_f16(gh1, bl, dw[2 * jj + 1]);
+                dw[2 * jj + 1] = mfma_f16(gl1, bh, dw[2 * jj + 1]);
             }
 #pragma unroll
             for (int rb = 0; rb < 2; ++rb) {
@@ -540,13 +550,15 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
             }
         }
     }
-    // partials: dW2[c = 16 wave + 4 g + q][kk = 16 j + r], db2[col]
+    // partials: dW2[c = 32 (wave & 3) + 16 (j & 1) + 4 g + q][kk = 16 (4 (wave >> 2) + (j >> 1)) + r], db2[col]
     const float und = pow2_inv(sg) * pow2_inv(sz);
     float *pw = p.pw2 + (int64_t)blockIdx.x * BH * BH;
 #pragma unroll
     for (int j = 0; j < 8; ++j)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) pw[(16 * wave + 4 * g + q) * BH + 16 * j + r] = dw[j][q] * und;
+        for (int q = 0; q < 4; ++q)
+            pw[(32 * (wave & 3) + 16 * (j & 1) + 4 * g + q) * BH + 16 * (4 * (wave >> 2) + (j >> 1)) + r] =
+                dw[j][q] * und;
     const float v1 = __shfl(db, r + 16, 64), v2 = __shfl(db, r + 32, 64), v3 = __shfl(db, r + 48, 64);
     if (g == 0) p.pb2[(int64_t)blockIdx.x * BH + col] = ((db + v1) + v2) + v3;
 }
