@@ -64,6 +64,43 @@ __device__ __forceinline__ float wave_max(float v) {
     return v;
 }
 
+// Max reductions of non-negative floats (|x| maxima, never NaN) without the
+// LDS pipe (a __shfl_xor is a ds_bpermute round trip): on their bit patterns
+// (for x, y >= 0, bits(max(x, y)) = max(bits(x), bits(y)), and the integer max
+// needs no NaN canonicalisation), DPP within 16-lane rows, v_permlane16/32_swap
+// across rows.  Every lane of the wave must be active (a DPP read of a
+// disabled lane is not defined).  The swaps' outputs with both operands v:
+// lane l's partner value (l ^ 16, l ^ 32) is output 0 in the upper row (half),
+// output 1 in the lower (as knn.hip's xor_lane).
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t umax_rows16(uint32_t v) {  // max with lane ^ 16
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return max(v, (__lane_id() & 16) ? r[0] : r[1]);
+}
+__device__ __forceinline__ uint32_t umax_rows32(uint32_t v) {  // max with lane ^ 32
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return max(v, (__lane_id() & 32) ? r[0] : r[1]);
+}
+// max over the wave of v >= 0 (quad [1,0,3,2], quad [2,3,0,1], row_half_mirror,
+// row_mirror, then across rows)
+__device__ __forceinline__ float wave_absmax(float v) {
+    uint32_t u = __builtin_bit_cast(uint32_t, v);
+    u = max(u, dpp_u<0xB1>(u));
+    u = max(u, dpp_u<0x4E>(u));
+    u = max(u, dpp_u<0x141>(u));
+    u = max(u, dpp_u<0x140>(u));
+    return __builtin_bit_cast(float, umax_rows32(umax_rows16(u)));
+}
+// max of v >= 0 over lanes l, l ^ 8, l ^ 16, ... l ^ 56 (row_ror:8 = lane ^ 8 in a 16-lane row)
+__device__ __forceinline__ float absmax_stride8(float v) {
+    uint32_t u = __builtin_bit_cast(uint32_t, v);
+    u = max(u, dpp_u<0x128>(u));
+    return __builtin_bit_cast(float, umax_rows32(umax_rows16(u)));
+}
+
 __device__ __forceinline__ float act_apply(float v, int act) {
     if (act == MMPDE_ACT_TANH) return tanhf(v);
     if (act == MMPDE_ACT_RELU) return fmaxf(v, 0.0f);

@@ -616,10 +616,25 @@ __device__ __forceinline__ void prep_finish(float4 (&x)[4], const float *src, in
         // side blocks of the units u of this row's segment whose first slot
         // s0(u) = floor(u S / U) lies strictly inside the row's 16-row tile
         // t (local): t k < s0(u) < (t + 1) k
-        const int64_t sg = srow / split->seg_n, q = srow - sg * split->seg_n, t = q / 16;
         const int64_t S = split->S, G = split->units, kk = split->k;
-        const int64_t lo = max(((t * kk + 1) * G + S - 1) / S, (int64_t)1);
-        const int64_t hi = min(((t + 1) * kk * G + S - 1) / S - 1, G - 1);
+        int64_t sg, q, lo, hi;
+        if ((uint64_t)(S + 1) * (uint64_t)(G + 1) + (uint64_t)split->seg_n < 0xffffffffull) {
+            // 32-bit divisions (wave-uniform test: a 64-bit one is a long
+            // instruction sequence, three per row here)
+            const uint32_t sn = (uint32_t)split->seg_n, r32 = (uint32_t)srow;
+            const uint32_t sg32 = r32 / sn, q32 = r32 - sg32 * sn, t = q32 / 16;
+            const uint32_t S32 = (uint32_t)S, G32 = (uint32_t)G, k32 = (uint32_t)kk;
+            sg = sg32;
+            q = q32;
+            lo = max(((t * k32 + 1) * G32 + S32 - 1) / S32, 1u);
+            hi = min(((t + 1) * k32 * G32 + S32 - 1) / S32 - 1, G32 - 1);
+        } else {
+            sg = srow / split->seg_n;
+            q = srow - sg * split->seg_n;
+            const int64_t t = q / 16;
+            lo = max(((t * kk + 1) * G + S - 1) / S, (int64_t)1);
+            hi = min(((t + 1) * kk * G + S - 1) / S - 1, G - 1);
+        }
         for (int64_t w = lo; w <= hi; ++w) {
             const float *q4 = split->side + ((sg * G + w) * 16 + (q & 15)) * 128 + 16 * part;
 #pragma unroll
@@ -642,9 +657,7 @@ __device__ __forceinline__ void prep_finish(float4 (&x)[4], const float *src, in
         float m = 0.0f;
 #pragma unroll
         for (int q = 0; q < 4; ++q) m = absmax4(m, x[q]);
-        m = fmaxf(m, __shfl_xor(m, 8, 64));
-        m = fmaxf(m, __shfl_xor(m, 16, 64));
-        m = fmaxf(m, __shfl_xor(m, 32, 64));
+        m = absmax_stride8(m);  // the row's 8 parts (lanes l ^ 8, ^ 16, ^ 32)
         const float s = split_scale(m);
         if (part == 0) rs[row] = s;
 #pragma unroll
@@ -768,7 +781,7 @@ __device__ __forceinline__ void proj_phase(const BOps<F16X3, F16X3 ? 4 : 8> &bA,
                                            const float *rs, const float *rowv, const W1C &w,
                                            const char *pk, const float *w1r, int tw, int64_t row0,
                                            int64_t n, int64_t seg_n, float *a_out, float *b_out,
-                                           float *rng_out, int wave, int lane,
+                                           float *rng_out, uint32_t *arrived, int wave, int lane,
                                            const BOps<F16X3, F16X3 ? 4 : 8> *bBpre = nullptr) {
     constexpr int ROWS = 16 * RB, S1 = F16X3 ? 4 : 8;
     const int col = 16 * wave + (lane & 15), g = lane >> 4;
@@ -778,9 +791,11 @@ __device__ __forceinline__ void proj_phase(const BOps<F16X3, F16X3 ? 4 : 8> &bA,
     // |a|, |b| maxima of each 16-row block's rows in the block's first segment
     // (0) and in the next one (1), for the block's range record (layer.hpp:
     // kRangeRows = 16; seg_n >= 16: a block touches at most two segments)
-    float amx[RB][2], bmx[RB][2];
+    // (as bit patterns: for x, y >= 0 the integer max is the float max, with no
+    // NaN canonicalisation)
+    uint32_t amx[RB][2], bmx[RB][2];
 #pragma unroll
-    for (int rb = 0; rb < RB; ++rb) amx[rb][0] = amx[rb][1] = bmx[rb][0] = bmx[rb][1] = 0.0f;
+    for (int rb = 0; rb < RB; ++rb) amx[rb][0] = amx[rb][1] = bmx[rb][0] = bmx[rb][1] = 0u;
     // stores at immediate offsets from one base per lane; the row test only
     // for a tile that runs past n (wave-uniform)
     const bool full = row0 + ROWS <= n;
@@ -791,7 +806,15 @@ __device__ __forceinline__ void proj_phase(const BOps<F16X3, F16X3 ? 4 : 8> &bA,
         for (int c = 1; c < tw; ++c) node += w1r[256 + c] * rowv[(3 + c) * ROWS + lr];
         return node + w.dx * rowv[ROWS + lr] + w.dy * rowv[2 * ROWS + lr];
     };
-    auto seg_of = [&](int rb, int lr) { return (int)(row0 + lr >= ((row0 + 16 * rb) / seg_n + 1) * seg_n); };
+    // first row of the segment after block rb's first segment: two divisions
+    // per wave here, not a 64-bit division per stored value in the epilogue
+    int64_t seg_next[RB];
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) seg_next[rb] = ((row0 + 16 * rb) / seg_n + 1) * seg_n;
+    auto seg_of = [&](int rb, int lr) { return (int)(row0 + lr >= seg_next[rb]); };
+    // the tile crosses a segment boundary (wave-uniform): only then are there
+    // second-segment maxima to keep
+    const bool cross = seg_next[0] < row0 + ROWS;
     gemm_tile<F16X3, RB, S1>(aA, img, 128, 0, bA, lane);
     {
         if (bBpre) {  // operands of b preloaded (the weight-stationary node kernel)
@@ -801,38 +824,56 @@ __device__ __forceinline__ void proj_phase(const BOps<F16X3, F16X3 ? 4 : 8> &bA,
             bB.load(pk + kPkW1, 4, 8 + wave, 0, w1r, 128, lane);
             gemm_tile<F16X3, RB, S1>(aB, img, 128, 0, bB, lane);
         }
+        auto epilogue = [&](auto CROSS) {
 #pragma unroll
-        for (int rb = 0; rb < RB; ++rb) {
+            for (int rb = 0; rb < RB; ++rb) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int lr = 16 * rb + 4 * g + q;
-                if (full || row0 + lr < n) {
-                    float za = aA[rb][q], zb = aB[rb][q];
-                    if (F16X3) {
-                        const float ir = pow2_inv(rs[lr]);
-                        za = za * ir * w.isa;
-                        zb = zb * ir * w.isb;
+                for (int q = 0; q < 4; ++q) {
+                    const int lr = 16 * rb + 4 * g + q;
+                    if (full || row0 + lr < n) {
+                        float za = aA[rb][q], zb = aB[rb][q];
+                        if (F16X3) {
+                            const float ir = pow2_inv(rs[lr]);
+                            za = za * ir * w.isa;
+                            zb = zb * ir * w.isb;
+                        }
+                        const float node = node_term(lr);
+                        const float va = za + node + w.t * rowv[lr] + w.b;
+                        const float vb = zb - node;
+                        ap[(16 * rb + q) * LH] = va;
+                        bp[(16 * rb + q) * LH] = vb;
+                        // |v| with NaN -> 0 (fmaxf ignores a NaN, as the float max did)
+                        const uint32_t ua = __builtin_bit_cast(uint32_t, fmaxf(fabsf(va), 0.0f));
+                        const uint32_t ub = __builtin_bit_cast(uint32_t, fmaxf(fabsf(vb), 0.0f));
+                        if (decltype(CROSS)::value) {
+                            const int sx = seg_of(rb, lr);
+                            amx[rb][sx] = max(amx[rb][sx], ua);
+                            bmx[rb][sx] = max(bmx[rb][sx], ub);
+                        } else {
+                            amx[rb][0] = max(amx[rb][0], ua);
+                            bmx[rb][0] = max(bmx[rb][0], ub);
+                        }
                     }
-                    const float node = node_term(lr);
-                    const float va = za + node + w.t * rowv[lr] + w.b;
-                    const float vb = zb - node;
-                    ap[(16 * rb + q) * LH] = va;
-                    bp[(16 * rb + q) * LH] = vb;
-                    const int sx = seg_of(rb, lr);
-                    amx[rb][sx] = fmaxf(amx[rb][sx], fabsf(va));
-                    bmx[rb][sx] = fmaxf(bmx[rb][sx], fabsf(vb));
                 }
             }
-        }
+        };
+        if (cross) epilogue(std::true_type{});
+        else epilogue(std::false_type{});
     }
     if (rng_out) {
-        // wave maxima, then the workgroup's through LDS: one float4 record per
-        // 16-row block
+        // wave maxima, then the workgroup's, one float4 record per 16-row block,
+        // without a barrier: each wave posts its maxima to LDS and counts itself
+        // in (LDS atomic); the last of the 8 to arrive reduces and stores.  (A
+        // __syncthreads here also waits for every wave's a' / b' stores: 7-8 us
+        // of the 54 us node launch at cy B=16.)  The max is order-free, so the
+        // record does not depend on the arrival order.
         __shared__ float red[8][RB][4];
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) {
-            const float m0 = wave_max(amx[rb][0]), m1 = wave_max(bmx[rb][0]), m2 = wave_max(amx[rb][1]),
-                        m3 = wave_max(bmx[rb][1]);
+            const float m0 = wave_absmax(__builtin_bit_cast(float, amx[rb][0]));
+            const float m1 = wave_absmax(__builtin_bit_cast(float, bmx[rb][0]));
+            const float m2 = cross ? wave_absmax(__builtin_bit_cast(float, amx[rb][1])) : 0.0f;
+            const float m3 = cross ? wave_absmax(__builtin_bit_cast(float, bmx[rb][1])) : 0.0f;
             if (lane == 0) {
                 red[wave][rb][0] = m0;
                 red[wave][rb][1] = m1;
@@ -840,8 +881,12 @@ __device__ __forceinline__ void proj_phase(const BOps<F16X3, F16X3 ? 4 : 8> &bA,
                 red[wave][rb][3] = m3;
             }
         }
-        __syncthreads();
-        if (wave == 0 && lane < 4 * RB) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // posted before counted
+        uint32_t prev = 0;
+        if (lane == 0) prev = __hip_atomic_fetch_add(arrived, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        prev = __builtin_amdgcn_readfirstlane(prev);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (prev == 7 && lane < 4 * RB) {
             const int rb = lane >> 2, e = lane & 3;
             float m = red[0][rb][e];
 #pragma unroll
@@ -876,9 +921,11 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs p) {
     __shared__ float hres[ROWS * NLD];          // fp32 h (residual)
     __shared__ float rs[4][ROWS];               // row scales: h, mean, v, h'
     __shared__ float rowv[3 + MAX_TW][ROWS];    // per row: t / tmax, x / Lx, y / Ly, u_0 .. u_{tw-1}
+    __shared__ uint32_t rng_arrived;            // waves done with their range maxima (proj_phase)
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int r = lane & 15, g = lane >> 4;
     const int col = 16 * wave + r;  // this lane's output column (tile = wave)
+    if (tid == 0) rng_arrived = 0;  // read after the first barrier
     const int tw = p.sc.tw > 1 ? p.sc.tw : 1;
     constexpr int S1 = F16X3 ? 4 : 8;    // K steps per 128 columns of K
     const float *wu1 = p.u1 + (int64_t)col * p.ld_u1, *wu2 = p.u2 + (int64_t)col * LH;
@@ -992,7 +1039,7 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs p) {
         NODE_STAMP(6);
         // ---- next layer's message_net_1 node halves
         proj_phase<F16X3, RB>(bA, img, rs[3], &rowv[0][0], w1c, p.pkn, w1r, tw, row0, p.n, p.seg_n,
-                              p.a_out, p.b_out, p.rng_out, wave, lane, NODE_EARLY_B ? &bB : nullptr);
+                              p.a_out, p.b_out, p.rng_out, &rng_arrived, wave, lane, NODE_EARLY_B ? &bB : nullptr);
     }
     NODE_STAMP(7);
 }
@@ -1025,6 +1072,7 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_embed_kernel(EmbedArgs p) {
     __shared__ float4 img[RB * 8 * 64];   // K = 128 operand image
     __shared__ float stage[ROWS * NLD];   // fp32 z, then h0
     __shared__ float rs[ROWS];            // h0 row scales
+    __shared__ uint32_t rng_arrived;      // waves done with their range maxima (proj_phase)
     __shared__ float rsz[ROWS];           // z row scales (F16X3 embedding GEMM)
     __shared__ float rowv[3 + MAX_TW][ROWS];  // per row: t / tmax, x / Lx, y / Ly, u_0 .. u_{tw-1}
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -1032,6 +1080,7 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_embed_kernel(EmbedArgs p) {
     const int64_t row0 = (int64_t)blockIdx.x * ROWS;
     const int col = 16 * wave + (lane & 15);
     const int tw = p.sc.tw > 1 ? p.sc.tw : 1;
+    if (tid == 0) rng_arrived = 0;  // read after the first barrier
     if (tid < ROWS) {
         const int64_t row = min(row0 + tid, p.n - 1);
         rowv[0][tid] = node_t(p.sc, p.pos, row) * p.sc.inv_tmax;
@@ -1125,7 +1174,7 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_embed_kernel(EmbedArgs p) {
     prep<F16X3, ROWS>(stage, NLD, 0, ROWS, false, img, 128, 0, rs);
     __syncthreads();
     proj_phase<F16X3, RB>(bA, img, rs, &rowv[0][0], w1c, p.pk, w1r, tw, row0, p.n, p.seg_n,
-                          p.a_out, p.b_out, p.rng_out, wave, lane, NODE_EARLY_B ? &bB : nullptr);
+                          p.a_out, p.b_out, p.rng_out, &rng_arrived, wave, lane, NODE_EARLY_B ? &bB : nullptr);
 }
 
 inline bool al16(const void *q) { return ((uintptr_t)q & 15u) == 0; }
