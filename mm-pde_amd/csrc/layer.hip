@@ -750,6 +750,33 @@ __device__ __forceinline__ void gemm_tile(f32x4 *acc, const float4 *img, int KT,
 
 constexpr int MAX_TW = 16;  // time_window (u channels) of the fused kernels
 
+// Per-row node values of one row: t / tmax, x / Lx, y / Ly, u_0 .. u_{tw-1}.
+// fetch() issues every load first (written value by value, node_t / node_x /
+// node_y's branches kept the compiler from hoisting the loads past each
+// other's LDS writes: one memory round trip per value); store() writes them
+// to rowv[.][tid].
+struct RowValues {
+    float t = 0.0f, x = 0.0f, y = 0.0f, u[MAX_TW];
+    __device__ __forceinline__ void fetch(const mmpde_gnn_scales &sc, const float *pos, const float *uu,
+                                          int64_t row, int tw) {
+        const float *pr = sc.pos_xy ? pos + row * 2 : pos + row * 3 + 1;
+        x = pr[0];
+        y = pr[1];
+        t = sc.pos_xy ? (sc.t_ptr ? *sc.t_ptr : sc.t) : pr[-1];
+#pragma unroll
+        for (int c = 0; c < MAX_TW; ++c) u[c] = c < tw ? uu[row * tw + c] : 0.0f;
+    }
+    template <int ROWS>
+    __device__ __forceinline__ void store(float (*rowv)[ROWS], const mmpde_gnn_scales &sc, int tid, int tw) const {
+        rowv[0][tid] = t * sc.inv_tmax;
+        rowv[1][tid] = x * sc.inv_lx;
+        rowv[2][tid] = y * sc.inv_ly;
+#pragma unroll
+        for (int c = 0; c < MAX_TW; ++c)
+            if (c < tw) rowv[3 + c][tid] = u[c];
+    }
+};
+
 // Per-column constants of a message_net_1 node projection (weight row w1r of
 // this lane's column: node-term columns 256 .. 256 + tw - 1 (u_i - u_j, du holds
 // the first), 256 + tw (x), 257 + tw (y), 258 + tw (t), bias, F16X3 unscale).
@@ -933,13 +960,8 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs p) {
     // everything the epilogues read from global memory is fetched up front
     // (per-row node values to LDS, per-column constants to registers), so no
     // epilogue waits on a memory round trip
-    if (tid < ROWS) {
-        const int64_t row = min(row0 + tid, p.n - 1);
-        rowv[0][tid] = node_t(p.sc, p.pos, row) * p.sc.inv_tmax;
-        rowv[1][tid] = node_x(p.sc, p.pos, row) * p.sc.inv_lx;
-        rowv[2][tid] = node_y(p.sc, p.pos, row) * p.sc.inv_ly;
-        for (int c = 0; c < tw; ++c) rowv[3 + c][tid] = p.u[row * tw + c];
-    }
+    RowValues rv;
+    if (tid < ROWS) rv.fetch(p.sc, p.pos, p.u, min(row0 + tid, p.n - 1), tw);
     const float u1_wt = wu1[256], u1_b = p.c1[col];
     const float u1_is = F16X3 ? pow2_inv(((const float *)(p.pk + kPkU1 + 131072))[col]) : 1.0f;
     const float u2_b = p.c2[col];
@@ -960,6 +982,7 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs p) {
     if (PRE) {
         bU2.load(p.pk + kPkU2, 4, wave, 0, wu2, 0, lane);
     }
+    if (tid < ROWS) rv.store<ROWS>(rowv, p.sc, tid, tw);
 
     NODE_STAMP(1);
     // ---- [h | mean] -> image (K = 256)
@@ -1081,13 +1104,8 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_embed_kernel(EmbedArgs p) {
     const int col = 16 * wave + (lane & 15);
     const int tw = p.sc.tw > 1 ? p.sc.tw : 1;
     if (tid == 0) rng_arrived = 0;  // read after the first barrier
-    if (tid < ROWS) {
-        const int64_t row = min(row0 + tid, p.n - 1);
-        rowv[0][tid] = node_t(p.sc, p.pos, row) * p.sc.inv_tmax;
-        rowv[1][tid] = node_x(p.sc, p.pos, row) * p.sc.inv_lx;
-        rowv[2][tid] = node_y(p.sc, p.pos, row) * p.sc.inv_ly;
-        for (int c = 0; c < tw; ++c) rowv[3 + c][tid] = p.u[row * tw + c];
-    }
+    RowValues rv;
+    if (tid < ROWS) rv.fetch(p.sc, p.pos, p.u, min(row0 + tid, p.n - 1), tw);
     const mmpde_gnn_embed_params &e = p.e;
     // embedding_mlp.3 weight row of this lane's column: F32 as the exact fp32
     // B operand; F16X3 split here into the fp16 hi / lo operand with a
@@ -1131,6 +1149,7 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_embed_kernel(EmbedArgs p) {
     const float zb = e.b0[c];
     BnAffine bn1;
     bn1.set(e.bn1_rm[c], e.bn1_rv[c], e.bn1_w[c], e.bn1_b[c], e.eps);
+    if (tid < ROWS) rv.store<ROWS>(rowv, p.sc, tid, tw);
     __syncthreads();
     for (int row = tid >> 7; row < ROWS; row += 4) {
         float v = zb + zw0 * rowv[3][row];

@@ -5,6 +5,8 @@
 // every workgroup stamps the shader clock at the phase boundaries.  Prints the
 // launch time (hipEvents), the mean of every phase over the workgroups, and how
 // many workgroups run at once.
+// Then times the embed kernel (embedding + layer 0's projections) with its
+// output hash.
 //   make -C tools/ubench node_phases && tools/ubench/node_phases [B]
 #include "../../mm-pde_amd/csrc/gnn.hip"
 #include "../../mm-pde_amd/csrc/layer.hip"
@@ -156,6 +158,32 @@ int main(int argc, char **argv) {
             fold(rout, 4 * range_tiles(n));
         }
         printf("  output hash %016llx\n", (unsigned long long)hsh);
+    }
+    {   // the embed kernel (embedding + layer 0's projections), time and output hash
+        auto embed = [&]() { return launch_embed_stage(u, pos, n, N, sc, &ep, &lp, pack, rngr, h0, wa, wb, 0); };
+        for (int i = 0; i < 5; ++i)
+            if (embed()) return 1;
+        hipEvent_t a, b;
+        hipEventCreate(&a);
+        hipEventCreate(&b);
+        const int it = 20;
+        hipEventRecord(a, 0);
+        for (int i = 0; i < it; ++i) embed();
+        hipEventRecord(b, 0);
+        CK(hipEventSynchronize(b));
+        float ms = 0;
+        hipEventElapsedTime(&ms, a, b);
+        uint64_t hsh = 1469598103934665603ull;
+        auto fold = [&](const float *d, size_t cnt) {
+            std::vector<uint32_t> v(cnt);
+            hipMemcpy(v.data(), d, cnt * 4, hipMemcpyDeviceToHost);
+            for (uint32_t w : v) hsh = (hsh ^ w) * 1099511628211ull;
+        };
+        fold(h0, n * H);
+        fold(wa, n * H);
+        fold(wb, n * H);
+        fold(rngr, 4 * range_tiles(n));
+        printf("embed kernel: %.2f us per launch; output hash %016llx\n", 1e3 * ms / it, (unsigned long long)hsh);
     }
     CK(hipGetLastError());
     return 0;
