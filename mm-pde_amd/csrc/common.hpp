@@ -94,6 +94,53 @@ __device__ __forceinline__ float wave_absmax(float v) {
     u = max(u, dpp_u<0x140>(u));
     return __builtin_bit_cast(float, umax_rows32(umax_rows16(u)));
 }
+// v of lane ^ O (O = 1 .. 32) without the LDS pipe; every lane active.  The
+// same exchange as __shfl_xor(v, O), so a butterfly built from it adds the
+// same operands in the same order as one built from __shfl_xor.
+template <int O>
+__device__ __forceinline__ float xor_lane_f(float v) {
+    const uint32_t u = __builtin_bit_cast(uint32_t, v);
+    uint32_t r;
+    if constexpr (O == 1) {
+        r = dpp_u<0xB1>(u);  // quad [1,0,3,2]
+    } else if constexpr (O == 2) {
+        r = dpp_u<0x4E>(u);  // quad [2,3,0,1]
+    } else if constexpr (O == 4) {
+        const uint32_t up = dpp_u<0x104>(u), dn = dpp_u<0x114>(u);  // row_shl:4 / row_shr:4
+        r = (__lane_id() & 4) ? dn : up;
+    } else if constexpr (O == 8) {
+        r = dpp_u<0x128>(u);  // row_ror:8
+    } else if constexpr (O == 16) {
+        const auto q = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+        r = (__lane_id() & 16) ? q[0] : q[1];
+    } else {
+        static_assert(O == 32, "xor_lane_f: O in 1, 2, 4, 8, 16, 32");
+        const auto q = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+        r = (__lane_id() & 32) ? q[0] : q[1];
+    }
+    return __builtin_bit_cast(float, r);
+}
+// wave_sum / wave_max with every lane active: the same butterfly (32, 16, ...,
+// 1), so the same bits, without a ds_bpermute round trip per step.
+__device__ __forceinline__ float wave_sum_full(float v) {
+    v += xor_lane_f<32>(v);
+    v += xor_lane_f<16>(v);
+    v += xor_lane_f<8>(v);
+    v += xor_lane_f<4>(v);
+    v += xor_lane_f<2>(v);
+    v += xor_lane_f<1>(v);
+    return v;
+}
+__device__ __forceinline__ float wave_max_full(float v) {
+    v = fmaxf(v, xor_lane_f<32>(v));
+    v = fmaxf(v, xor_lane_f<16>(v));
+    v = fmaxf(v, xor_lane_f<8>(v));
+    v = fmaxf(v, xor_lane_f<4>(v));
+    v = fmaxf(v, xor_lane_f<2>(v));
+    v = fmaxf(v, xor_lane_f<1>(v));
+    return v;
+}
+
 // max of v >= 0 over lanes l, l ^ 8, l ^ 16, ... l ^ 56 (row_ror:8 = lane ^ 8 in a 16-lane row)
 __device__ __forceinline__ float absmax_stride8(float v) {
     uint32_t u = __builtin_bit_cast(uint32_t, v);

@@ -110,8 +110,8 @@ __device__ __forceinline__ float4 dmm_node_update(const DmmGnnSmem &w, const flo
                                                   const float *bnrm, const float *bnrv, float eps) {
 #pragma unroll
     for (int o = 0; o < 4; ++o) {
-        sum[o] += __shfl_xor(sum[o], 1, 64);
-        sum[o] += __shfl_xor(sum[o], 2, 64);
+        sum[o] += xor_lane_f<1>(sum[o]);
+        sum[o] += xor_lane_f<2>(sum[o]);
     }
     float cat[8];
 #pragma unroll
@@ -357,8 +357,8 @@ __global__ __launch_bounds__(256) void mesh_vjp_kernel(const float *__restrict__
             gx += g * jj.x;
             gy += g * jj.y;
         }
-        gx = wave_sum(gx);
-        gy = wave_sum(gy);
+        gx = wave_sum_full(gx);
+        gy = wave_sum_full(gy);
         if (lane == 0) mesh[b * n_per + nidx] = make_float2(gx + x.x, gy + x.y);
     }
 }
@@ -402,8 +402,8 @@ __global__ __launch_bounds__(256) void mesh_vjp_wave_kernel(const float *__restr
             gx += g * jj[i].x;
             gy += g * jj[i].y;
         }
-        gx = wave_sum(gx);
-        gy = wave_sum(gy);
+        gx = wave_sum_full(gx);
+        gy = wave_sum_full(gy);
         if (lane == 0) mesh[(int64_t)b * n_per + nidx] = make_float2(gx + x.x, gy + x.y);
     }
 }
@@ -426,7 +426,7 @@ __global__ __launch_bounds__(256) void phi_kernel(const float *__restrict__ P, c
         if (second) second[i * hidden + kk] = t;
         acc += wo[kk] * t;
     }
-    acc = wave_sum(acc);
+    acc = wave_sum_full(acc);
     if (lane == 0) phi[i] = acc + (bo ? bo[0] : 0.0f);
 }
 

@@ -685,10 +685,10 @@ __global__ __launch_bounds__(kCellThreads) void knn_cells_kernel(const float2 *_
         mxx = fmaxf(mxx, c.x);
         mxy = fmaxf(mxy, c.y);
     }
-    mnx = -wave_max(-mnx);
-    mny = -wave_max(-mny);
-    mxx = wave_max(mxx);
-    mxy = wave_max(mxy);
+    mnx = -wave_max_full(-mnx);
+    mny = -wave_max_full(-mny);
+    mxx = wave_max_full(mxx);
+    mxy = wave_max_full(mxy);
     if (lane == 0) {
         red[wave][0] = mnx;
         red[wave][1] = mny;
@@ -728,7 +728,7 @@ __global__ __launch_bounds__(kCellThreads) void knn_cells_kernel(const float2 *_
         // statistic skip_above is compared with), empty cells last
         srt[tid] = v == 0u ? 3.0e38f : dc;
     }
-    const float dall = wave_max(fmaxf(dc, 0.0f));
+    const float dall = wave_max_full(fmaxf(dc, 0.0f));
     const int nonempty = __popcll(__ballot(v != 0u));
     __syncthreads();  // red (read above) and srt
     if (lane == 0 && wave < kCells / 64) {
