@@ -26,7 +26,7 @@ __device__ __forceinline__ float segment_range(const float *rng, int64_t seg_n, 
         ma = fmaxf(ma, own ? v.x : v.z);
         mb = fmaxf(mb, own ? v.y : v.w);
     }
-    return wave_max(ma) + wave_max(mb);
+    return wave_absmax(ma) + wave_absmax(mb);  // maxima of |x| >= 0; every lane active
 }
 
 // How the wave edge kernel split a layer's neighbour slots (edge_wave.hip
