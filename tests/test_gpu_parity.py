@@ -635,6 +635,34 @@ def test_gnn_forward_ragged_k(dev, k, mode):
     _close(out, ref, 1e-5, 1e-9, f"gnn k={k} {mode}")
 
 
+@pytest.mark.parametrize("mode", ["f32", "f16x3"])
+def test_gnn_forward_segments_cross_tiles(dev, mode):
+    """Trajectory segments of 37 rows, so 16-row range blocks and 32-row node
+    tiles straddle segment boundaries (the node epilogue's second-segment
+    maxima, the edge kernel's per-segment units and side blocks): against the
+    oracle, and each trajectory of the batch bitwise equal to it launched alone."""
+    from mmpde_amd.rollout import _Nodes
+    from mmpde_amd.synth import build_models
+
+    pde, model, _, _, _, _ = build_models("cy", moving_mesh=False, seed=5)
+    B, N, k = 3, 37, 35
+    torch.manual_seed(11)
+    pts = torch.rand(B * N, 2)
+    pos = torch.cat((torch.full((B * N, 1), 0.4), pts), 1)
+    u = torch.randn(B * N, 1)
+    ei, nbr, _ = refcpu.knn_graph(pts, k, B)
+    opde = refcpu.PDEConst("cy", pde.grid_size, ori_grid=pde.ori_grid)
+    ref = refcpu.mp_pde_solver(_sds(m=model)["m"], opde, u, pos, ei)
+    model.to(dev)
+    model.edge_gemm = mode
+    out = model(_Nodes(u.to(dev), pos.to(dev), nbr.int().to(dev), seg_n=N))
+    _close(out, ref, 1e-5, 1e-9, f"gnn 3 x 37-row segments {mode}")
+    for j in range(B):
+        rows = slice(j * N, (j + 1) * N)
+        alone = model(_Nodes(u[rows].to(dev), pos[rows].to(dev), (nbr[rows] - j * N).int().to(dev), seg_n=N))
+        assert torch.equal(out[rows], alone), (mode, j)
+
+
 # ============================================================================ hipGraph replay
 @pytest.mark.parametrize("kind", ["cy", "burgers"])
 def test_graph_replay_matches_eager(dev, kind):
