@@ -139,6 +139,20 @@ __device__ __forceinline__ uint32_t xor_lane(uint32_t v, int j, int lane) {
     }
 }
 
+// v of lane l, l wave-uniform (a kernel argument or from a ballot): v_readlane
+// into an SGPR instead of a ds_bpermute round trip (the same value).
+template <typename T>
+__device__ __forceinline__ T lane_value(T v, int l) {
+    if constexpr (sizeof(T) == 8) {
+        const uint64_t u = (uint64_t)v;
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+        return (T)(((uint64_t)hi << 32) | lo);
+    } else {
+        return (T)__builtin_amdgcn_readlane((int)v, l);
+    }
+}
+
 template <typename K>
 __device__ __forceinline__ K shfl_xor_key(K v, int m, int lane) {
     if constexpr (sizeof(K) == 8) {
@@ -276,7 +290,7 @@ __device__ __forceinline__ void knn_finish(const float2 *sP, typename KeyTraits<
         if (lane < kk) mi = i0;
         if (QUERY) {  // element lane + 1: lane 63's is element 64 (k1 of lane 0)
             const key_t n0 = (key_t)__shfl((unsigned long long)k0, (lane + 1) & 63, 64);
-            const key_t n1 = (key_t)__shfl((unsigned long long)k1, 0, 64);
+            const key_t n1 = lane_value(k1, 0);
             tie = __ballot(lane < kk && k0 == (lane == 63 ? n1 : n0)) != 0ull;
         }
     } else if (m <= kCap) {
@@ -361,7 +375,7 @@ __device__ __forceinline__ void knn_finish(const float2 *sP, typename KeyTraits<
     } else {
         const uint64_t smask = __ballot(lane < kk && mi == qi);
         const bool has_self = smask != 0ull;
-        const int self_rank = has_self ? __shfl(rank, __ffsll((unsigned long long)smask) - 1, 64) : kk;
+        const int self_rank = has_self ? lane_value(rank, __ffsll((unsigned long long)smask) - 1) : kk;
         const int pos = rank - ((has_self && rank > self_rank) ? 1 : 0);
         if (lane < kk && !(has_self && mi == qi) && pos < k)
             out[row + pos] = b * n_src + mi;
@@ -463,7 +477,7 @@ __global__ __launch_bounds__(256) void knn_kernel(const float2 *__restrict__ pts
         // the fp32 key, with the margin of filter_threshold; exact fp64 keys
         // are formed for C only.)  C is small (~2 kk on a mesh), so it is
         // compacted into LDS and sorted.
-        const uint32_t thr = KT::filter_threshold(__shfl(wave_sort64(lmin, lane), kk - 1, 64));
+        const uint32_t thr = KT::filter_threshold(lane_value(wave_sort64(lmin, lane), kk - 1));
         // Compaction (order is free: the list is sorted or ranked next): every
         // lane's candidates as a bit mask, the wave's exclusive prefix of their
         // counts from the counts' bit planes (ballot + mbcnt, no LDS), then each
@@ -535,7 +549,7 @@ __global__ __launch_bounds__(256) void knn_large_kernel(const float2 *__restrict
             const uint32_t f = (j < n_src) ? key_f32(sP[j], q) : ~0u;
             lmin = f < lmin ? f : lmin;
         }
-        const uint32_t thr = KT::filter_threshold(__shfl(wave_sort64(lmin, lane), kk - 1, 64));
+        const uint32_t thr = KT::filter_threshold(lane_value(wave_sort64(lmin, lane), kk - 1));
         int m = 0;
         for (int c0 = 0; c0 < cpl; c0 += 64) {
             const int cn = min(64, cpl - c0);
@@ -886,7 +900,7 @@ __global__ __launch_bounds__(256) void knn_cand_kernel(const float2 *__restrict_
         const uint64_t en = __shfl(e0, (lane + 1) & 63, 64);
         const int jn = __shfl(j0, (lane + 1) & 63, 64);
         const bool pair_ok = lane >= kk - 1 || ki_less(e0, j0, en, jn);
-        const uint32_t fk = __shfl(f0, kk, 64), fk1 = __shfl(f0, kk - 1, 64);
+        const uint32_t fk = lane_value(f0, kk), fk1 = lane_value(f0, kk - 1);
         if (__ballot(!pair_ok) == 0ull && fk > KT::filter_threshold(fk1)) {
             k0 = e0;
             i0 = j0;
@@ -901,11 +915,11 @@ __global__ __launch_bounds__(256) void knn_cand_kernel(const float2 *__restrict_
         wave_sort128(k0, i0, k1, i1, lane);
         if (QUERY) {  // element lane + 1 (lane 63: element 64, k1 of lane 0)
             const key_t n0 = (key_t)__shfl((unsigned long long)k0, (lane + 1) & 63, 64);
-            const key_t n1 = (key_t)__shfl((unsigned long long)k1, 0, 64);
+            const key_t n1 = lane_value(k1, 0);
             tie = __ballot(lane < kk && k0 == (lane == 63 ? n1 : n0)) != 0ull;
         }
     }
-    const key_t key_kk = __shfl(k0, kk - 1, 64);
+    const key_t key_kk = lane_value(k0, kk - 1);
     float d_kk;
     if constexpr (QUERY)
         d_kk = (float)sqrt(__longlong_as_double((long long)key_kk)) * kUp;
@@ -924,7 +938,7 @@ __global__ __launch_bounds__(256) void knn_cand_kernel(const float2 *__restrict_
     } else {
         const uint64_t smask = __ballot(lane < kk && mi == pl);
         const bool has_self = smask != 0ull;
-        const int self_rank = has_self ? __shfl(rank, __ffsll((unsigned long long)smask) - 1, 64) : kk;
+        const int self_rank = has_self ? lane_value(rank, __ffsll((unsigned long long)smask) - 1) : kk;
         const int pos = rank - ((has_self && rank > self_rank) ? 1 : 0);
         if (lane < kk && !(has_self && mi == pl) && pos < k) out[p * k + pos] = b * n_per + mi;
         if (!has_self && lane == 0 && degenerate) atomicAdd(degenerate, 1);
