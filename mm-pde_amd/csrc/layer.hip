@@ -978,7 +978,7 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs p) {
     constexpr bool PRE = RB >= 4;
     BOps<F16X3, S1> bH, bM, bU2;
     bH.load(p.pk + kPkU1, 8, wave, 0, wu1, 0, lane);
-    if (PRE || (NODE_EARLY_M && (!NEXT || MMPDE_NODE_EARLY_M > 1))) bM.load(p.pk + kPkU1, 8, wave, S1, wu1, 128, lane);
+    if (PRE || (NODE_EARLY_M && !NEXT)) bM.load(p.pk + kPkU1, 8, wave, S1, wu1, 128, lane);
     if (PRE) {
         bU2.load(p.pk + kPkU2, 4, wave, 0, wu2, 0, lane);
     }
@@ -1004,7 +1004,7 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs p) {
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) aH[rb] = aM[rb] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
         gemm_tile<F16X3, RB, S1>(aH, img, 256, 0, bH, lane);
-        if (!PRE && !(NODE_EARLY_M && (!NEXT || MMPDE_NODE_EARLY_M > 1))) bM.load(p.pk + kPkU1, 8, wave, S1, wu1, 128, lane);
+        if (!PRE && !(NODE_EARLY_M && !NEXT)) bM.load(p.pk + kPkU1, 8, wave, S1, wu1, 128, lane);
         gemm_tile<F16X3, RB, S1>(F16X3 ? aM : aH, img, 256, S1, bM, lane);
         // update_net_2's operands issued now (bH / bM are dead): in flight over
         // this epilogue, the operand prep and its two barriers
