@@ -1,12 +1,12 @@
 #!/bin/bash
-# Round-4 closing GPU pass: the -m gpu suite, smoke(), the default bench line,
+# Closing GPU pass (regenerates the r04_final* records): the -m gpu suite, smoke(), the default bench line,
 # the configs[4] strong-scaling line at one GPU (64 trajectories), a serial
 # rocprofv3 kernel trace of the default bench, the training-iteration benches
 # (f16x3 and exact fp32 edge GEMMs) and the configs[1] / configs[2] lines.
 # Stops at the first crash / timeout.
 set -u
 export TMPDIR=/tmp
-O=gpurun_out/r4final
+O=gpurun_out/closing
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -q -v --timeout 240 --timeout-method thread \
     > $O/gpu_tests.log 2>&1
@@ -20,10 +20,10 @@ tail -1 $O/bench.json
 timeout -k 10 400 python -u bench.py --steps 10 --warmup 3 --global-trajectories 64 --no-cpu-baseline \
     > $O/bench_g64.json 2> $O/bench_g64.err || { tail $O/bench_g64.err; exit 4; }
 tail -1 $O/bench_g64.json
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/r4final_prof -o run -- \
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/closing_prof -o run -- \
     python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-f32-exact --serial > $O/prof_bench.json 2>&1 \
     || { tail $O/prof_bench.json; exit 5; }
-f=$(find /tmp/r4final_prof -name '*kernel_stats.csv' | head -1)
+f=$(find /tmp/closing_prof -name '*kernel_stats.csv' | head -1)
 cp $f $O/kernel_stats_serial.csv
 python3 - "$f" <<'PY'
 import csv, sys

@@ -1,4 +1,6 @@
 set -u
+# Round 4: DPP max reductions in segment_range (edge kernels' prologue): node_phases hashes (the
+# edge sums feed the node stage) of HEAD~ (old) and HEAD (new), then one bench line.
 O=gpurun_out/r4q; mkdir -p $O
 for v in old new; do timeout -k 10 90 tools/ubench/node_phases_$v 16 > $O/np_$v.log 2>&1 || exit 2; echo "$v: $(grep -E 'output hash|embed kernel' $O/np_$v.log | tr -s ' ' | tr '\n' ' ')"; done
 timeout -k 10 300 python -u bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-f32-exact > $O/b.json 2> $O/b.err || { tail $O/b.err; exit 3; }
