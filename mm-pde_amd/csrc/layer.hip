@@ -561,7 +561,7 @@ constexpr int NODE_WPE = MMPDE_NODE_WPE;  // node / embed launch bounds: waves p
 constexpr bool NODE_EARLY_U2 = MMPDE_NODE_EARLY_U2 != 0;
 // EARLY_M: update_net_1's mean-half operands beside the h-half ones at the
 // start, in the last layer's kernel (with the next projections it spills);
-// not yet measured on the GPU, so off
+// measured 31.9 against 31.3-31.4 us (profiles/r04_node_early_m_ab.log), so off
 #ifndef MMPDE_NODE_EARLY_M
 #define MMPDE_NODE_EARLY_M 0
 #endif
