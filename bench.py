@@ -43,7 +43,7 @@ F32_MFMA_PEAK_TFLOPS = 157.3          # MI355X_MICROARCH.md: dense fp32 matrix p
 F16_MFMA_PEAK_TFLOPS = 2516.6         # 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz (~2.5 PF dense)
 HBM_PEAK_GBS = 8000.0
 # counter records regenerated on the current kernels (tools/gpu_pmc.sh with
-# PMC_NAME=edge_pmc_r04; tools/gpu_configs.sh with STEP_HBM=r04_cy_gnn_step_hbm, tools/gpu_r4j.sh)
+# PMC_NAME=edge_pmc_r04; tools/gpu_configs.sh with STEP_HBM=...: tools/gpu_records.sh pmc:NAME)
 EDGE_PMC_RECORD = "edge_pmc_r04.json"
 STEP_HBM_RECORD = "r04_cy_gnn_step_hbm.json"
 CONFIGS = {
@@ -187,6 +187,9 @@ def main():
                     help="replay one hipGraph capture of the step instead of launching it "
                          "eagerly (measured 2.50 vs 2.44 ms/step eager at cy B=16: the "
                          "eager three-stream step is not launch-bound)")
+    ap.add_argument("--dist-backend", default=None, choices=["nccl", "gloo"],
+                    help="process-group backend under torchrun (default nccl = RCCL; gloo "
+                         "lets several ranks share one GPU, for rehearsing the multi-rank path)")
     ap.add_argument("--serial", action="store_true",
                     help="one stream in every pass (per-kernel profiles without concurrent "
                          "kernels sharing the GPU)")
@@ -196,10 +199,10 @@ def main():
     from mmpde_amd.rollout import MMPDERollout
     from mmpde_amd.synth import build_models, burgers_grid_points, fields
 
-    rank, local, world = D.init()
+    rank, local, world = D.init(args.dist_backend)
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    device = torch.device(f"cuda:{local}")
+    device = D.local_device(local)
     torch.cuda.set_device(device)
     kind, moving, b_default, cfg_name, side = CONFIGS[args.config]
     strong = args.global_trajectories is not None
@@ -321,7 +324,10 @@ def main():
         "higher_is_better": True,
         "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
-        "dtype": "f32" if args.edge_gemm == "f32" else "f32 (edge GEMM fp32-emulated by fp16x3 split, fp32 accumulate)",
+        "dtype": "f32" if args.edge_gemm == "f32" else
+                 ("f32 (every GNN GEMM fp32-emulated by the fp16x3 split with fp32 accumulate: "
+                  "edge message_net_2, node update_net_1/_2 and message_net_1 projections, "
+                  "embedding; DMM, ItpNet, res_cut, kNN and heads exact fp32)"),
         "data": "synthetic: seeded cy-synth 2521-node mesh / 48x48 grid, seeded sin-cos+noise "
                 "fields, seeded default-init weights (no dataset or checkpoint offline)",
         "config": {"workload": args.config, "baseline_config": cfg_name,
@@ -329,6 +335,8 @@ def main():
                    "global_trajectories": total,
                    "nodes_per_trajectory": n_nodes, "neighbors": gc.n, "time_window": 1,
                    "parallelism": f"trajectory-shard x{world} (no data-path collective)",
+                   "dist_backend": (torch.distributed.get_backend() if torch.distributed.is_initialized()
+                                    else None),
                    "shard": "contiguous trajectory blocks, dist.shard_range; rank 0 holds "
                             f"{hi - lo}",
                    "rollout": "autoregressive (pred -> next input)",

@@ -174,6 +174,7 @@ class GraphCreator_FS_2D(nn.Module):  # noqa: N801 - reference name
         g.pos = pos
         g.batch = batch
         g.nbr = nbr
+        g.nbr_checked = True   # from the engine's kNN / radius kernels: sources in range
         g.deg = deg
         g.seg_n = n
         return g

@@ -25,7 +25,9 @@ def env_world():
 
 def init(backend: str | None = None, force: bool = False):
     """Initialise the process group when launched under torchrun (or, with
-    force, for a one-rank world too); returns (rank, local_rank, world)."""
+    force, for a one-rank world too); returns (rank, local_rank, world).
+    backend: "nccl" (RCCL, the default with a GPU) or "gloo" (CPU collectives:
+    the CPU tests, and several ranks sharing one GPU, which RCCL refuses)."""
     rank, local, world = env_world()
     if (world > 1 or force) and not dist.is_initialized():
         if backend is None:
@@ -34,6 +36,18 @@ def init(backend: str | None = None, force: bool = False):
             torch.cuda.set_device(local)
         dist.init_process_group(backend=backend, rank=rank, world_size=world)
     return rank, local, world
+
+
+def local_device(local: int) -> torch.device:
+    """The GPU of local rank `local`: one per rank on a full node; ranks beyond
+    the visible devices share them round-robin (gloo only: RCCL needs one GPU
+    per rank)."""
+    return torch.device(f"cuda:{local % max(torch.cuda.device_count(), 1)}")
+
+
+def _cpu_collectives() -> bool:
+    """gloo group: collectives on host tensors."""
+    return dist.get_backend() == "gloo"
 
 
 def shard_range(total: int, rank: int, world: int):
@@ -86,14 +100,14 @@ def all_gather_losses(local: torch.Tensor, total: int) -> torch.Tensor:
 def max_over_ranks(value: float, device=None) -> float:
     if not _group():
         return value
-    t = torch.tensor([value], dtype=torch.float64, device=device)
+    t = torch.tensor([value], dtype=torch.float64, device=None if _cpu_collectives() else device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
 
 def barrier(device=None):
     if _group():
-        if device is not None and device.type == "cuda":
+        if device is not None and device.type == "cuda" and not _cpu_collectives():
             dist.barrier(device_ids=[device.index])
         else:
             dist.barrier()

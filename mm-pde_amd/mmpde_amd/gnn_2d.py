@@ -53,27 +53,33 @@ class BatchNorm(nn.Module):
 class EdgeGraph:
     """A message-passing graph as the HIP edge kernels take it: target-major
     neighbour table nbr int32 [n, k], optional in-degrees int32 [n] (ragged
-    tables), and -- built on first use by a backward -- the reverse adjacency."""
+    tables), and -- built on first use by a backward -- the reverse adjacency.
+    checked: the table's sources are known to lie in [0, n) (built by
+    nbr_table_from_edge_index, which range-checks them); any other table is
+    range-checked once, when its reverse adjacency is built (a source outside
+    [0, n) would otherwise lose its gradient silently)."""
 
-    def __init__(self, nbr: torch.Tensor, deg: torch.Tensor | None = None):
+    def __init__(self, nbr: torch.Tensor, deg: torch.Tensor | None = None, checked: bool = False):
         self.nbr = nbr.to(torch.int32).contiguous()
         self.deg = deg.to(torch.int32).contiguous() if deg is not None else None
+        self.checked = checked
         self._rev = None
 
     @classmethod
     def of(cls, data, n: int):
         nbr = getattr(data, "nbr", None)
         deg = getattr(data, "deg", None) if nbr is not None else None
+        # engine tables (kNN / radius kernels) are marked nbr_checked by the graph creator
+        checked = nbr is None or bool(getattr(data, "nbr_checked", False))
         if nbr is None:
             nbr, deg = nbr_table_from_edge_index(data.edge_index, n)
-        return cls(nbr, deg)
+        return cls(nbr, deg, checked)
 
     def reverse(self):
         if self._rev is None:
-            # tables from the engine's kNN / radius kernels or from
-            # nbr_table_from_edge_index (range-checked there); with the slot
-            # positions of the source-major backward
-            self._rev = reverse_adjacency(self.nbr, self.deg, check=False, slot_pos=True)
+            # with the slot positions of the source-major backward
+            self._rev = reverse_adjacency(self.nbr, self.deg, check=not self.checked, slot_pos=True)
+            self.checked = True
         return self._rev
 
 
@@ -227,7 +233,7 @@ class GNN_Layer_FS_2D(nn.Module):  # noqa: N801 - reference name
         if self.training or not self.supported() or deg is not None:
             if u.dim() == 1:
                 u = u[:, None]
-            return self.train_forward(x, u, pos_x, pos_y, variables, EdgeGraph(nbr, deg))
+            return self.train_forward(x, u, pos_x, pos_y, variables, EdgeGraph(nbr, deg, checked=True))
         pos = torch.cat((variables, pos_x, pos_y), dim=-1).float().contiguous()
         ws = torch.empty((4 * n * 128,), dtype=torch.float32, device=x.device)
         out = torch.empty((n, 128), dtype=torch.float32, device=x.device)

@@ -23,6 +23,7 @@ class Data:
         self.pos = None
         self.batch = None
         self.nbr = None
+        self.nbr_checked = False  # nbr built by the engine's graph kernels (sources in range)
         self.deg = None   # ragged graphs (radius): in-degree per target, nbr rows padded
         self.seg_n = None  # nodes per trajectory (batch segment), when all are equal
         for k, v in kwargs.items():

@@ -119,6 +119,11 @@ def knn_table_share(cells: torch.Tensor, batches: int, n_per: int) -> torch.Tens
     return 1.0 - miss.float() / n_per
 
 
+def _capturing() -> bool:
+    """A hipGraph capture is in progress on the current stream."""
+    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+
+
 class KnnTablePolicy:
     """Per-role choice between the candidate table (knn_graph_moved /
     knn_query_moved) and the plain full search for a rollout, from a cost model
@@ -168,7 +173,9 @@ class KnnTablePolicy:
         self._resolve(st)
         if st["mode"] == "full":
             st["wait"] -= 1
-            if st["wait"] < 0:
+            # no probe inside a hipGraph capture: its read-back cannot be queued
+            # there (after_table), so the probe would never resolve
+            if st["wait"] < 0 and not _capturing():
                 st["mode"], st["since"] = "probe", 0
                 return True                          # the probe call
             return False
@@ -187,7 +194,9 @@ class KnnTablePolicy:
         st["since"] += 1
         if st["pending"] is not None or (st["mode"] == "table" and (st["since"] - 1) % self.CHECK_EVERY):
             return
-        if torch.cuda.is_current_stream_capturing():
+        if _capturing():
+            if st["mode"] == "probe":                # cannot read back: retry after capture
+                st["mode"], st["wait"] = "full", self.PROBE_EVERY
             return
         miss = torch.empty((self.B, 2), dtype=torch.int32, device=self.device)
         L.check(L.lib().mmpde_knn_table_misses(L.ptr(cells), self.B, L.ptr(miss), L.stream(self.device)),
@@ -504,6 +513,8 @@ class LinearRows(torch.autograd.Function):
         n, k = x.shape
         nout = w.shape[0]
         want_b = ctx.has_bias and ctx.needs_input_grad[2]
+        if not (want_b or ctx.needs_input_grad[1]):
+            return gx, None, None          # frozen weight and bias: dX only
         if n >= 4096 and rows_grad_fits(k, nout):
             # skinny map (head windows, embedding): dW and db in one row pass
             gw, gb = rows_grad_weight(x, dy, k if ctx.needs_input_grad[1] else 0, want_b)

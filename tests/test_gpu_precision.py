@@ -56,6 +56,132 @@ def test_edge_gemm_f16x3_vs_fp64(dev, kind):
     assert errs["f16x3"] <= 2e-4 * scale + 1e-7
 
 
+def _hot_rows(pts, B, frac, seed):
+    """Row mask [B * N]: per trajectory the ceil(frac * N) nodes nearest to a
+    random mesh node (one compact hot region per trajectory)."""
+    N = pts.shape[0]
+    g = torch.Generator().manual_seed(seed)
+    m = torch.zeros((B, N), dtype=torch.bool)
+    cnt = max(1, int(round(frac * N)))
+    for b in range(B):
+        c = pts[int(torch.randint(N, (1,), generator=g))]
+        m[b, torch.argsort(((pts - c) ** 2).sum(1))[:cnt]] = True
+    return m.reshape(-1)
+
+
+def _row_err(out, ref64, mag):
+    """max and rms of |out_i - ref_i| / mag_i over the rows."""
+    r = (out - ref64).abs() / mag
+    return r.max().item(), r.pow(2).mean().sqrt().item()
+
+
+# Wide-range pin of the f16x3 split (gnn_2d.py:59-69 on the wave edge kernel,
+# the node and the embed kernels): u is scaled by 2^p on a compact region of
+# 1.5 % of each trajectory's nodes, which carries hidden states far above the
+# rest (eval BatchNorm is affine; with layers = 1 the hot rows reach one hop).
+# The edge kernel's split scale is one per trajectory segment, so the cold
+# rows sit far below it; the node / embed kernels scale per row.  Each row's
+# error vs float64, relative to that row's own magnitude (max |h_L| of the row
+# in float64), stays within 4x of the fp32 errors on the cold and the hot rows.
+@pytest.mark.parametrize("layers", [1, 6])
+@pytest.mark.parametrize("p", [8, 12, 16, 20])
+def test_f16x3_wide_range_solver(dev, p, layers):
+    from mmpde_amd.rollout import _Nodes
+
+    B = 2
+    pde, model, u, pos, ei, nbr = _gnn_case("cy", B, seed=3)
+    model.gnn_layers = model.gnn_layers[:layers]   # 1: the hot rows reach one hop only
+    model.hidden_layer = layers
+    N = pde.ori_grid.shape[0]
+    hot = _hot_rows(pde.ori_grid, B, 0.015, seed=p)
+    u = u.clone()
+    u[hot] *= float(2 ** p)
+    opde = refcpu.PDEConst("cy", pde.grid_size, ori_grid=pde.ori_grid)
+    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    sd64 = {k: (v.double() if v.is_floating_point() else v) for k, v in sd.items()}
+    ref64, hs = refcpu.mp_pde_solver(sd64, opde, u.double(), pos.double(), ei, hidden_layer=layers,
+                                     return_hidden=True)
+    ref64 = ref64.reshape(-1)
+    mag = hs[-1].abs().amax(1)
+    outs = {"cpu-f32": refcpu.mp_pde_solver(sd, opde, u, pos, ei, hidden_layer=layers).reshape(-1).double()}
+    model.to(dev)
+    g = _Nodes(u.to(dev), pos.to(dev), nbr.int().to(dev), seg_n=N)
+    for mode in ("f32", "f16x3"):
+        model.edge_gemm = mode
+        outs[mode] = model(g).reshape(-1).double().cpu()
+    model.edge_gemm = "f32"
+    q = torch.tensor([0.0, 0.5, 1.0], dtype=torch.float64)
+    msg = [f"p={p} layers={layers}: row magnitude quantiles (0, .5, 1) hot "
+           f"{mag[hot].quantile(q).tolist()} cold {mag[~hot].quantile(q).tolist()}"]
+    for name, rows in (("cold", ~hot), ("hot", hot)):
+        e = {m: _row_err(o[rows], ref64[rows], mag[rows]) for m, o in outs.items()}
+        msg.append(f"{name} rows ({int(rows.sum())}) rel err max / rms: "
+                   + ", ".join(f"{m} {e[m][0]:.3e} / {e[m][1]:.3e}" for m in e))
+        for i in (0, 1):
+            assert e["f16x3"][i] <= 4.0 * max(e["f32"][i], e["cpu-f32"][i]) + 1e-12, "\n".join(msg)
+    print("\n".join(msg))
+
+
+# The split's range (f16x3.hpp split2_relu_rtz): relu(a_i + b_j) is scaled by
+# sc with sc * M in [2^10, 2^11), M = max|a| + max|b| over the trajectory
+# segment; hi is fp16 (RTZ), lo = RN_f16(x - hi).  lo stays a normal fp16 number
+# -- 22 significant bits in all, fp32-class -- while |x| >= 2^-14 M; below it
+# lo's spacing is the fp16 subnormal 2^-24, an absolute error <= 2^-25 / sc
+# <= 2^-35 M per element.  Per output row i (|z1| <= m_i):
+#     |err_i| <= fp32-class + 2^-35 M L1(W2)   (relative: + 2^-35 M / m_i).
+# Rows within 2^14 of M meet the 4x-of-fp32 bar; p = 16, 20 check the floor.
+@pytest.mark.parametrize("p", [8, 12, 16, 20])
+def test_f16x3_wide_range_edge_mean(dev, p):
+    """EdgeMean (the training forward's f16x3 edge stage, gnn_2d.py:59-63 +
+    mean) on a, b whose hot rows (1.5 %) are 2^p above the rest, against
+    float64 per row, relative to the row's own magnitude m_i L1(W2),
+    m_i = max_e |a_i + b_j|."""
+    from mmpde_amd.gnn_2d import EdgeGraph, EdgeMean
+    from mmpde_amd.synth import cy_synth_mesh
+
+    torch.manual_seed(11)
+    pts = cy_synth_mesh()
+    B, N = 2, pts.shape[0]
+    _, nbr, _ = refcpu.knn_graph(pts.repeat(B, 1), 35, B)
+    hot = _hot_rows(pts, B, 0.015, seed=100 + p)
+    n = B * N
+    a = torch.randn(n, 128) * 0.5
+    b = torch.randn(n, 128) * 0.5
+    a[hot] *= float(2 ** p)
+    b[hot] *= float(2 ** p)
+    lin = torch.nn.Linear(128, 128)
+    w2, b2 = lin.weight.detach(), lin.bias.detach()
+    nb = nbr.long()
+    s64 = a.double()[:, None, :] + b.double()[nb]                         # [n, k, 128]
+    ref64 = torch.relu(torch.relu(s64) @ w2.double().t() + b2.double()).mean(1)
+    cpu32 = torch.relu(torch.relu(a[:, None, :] + b[nb]) @ w2.t() + b2).mean(1).double()
+    m_row = s64.abs().amax((1, 2))
+    l1 = w2.abs().sum(1).max().double()
+    mag = m_row * l1
+    # the kernel's M: one segment (the whole call)
+    M = (a.abs().max() + b.abs().max()).double()
+    graph = EdgeGraph(nbr.int().to(dev))
+    outs = {"cpu-f32": cpu32}
+    for mode in ("f32", "f16x3"):
+        outs[mode] = EdgeMean.apply(a.to(dev), b.to(dev), w2.to(dev), b2.to(dev), graph,
+                                    mode).double().cpu()
+    rows_hot = m_row > 2 ** (p - 2)
+    msg = [f"p={p}: M / min m_i = {(M / m_row.min()).item():.3g}"]
+    for name, rows in (("cold", ~rows_hot), ("hot", rows_hot)):
+        e = {m: _row_err(o[rows], ref64[rows], mag[rows][:, None]) for m, o in outs.items()}
+        msg.append(f"{name} rows ({int(rows.sum())}) rel err max / rms: "
+                   + ", ".join(f"{m} {e[m][0]:.3e} / {e[m][1]:.3e}" for m in e))
+        f32_max = max(e["f32"][0], e["cpu-f32"][0])
+        if p <= 12:
+            for i in (0, 1):
+                assert e["f16x3"][i] <= 4.0 * max(e["f32"][i], e["cpu-f32"][i]) + 1e-12, "\n".join(msg)
+        else:
+            rel = ((outs["f16x3"][rows] - ref64[rows]).abs() / mag[rows][:, None]).amax(1)
+            bound = 4.0 * f32_max + 2.0 ** -35 * M / m_row[rows]
+            assert bool((rel <= bound).all()), "\n".join(msg)
+    print("\n".join(msg))
+
+
 def test_edge_gemm_f16x3_mmpde_step(dev):
     """Whole cylinder MM-PDE step with the split edge GEMM in both GNNs, against
     the fp32 oracle at the parity tolerance of test_mmpde_step_matches_oracle."""

@@ -73,6 +73,54 @@ def test_linear_rows_head_shapes_use_rows_kernel(dev):
         _close(t.grad, r.grad, 2e-5, f"LinearRows d{name}")
 
 
+def test_frozen_head_backward_returns_input_grad(dev):
+    """A frozen output head (output_mlp without gradients) while the rest of the
+    GNN trains: LinearRows' backward returns dL/dh alone (no weight or bias
+    gradient is formed for the skinny head windows)."""
+    from mmpde_amd import ops
+    from mmpde_amd.synth import build_models
+
+    _, model, _, _, _, _ = build_models("cy", moving_mesh=False)
+    model.to(dev)
+    for prm in model.output_mlp.parameters():
+        prm.requires_grad_(False)
+    g = torch.Generator().manual_seed(5)
+    h = torch.randn(6000, 128, generator=g)
+    hd = h.to(dev).requires_grad_()
+    model._head_train(hd).sum().backward()
+    assert all(prm.grad is None for prm in model.output_mlp.parameters())
+    hr = h.double().requires_grad_()
+    o = model.output_mlp
+    d = hr[:, None]
+    for i, idx in enumerate((0, 2, 4)):
+        c = o[idx]
+        d = torch.nn.functional.conv1d(d, c.weight.double().cpu(), c.bias.double().cpu(), stride=c.stride)
+        if idx != 4:
+            d = torch.relu(d)
+    d.squeeze(1).sum().backward()
+    _close(hd.grad, hr.grad, 2e-5, "frozen head dL/dh")
+    # a bias-only gradient (weight frozen) on the skinny path too
+    x = torch.randn(20000, 48, generator=g).to(dev)
+    w = (torch.randn(8, 48, generator=g) / 7).to(dev)
+    b = torch.randn(8, generator=g).to(dev).requires_grad_()
+    ops.LinearRows.apply(x, w, b).sum().backward()
+    _close(b.grad, torch.full((8,), 20000.0, dtype=torch.float64), 1e-6, "bias-only db")
+
+
+def test_edge_graph_checks_caller_tables(dev):
+    """EdgeGraph built by a caller from a table with a source outside [0, n):
+    the reverse adjacency (built by the first backward) raises instead of
+    dropping that edge's gradient."""
+    from mmpde_amd.gnn_2d import EdgeGraph
+
+    nbr = torch.randint(0, 50, (50, 4), dtype=torch.int32)
+    nbr[7, 2] = 50
+    with pytest.raises(ValueError):
+        EdgeGraph(nbr.to(dev)).reverse()
+    nbr[7, 2] = 3
+    EdgeGraph(nbr.to(dev)).reverse()
+
+
 @pytest.mark.parametrize("n,C,res,affine", [
     (40336, 128, True, True),           # GNN layer norm(h + upd) at cy B=16
     (5042, 128, False, True),           # embedding BatchNorm1d, B=2

@@ -128,3 +128,23 @@ def test_graph_creator_signature():
     gc = GraphCreator_FS_2D(cy(ori_grid=torch.zeros(5, 2)), neighbors=35, connect_edge="knn",
                             time_window=1, t_resolution=30)
     assert gc.n == 35 and gc.tw == 1 and gc.t_res == 30 and gc.e == "knn"
+
+
+def test_knn_policy_no_probe_during_capture(monkeypatch):
+    """ops.KnnTablePolicy (the kNN table-or-scan choice of the rollout): a probe
+    is never started inside a hipGraph capture, and a probe pending when a
+    capture begins goes back to the full search instead of staying unresolved."""
+    from mmpde_amd import ops
+
+    pol = ops.KnnTablePolicy("cpu", 2, 100, ("graph",))
+    st = pol.state["graph"]
+    st["mode"], st["wait"] = "full", 0
+    monkeypatch.setattr(ops, "_capturing", lambda: True)
+    assert pol.use_table("graph") is False and pol.mode("graph") == "full"
+    monkeypatch.setattr(ops, "_capturing", lambda: False)
+    assert pol.use_table("graph") is True and pol.mode("graph") == "probe"
+    # the probe's table call lands in a capture: no read-back can be queued
+    monkeypatch.setattr(ops, "_capturing", lambda: True)
+    pol.after_table("graph", None, 0)
+    assert pol.mode("graph") == "full" and st["wait"] == ops.KnnTablePolicy.PROBE_EVERY
+    assert st["pending"] is None
