@@ -244,9 +244,13 @@ def main():
     u0 = u_all[:, 0].to(device).contiguous()
     n_t = t_len - 1
 
+    host_s = {}
+
     def timed_run(mode, trace):
         """W warmup + K timed autoregressive steps from u0; returns (max-over-ranks
-        seconds, final state).  trace: record the edge-kernel events, one stream."""
+        seconds, final state).  trace: record the edge-kernel events, one stream.
+        host_s[(mode, trace)]: seconds the host spent inside the K step calls (issuing
+        launches; equal to the wall time when the pass is host-bound)."""
         for m in (model, model_b):
             if m is not None:
                 m.edge_gemm = mode
@@ -268,6 +272,7 @@ def main():
             t0 = time.perf_counter()
             for i in range(args.steps):
                 u = run(u, 1 + (args.warmup + i) % n_t)
+            host_s[(mode, trace)] = time.perf_counter() - t0
             torch.cuda.synchronize(device)
             D.barrier(device)
             t1 = time.perf_counter()
@@ -349,11 +354,13 @@ def main():
                      "traffic": traffic, "launch_ms": launch_ms, "launches": len(launches),
                      "flop_per_launch": edge_f,
                      "traced_pass_ms_per_step": 1e3 * elapsed_traced / args.steps,
+                     "traced_pass_host_ms_per_step": 1e3 * host_s[(args.edge_gemm, True)] / args.steps,
                      "algorithmic_bytes_per_launch": n_local * (128 * 4 * 2 + k * 4 + 128 * 4),
                      "edge_gemm": args.edge_gemm,
                      "peak_basis": "dense fp32 MFMA" if args.edge_gemm == "f32" else
                                    "dense fp16 MFMA / 3 (three fp16 products per fp32 product)"},
         "node_stage_ms": node_ms / nl,
+        "host_issue_ms_per_step": 1e3 * host_s[(args.edge_gemm, False)] / args.steps,
         "finite": finite,
     }
     if moving:
