@@ -317,7 +317,7 @@ int mmpde_gnn_edge_mean_deg(const float *a, const float *b, const int32_t *nbr, 
  * W2 and the split scale (max|a| + max|b| over all n rows) into workspace
  * (>= mmpde_gnn_edge_mean_workspace_bytes(n, edge_gemm) bytes, 16-B aligned)
  * on every call: the forward of the f16x3 training path, whose weights
- * change every iteration.  relu_mask (nullable, F16X3 only, 16-B aligned):
+ * change every iteration.  relu_mask (nullable, 16-B aligned; F32 or F16X3):
  * [n * k][4] uint32, bit c % 32 of word c / 32 of slot q = i*k + e set where
  * message_net_2's pre-activation z2[c] > 0 for that edge -- the ReLU pattern
  * mmpde_gnn_edge_backward_sorted then reuses instead of recomputing z2. */
@@ -365,7 +365,7 @@ int mmpde_gnn_edge_source_sum(const float *grad_edge, const int64_t *rev_off, co
  * n*k-1), so that dL/db is the contiguous segmented sum
  * mmpde_gnn_edge_source_sum_sorted over rev_off: the same sums in the same
  * order as mmpde_gnn_edge_backward_ex + mmpde_gnn_edge_source_sum, read as a
- * stream instead of a gather.  n * k < 2^31.  relu_mask (nullable; F16X3,
+ * stream instead of a gather.  n * k < 2^31.  relu_mask (nullable; F32 or F16X3,
  * k <= 64): the forward's z2 > 0 bits (mmpde_gnn_edge_mean_ex): the ReLU
  * pattern of message_net_2 is taken from it and z2 is not recomputed (one of
  * the three per-edge GEMMs dropped). */
@@ -428,6 +428,90 @@ int mmpde_batch_norm_rows_backward(const float *x, const float *res, const float
                                    const float *weight, const float *stats, float *dx, float *dweight,
                                    float *dbias, float *workspace, int64_t workspace_bytes,
                                    mmpde_stream_t stream);
+
+/* Row GEMMs of the training path: the Linears of the train-mode GNN
+ * (message_net_1 as its target / source halves, update_net_1 / _2, the
+ * embedding; gnn_2d.py:53-69,99-106) and ItpNet's MLPs (interpolate.py:79-93),
+ * forward and input gradient, replacing the library GEMMs torch autograd
+ * would call under loss.backward() (train_helper_2d.py:126).  Exact fp32
+ * products on v_mfma_f32_32x32x2_f32, deterministic.
+ *
+ * mmpde_rgemm: for each output part p (1 or 2 blocks of <= 128 columns,
+ * ncols[p] of them) and row i < m, column c < ncols[p]:
+ *   y = sum_{h<2} sum_{k<kh} A_h[i][k] * B_h(p, k, c)  (+ bias[p][c])
+ *       (+ xscale[p] * sum_{e<ns[p]} xs[i][e] * XW(p, e, c))
+ *   relu (relu != 0); y = omask[p][i][c] > 0 ? y : 0 (omask nullable);
+ *   out[p][i][c] = y, or += y with accumulate[p].
+ * A_h[i][k] = a[h][i * lda[h] + k], times (amask[h][...] > 0) when amask[h] is
+ * given (same layout).  B: layout NT -> w[h][(wc[p] + c) * ldw + wk[p] + k]
+ * (a Linear's weight [out, in]: y = x W^T); layout NN ->
+ * w[h][(wk[p] + k) * ldw + wc[p] + c] (y = g W, the input gradient).  K halves
+ * of kh columns each (kh = 0: the small segment alone); ns[p] <= 4 more input
+ * columns with XW(p, e, c) = xw[p][c * ldxw + e] (NT), xw[p][e * ldxw + c] (NN). */
+#define MMPDE_RGEMM_NT 0
+#define MMPDE_RGEMM_NN 1
+typedef struct mmpde_rgemm_args {
+    int64_t m;
+    int kh, layout;
+    const float *w[2];
+    int64_t ldw;
+    const float *a[2];
+    const float *amask[2];
+    int64_t lda[2];
+    int parts;
+    float *out[2];
+    int64_t ldo[2], wc[2], wk[2];
+    int ncols[2];
+    const float *bias[2];
+    const float *omask[2];
+    int64_t ldom[2];
+    int accumulate[2];
+    int relu;
+    const float *xs; /* [m, >= ns] small input segment (row stride ldxs) */
+    int64_t ldxs;
+    int ns[2];
+    const float *xw[2];
+    int64_t ldxw;
+    float xscale[2];
+} mmpde_rgemm_args;
+int mmpde_rgemm(const mmpde_rgemm_args *g, mmpde_stream_t stream);
+
+/* Weight / bias gradient over the rows (K = m reduction) of a Linear with
+ * gcols <= 128 outputs: with G = g * (gmask > 0) ([m, gcols], row stride ldg;
+ * gmask nullable, same layout):
+ *   dw[c][dwcol[s] + j] = sum_i G[i][c] x[s][i][j]      (segments s < nseg <= 3
+ *                         of kx[s] columns, row stride ldx[s])
+ *   dw[c][dwcol_s + e] (+)= sign_s * sum_i G[i][c] xs[i][e]   (e < ns <= 4;
+ *                         accumulate_s adds to dw instead of storing)
+ *   db[c] = sum_i G[i][c]                            (db nullable)
+ * Rows are summed in fixed chunks of `chunk_rows` (partials in the workspace,
+ * then added in chunk order): deterministic.  workspace:
+ * mmpde_rgemm_tn_workspace_bytes(m, chunk_rows, sum over s of kx[s] rounded
+ * up to 32, + ns + 1). */
+typedef struct mmpde_rgemm_tn_args {
+    int64_t m;
+    int chunk_rows, gcols;
+    const float *g;
+    const float *gmask;
+    int64_t ldg;
+    int nseg;
+    const float *x[3];
+    int64_t ldx[3];
+    int kx[3];
+    int64_t dwcol[3];
+    const float *xs;
+    int64_t ldxs;
+    int ns;
+    int64_t dwcol_s;
+    float sign_s;
+    int accumulate_s;
+    float *dw;
+    int64_t lddw;
+    float *db;
+} mmpde_rgemm_tn_args;
+int64_t mmpde_rgemm_tn_workspace_bytes(int64_t m, int chunk_rows, int cols);
+int mmpde_rgemm_tn(const mmpde_rgemm_tn_args *g, void *workspace, int64_t workspace_bytes,
+                   mmpde_stream_t stream);
 
 /* out[n] = out_scale * output_mlp(h[:, None]) */
 int mmpde_gnn_head(const float *h, int64_t n, const mmpde_gnn_head_params *p, float *out,

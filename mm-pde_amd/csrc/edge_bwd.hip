@@ -43,8 +43,13 @@ struct EdgeBwdArgs {
     float *gz1;            // [n * k, 128] per edge (row q = i k + e, or pos[q])
     float *pw2, *pb2;      // [grid][128][128], [grid][128] partials
     const int32_t *pos;    // nullable: the gz1 row of slot q (source-major order)
+    const uint32_t *mask;  // MASK: the forward's z2 > 0 bits, [n * k][4] (mmpde_gnn_edge_mean_ex)
 };
 
+// MASK: the ReLU pattern of z2 comes from the forward (bit c % 32 of word c / 32
+// of the slot) instead of recomputing z2 -- the gradient of exactly the function
+// the forward evaluated, whose z2 summation order differs from this kernel's.
+template <bool MASK>
 __global__ __launch_bounds__(256, 1) void edge_bwd_kernel(EdgeBwdArgs p) {
     __shared__ float w2s[BH * BWS];    // W2 [c][kk], row stride BWS
     __shared__ float at[BT * BWS];     // a rows of the tile
@@ -110,8 +115,27 @@ __global__ __launch_bounds__(256, 1) void edge_bwd_kernel(EdgeBwdArgs p) {
             // z2 = W2 relu(z1) + b2 and gz2 = g / deg [z2 > 0]: wave owns columns
             // c of tiles 2 wave, 2 wave + 1 (A = relu(z1)[row][kk], B = W2[c][kk])
             float gz2v[2][4];
+            if (MASK) {
+                // columns 32 wave + 16 ci + r: bit 16 ci + r of word `wave`
+                uint32_t mw[4];
 #pragma unroll
-            for (int ci = 0; ci < 2; ++ci) {
+                for (int t = 0; t < 4; ++t)
+                    mw[t] = p.mask[(min(row0 + 4 * g + t, nmax) * k + e) * 4 + wave];
+#pragma unroll
+                for (int ci = 0; ci < 2; ++ci) {
+                    const int c = 16 * (2 * wave + ci) + r;
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        const int rr = 4 * g + t;
+                        const bool on = e < dgr[t] && ((mw[t] >> (16 * ci + r)) & 1u);
+                        const float v = on ? gms[rr * BWS + c] : 0.0f;
+                        gz2v[ci][t] = v;
+                        gz2s[rr * BWS + c] = v;
+                    }
+                }
+            }
+#pragma unroll
+            for (int ci = 0; ci < 2 && !MASK; ++ci) {
                 const int c = 16 * (2 * wave + ci) + r;
                 f32x4 acc = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll 8
@@ -717,8 +741,8 @@ extern "C" int64_t mmpde_gnn_edge_backward_partials(int *grid) {
 
 static int edge_backward_f32(const float *a, const float *b, const int32_t *nbr, const int32_t *deg, int64_t n,
                              int k, const float *msg2_w, const float *msg2_b, const float *grad_mean,
-                             const int32_t *pos, float *grad_a, float *grad_edge, float *partials, float *grad_w2,
-                             float *grad_b2, mmpde_stream_t stream) {
+                             const int32_t *pos, const uint32_t *mask, float *grad_a, float *grad_edge,
+                             float *partials, float *grad_w2, float *grad_b2, mmpde_stream_t stream) {
     MMPDE_REQUIRE(a && b && nbr && msg2_w && msg2_b && grad_mean && grad_a && grad_edge && partials);
     MMPDE_REQUIRE(grad_w2 && grad_b2 && n > 0 && k > 0 && n <= (int64_t)INT32_MAX);
     MMPDE_REQUIRE((((uintptr_t)a | (uintptr_t)b | (uintptr_t)msg2_w | (uintptr_t)grad_mean) & 15) == 0);
@@ -728,9 +752,11 @@ static int edge_backward_f32(const float *a, const float *b, const int32_t *nbr,
     MMPDE_REQUIRE(ntiles < (int64_t)INT32_MAX);
     if (grid > ntiles) grid = (int)ntiles;
     float *pw2 = partials, *pb2 = partials + (int64_t)grid * BH * BH;
-    EdgeBwdArgs p{a, b, nbr, deg, n, k, (int)ntiles, msg2_w, msg2_b, grad_mean, grad_a, grad_edge, pw2, pb2, pos};
+    EdgeBwdArgs p{a, b, nbr, deg, n, k, (int)ntiles, msg2_w, msg2_b, grad_mean, grad_a, grad_edge, pw2, pb2, pos,
+                  mask};
     hipStream_t st = as_stream(stream);
-    hipLaunchKernelGGL(edge_bwd_kernel, dim3(grid), dim3(256), 0, st, p);
+    if (mask) hipLaunchKernelGGL(edge_bwd_kernel<true>, dim3(grid), dim3(256), 0, st, p);
+    else hipLaunchKernelGGL(edge_bwd_kernel<false>, dim3(grid), dim3(256), 0, st, p);
     MMPDE_RET_LAUNCH();
     hipLaunchKernelGGL(partial_sum_kernel, dim3(ceil_div(BH * BH, 256)), dim3(256), 0, st, pw2, grid,
                        (int64_t)BH * BH, grad_w2);
@@ -745,7 +771,7 @@ static int edge_backward(const float *a, const float *b, const int32_t *nbr, con
                          float *grad_b2, int edge_gemm, mmpde_stream_t stream) {
     MMPDE_REQUIRE(edge_gemm == MMPDE_EDGE_GEMM_F32 || edge_gemm == MMPDE_EDGE_GEMM_F16X3);
     if (edge_gemm == MMPDE_EDGE_GEMM_F32 || k > FKMAX)
-        return edge_backward_f32(a, b, nbr, deg, n, k, msg2_w, msg2_b, grad_mean, pos, grad_a, grad_edge, partials,
+        return edge_backward_f32(a, b, nbr, deg, n, k, msg2_w, msg2_b, grad_mean, pos, mask, grad_a, grad_edge, partials,
                                  grad_w2, grad_b2, stream);
     MMPDE_REQUIRE(a && b && nbr && msg2_w && msg2_b && grad_mean && grad_a && grad_edge && partials);
     MMPDE_REQUIRE(grad_w2 && grad_b2 && n > 0 && k > 0 && n <= (int64_t)INT32_MAX);
@@ -796,7 +822,7 @@ extern "C" int mmpde_gnn_edge_backward(const float *a, const float *b, const int
                                        const float *grad_mean, float *grad_a, float *grad_edge,
                                        float *partials, float *grad_w2, float *grad_b2,
                                        mmpde_stream_t stream) {
-    return edge_backward_f32(a, b, nbr, deg, n, k, msg2_w, msg2_b, grad_mean, nullptr, grad_a, grad_edge, partials,
+    return edge_backward_f32(a, b, nbr, deg, n, k, msg2_w, msg2_b, grad_mean, nullptr, nullptr, grad_a, grad_edge, partials,
                              grad_w2, grad_b2, stream);
 }
 
@@ -816,7 +842,7 @@ extern "C" int mmpde_gnn_edge_backward_sorted(const float *a, const float *b, co
                                               float *partials, float *grad_w2, float *grad_b2, int edge_gemm,
                                               mmpde_stream_t stream) {
     MMPDE_REQUIRE(slot_pos);
-    MMPDE_REQUIRE(!relu_mask || (edge_gemm == MMPDE_EDGE_GEMM_F16X3 && k <= FKMAX));
+    MMPDE_REQUIRE(!relu_mask || k <= FKMAX);
     return edge_backward(a, b, nbr, deg, n, k, msg2_w, msg2_b, grad_mean, slot_pos, relu_mask, grad_a, grad_edge,
                          partials, grad_w2, grad_b2, edge_gemm, stream);
 }

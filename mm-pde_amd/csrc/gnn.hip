@@ -413,11 +413,17 @@ extern "C" int mmpde_gnn_edge_mean_ex(const float *a, const float *b, const int3
                                       uint32_t *relu_mask, int edge_gemm, void *workspace, int64_t workspace_bytes,
                                       mmpde_stream_t stream) {
     MMPDE_REQUIRE(edge_gemm == MMPDE_EDGE_GEMM_F32 || edge_gemm == MMPDE_EDGE_GEMM_F16X3);
-    MMPDE_REQUIRE(!relu_mask || edge_gemm == MMPDE_EDGE_GEMM_F16X3);
-    if (edge_gemm == MMPDE_EDGE_GEMM_F32)
-        return mmpde_gnn_edge_mean_deg(a, b, nbr, deg, n, k, msg2_w, msg2_b, mean_out, stream);
-    MMPDE_REQUIRE(n > 0 && workspace && workspace_bytes >= edge_mean_f16x3_ws_bytes(n));
     MMPDE_REQUIRE(!relu_mask || (n * k < (int64_t)INT32_MAX && ((uintptr_t)relu_mask & 15) == 0));
+    if (edge_gemm == MMPDE_EDGE_GEMM_F32) {
+        if (!relu_mask) return mmpde_gnn_edge_mean_deg(a, b, nbr, deg, n, k, msg2_w, msg2_b, mean_out, stream);
+        MMPDE_REQUIRE(a && b && nbr && msg2_w && msg2_b && mean_out && n > 0 && k > 0);
+        mmpde_gnn_layer_params p{};
+        p.msg2_w = msg2_w;
+        p.msg2_b = msg2_b;
+        return launch_edge_stage(a, b, nbr, deg, n, k, n, &p, nullptr, nullptr, mean_out, nullptr, 0, nullptr,
+                                 as_stream(stream), relu_mask);
+    }
+    MMPDE_REQUIRE(n > 0 && workspace && workspace_bytes >= edge_mean_f16x3_ws_bytes(n));
     return launch_edge_mean_f16x3(a, b, nbr, deg, n, k, msg2_w, msg2_b, mean_out, relu_mask, workspace,
                                   as_stream(stream));
 }

@@ -1218,14 +1218,15 @@ static_assert(16 * MMPDE_NODE_RB % kRangeRows == 0, "range records are per 16-ro
 int launch_edge_stage(const float *a, const float *b, const int32_t *nbr, const int32_t *deg,
                       int64_t n, int k, int64_t seg_n, const mmpde_gnn_layer_params *p, const char *pk,
                       const float *rng, float *mean, float *side, int64_t side_cap,
-                      EdgeSplit *split, hipStream_t st) {
+                      EdgeSplit *split, hipStream_t st, uint32_t *relu_mask) {
     if (split) *split = EdgeSplit{};
+    MMPDE_REQUIRE(!relu_mask || (!pk && al16(relu_mask)));  // the ring kernel's F32 training forward
     MMPDE_REQUIRE(a && b && nbr && p && mean && n > 0 && k > 0 && n <= (int64_t)INT32_MAX);
     MMPDE_REQUIRE(al16(a) && al16(b) && al16(p->msg2_w) && al16(mean));
     MMPDE_REQUIRE(!pk || (rng && al16(pk) && al16(rng)));
     const int64_t ntiles = (n + ET - 1) / ET;
     MMPDE_REQUIRE(ntiles * ((k + ESL - 1) / ESL) < (int64_t)INT32_MAX);
-    EdgeArgs e{a, b, nbr, n, k, (int)ntiles, p->msg2_w, p->msg2_b, pk, rng, mean, nullptr, deg};
+    EdgeArgs e{a, b, nbr, n, k, (int)ntiles, p->msg2_w, p->msg2_b, pk, rng, mean, nullptr, deg, relu_mask};
     const int cus = device_cus();
 #ifndef MMPDE_EDGE_RING
     // F16X3: one wave per SIMD with the operands in registers (edge_wave.hip)

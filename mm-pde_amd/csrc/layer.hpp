@@ -58,7 +58,7 @@ struct EdgeSplit {
 int launch_edge_stage(const float *a, const float *b, const int32_t *nbr, const int32_t *deg,
                       int64_t n, int k, int64_t seg_n, const mmpde_gnn_layer_params *p, const char *pk,
                       const float *rng, float *mean, float *side, int64_t side_cap,
-                      EdgeSplit *split, hipStream_t st);
+                      EdgeSplit *split, hipStream_t st, uint32_t *relu_mask = nullptr);
 
 // The training forward's F16X3 edge stage (writes the mean; packs W2 and
 // computes the range records of a, b itself in ws, edge_mean_f16x3_ws_bytes).

@@ -13,7 +13,7 @@ import os
 import torch
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libmmpde_hip.so")
-ABI_VERSION = 11700
+ABI_VERSION = 11800
 
 ACT_NONE, ACT_TANH, ACT_RELU, ACT_ELU = 0, 1, 2, 3
 PAD_ZEROS, PAD_CIRCULAR = 0, 1
@@ -90,6 +90,27 @@ class ItpMlp(ctypes.Structure):
     _fields_ = [(n, _P) for n in ("w0", "b0", "w1", "b1", "w2", "b2")]
 
 
+class RgemmArgs(ctypes.Structure):
+    """mmpde_rgemm_args (include/mmpde_hip.h)."""
+    _fields_ = [("m", _I64), ("kh", _I), ("layout", _I), ("w", _P * 2), ("ldw", _I64),
+                ("a", _P * 2), ("amask", _P * 2), ("lda", _I64 * 2), ("parts", _I),
+                ("out", _P * 2), ("ldo", _I64 * 2), ("wc", _I64 * 2), ("wk", _I64 * 2),
+                ("ncols", _I * 2), ("bias", _P * 2), ("omask", _P * 2), ("ldom", _I64 * 2),
+                ("accumulate", _I * 2), ("relu", _I), ("xs", _P), ("ldxs", _I64), ("ns", _I * 2),
+                ("xw", _P * 2), ("ldxw", _I64), ("xscale", _F * 2)]
+
+
+class RgemmTnArgs(ctypes.Structure):
+    """mmpde_rgemm_tn_args (include/mmpde_hip.h)."""
+    _fields_ = [("m", _I64), ("chunk_rows", _I), ("gcols", _I), ("g", _P), ("gmask", _P), ("ldg", _I64),
+                ("nseg", _I), ("x", _P * 3), ("ldx", _I64 * 3), ("kx", _I * 3), ("dwcol", _I64 * 3),
+                ("xs", _P), ("ldxs", _I64), ("ns", _I), ("dwcol_s", _I64), ("sign_s", _F),
+                ("accumulate_s", _I), ("dw", _P), ("lddw", _I64), ("db", _P)]
+
+
+RGEMM_NT, RGEMM_NN = 0, 1
+
+
 # --------------------------------------------------------------------------- loader
 _SIGS = {
     "mmpde_version": (_I, []),
@@ -125,6 +146,9 @@ _SIGS = {
     "mmpde_batch_norm_rows_workspace_bytes": (_I64, [_I64, _I]),
     "mmpde_batch_norm_rows_train": (_I, [_P, _P, _I64, _I, _P, _P, _F, _F, _P, _P, _P, _P, _P, _I64, _P]),
     "mmpde_batch_norm_rows_backward": (_I, [_P, _P, _P, _I64, _I, _P, _P, _P, _P, _P, _P, _I64, _P]),
+    "mmpde_rgemm": (_I, [_P, _P]),
+    "mmpde_rgemm_tn_workspace_bytes": (_I64, [_I64, _I, _I]),
+    "mmpde_rgemm_tn": (_I, [_P, _P, _I64, _P]),
     "mmpde_gnn_workspace_bytes": (_I64, [_I64]),
     "mmpde_gnn_embed": (_I, [_P, _P, _I64, GnnScales, _P, _P, _P, _P]),
     "mmpde_gnn_layer": (_I, [_P, _P, _P, _I64, _I, _P, GnnScales, _P, _P, _P, _P]),

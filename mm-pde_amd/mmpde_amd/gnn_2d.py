@@ -83,6 +83,51 @@ class EdgeGraph:
         return self._rev
 
 
+def _edge_mean_fwd(a, b, w2, b2, graph: EdgeGraph, edge_gemm: str):
+    """mean_i over the in-edges of relu(W2 relu(a_i + b_j) + b2) (EdgeMean's
+    forward): (mean [n, 128], the f16x3 ReLU pattern of message_net_2 or None)."""
+    n, k = graph.nbr.shape
+    mean = torch.empty((n, 128), dtype=torch.float32, device=a.device)
+    mode = L.EDGE_GEMM[edge_gemm]
+    lib = L.lib()
+    wsb = lib.mmpde_gnn_edge_mean_workspace_bytes(n, mode)
+    ws = torch.empty((max(wsb, 16) // 4,), dtype=torch.float32, device=a.device) if wsb else None
+    # the forward keeps message_net_2's ReLU pattern (16 B per edge) for the
+    # backward, which then skips recomputing z2 (and differentiates exactly the
+    # function the forward evaluated: its own z2 summation order differs)
+    mask = torch.empty((n * k, 4), dtype=torch.int32, device=a.device) if k <= 64 else None
+    L.check(lib.mmpde_gnn_edge_mean_ex(L.ptr(a), L.ptr(b), L.ptr(graph.nbr), L.ptr(graph.deg), n, k,
+                                       L.ptr(w2), L.ptr(b2), L.ptr(mean), L.ptr(mask), mode, L.ptr(ws), wsb,
+                                       L.stream(a.device)),
+            "mmpde_gnn_edge_mean_ex")
+    return mean, mask
+
+
+def _edge_mean_bwd(a, b, w2, b2, graph: EdgeGraph, mask, edge_gemm: str, g):
+    """(dL/da, dL/db, dL/dW2, dL/db2) of _edge_mean_fwd for dL/dmean = g: the
+    per-edge dL/dz1 rows written source-major (slot_pos), then summed per
+    source as contiguous runs."""
+    n, k = graph.nbr.shape
+    dev = a.device
+    lib = L.lib()
+    ga = torch.empty_like(a)
+    gb = torch.empty_like(b)
+    gedge = torch.empty((n * k, 128), dtype=torch.float32, device=dev)
+    part = torch.empty((lib.mmpde_gnn_edge_backward_partials(None),), dtype=torch.float32, device=dev)
+    gw2 = torch.empty((128, 128), dtype=torch.float32, device=dev)
+    gb2 = torch.empty((128,), dtype=torch.float32, device=dev)
+    st = L.stream(dev)
+    rev_off, _, slot_pos = graph.reverse()
+    L.check(lib.mmpde_gnn_edge_backward_sorted(L.ptr(a), L.ptr(b), L.ptr(graph.nbr), L.ptr(graph.deg),
+                                               n, k, L.ptr(w2), L.ptr(b2), L.ptr(g), L.ptr(slot_pos),
+                                               L.ptr(mask), L.ptr(ga), L.ptr(gedge), L.ptr(part),
+                                               L.ptr(gw2), L.ptr(gb2), L.EDGE_GEMM[edge_gemm], st),
+            "mmpde_gnn_edge_backward_sorted")
+    L.check(lib.mmpde_gnn_edge_source_sum_sorted(L.ptr(gedge), L.ptr(rev_off), n, L.ptr(gb), st),
+            "mmpde_gnn_edge_source_sum_sorted")
+    return ga, gb, gw2, gb2
+
+
 class EdgeMean(torch.autograd.Function):
     """mean_i = 1/max(deg_i, 1) sum_{e < deg_i} relu(W2 relu(a_i + b_{nbr[i,e]}) + b2):
     message_net_2 over the in-edges and PyG's aggr='mean' (gnn_2d.py:36,59-63),
@@ -100,52 +145,147 @@ class EdgeMean(torch.autograd.Function):
             raise ValueError("EdgeMean takes a, b [n, 128] and W2 [128, 128]")
         L.require_device(a, b, w2, b2, graph.nbr, graph.deg)
         a, b, w2, b2 = L.f32c(a), L.f32c(b), L.f32c(w2), L.f32c(b2)
-        mean = torch.empty((n, 128), dtype=torch.float32, device=a.device)
-        mode = L.EDGE_GEMM[edge_gemm]
-        lib = L.lib()
-        wsb = lib.mmpde_gnn_edge_mean_workspace_bytes(n, mode)
-        ws = torch.empty((max(wsb, 16) // 4,), dtype=torch.float32, device=a.device) if wsb else None
-        # f16x3: the forward keeps message_net_2's ReLU pattern (16 B per edge)
-        # for the backward, which then skips recomputing z2
-        mask = (torch.empty((n * k, 4), dtype=torch.int32, device=a.device)
-                if edge_gemm == "f16x3" and k <= 64 else None)
-        L.check(lib.mmpde_gnn_edge_mean_ex(L.ptr(a), L.ptr(b), L.ptr(graph.nbr), L.ptr(graph.deg), n, k,
-                                           L.ptr(w2), L.ptr(b2), L.ptr(mean), L.ptr(mask), mode, L.ptr(ws), wsb,
-                                           L.stream(a.device)),
-                "mmpde_gnn_edge_mean_ex")
+        mean, mask = _edge_mean_fwd(a, b, w2, b2, graph, edge_gemm)
         ctx.save_for_backward(a, b, w2, b2)
         ctx.graph = graph
         ctx.mask = mask
-        ctx.edge_gemm = L.EDGE_GEMM[edge_gemm]
+        ctx.edge_gemm = edge_gemm
         return mean
 
     @staticmethod
     def backward(ctx, g):
         a, b, w2, b2 = ctx.saved_tensors
-        graph = ctx.graph
-        n, k = graph.nbr.shape
-        dev = a.device
-        g = L.f32c(g)
-        lib = L.lib()
-        ga = torch.empty_like(a)
-        gb = torch.empty_like(b)
-        gedge = torch.empty((n * k, 128), dtype=torch.float32, device=dev)
-        part = torch.empty((lib.mmpde_gnn_edge_backward_partials(None),), dtype=torch.float32,
-                           device=dev)
-        gw2 = torch.empty((128, 128), dtype=torch.float32, device=dev)
-        gb2 = torch.empty((128,), dtype=torch.float32, device=dev)
-        st = L.stream(dev)
-        # per-edge dL/dz1 written source-major (slot_pos), then summed per
-        # source as contiguous runs
-        rev_off, _, slot_pos = graph.reverse()
-        L.check(lib.mmpde_gnn_edge_backward_sorted(L.ptr(a), L.ptr(b), L.ptr(graph.nbr), L.ptr(graph.deg),
-                                                   n, k, L.ptr(w2), L.ptr(b2), L.ptr(g), L.ptr(slot_pos),
-                                                   L.ptr(ctx.mask), L.ptr(ga), L.ptr(gedge), L.ptr(part),
-                                                   L.ptr(gw2), L.ptr(gb2), ctx.edge_gemm, st),
-                "mmpde_gnn_edge_backward_sorted")
-        L.check(lib.mmpde_gnn_edge_source_sum_sorted(L.ptr(gedge), L.ptr(rev_off), n, L.ptr(gb), st),
-                "mmpde_gnn_edge_source_sum_sorted")
+        ga, gb, gw2, gb2 = _edge_mean_bwd(a, b, w2, b2, ctx.graph, ctx.mask, ctx.edge_gemm, L.f32c(g))
         return ga, gb, gw2, gb2, None, None
+
+
+class GnnLayerTrain(torch.autograd.Function):
+    """One train-mode GNN_Layer_FS_2D (gnn_2d.py:53-69; time_window 1, one
+    variable, width 128) on HIP kernels, forward and backward:
+
+        a   = h W1[:, :128]^T + (u, x, y, t) W1[:, 256:260]^T + b1     (target half)
+        b   = h W1[:, 128:256]^T - (u, x, y) W1[:, 256:259]^T          (source half)
+        m   = EdgeMean(a, b)                        (message_net_2 + PyG mean)
+        v   = relu([h | m] U1[:, :256]^T + t U1[:, 256] + c1)           (update_net_1)
+        upd = relu(v U2^T + c2)                                          (update_net_2)
+        h'  = BatchNorm1d_train(h + upd)
+
+    every GEMM on mmpde_rgemm (exact fp32 MFMA; the concatenations read in
+    place, bias / ReLU / the ReLU-backward masks / the residual fused), the
+    weight gradients on mmpde_rgemm_tn, BatchNorm on the row kernels.  The
+    backward accumulates dL/dh (residual + update_net_1 + both message_net_1
+    halves) in one buffer.  extras = (u, x/Lx, y/Ly, t/tmax) [n, 4]."""
+
+    @staticmethod
+    def forward(ctx, h, extras, w1, b1, w2, b2, u1, c1, u2, c2, bnw, bnb, graph, edge_gemm, bn):
+        from . import rows
+        L.require_device(h, extras, w1, u1, u2)
+        h, extras = L.f32c(h), L.f32c(extras)
+        W1, B1, W2, B2 = (L.f32c(t) for t in (w1, b1, w2, b2))
+        U1 = torch.nn.functional.pad(u1.detach().float(), (0, 3)).contiguous()   # [128, 260]: 16-B rows
+        C1, U2, C2 = L.f32c(c1), L.f32c(u2), L.f32c(c2)
+        n = h.shape[0]
+        dev = h.device
+        st = L.stream(dev)
+        P = rows._p
+        f32 = dict(dtype=torch.float32, device=dev)
+        ab = torch.empty((2, n, 128), **f32)
+        a, b = ab[0], ab[1]
+        rows.rgemm(n, 64, L.RGEMM_NT, (P(W1), P(W1, 64)), 260, (P(h), P(h, 64)), (128, 128),
+                   [dict(out=P(a), ldo=128, wc=0, wk=0, ncols=128, bias=P(B1), ns=4, xw=P(W1, 256)),
+                    dict(out=P(b), ldo=128, wc=0, wk=128, ncols=128, ns=3, xw=P(W1, 256), xscale=-1.0)],
+                   xs=P(extras), ldxs=4, ldxw=260, stream=st)
+        mean, mask = _edge_mean_fwd(a, b, W2, B2, graph, edge_gemm)
+        v = torch.empty((n, 128), **f32)
+        rows.rgemm(n, 128, L.RGEMM_NT, (P(U1), P(U1, 128)), 260, (P(h), P(mean)), (128, 128),
+                   [dict(out=P(v), ldo=128, ncols=128, bias=P(C1), ns=1, xw=P(U1, 256))],
+                   relu=True, xs=P(extras, 3), ldxs=4, ldxw=260, stream=st)
+        upd = torch.empty((n, 128), **f32)
+        rows.rgemm(n, 64, L.RGEMM_NT, (P(U2), P(U2, 64)), 128, (P(v), P(v, 64)), (128, 128),
+                   [dict(out=P(upd), ldo=128, ncols=128, bias=P(C2))], relu=True, stream=st)
+        # BatchNorm1d(h + upd) in train mode (running statistics as nn.BatchNorm1d)
+        factor = 0.0
+        if bn.track_running_stats and bn.num_batches_tracked is not None:
+            bn.num_batches_tracked.add_(1)
+            factor = 1.0 / float(bn.num_batches_tracked) if bn.momentum is None else bn.momentum
+        rm = bn.running_mean if bn.track_running_stats else None
+        rv = bn.running_var if bn.track_running_stats else None
+        lib = L.lib()
+        nb = lib.mmpde_batch_norm_rows_workspace_bytes(n, 128) + 3 * 128 * 4
+        ws = torch.empty((nb // 4,), **f32)
+        stats = torch.empty((4 * 128,), **f32)
+        hn = torch.empty((n, 128), **f32)
+        BW = L.f32c(bnw) if bnw is not None else None
+        L.check(lib.mmpde_batch_norm_rows_train(
+            L.ptr(h), L.ptr(upd), n, 128, L.ptr(BW), L.ptr(L.f32c(bnb) if bnb is not None else None),
+            float(bn.eps), float(factor), L.ptr(rm), L.ptr(rv), L.ptr(hn), L.ptr(stats), L.ptr(ws), nb, st),
+            "mmpde_batch_norm_rows_train")
+        ctx.save_for_backward(h, extras, a, b, mean, v, upd, stats, W1, B1, W2, B2, U1, U2, BW)
+        ctx.graph, ctx.mask, ctx.edge_gemm, ctx.bn_ws = graph, mask, edge_gemm, nb
+        ctx.has_bn = (bnw is not None, bnb is not None)
+        return hn
+
+    @staticmethod
+    def backward(ctx, dhn):
+        from . import rows
+        h, extras, a, b, mean, v, upd, stats, W1, B1, W2, B2, U1, U2, BW = ctx.saved_tensors
+        n = h.shape[0]
+        dev = h.device
+        st = L.stream(dev)
+        P = rows._p
+        f32 = dict(dtype=torch.float32, device=dev)
+        lib = L.lib()
+        dhn = L.f32c(dhn)
+        # BatchNorm backward: dx = dL/d(h + upd), the residual's and update's alike
+        dx = torch.empty((n, 128), **f32)
+        dgam = torch.empty((128,), **f32) if ctx.has_bn[0] else None
+        dbet = torch.empty((128,), **f32) if ctx.has_bn[1] else None
+        ws = torch.empty((ctx.bn_ws // 4,), **f32)
+        L.check(lib.mmpde_batch_norm_rows_backward(L.ptr(h), L.ptr(upd), L.ptr(dhn), n, 128, L.ptr(BW),
+                                                   L.ptr(stats), L.ptr(dx), L.ptr(dgam), L.ptr(dbet),
+                                                   L.ptr(ws), ctx.bn_ws, st),
+                "mmpde_batch_norm_rows_backward")
+        # update_net_2: dv = ((dx * [upd > 0]) U2) * [v > 0] (update_net_1's pre-activation gradient)
+        dv = torch.empty((n, 128), **f32)
+        rows.rgemm(n, 64, L.RGEMM_NN, (P(U2), P(U2, 64 * 128)), 128, (P(dx), P(dx, 64)), (128, 128),
+                   [dict(out=P(dv), ldo=128, ncols=128, omask=P(v), ldom=128)],
+                   amask=(P(upd), P(upd, 64)), stream=st)
+        dU2 = torch.empty((128, 128), **f32)
+        dc2 = torch.empty((128,), **f32)
+        rows.rgemm_tn(n, P(dx), 128, 128, [(P(v), 128, 128, 0)], dU2, 128, db=dc2, gmask=P(upd), stream=st)
+        # update_net_1: dh += dv U1[:, :128] (onto the residual's dx), dmean = dv U1[:, 128:256]
+        dmean = torch.empty((n, 128), **f32)
+        rows.rgemm(n, 64, L.RGEMM_NN, (P(U1), P(U1, 64 * 260)), 260, (P(dv), P(dv, 64)), (128, 128),
+                   [dict(out=P(dx), ldo=128, wc=0, ncols=128, acc=True),
+                    dict(out=P(dmean), ldo=128, wc=128, ncols=128)], stream=st)
+        dU1 = torch.empty((128, 257), **f32)
+        dc1 = torch.empty((128,), **f32)
+        rows.rgemm_tn(n, P(dv), 128, 128, [(P(h), 128, 128, 0), (P(mean), 128, 128, 128)], dU1, 257,
+                      db=dc1, xs=P(extras, 3), ldxs=4, ns=1, dwcol_s=256, stream=st)
+        # message_net_2 + mean
+        da, db, dW2, db2 = _edge_mean_bwd(a, b, W2, B2, ctx.graph, ctx.mask, ctx.edge_gemm, dmean)
+        # message_net_1 halves: dh += da W1[:, :128] + db W1[:, 128:256]
+        rows.rgemm(n, 128, L.RGEMM_NN, (P(W1), P(W1, 128)), 260, (P(da), P(db)), (128, 128),
+                   [dict(out=P(dx), ldo=128, wc=0, ncols=128, acc=True)], stream=st)
+        dW1 = torch.empty((128, 260), **f32)
+        db1 = torch.empty((128,), **f32)
+        rows.rgemm_tn(n, P(da), 128, 128, [(P(h), 128, 128, 0)], dW1, 260, db=db1,
+                      xs=P(extras), ldxs=4, ns=4, dwcol_s=256, stream=st)
+        rows.rgemm_tn(n, P(db), 128, 128, [(P(h), 128, 128, 128)], dW1, 260,
+                      xs=P(extras), ldxs=4, ns=3, dwcol_s=256, sign_s=-1.0, accumulate_s=True, stream=st)
+        dext = None
+        if ctx.needs_input_grad[1]:
+            # (u, x, y, t) enter a with W1[:, 256:260], b with -W1[:, 256:259] and v
+            # with t U1[:, 256] (u needs it when ItpNet interpolated it, Burgers)
+            dext = torch.empty((n, 4), **f32)
+            # the halves share one row stride: -W1[:, 256:259] as a padded copy
+            nwp = torch.zeros((128, 260), **f32)
+            nwp[:, 256:259] = -W1[:, 256:259]
+            rows.rgemm(n, 128, L.RGEMM_NN, (P(W1, 256), P(nwp, 256)), 260, (P(da), P(db)), (128, 128),
+                       [dict(out=P(dext), ldo=4, ncols=4)], stream=st)
+            rows.rgemm(n, 64, L.RGEMM_NN, (P(U1, 256), P(U1, 64 * 260 + 256)), 260, (P(dv), P(dv, 64)),
+                       (128, 128), [dict(out=P(dext, 3), ldo=4, ncols=1, acc=True)], stream=st)
+        return (dx, dext, dW1, db1, dW2, db2, dU1, dc1, dU2, dc2, dgam, dbet, None, None, None)
 
 
 class GNN_Layer_FS_2D(nn.Module):  # noqa: N801 - reference name
@@ -197,6 +337,21 @@ class GNN_Layer_FS_2D(nn.Module):  # noqa: N801 - reference name
                                  w1.shape[1], 260)
             self._pack, self._pack_key = (p, keep), key
         return self._pack[0]
+
+    def fused_train_ok(self):
+        """GnnLayerTrain covers the reference defaults (width 128, time_window 1,
+        one variable)."""
+        return (self.in_features == self.out_features == self.hidden_features == 128
+                and self.time_window == 1 and self.n_variables == 1)
+
+    def train_forward_fused(self, h, extras, graph: EdgeGraph, edge_gemm: str = "f32"):
+        """gnn_2d.py:53-69 in train mode as one GnnLayerTrain (extras = (u, x/Lx,
+        y/Ly, t/tmax) [n, 4])."""
+        m1, m2 = self.message_net_1[0], self.message_net_2[0]
+        u1, u2 = self.update_net_1[0], self.update_net_2[0]
+        bn = self.norm.module
+        return GnnLayerTrain.apply(h, extras, m1.weight, m1.bias, m2.weight, m2.bias, u1.weight, u1.bias,
+                                   u2.weight, u2.bias, bn.weight, bn.bias, graph, edge_gemm, bn)
 
     def train_forward(self, h, u, pos_x, pos_y, variables, graph: EdgeGraph, edge_gemm: str = "f32"):
         """Differentiable layer (gnn_2d.py:53-69).  message_net_1 of the edge (i, j)
@@ -417,10 +572,15 @@ class MP_PDE_Solver_2D(nn.Module):  # noqa: N801 - reference name
         pos_y = pos[:, 2][:, None] / self.pde.Ly
         variables = pos[:, 0][:, None] / self.pde.tmax
         e = self.embedding_mlp
-        z = torch.relu(batch_norm_rows(e[1], linear_train(torch.cat((u, pos_x, pos_y, variables), -1), e[0])))
+        node_input = torch.cat((u, pos_x, pos_y, variables), -1)
+        z = torch.relu(batch_norm_rows(e[1], linear_train(node_input, e[0])))
         h = batch_norm_rows(e[4], linear_train(z, e[3]))
         for layer in self.gnn_layers:
-            h = layer.train_forward(h, u, pos_x, pos_y, variables, graph, self.edge_gemm)
+            if layer.fused_train_ok() and self.time_window == 1 and h.shape[0] >= 2:
+                # (u, x, y, t) is the embedding input itself (tw = 1)
+                h = layer.train_forward_fused(h, node_input, graph, self.edge_gemm)
+            else:
+                h = layer.train_forward(h, u, pos_x, pos_y, variables, graph, self.edge_gemm)
         diff = self._head_train(h)
         return self.out_scales()[None].to(h.device) * diff
 

@@ -10,6 +10,7 @@ import ctypes
 import torch
 
 from . import _lib as L
+from . import rows
 
 # kNN kernels stage one trajectory's points in LDS and keep its distances in
 # registers (csrc/knn.hip): at most this many points per trajectory
@@ -483,33 +484,29 @@ def conv2d_grad_weight(x: torch.Tensor, dy: torch.Tensor, ks: int, pad: int, cir
 
 
 class LinearRows(torch.autograd.Function):
-    """y = x W^T + b over many rows (the train-mode node GEMMs of
-    GNN_Layer_FS_2D / MP_PDE_Solver_2D, gnn_2d.py:53-69,99-106), with a
-    weight gradient that reduces over the rows in chunks: dW = sum_c dY_c^T X_c
-    as one batched GEMM over C equal row chunks plus the remainder rows,
-    summed in chunk order.  The library's single GEMM with K = n rows
-    (hipBLASLt picks 32 x 32 tiles and a serial K loop) takes 105-247 us per
-    layer GEMM at n = 40336; the batched form 26-53 us (tools/gemm_shapes.py,
-    profiles/r04_gemm_shapes.log).  dX = dY W and the forward stay single GEMMs.
-    Deterministic for a given shape (fixed chunking, fixed reduction order)."""
-
-    @staticmethod
-    def chunks(n: int, k: int) -> int:
-        return 0 if n < 4096 else (64 if k > 160 else 16)
+    """y = x W^T + b over many rows: the train-mode Linears of GNN_Layer_FS_2D /
+    MP_PDE_Solver_2D (gnn_2d.py:53-69,99-114) and ItpNet (interpolate.py:79-93)
+    on the HIP row GEMMs (rows.py, csrc/rgemm.hip: exact fp32 MFMA): forward
+    mmpde_rgemm (NT), dX = dY W mmpde_rgemm (NN), dW = dY^T X and db over the
+    rows in fixed row chunks (mmpde_rgemm_tn), or for a skinny map (the Conv1d
+    head's windows, the embedding's first Linear) mmpde_rows_grad_weight.  No
+    library GEMM; deterministic for a given shape."""
 
     @staticmethod
     def forward(ctx, x, w, b):
-        ctx.save_for_backward(x, w)
+        L.require_device(x, w, b)
+        x, wc = L.f32c(x), L.f32c(w)
+        ctx.save_for_backward(x, wc)
         ctx.has_bias = b is not None
-        y = x @ w.t()
-        return y + b if b is not None else y
+        return rows.linear_fwd(x, wc, L.f32c(b) if b is not None else None)
 
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
+        dy = L.f32c(dy)
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
-            gx = dy @ w
+            gx = rows.linear_bwd_input(dy, w)
         n, k = x.shape
         nout = w.shape[0]
         want_b = ctx.has_bias and ctx.needs_input_grad[2]
@@ -519,18 +516,9 @@ class LinearRows(torch.autograd.Function):
             # skinny map (head windows, embedding): dW and db in one row pass
             gw, gb = rows_grad_weight(x, dy, k if ctx.needs_input_grad[1] else 0, want_b)
             return gx, gw, gb
-        if want_b:
-            gb = rows_grad_weight(x, dy, 0, True)[1] if n >= 4096 and nout <= 128 else dy.sum(0)
-        if ctx.needs_input_grad[1]:
-            C = LinearRows.chunks(n, k)
-            if C:
-                R = n // C
-                xs, dys = x[:C * R].reshape(C, R, k), dy[:C * R].reshape(C, R, dy.shape[1])
-                gw = torch.bmm(dys.transpose(1, 2), xs).sum(0)
-                if C * R < n:
-                    gw = gw + dy[C * R:].t() @ x[C * R:]
-            else:
-                gw = dy.t() @ x
+        gw = torch.empty_like(w) if ctx.needs_input_grad[1] else None
+        gb = torch.empty((nout,), dtype=torch.float32, device=x.device) if want_b else None
+        rows.linear_bwd_weight(dy, x, gw, gb)
         return gx, gw, gb
 
 

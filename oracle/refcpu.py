@@ -139,8 +139,22 @@ def knn_query(src: torch.Tensor, qry: torch.Tensor, batches: int, k: int):
 # ----------------------------------------------------------------------------
 # small functional helpers, same torch ops as the reference modules
 # ----------------------------------------------------------------------------
+# Summation order of every Linear (_lin): None = torch's own (the reference's
+# op); an int = the same map with its input features taken in a fixed
+# pseudo-random order -- mathematically identical, a different fp32 rounding.
+# The training tests use such reordered fp32 evaluations as further fp32
+# floors: an activation within fp32 rounding of a ReLU's kink lands on either
+# side depending on the summation order alone.
+LINEAR_ORDER = None
+
+
 def _lin(sd, p, x):
-    return F.linear(x, sd[p + ".weight"], sd[p + ".bias"])
+    w, b = sd[p + ".weight"], sd[p + ".bias"]
+    if LINEAR_ORDER is not None and x.dtype == torch.float32 and x.shape[-1] > 1:
+        g = torch.Generator().manual_seed(7919 * LINEAR_ORDER + x.shape[-1])
+        perm = torch.randperm(x.shape[-1], generator=g)
+        return F.linear(x[..., perm], w[:, perm], b)
+    return F.linear(x, w, b)
 
 
 def _bn(sd, p, x, eps=1e-5, train=False, momentum=0.1):

@@ -63,10 +63,15 @@ def _grad_close(got, ref, floor32, what, atol=0.0):
     sides, which sets a floor near 1e-4 for burgers -- and 1e-3 of max|ref|
     (+atol) element-wise."""
     err, scale = _err(got, ref, what)
-    rn, floor = _rel_norm(got, ref), _rel_norm(floor32, ref)
-    print(f"    rel-L2 {rn:.2e} (fp32 oracle {floor:.2e})")
+    floors = floor32 if isinstance(floor32, (list, tuple)) else [floor32]
+    rn, floor = _rel_norm(got, ref), max(_rel_norm(f, ref) for f in floors)
+    print(f"    rel-L2 {rn:.2e} (fp32 oracle {floor:.2e} over {len(floors)} summation order(s))")
     assert rn <= max(1e-4, 2 * floor) or (atol and err <= atol), (what, rn, floor)
-    assert err <= 1e-3 * scale + atol, (what, err, 1e-3 * scale + atol)
+    # element-wise: 1e-3 of max|ref|, or 2x the worst fp32 oracle's own max error
+    # when it is larger (a ReLU flip moves single elements)
+    ef = max((f.detach().double().cpu().reshape(-1) - ref.detach().double().cpu().reshape(-1)).abs().max().item()
+             for f in floors) if len(floors) > 1 else 0.0
+    assert err <= max(1e-3 * scale, 2 * ef) + atol, (what, err, 1e-3 * scale + atol, ef)
 
 
 # --------------------------------------------------------------------------- edge stage
@@ -192,6 +197,26 @@ def test_training_step_gradients_vs_oracle(dev, kind, edge_gemm):
     _close(pred, aux["pred"], 2e-5, f"{kind} train-mode pred")
     assert abs(loss.item() - rloss.item()) <= 1e-5 * rloss.item(), (loss.item(), rloss.item())
 
+    # the fp32 floor: the fp32 oracle in torch's summation order and, for a
+    # gradient that misses the bar against it, in two more orders of every
+    # Linear's inputs (refcpu.LINEAR_ORDER; the same function): a ReLU input
+    # within fp32 rounding of 0 (the Burgers case has one at 8e-9 of its row's
+    # max in layer 2's update_net_2) takes either side by summation order
+    alt = []
+
+    def alt_floors():
+        if not alt:
+            for order in (1, 2):
+                refcpu.LINEAR_ORDER = order
+                try:
+                    s32 = _sds(torch.float32, model=model, model_b=model_b, itp=itp)
+                    l32, _ = refcpu.mmpde_train_loss(opde32, s32, data, labels, steps, mesh_override=mesh.float())
+                    l32.backward()
+                finally:
+                    refcpu.LINEAR_ORDER = None
+                alt.append(s32)
+        return alt
+
     checked = 0
     for key, mod in (("model", model), ("model_b", model_b), ("itp", itp)):
         for name, p in mod.named_parameters():
@@ -203,7 +228,13 @@ def test_training_step_gradients_vs_oracle(dev, kind, edge_gemm):
             atol = 0.0
             if name.endswith(".bias"):
                 atol = 1e-4 * sds[key][name[:-5] + ".weight"].grad.abs().max().item()
-            _grad_close(p.grad, r, sds32[key][name].grad, f"{kind} grad {key}.{name}", atol=atol)
+            floors = [sds32[key][name].grad]
+            rn = _rel_norm(p.grad, r)
+            e0, s0 = _err(p.grad, r, "")
+            if (rn > max(1e-4, 2 * _rel_norm(floors[0], r)) and not (atol and e0 <= atol)) or \
+                    e0 > 1e-3 * s0 + atol:
+                floors += [s[key][name].grad for s in alt_floors()]
+            _grad_close(p.grad, r, floors, f"{kind} grad {key}.{name}", atol=atol)
             checked += 1
         for name, buf in mod.named_buffers():
             if name.endswith(("running_mean", "running_var")):

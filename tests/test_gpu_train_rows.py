@@ -98,7 +98,12 @@ def test_frozen_head_backward_returns_input_grad(dev):
         if idx != 4:
             d = torch.relu(d)
     d.squeeze(1).sum().backward()
-    _close(hd.grad, hr.grad, 2e-5, "frozen head dL/dh")
+    # two ReLUs on the way: an fp32 pre-activation within rounding of 0 may take
+    # the other side than in float64 and move that node's row, so the bar is a
+    # relative L2 error (as tests/test_gpu_train.py's)
+    rel = ((hd.grad.double().cpu() - hr.grad).norm() / hr.grad.norm()).item()
+    print(f"frozen head dL/dh rel-L2 {rel:.2e}")
+    assert rel <= 1e-4
     # a bias-only gradient (weight frozen) on the skinny path too
     x = torch.randn(20000, 48, generator=g).to(dev)
     w = (torch.randn(8, 48, generator=g) / 7).to(dev)
