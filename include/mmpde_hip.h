@@ -487,7 +487,7 @@ int mmpde_rgemm(const mmpde_rgemm_args *g, mmpde_stream_t stream);
  * Rows are summed in fixed chunks of `chunk_rows` (partials in the workspace,
  * then added in chunk order): deterministic.  workspace:
  * mmpde_rgemm_tn_workspace_bytes(m, chunk_rows, sum over s of kx[s] rounded
- * up to 32, + ns + 1). */
+ * up to 64, + ns + 1). */
 typedef struct mmpde_rgemm_tn_args {
     int64_t m;
     int chunk_rows, gcols;

@@ -12,137 +12,317 @@
 //             (partials, then a fixed-order sum): deterministic.
 //
 // Exact fp32 products on v_mfma_f32_32x32x2_f32 (lane l supplies A[l & 31][l
-// >> 5] and B[l >> 5][l & 31]).  A workgroup is 4 waves: rgemm covers 32 rows
-// x 128 columns (each wave one 32 x 32 tile); k-lane 0 walks K half 0, k-lane
-// 1 half 1, so one GEMM consumes two input tensors side by side without
-// building their concatenation.  VEC: float4 row loads (kh % 4 == 0, 16-byte
-// aligned rows; NT: W rows too), else one k per step.
+// >> 5] and B[l >> 5][l & 31]).  Operand reuse is what bounds these kernels
+// (each MFMA consumes one value per lane of A and of B, 64 cycles of matrix
+// work per 512 B of operands): every wave computes a 2 x 2 block of 32 x 32
+// tiles, so each loaded operand feeds two MFMAs.
 #include "common.hpp"
+
+#include <algorithm>
 
 namespace {
 
-constexpr int RG_TILE = 32;
 
 __device__ __forceinline__ float4 mask4(float4 a, const float4 &q) {
     return make_float4(q.x > 0.0f ? a.x : 0.0f, q.y > 0.0f ? a.y : 0.0f, q.z > 0.0f ? a.z : 0.0f,
                        q.w > 0.0f ? a.w : 0.0f);
 }
 
+// rgemm: one wave = 64 rows x 64 columns (row tiles rt, column tiles ct, each
+// 32 x 32); workgroup = 4 waves = 128 rows x 128 columns.  K: k-lane 0 walks
+// half 0, k-lane 1 half 1 (two input tensors side by side); VEC (kh % 4 == 0,
+// 16-byte aligned rows; NT: W rows too): float4 operand loads, the next 4-k
+// step's loaded under the current step's 16 MFMAs; two accumulation chains
+// per tile (alternate 4-k steps), added at the end.
 template <int LAYOUT, bool VEC, bool AMASK, bool XS>
-__global__ __launch_bounds__(256) void rgemm_kernel(mmpde_rgemm_args g) {
+__global__ __launch_bounds__(256, 2) void rgemm_kernel(mmpde_rgemm_args g) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int h = lane >> 5, j = lane & 31;
     const int p = blockIdx.y;
-    if (32 * wave >= g.ncols[p]) return;          // a wave of columns past the part (skinny maps)
-    const int64_t row0 = (int64_t)blockIdx.x * RG_TILE;
-    const int64_t m = g.m;
-    const int64_t row = min(row0 + j, m - 1);   // clamped: loads stay in bounds
-    const int col = 32 * wave + j;                // output column within the part
     const int ncols = g.ncols[p];
-    const int colc = min(col, ncols - 1);         // clamped for the W loads
-    // four accumulation chains (k = 4 s + q goes to chain q), added pairwise at
-    // the end: sums of kh / 4 terms per chain instead of one chain of kh
-    f32x16 c0 = {0}, c1 = {0}, c2 = {0}, c3 = {0};
-    if (g.kh > 0) {
-        const float *ap = g.a[h] + row * g.lda[h];
-        const float *mp = AMASK ? g.amask[h] + row * g.lda[h] : nullptr;
-        const int64_t ldw = g.ldw;
-        const int kh = g.kh;
-        if (LAYOUT == MMPDE_RGEMM_NT) {
-            const float *wp = g.w[h] + (g.wc[p] + colc) * ldw + g.wk[p];
-            if (VEC) {
-#pragma unroll 2
-                for (int s = 0; s < kh; s += 4) {
-                    float4 a = *(const float4 *)(ap + s);
-                    if (AMASK) a = mask4(a, *(const float4 *)(mp + s));
-                    const float4 w = *(const float4 *)(wp + s);
-                    c0 = mfma32(a.x, w.x, c0);
-                    c1 = mfma32(a.y, w.y, c1);
-                    c2 = mfma32(a.z, w.z, c2);
-                    c3 = mfma32(a.w, w.w, c3);
-                }
-            } else {
-                for (int s = 0; s < kh; s += 4) {
+    const int cbase = 64 * (wave & 1);
+    const int64_t row0 = (int64_t)blockIdx.x * 128 + 64 * (wave >> 1);
+    const int64_t m = g.m;
+    if (cbase >= ncols || row0 >= m) return;      // wave-uniform: no column / row of this wave
+    const int kh = g.kh;
+    f32x16 acc[2][2][2];  // [row tile][column tile][chain]
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const int kk = min(s + q, kh - 1);
-                        float a = ap[kk];
-                        if (AMASK) a = mp[kk] > 0.0f ? a : 0.0f;
-                        a = s + q < kh ? a : 0.0f;
-                        f32x16 &c = q == 0 ? c0 : q == 1 ? c1 : q == 2 ? c2 : c3;
-                        c = mfma32(a, wp[kk], c);
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b][0] = acc[a][b][1] = (f32x16){0};
+    if (kh > 0) {
+        const int64_t ldw = g.ldw;
+        const float *ap[2], *mp[2], *wp[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int64_t row = min(row0 + 32 * t + j, m - 1);    // clamped: loads stay in bounds
+            ap[t] = g.a[h] + row * g.lda[h];
+            mp[t] = AMASK ? g.amask[h] + row * g.lda[h] : nullptr;
+            const int colc = min(cbase + 32 * t + j, ncols - 1);  // clamped for the W loads
+            wp[t] = LAYOUT == MMPDE_RGEMM_NT ? g.w[h] + (g.wc[p] + colc) * ldw + g.wk[p]
+                                             : g.w[h] + g.wk[p] * ldw + g.wc[p] + colc;
+        }
+        if (VEC) {
+            struct Ops {
+                float4 a[2], w[2];
+            };
+            auto load = [&](int s, Ops &o) {
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    float4 a = *(const float4 *)(ap[t] + s);
+                    if (AMASK) a = mask4(a, *(const float4 *)(mp[t] + s));
+                    o.a[t] = a;
+                    if (LAYOUT == MMPDE_RGEMM_NT) {
+                        o.w[t] = *(const float4 *)(wp[t] + s);
+                    } else {
+                        const float *w = wp[t] + s * ldw;
+                        o.w[t] = make_float4(w[0], w[ldw], w[2 * ldw], w[3 * ldw]);
                     }
                 }
+            };
+            auto step = [&](const Ops &o, int c) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+                        for (int ct = 0; ct < 2; ++ct)
+                            acc[rt][ct][c] = mfma32(f4c(o.a[rt], q), f4c(o.w[ct], q), acc[rt][ct][c]);
+            };
+            // two 4-k steps per iteration (one per chain); the next iteration's
+            // operands are loaded (clamped to the last step: in bounds, unused
+            // past kh) before this iteration's 32 MFMAs
+            Ops c0, c1, n0, n1;
+            load(0, c0);
+            load(min(4, kh - 4), c1);
+            for (int s = 0; s < kh; s += 8) {
+                load(min(s + 8, kh - 4), n0);
+                load(min(s + 12, kh - 4), n1);
+                step(c0, 0);
+                if (s + 4 < kh) step(c1, 1);  // wave-uniform
+                c0 = n0;
+                c1 = n1;
             }
         } else {
-            const float *wp = g.w[h] + g.wk[p] * ldw + g.wc[p] + colc;
-            if (VEC) {
-#pragma unroll 2
-                for (int s = 0; s < kh; s += 4) {
-                    float4 a = *(const float4 *)(ap + s);
-                    if (AMASK) a = mask4(a, *(const float4 *)(mp + s));
-                    const float *w = wp + s * ldw;
-                    c0 = mfma32(a.x, w[0], c0);
-                    c1 = mfma32(a.y, w[ldw], c1);
-                    c2 = mfma32(a.z, w[2 * ldw], c2);
-                    c3 = mfma32(a.w, w[3 * ldw], c3);
-                }
-            } else {
-                for (int s = 0; s < kh; s += 4) {
+            for (int s = 0; s < kh; s += 2) {
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const int kk = min(s + q, kh - 1);
-                        float a = ap[kk];
-                        if (AMASK) a = mp[kk] > 0.0f ? a : 0.0f;
-                        a = s + q < kh ? a : 0.0f;
-                        f32x16 &c = q == 0 ? c0 : q == 1 ? c1 : q == 2 ? c2 : c3;
-                        c = mfma32(a, wp[kk * ldw], c);
+                for (int c = 0; c < 2; ++c) {
+                    if (s + c >= kh) break;  // wave-uniform
+                    const int k = s + c;
+                    float a[2], w[2];
+#pragma unroll
+                    for (int t = 0; t < 2; ++t) {
+                        a[t] = ap[t][k];
+                        if (AMASK) a[t] = mp[t][k] > 0.0f ? a[t] : 0.0f;
+                        w[t] = LAYOUT == MMPDE_RGEMM_NT ? wp[t][k] : wp[t][(int64_t)k * ldw];
                     }
+#pragma unroll
+                    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+                        for (int ct = 0; ct < 2; ++ct)
+                            acc[rt][ct][c] = mfma32(a[rt], w[ct], acc[rt][ct][c]);
                 }
             }
         }
     }
-    const f32x16 acc = (c0 + c1) + (c2 + c3);
-    if (col >= ncols) return;
-    // epilogue: D[acc_row(r)][col]
-    const float bias = g.bias[p] ? g.bias[p][col] : 0.0f;
-    const int ns = XS ? g.ns[p] : 0;
-    float xw[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-    if (XS) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-            if (e < ns)
-                xw[e] = g.xscale[p] * (LAYOUT == MMPDE_RGEMM_NT ? g.xw[p][(int64_t)col * g.ldxw + e]
-                                                                : g.xw[p][(int64_t)e * g.ldxw + col]);
-    }
-    float *out = g.out[p];
+    // epilogue: D[acc_row(r)][j] of each tile
     const float *om = g.omask[p];
     const bool accum = g.accumulate[p] != 0;
+    const int ns = XS ? g.ns[p] : 0;
+    float *out = g.out[p];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int64_t i = row0 + acc_row(r, lane);
-        if (i >= m) continue;
-        float y = acc[r] + bias;
+    for (int ct = 0; ct < 2; ++ct) {
+        const int col = cbase + 32 * ct + j;
+        if (col >= ncols) continue;
+        const float bias = g.bias[p] ? g.bias[p][col] : 0.0f;
+        float xw[4] = {0.0f, 0.0f, 0.0f, 0.0f};
         if (XS) {
 #pragma unroll
             for (int e = 0; e < 4; ++e)
-                if (e < ns) y = fmaf(g.xs[i * g.ldxs + e], xw[e], y);
+                if (e < ns)
+                    xw[e] = g.xscale[p] * (LAYOUT == MMPDE_RGEMM_NT ? g.xw[p][(int64_t)col * g.ldxw + e]
+                                                                    : g.xw[p][(int64_t)e * g.ldxw + col]);
         }
-        if (g.relu) y = fmaxf(y, 0.0f);
-        if (om) y = om[i * g.ldom[p] + col] > 0.0f ? y : 0.0f;
-        float *o = out + i * g.ldo[p] + col;
-        *o = accum ? *o + y : y;
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) {
+            const f32x16 d = acc[rt][ct][0] + acc[rt][ct][1];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int64_t i = row0 + 32 * rt + acc_row(r, lane);
+                if (i >= m) continue;
+                float y = d[r] + bias;
+                if (XS) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (e < ns) y = fmaf(g.xs[i * g.ldxs + e], xw[e], y);
+                }
+                if (g.relu) y = fmaxf(y, 0.0f);
+                if (om) y = om[i * g.ldom[p] + col] > 0.0f ? y : 0.0f;
+                float *o = out + i * g.ldo[p] + col;
+                *o = accum ? *o + y : y;
+            }
+        }
     }
+}
+
+// The weight-stationary form for kh in {32, 64, 128} (every shape of the GNN
+// layers): persistent workgroups of 4 waves, wave w owning output columns
+// 32 w .. 32 w + 31 of the part, its B operand (W, kh values per lane) in
+// registers for the whole launch; the rows stream through LDS in tiles of 32
+// (both K halves, the ReLU-backward input mask applied while staging), the
+// next tile loaded into registers under the current tile's kh MFMAs and
+// stored to the other LDS buffer; one barrier per tile.
+template <int LAYOUT, int KH, bool AMASK, bool XS>
+__global__ __launch_bounds__(256, 1) void rgemm_ws_kernel(mmpde_rgemm_args g) {
+    constexpr int PITCH = 2 * KH + 4;        // floats per staged row (both halves)
+    constexpr int NF4 = 32 * 2 * KH / 4;     // float4 pieces of a tile
+    constexpr int PER = NF4 / 256;           // per thread
+    __shared__ float xt[2][32 * PITCH];
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int h = lane >> 5, j = lane & 31;
+    const int p = blockIdx.y;
+    const int ncols = g.ncols[p];
+    const bool active = 32 * wave < ncols;   // wave-uniform: this wave has output columns
+    const int col = 32 * wave + j;
+    const int colc = min(col, ncols - 1);
+    const int64_t m = g.m;
+    const int64_t ntiles = (m + 31) / 32;
+    // W operand: lane (j, h) holds B_h(s, colc) for s < KH
+    float wreg[KH];
+    {
+        const int64_t ldw = g.ldw;
+        if (LAYOUT == MMPDE_RGEMM_NT) {
+            const float *wp = g.w[h] + (g.wc[p] + colc) * ldw + g.wk[p];
+#pragma unroll
+            for (int s = 0; s < KH; s += 4) {
+                const float4 v = *(const float4 *)(wp + s);
+                wreg[s] = v.x;
+                wreg[s + 1] = v.y;
+                wreg[s + 2] = v.z;
+                wreg[s + 3] = v.w;
+            }
+        } else {
+            const float *wp = g.w[h] + g.wk[p] * ldw + g.wc[p] + colc;
+#pragma unroll
+            for (int s = 0; s < KH; ++s) wreg[s] = wp[(int64_t)s * ldw];
+        }
+    }
+    // staging: piece f = tid + 256 u -> row f / (KH / 2), half, float4 q
+    float4 stg[PER];
+    auto fetch = [&](int64_t tile) {
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int f = tid + 256 * u;
+            const int r = f / (KH / 2), rem = f % (KH / 2), hh = rem / (KH / 4), q = rem % (KH / 4);
+            const int64_t row = min(tile * 32 + r, m - 1);
+            float4 v = *(const float4 *)(g.a[hh] + row * g.lda[hh] + 4 * q);
+            if (AMASK) v = mask4(v, *(const float4 *)(g.amask[hh] + row * g.lda[hh] + 4 * q));
+            stg[u] = v;
+        }
+    };
+    auto stash = [&](float *buf) {
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int f = tid + 256 * u;
+            const int r = f / (KH / 2), rem = f % (KH / 2), hh = rem / (KH / 4), q = rem % (KH / 4);
+            *(float4 *)(buf + r * PITCH + hh * KH + 4 * q) = stg[u];
+        }
+    };
+    // epilogue constants of this lane's column
+    const float bias = active && g.bias[p] ? g.bias[p][colc] : 0.0f;
+    const int ns = XS ? g.ns[p] : 0;
+    float xw[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (XS && active) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            if (e < ns)
+                xw[e] = g.xscale[p] * (LAYOUT == MMPDE_RGEMM_NT ? g.xw[p][(int64_t)colc * g.ldxw + e]
+                                                                : g.xw[p][(int64_t)e * g.ldxw + colc]);
+    }
+    const float *om = g.omask[p];
+    const bool accum = g.accumulate[p] != 0;
+    float *out = g.out[p];
+    int64_t tile = blockIdx.x;
+    if (tile >= ntiles) return;  // workgroup-uniform, before any barrier
+    int cur = 0;
+    fetch(tile);
+    stash(xt[0]);
+    __syncthreads();
+    for (;;) {
+        const int64_t next = tile + gridDim.x;
+        const bool more = next < ntiles;  // workgroup-uniform
+        if (more) fetch(next);
+        if (active) {
+            // the epilogue's row inputs (small segment, output mask, the old
+            // output values) are loaded before the MFMAs, so their latency hides
+            // under them
+            float ex[16], em[16], eo[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int64_t i = min(tile * 32 + acc_row(r, lane), m - 1);
+                ex[r] = XS && ns > 0 ? g.xs[i * g.ldxs] : 0.0f;
+                em[r] = om ? om[i * g.ldom[p] + colc] : 1.0f;
+                eo[r] = accum ? out[i * g.ldo[p] + colc] : 0.0f;
+            }
+            const float *xr = xt[cur] + j * PITCH + h * KH;  // A: row j, half h
+            f32x16 c0 = {0}, c1 = {0};
+#pragma unroll
+            for (int s = 0; s < KH; s += 4) {
+                const float4 a = *(const float4 *)(xr + s);
+                c0 = mfma32(a.x, wreg[s], c0);
+                c1 = mfma32(a.y, wreg[s + 1], c1);
+                c0 = mfma32(a.z, wreg[s + 2], c0);
+                c1 = mfma32(a.w, wreg[s + 3], c1);
+            }
+            const f32x16 d = c0 + c1;
+            if (col < ncols) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int64_t i = tile * 32 + acc_row(r, lane);
+                    if (i >= m) continue;
+                    float y = d[r] + bias;
+                    if (XS) {
+                        if (ns > 0) y = fmaf(ex[r], xw[0], y);
+#pragma unroll
+                        for (int e = 1; e < 4; ++e)
+                            if (e < ns) y = fmaf(g.xs[i * g.ldxs + e], xw[e], y);
+                    }
+                    if (g.relu) y = fmaxf(y, 0.0f);
+                    if (om) y = em[r] > 0.0f ? y : 0.0f;
+                    out[i * g.ldo[p] + col] = accum ? eo[r] + y : y;
+                }
+            }
+        }
+        if (!more) break;
+        stash(xt[cur ^ 1]);
+        __syncthreads();  // the other buffer is complete; this one's readers are done
+        cur ^= 1;
+        tile = next;
+    }
+}
+
+int rgemm_cus() {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        cus = 256;
+    return cus;
 }
 
 // ---------------------------------------------------------------------------
 // dW = G^T X over the rows.  Partials: workspace [chunks][128][cols]; the
-// column space is every segment rounded up to 32 columns (segment s starts at
-// base(s) = sum of the rounded widths before it), then the ns small-segment
-// columns, then db.  Workgroup (kt, chunk): wave w the 32 x 32 tile (c = 32 w
-// .., k = 32 kt ..) over the chunk's rows, two rows per MFMA (row parity =
-// k-lane); the kt = 0 workgroups also sum the small segment and db from the
-// same G values on the VALU.
+// column space is every segment rounded up to 64 columns (segment s starts at
+// base(s) = the sum of the rounded widths before it), then the ns
+// small-segment columns, then db.  Workgroup (k block of 64 columns, chunk, c
+// block of 64 columns): 4 waves over the same 64 x 64 output block, wave w
+// the w-th quarter of the chunk's rows; the block is 2 x 2 tiles of 32 x 32:
+// lane j of tile (ct, kt) holds c = c0 + 2 j + ct and k = k0 + 2 j + kt, so one
+// float2 load of G and one of X per row feed four MFMAs (two rows per MFMA,
+// row parity = k-lane).  The four waves'
+// blocks are then added through LDS in wave order (fixed: deterministic).
+// The k block 0 workgroups also sum the small segment and db from the same G
+// values on the VALU.
 // ---------------------------------------------------------------------------
 struct TnArgs {
     mmpde_rgemm_tn_args g;
@@ -151,70 +331,182 @@ struct TnArgs {
     float *part;
 };
 
-template <bool GMASK>
-__global__ __launch_bounds__(256) void rgemm_tn_partial_kernel(TnArgs t) {
+__device__ __forceinline__ float2 ld2(const float *p, bool vec) {
+    return vec ? *(const float2 *)p : make_float2(p[0], p[1]);
+}
+
+template <bool GMASK, bool VEC>
+__global__ __launch_bounds__(256, 2) void rgemm_tn_partial_kernel(TnArgs t) {
+    constexpr int NRED = 64 + 2 + 8;  // per lane: the block (4 tiles x 16), db (2), small segment (2 x 4)
+    __shared__ float red[3][NRED][64];
     const mmpde_rgemm_tn_args &g = t.g;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int par = lane >> 5, j = lane & 31;
     const int chunk = blockIdx.y;
-    const int64_t r0 = (int64_t)chunk * g.chunk_rows;
-    const int64_t r1 = min(r0 + (int64_t)g.chunk_rows, g.m);
-    const int c = 32 * wave + j;  // G column of this lane's A element
-    if (32 * wave >= g.gcols) return;  // no G column in this wave (the reduce never reads its rows)
-    const bool cl = c < g.gcols;
-    const int cc = cl ? c : g.gcols - 1;
-    // k-tile -> segment, column within it
-    const int kt = blockIdx.x * RG_TILE;
+    const int gcols = g.gcols;
+    const int cb = 64 * blockIdx.z;       // first G column of this block
+    const int kb = 64 * blockIdx.x;       // first partial column of this block
+    const int64_t c0r = (int64_t)chunk * g.chunk_rows;
+    const int64_t c1r = min(c0r + (int64_t)g.chunk_rows, g.m);
+    const int64_t qrows = (g.chunk_rows / 4 + 1) & ~(int64_t)1;  // even rows per wave
+    const int64_t r0 = min(c0r + wave * qrows, c1r), r1 = min(r0 + qrows, c1r);
+    // G columns c0, c0 + 1 of this lane (tiles ct = 0, 1); clamped loads, masked values
+    const int c0 = cb + 2 * j;
+    const bool cl0 = c0 < gcols, cl1 = c0 + 1 < gcols;
+    const int cc = gcols >= 2 ? min(c0, gcols - 2) : 0;
+    // X segment of this block, columns k0, k0 + 1 of this lane (tiles kt = 0, 1)
     int seg = 0;
-    while (seg < g.nseg - 1 && kt >= t.base[seg + 1]) ++seg;
-    const int kl = kt - t.base[seg] + j;        // column of this lane's B element in the segment
-    const bool kv = kl < g.kx[seg];
-    const float *xp = g.x[seg] + (kv ? kl : g.kx[seg] - 1);
+    while (seg < g.nseg - 1 && kb >= t.base[seg + 1]) ++seg;
+    const int kx = g.kx[seg];
+    const int k0 = kb - t.base[seg] + 2 * j;
+    const bool kl0 = k0 < kx, kl1 = k0 + 1 < kx;
+    const int kc = kx >= 2 ? min(k0, kx - 2) : 0;
+    const float *xp = g.x[seg] + kc;
     const int64_t ldx = g.ldx[seg];
+    const float *gp = g.g + cc;
+    const float *gm = GMASK ? g.gmask + cc : nullptr;
     const bool first = blockIdx.x == 0;
     const int ns = first ? g.ns : 0;
-    // four accumulation chains over the row steps (step s to chain s % 4),
-    // added pairwise at the end
-    f32x16 ch[4] = {{0}, {0}, {0}, {0}};
-    float sx[4] = {0.0f, 0.0f, 0.0f, 0.0f}, sb = 0.0f;
+    // [c tile][k tile]: four independent accumulators cover the MFMA latency
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = (f32x16){0};
+    float sx[2][4] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}}, sb[2] = {0.0f, 0.0f};
     // wave-uniform trip count (an MFMA reads every lane): a row past r1 (odd
     // row count, k-lane 1 of the last step) contributes zeros
     const int64_t steps = (r1 - r0 + 1) / 2;
-    for (int64_t s0 = 0; s0 < steps; s0 += 4) {
+    const bool g1 = gcols >= 2, kx1 = kx >= 2;  // single-column operands read one value
+    // batches of 4 row steps, double-buffered: the next batch's loads are
+    // issued before this batch's 16 MFMAs
+    auto load = [&](int64_t s0, float2 *av, float2 *bv) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const int64_t s = s0 + q;
-            const int64_t i0 = r0 + 2 * s + par;
-            const bool live = i0 < r1 && cl;
-            const int64_t i = i0 < r1 ? i0 : r1 - 1;
-            float a = g.g[i * g.ldg + cc];
-            if (GMASK) a = g.gmask[i * g.ldg + cc] > 0.0f ? a : 0.0f;
-            a = live ? a : 0.0f;
-            ch[q] = mfma32(a, xp[i * ldx], ch[q]);
-            if (first) {
-                sb += a;
+            const int64_t i0 = r0 + 2 * (s0 + q) + par;
+            const bool live = i0 < r1 && s0 + q < steps;
+            const int64_t i = i0 < r1 ? i0 : (r1 > r0 ? r1 - 1 : min(r0, g.m - 1));
+            float2 a = g1 ? ld2(gp + i * g.ldg, VEC) : make_float2(gp[i * g.ldg], 0.0f);
+            if (GMASK) {
+                const float2 q2 = g1 ? ld2(gm + i * g.ldg, VEC) : make_float2(gm[i * g.ldg], 0.0f);
+                a.x = q2.x > 0.0f ? a.x : 0.0f;
+                a.y = q2.y > 0.0f ? a.y : 0.0f;
+            }
+            // a clamped pair past the edge read the last pair: shift its live
+            // first column into place
+            if (cc != c0) a = make_float2(a.y, 0.0f);
+            a.x = live && cl0 ? a.x : 0.0f;
+            a.y = live && cl1 ? a.y : 0.0f;
+            float2 b = kx1 ? ld2(xp + i * ldx, VEC) : make_float2(xp[i * ldx], 0.0f);
+            if (kc != k0) b = make_float2(b.y, 0.0f);
+            b.x = kl0 ? b.x : 0.0f;
+            b.y = kl1 ? b.y : 0.0f;
+            av[q] = a;
+            bv[q] = b;
+        }
+    };
+    auto compute = [&](int64_t s0, const float2 *av, const float2 *bv) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            acc[0][0] = mfma32(av[q].x, bv[q].x, acc[0][0]);
+            acc[0][1] = mfma32(av[q].x, bv[q].y, acc[0][1]);
+            acc[1][0] = mfma32(av[q].y, bv[q].x, acc[1][0]);
+            acc[1][1] = mfma32(av[q].y, bv[q].y, acc[1][1]);
+        }
+        if (first) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int64_t i0 = r0 + 2 * (s0 + q) + par;
+                const int64_t i = i0 < r1 ? i0 : (r1 > r0 ? r1 - 1 : min(r0, g.m - 1));
+                sb[0] += av[q].x;
+                sb[1] += av[q].y;
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
-                    if (e < ns) sx[e] = fmaf(a, g.xs[i * g.ldxs + e], sx[e]);
+                    if (e < ns) {
+                        const float xe = g.xs[i * g.ldxs + e];
+                        sx[0][e] = fmaf(av[q].x, xe, sx[0][e]);
+                        sx[1][e] = fmaf(av[q].y, xe, sx[1][e]);
+                    }
+            }
+        }
+    };
+    if (steps > 0) {
+        float2 a0[4], x0[4], a1[4], x1[4];
+        load(0, a0, x0);
+        for (int64_t s0 = 0; s0 < steps; s0 += 8) {
+            if (s0 + 4 < steps) load(s0 + 4, a1, x1);
+            compute(s0, a0, x0);
+            if (s0 + 4 >= steps) break;
+            if (s0 + 8 < steps) load(s0 + 8, a0, x0);
+            compute(s0 + 4, a1, x1);
+        }
+    }
+    // this wave's block, db and small-segment sums (the two row parities of a
+    // column added in a fixed order); waves 1..3 hand theirs to wave 0, which
+    // adds them in wave order
+    if (first) {
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) {
+            sb[ct] += __shfl_xor(sb[ct], 32, 64);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) sx[ct][e] += __shfl_xor(sx[ct][e], 32, 64);
+        }
+    }
+    if (wave > 0) {
+        float(*rw)[64] = red[wave - 1];
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) rw[(2 * ct + kt) * 16 + r][lane] = acc[ct][kt][r];
+        if (first) {
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct) {
+                rw[64 + ct][lane] = sb[ct];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) rw[66 + 4 * ct + e][lane] = sx[ct][e];
             }
         }
     }
-    const f32x16 acc = (ch[0] + ch[1]) + (ch[2] + ch[3]);
+    __syncthreads();
+    if (wave != 0) return;
+#pragma unroll 1
+    for (int w = 0; w < 3; ++w) {
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[ct][kt][r] += red[w][(2 * ct + kt) * 16 + r][lane];
+        if (first) {
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct) {
+                sb[ct] += red[w][64 + ct][lane];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) sx[ct][e] += red[w][66 + 4 * ct + e][lane];
+            }
+        }
+    }
+    if (cb >= gcols) return;
     float *pp = t.part + (int64_t)chunk * 128 * t.cols;
-    const int kcol = kt + j;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) pp[(int64_t)(32 * wave + acc_row(r, lane)) * t.cols + kcol] = acc[r];
-    if (first) {
-        // the two row parities of column c, in a fixed order
-        sb += __shfl_xor(sb, 32, 64);
+    for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) sx[e] += __shfl_xor(sx[e], 32, 64);
-        if (par == 0) {
-            float *q = pp + (int64_t)c * t.cols + t.kbig;
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int c = cb + 2 * acc_row(r, lane) + ct;
+                pp[(int64_t)c * t.cols + kb + 2 * j + kt] = acc[ct][kt][r];
+            }
+    if (first && par == 0) {
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) {
+            float *q = pp + (int64_t)(c0 + ct) * t.cols + t.kbig;
 #pragma unroll
             for (int e = 0; e < 4; ++e)
-                if (e < ns) q[e] = sx[e];
-            q[g.ns] = sb;
+                if (e < ns) q[e] = sx[ct][e];
+            q[g.ns] = sb[ct];
         }
     }
 }
@@ -232,8 +524,19 @@ __global__ __launch_bounds__(256) void rgemm_tn_reduce_kernel(TnArgs t, int chun
         kk = k - t.base[seg];
         if (kk >= g.kx[seg]) return;  // padding column
     }
+    // chunks added in order; the loads of 8 chunks are issued before their adds
     float s = 0.0f;
-    for (int q = 0; q < chunks; ++q) s += t.part[((int64_t)q * 128 + c) * t.cols + k];
+    const float *pp = t.part + (int64_t)c * t.cols + k;
+    const int64_t cs = (int64_t)128 * t.cols;
+    int q = 0;
+    for (; q + 8 <= chunks; q += 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = pp[(q + u) * cs];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; q < chunks; ++q) s += pp[q * cs];
     if (seg >= 0) {
         g.dw[(int64_t)c * g.lddw + g.dwcol[seg] + kk] = s;
     } else if (k < t.kbig + g.ns) {
@@ -246,6 +549,7 @@ __global__ __launch_bounds__(256) void rgemm_tn_reduce_kernel(TnArgs t, int chun
 }
 
 bool al16(const void *p) { return ((uintptr_t)p & 15) == 0; }
+bool al8(const void *p) { return ((uintptr_t)p & 7) == 0; }
 
 }  // namespace
 
@@ -275,35 +579,55 @@ extern "C" int mmpde_rgemm(const mmpde_rgemm_args *gp, mmpde_stream_t stream) {
         for (int p = 0; p < g.parts; ++p)
             if (g.layout == MMPDE_RGEMM_NT) vec = vec && g.wk[p] % 4 == 0;
     }
-    const dim3 grid((unsigned)ceil_div(g.m, RG_TILE), (unsigned)g.parts);
     const bool am = g.kh > 0 && g.amask[0] != nullptr;
     hipStream_t st = as_stream(stream);
-#define RG_LAUNCH(L, V, A, X) hipLaunchKernelGGL((rgemm_kernel<L, V, A, X>), grid, dim3(256), 0, st, g)
-    if (g.layout == MMPDE_RGEMM_NT) {
-        if (vec) {
-            if (am && xs) RG_LAUNCH(MMPDE_RGEMM_NT, true, true, true);
-            else if (am) RG_LAUNCH(MMPDE_RGEMM_NT, true, true, false);
-            else if (xs) RG_LAUNCH(MMPDE_RGEMM_NT, true, false, true);
-            else RG_LAUNCH(MMPDE_RGEMM_NT, true, false, false);
+    if (vec && (g.kh == 32 || g.kh == 64 || g.kh == 128)) {
+        // weight-stationary persistent form: two workgroups per CU at most
+        // workgroups that fit a CU at once: the kh = 128 form holds ~240 registers per lane
+        const int64_t ntiles = (g.m + 31) / 32;
+        const int per_cu = g.kh == 128 ? 1 : 2;
+        const dim3 wgrid((unsigned)std::min<int64_t>(ntiles, (int64_t)per_cu * rgemm_cus()), (unsigned)g.parts);
+#define WS_LAUNCH(L, K, A, X) hipLaunchKernelGGL((rgemm_ws_kernel<L, K, A, X>), wgrid, dim3(256), 0, st, g)
+#define WS_K(L, A, X)                          \
+    if (g.kh == 32) WS_LAUNCH(L, 32, A, X);    \
+    else if (g.kh == 64) WS_LAUNCH(L, 64, A, X); \
+    else WS_LAUNCH(L, 128, A, X);
+#define WS_AX(L)                               \
+    if (am && xs) { WS_K(L, true, true) }      \
+    else if (am) { WS_K(L, true, false) }      \
+    else if (xs) { WS_K(L, false, true) }      \
+    else { WS_K(L, false, false) }
+        if (g.layout == MMPDE_RGEMM_NT) {
+            WS_AX(MMPDE_RGEMM_NT)
         } else {
-            if (am && xs) RG_LAUNCH(MMPDE_RGEMM_NT, false, true, true);
-            else if (am) RG_LAUNCH(MMPDE_RGEMM_NT, false, true, false);
-            else if (xs) RG_LAUNCH(MMPDE_RGEMM_NT, false, false, true);
-            else RG_LAUNCH(MMPDE_RGEMM_NT, false, false, false);
+            WS_AX(MMPDE_RGEMM_NN)
         }
-    } else {
-        if (vec) {
-            if (am && xs) RG_LAUNCH(MMPDE_RGEMM_NN, true, true, true);
-            else if (am) RG_LAUNCH(MMPDE_RGEMM_NN, true, true, false);
-            else if (xs) RG_LAUNCH(MMPDE_RGEMM_NN, true, false, true);
-            else RG_LAUNCH(MMPDE_RGEMM_NN, true, false, false);
-        } else {
-            if (am && xs) RG_LAUNCH(MMPDE_RGEMM_NN, false, true, true);
-            else if (am) RG_LAUNCH(MMPDE_RGEMM_NN, false, true, false);
-            else if (xs) RG_LAUNCH(MMPDE_RGEMM_NN, false, false, true);
-            else RG_LAUNCH(MMPDE_RGEMM_NN, false, false, false);
-        }
+#undef WS_AX
+#undef WS_K
+#undef WS_LAUNCH
+        MMPDE_RET_LAUNCH();
+        return MMPDE_OK;
     }
+    const dim3 grid((unsigned)ceil_div(g.m, 128), (unsigned)g.parts);
+#define RG_LAUNCH(L, V, A, X) hipLaunchKernelGGL((rgemm_kernel<L, V, A, X>), grid, dim3(256), 0, st, g)
+#define RG_LAYOUT(L)                                           \
+    if (vec) {                                                 \
+        if (am && xs) RG_LAUNCH(L, true, true, true);          \
+        else if (am) RG_LAUNCH(L, true, true, false);          \
+        else if (xs) RG_LAUNCH(L, true, false, true);          \
+        else RG_LAUNCH(L, true, false, false);                 \
+    } else {                                                   \
+        if (am && xs) RG_LAUNCH(L, false, true, true);         \
+        else if (am) RG_LAUNCH(L, false, true, false);         \
+        else if (xs) RG_LAUNCH(L, false, false, true);         \
+        else RG_LAUNCH(L, false, false, false);                \
+    }
+    if (g.layout == MMPDE_RGEMM_NT) {
+        RG_LAYOUT(MMPDE_RGEMM_NT)
+    } else {
+        RG_LAYOUT(MMPDE_RGEMM_NN)
+    }
+#undef RG_LAYOUT
 #undef RG_LAUNCH
     MMPDE_RET_LAUNCH();
     return MMPDE_OK;
@@ -324,10 +648,12 @@ extern "C" int mmpde_rgemm_tn(const mmpde_rgemm_tn_args *gp, void *workspace, in
     TnArgs t{};
     t.g = g;
     int kbig = 0;
+    bool vec = g.ldg % 2 == 0 && al8(g.g) && (!g.gmask || al8(g.gmask));
     for (int s = 0; s < g.nseg; ++s) {
         MMPDE_REQUIRE(g.x[s] && g.kx[s] > 0 && g.ldx[s] >= g.kx[s]);
         t.base[s] = kbig;
-        kbig += (g.kx[s] + RG_TILE - 1) / RG_TILE * RG_TILE;
+        kbig += (g.kx[s] + 63) / 64 * 64;
+        vec = vec && (g.kx[s] < 2 || (g.ldx[s] % 2 == 0 && al8(g.x[s])));
     }
     t.kbig = kbig;
     t.cols = kbig + g.ns + 1;
@@ -336,9 +662,14 @@ extern "C" int mmpde_rgemm_tn(const mmpde_rgemm_tn_args *gp, void *workspace, in
     MMPDE_REQUIRE(workspace_bytes >= mmpde_rgemm_tn_workspace_bytes(g.m, g.chunk_rows, t.cols));
     MMPDE_REQUIRE(chunks < 65536);
     hipStream_t st = as_stream(stream);
-    const dim3 grid((unsigned)(kbig / RG_TILE), (unsigned)chunks);
-    if (g.gmask) hipLaunchKernelGGL((rgemm_tn_partial_kernel<true>), grid, dim3(256), 0, st, t);
-    else hipLaunchKernelGGL((rgemm_tn_partial_kernel<false>), grid, dim3(256), 0, st, t);
+    const dim3 grid((unsigned)(kbig / 64), (unsigned)chunks, (unsigned)((g.gcols + 63) / 64));
+    if (g.gmask) {
+        if (vec) hipLaunchKernelGGL((rgemm_tn_partial_kernel<true, true>), grid, dim3(256), 0, st, t);
+        else hipLaunchKernelGGL((rgemm_tn_partial_kernel<true, false>), grid, dim3(256), 0, st, t);
+    } else {
+        if (vec) hipLaunchKernelGGL((rgemm_tn_partial_kernel<false, true>), grid, dim3(256), 0, st, t);
+        else hipLaunchKernelGGL((rgemm_tn_partial_kernel<false, false>), grid, dim3(256), 0, st, t);
+    }
     MMPDE_RET_LAUNCH();
     const int64_t outs = (int64_t)g.gcols * t.cols;
     hipLaunchKernelGGL(rgemm_tn_reduce_kernel, dim3((unsigned)ceil_div(outs, 256)), dim3(256), 0, st, t,

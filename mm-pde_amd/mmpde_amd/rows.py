@@ -68,7 +68,7 @@ def rgemm_tn(m: int, g_ptr: int, ldg: int, gcols: int, segs, dw: torch.Tensor, l
     cols = 0
     for i, (x, ldx, kx, dwcol) in enumerate(segs):
         a.x[i], a.ldx[i], a.kx[i], a.dwcol[i] = x, ldx, kx, dwcol
-        cols += (kx + 31) // 32 * 32
+        cols += (kx + 63) // 64 * 64
     cols += ns + 1
     a.xs, a.ldxs, a.ns, a.dwcol_s, a.sign_s, a.accumulate_s = xs, ldxs, ns, dwcol_s, sign_s, int(accumulate_s)
     a.dw, a.lddw, a.db = dw.data_ptr(), lddw, _p(db)

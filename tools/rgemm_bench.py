@@ -1,7 +1,7 @@
 """Row-GEMM timing (csrc/rgemm.hip via ops.LinearRows) against torch's library
 GEMM at the train-mode GNN shapes (cy B=16: n = 40336 rows): forward
 y = x W^T + b, input gradient dX = dY W, weight gradient dW = dY^T X (+ db).
-HIP events on the current stream, median of 20 calls each.
+HIP events on the current stream around 20 back-to-back calls.
 
     python tools/rgemm_bench.py
 """
@@ -16,17 +16,18 @@ import torch  # noqa: E402
 
 
 def timed(fn, reps=20):
+    """Microseconds per call of `reps` back-to-back calls (the host's issue time
+    overlaps the device work when the kernels are the longer part)."""
     for _ in range(3):
         fn()
-    ts = []
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    a.record()
     for _ in range(reps):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record()
         fn()
-        b.record()
-        b.synchronize()
-        ts.append(a.elapsed_time(b) * 1e3)
-    return sorted(ts)[len(ts) // 2]
+    b.record()
+    b.synchronize()
+    return a.elapsed_time(b) * 1e3 / reps
 
 
 def main():
