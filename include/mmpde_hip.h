@@ -513,6 +513,18 @@ int64_t mmpde_rgemm_tn_workspace_bytes(int64_t m, int chunk_rows, int cols);
 int mmpde_rgemm_tn(const mmpde_rgemm_tn_args *g, void *workspace, int64_t workspace_bytes,
                    mmpde_stream_t stream);
 
+/* Skinny row maps (one side of the map narrow: the Conv1d head's windows,
+ * gnn_2d.py:108-114; the embedding's first Linear, gnn_2d.py:99-106; ItpNet's
+ * 62-wide input layer, interpolate.py:79-93), forward and input gradient, on
+ * the VALU (exact fp32 products summed in a fixed order; the map staged in
+ * LDS).  layout MMPDE_RGEMM_NT: y[i][o] = bias[o] + sum_{k<ki} x[i][k] w[o *
+ * ldw + k] for o < no (bias nullable; y = x W^T + b, W [no, ki]).  layout
+ * MMPDE_RGEMM_NN: y[i][c] = sum_{o<no} x[i][o] w[o * ldw + c] for c < ki (bias
+ * null; dX = dY W, W [no, ki]).  ki, no <= 128; rows i < n with strides ldx /
+ * ldy. */
+int mmpde_rows_small(const float *x, int64_t ldx, int64_t n, int ki, const float *w, int64_t ldw, int layout,
+                     const float *bias, int no, float *y, int64_t ldy, mmpde_stream_t stream);
+
 /* out[n] = out_scale * output_mlp(h[:, None]) */
 int mmpde_gnn_head(const float *h, int64_t n, const mmpde_gnn_head_params *p, float *out,
                    mmpde_stream_t stream);

@@ -208,17 +208,32 @@ __global__ __launch_bounds__(256, 1) void rgemm_ws_kernel(mmpde_rgemm_args g) {
             for (int s = 0; s < KH; ++s) wreg[s] = wp[(int64_t)s * ldw];
         }
     }
-    // staging: piece f = tid + 256 u -> row f / (KH / 2), half, float4 q
+    // staging: piece f = tid + 256 u -> row f / (KH / 2), half, float4 q; the
+    // small segment's row (XS: ns <= 4 values) goes to the row's 4 pad floats.
+    // Every load is unconditional (the last tile re-read past the end): a load
+    // under a condition is waited for where the condition ends.
+    const float *a0 = g.a[0], *a1 = g.a[1];
+    const float *m0 = AMASK ? g.amask[0] : nullptr, *m1 = AMASK ? g.amask[1] : nullptr;
+    const int64_t lda0 = g.lda[0], lda1 = g.lda[1];
+    const int ns = XS ? g.ns[p] : 0;
+    const float *xs = g.xs;
+    const int64_t ldxs = g.ldxs;
     float4 stg[PER];
+    float4 sxs;
     auto fetch = [&](int64_t tile) {
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
             const int f = tid + 256 * u;
             const int r = f / (KH / 2), rem = f % (KH / 2), hh = rem / (KH / 4), q = rem % (KH / 4);
             const int64_t row = min(tile * 32 + r, m - 1);
-            float4 v = *(const float4 *)(g.a[hh] + row * g.lda[hh] + 4 * q);
-            if (AMASK) v = mask4(v, *(const float4 *)(g.amask[hh] + row * g.lda[hh] + 4 * q));
+            const int64_t off = row * (hh ? lda1 : lda0) + 4 * q;
+            float4 v = *(const float4 *)((hh ? a1 : a0) + off);
+            if (AMASK) v = mask4(v, *(const float4 *)((hh ? m1 : m0) + off));
             stg[u] = v;
+        }
+        if (XS && tid < 32) {
+            const float *xr = xs + min(tile * 32 + tid, m - 1) * ldxs;
+            sxs = make_float4(xr[0], xr[min(1, ns - 1)], xr[min(2, ns - 1)], xr[min(3, ns - 1)]);
         }
     };
     auto stash = [&](float *buf) {
@@ -228,10 +243,10 @@ __global__ __launch_bounds__(256, 1) void rgemm_ws_kernel(mmpde_rgemm_args g) {
             const int r = f / (KH / 2), rem = f % (KH / 2), hh = rem / (KH / 4), q = rem % (KH / 4);
             *(float4 *)(buf + r * PITCH + hh * KH + 4 * q) = stg[u];
         }
+        if (XS && tid < 32) *(float4 *)(buf + tid * PITCH + 2 * KH) = sxs;
     };
     // epilogue constants of this lane's column
     const float bias = active && g.bias[p] ? g.bias[p][colc] : 0.0f;
-    const int ns = XS ? g.ns[p] : 0;
     float xw[4] = {0.0f, 0.0f, 0.0f, 0.0f};
     if (XS && active) {
 #pragma unroll
@@ -242,6 +257,8 @@ __global__ __launch_bounds__(256, 1) void rgemm_ws_kernel(mmpde_rgemm_args g) {
     }
     const float *om = g.omask[p];
     const bool accum = g.accumulate[p] != 0;
+    const bool relu = g.relu != 0;
+    const int64_t ldom = g.ldom[p], ldo = g.ldo[p];
     float *out = g.out[p];
     int64_t tile = blockIdx.x;
     if (tile >= ntiles) return;  // workgroup-uniform, before any barrier
@@ -252,18 +269,16 @@ __global__ __launch_bounds__(256, 1) void rgemm_ws_kernel(mmpde_rgemm_args g) {
     for (;;) {
         const int64_t next = tile + gridDim.x;
         const bool more = next < ntiles;  // workgroup-uniform
-        if (more) fetch(next);
+        fetch(min(next, ntiles - 1));
         if (active) {
-            // the epilogue's row inputs (small segment, output mask, the old
-            // output values) are loaded before the MFMAs, so their latency hides
-            // under them
-            float ex[16], em[16], eo[16];
+            // the epilogue's row inputs (output mask, the old output values) are
+            // loaded before the MFMAs, so their latency hides under them
+            float em[16], eo[16];
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int64_t i = min(tile * 32 + acc_row(r, lane), m - 1);
-                ex[r] = XS && ns > 0 ? g.xs[i * g.ldxs] : 0.0f;
-                em[r] = om ? om[i * g.ldom[p] + colc] : 1.0f;
-                eo[r] = accum ? out[i * g.ldo[p] + colc] : 0.0f;
+                em[r] = om ? om[i * ldom + colc] : 1.0f;
+                eo[r] = accum ? out[i * ldo + colc] : 0.0f;
             }
             const float *xr = xt[cur] + j * PITCH + h * KH;  // A: row j, half h
             f32x16 c0 = {0}, c1 = {0};
@@ -276,21 +291,28 @@ __global__ __launch_bounds__(256, 1) void rgemm_ws_kernel(mmpde_rgemm_args g) {
                 c1 = mfma32(a.w, wreg[s + 3], c1);
             }
             const f32x16 d = c0 + c1;
+            // pin the uses of em / eo after the MFMAs (the compiler would
+            // otherwise test them right after their loads, waiting there)
+            const float dep = d[0];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) asm volatile("" : "+v"(em[r]), "+v"(eo[r]) : "v"(dep));
             if (col < ncols) {
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    const int64_t i = tile * 32 + acc_row(r, lane);
+                    const int rr = acc_row(r, lane);
+                    const int64_t i = tile * 32 + rr;
                     if (i >= m) continue;
                     float y = d[r] + bias;
                     if (XS) {
-                        if (ns > 0) y = fmaf(ex[r], xw[0], y);
-#pragma unroll
-                        for (int e = 1; e < 4; ++e)
-                            if (e < ns) y = fmaf(g.xs[i * g.ldxs + e], xw[e], y);
+                        const float4 x4 = *(const float4 *)(xt[cur] + rr * PITCH + 2 * KH);
+                        y = fmaf(x4.x, xw[0], y);   // xw[e] = 0 for e >= ns
+                        y = fmaf(x4.y, xw[1], y);
+                        y = fmaf(x4.z, xw[2], y);
+                        y = fmaf(x4.w, xw[3], y);
                     }
-                    if (g.relu) y = fmaxf(y, 0.0f);
+                    if (relu) y = fmaxf(y, 0.0f);
                     if (om) y = em[r] > 0.0f ? y : 0.0f;
-                    out[i * g.ldo[p] + col] = accum ? eo[r] + y : y;
+                    out[i * ldo + col] = accum ? eo[r] + y : y;
                 }
             }
         }
@@ -335,7 +357,7 @@ __device__ __forceinline__ float2 ld2(const float *p, bool vec) {
     return vec ? *(const float2 *)p : make_float2(p[0], p[1]);
 }
 
-template <bool GMASK, bool VEC>
+template <bool GMASK, bool VEC, bool XS>
 __global__ __launch_bounds__(256, 2) void rgemm_tn_partial_kernel(TnArgs t) {
     constexpr int NRED = 64 + 2 + 8;  // per lane: the block (4 tiles x 16), db (2), small segment (2 x 4)
     __shared__ float red[3][NRED][64];
@@ -379,33 +401,56 @@ __global__ __launch_bounds__(256, 2) void rgemm_tn_partial_kernel(TnArgs t) {
     const int64_t steps = (r1 - r0 + 1) / 2;
     const bool g1 = gcols >= 2, kx1 = kx >= 2;  // single-column operands read one value
     // batches of 4 row steps, double-buffered: the next batch's loads are
-    // issued before this batch's 16 MFMAs
-    auto load = [&](int64_t s0, float2 *av, float2 *bv) {
+    // issued before this batch's 16 MFMAs.  The loads are unconditional and
+    // keep raw values; compute() masks them (a select on a freshly loaded value
+    // lets the compiler sink the load under a branch, where it is waited for
+    // at once).  Single-column operands read their one column twice.
+    struct Buf {
+        float2 a[4], b[4], q[4];
+        float x[4][4];
+    };
+    const bool xsum = XS && first;  // XS: the launch has ns > 0
+    auto load = [&](int64_t s0, Buf &o) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int64_t i0 = r0 + 2 * (s0 + q) + par;
+            const int64_t i = i0 < r1 ? i0 : (r1 > r0 ? r1 - 1 : min(r0, g.m - 1));
+            const float *pa = gp + i * g.ldg;
+            o.a[q] = VEC ? *(const float2 *)pa : make_float2(pa[0], pa[g1 ? 1 : 0]);
+            const float *pb = xp + i * ldx;
+            o.b[q] = VEC ? *(const float2 *)pb : make_float2(pb[0], pb[kx1 ? 1 : 0]);
+            if (GMASK) {
+                const float *pm = gm + i * g.ldg;
+                o.q[q] = VEC ? *(const float2 *)pm : make_float2(pm[0], pm[g1 ? 1 : 0]);
+            }
+            if (xsum) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o.x[q][e] = g.xs[i * g.ldxs + min(e, ns - 1)];
+            }
+        }
+    };
+    auto compute = [&](int64_t s0, const Buf &o) {
+        float2 av[4], bv[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int64_t i0 = r0 + 2 * (s0 + q) + par;
             const bool live = i0 < r1 && s0 + q < steps;
-            const int64_t i = i0 < r1 ? i0 : (r1 > r0 ? r1 - 1 : min(r0, g.m - 1));
-            float2 a = g1 ? ld2(gp + i * g.ldg, VEC) : make_float2(gp[i * g.ldg], 0.0f);
+            float2 a = o.a[q], b = o.b[q];
+            // a clamped pair past the edge read the last pair: its live first
+            // column is the pair's second; dead rows and columns are zeroed
+            if (cc != c0) a.x = a.y;
+            if (kc != k0) b.x = b.y;
+            int ma0 = live && cl0 ? -1 : 0, ma1 = live && cl1 && cc == c0 ? -1 : 0;
             if (GMASK) {
-                const float2 q2 = g1 ? ld2(gm + i * g.ldg, VEC) : make_float2(gm[i * g.ldg], 0.0f);
-                a.x = q2.x > 0.0f ? a.x : 0.0f;
-                a.y = q2.y > 0.0f ? a.y : 0.0f;
+                const float2 q2 = o.q[q];
+                ma0 &= (cc != c0 ? q2.y : q2.x) > 0.0f ? -1 : 0;
+                ma1 &= q2.y > 0.0f ? -1 : 0;
             }
-            // a clamped pair past the edge read the last pair: shift its live
-            // first column into place
-            if (cc != c0) a = make_float2(a.y, 0.0f);
-            a.x = live && cl0 ? a.x : 0.0f;
-            a.y = live && cl1 ? a.y : 0.0f;
-            float2 b = kx1 ? ld2(xp + i * ldx, VEC) : make_float2(xp[i * ldx], 0.0f);
-            if (kc != k0) b = make_float2(b.y, 0.0f);
-            b.x = kl0 ? b.x : 0.0f;
-            b.y = kl1 ? b.y : 0.0f;
-            av[q] = a;
-            bv[q] = b;
+            int mb0 = kl0 ? -1 : 0, mb1 = kl1 && kc == k0 ? -1 : 0;
+            asm volatile("" : "+v"(ma0), "+v"(ma1), "+v"(mb0), "+v"(mb1));
+            av[q] = make_float2(__int_as_float(__float_as_int(a.x) & ma0), __int_as_float(__float_as_int(a.y) & ma1));
+            bv[q] = make_float2(__int_as_float(__float_as_int(b.x) & mb0), __int_as_float(__float_as_int(b.y) & mb1));
         }
-    };
-    auto compute = [&](int64_t s0, const float2 *av, const float2 *bv) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             acc[0][0] = mfma32(av[q].x, bv[q].x, acc[0][0]);
@@ -416,29 +461,30 @@ __global__ __launch_bounds__(256, 2) void rgemm_tn_partial_kernel(TnArgs t) {
         if (first) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const int64_t i0 = r0 + 2 * (s0 + q) + par;
-                const int64_t i = i0 < r1 ? i0 : (r1 > r0 ? r1 - 1 : min(r0, g.m - 1));
                 sb[0] += av[q].x;
                 sb[1] += av[q].y;
+                if (xsum) {
 #pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    if (e < ns) {
-                        const float xe = g.xs[i * g.ldxs + e];
-                        sx[0][e] = fmaf(av[q].x, xe, sx[0][e]);
-                        sx[1][e] = fmaf(av[q].y, xe, sx[1][e]);
+                    for (int e = 0; e < 4; ++e) {
+                        sx[0][e] = fmaf(av[q].x, o.x[q][e], sx[0][e]);
+                        sx[1][e] = fmaf(av[q].y, o.x[q][e], sx[1][e]);
                     }
+                }
             }
         }
     };
     if (steps > 0) {
-        float2 a0[4], x0[4], a1[4], x1[4];
-        load(0, a0, x0);
-        for (int64_t s0 = 0; s0 < steps; s0 += 8) {
-            if (s0 + 4 < steps) load(s0 + 4, a1, x1);
-            compute(s0, a0, x0);
+        Buf b0, b1;
+        load(0, b0);
+        // the next batch is loaded unconditionally (rows clamped, masked as
+        // dead): a load under a condition makes the compiler wait for it
+        for (int64_t s0 = 0;; s0 += 8) {
+            load(s0 + 4, b1);
+            compute(s0, b0);
             if (s0 + 4 >= steps) break;
-            if (s0 + 8 < steps) load(s0 + 8, a0, x0);
-            compute(s0 + 4, a1, x1);
+            load(s0 + 8, b0);
+            compute(s0 + 4, b1);
+            if (s0 + 8 >= steps) break;
         }
     }
     // this wave's block, db and small-segment sums (the two row parities of a
@@ -648,12 +694,12 @@ extern "C" int mmpde_rgemm_tn(const mmpde_rgemm_tn_args *gp, void *workspace, in
     TnArgs t{};
     t.g = g;
     int kbig = 0;
-    bool vec = g.ldg % 2 == 0 && al8(g.g) && (!g.gmask || al8(g.gmask));
+    bool vec = g.gcols >= 2 && g.ldg % 2 == 0 && al8(g.g) && (!g.gmask || al8(g.gmask));
     for (int s = 0; s < g.nseg; ++s) {
         MMPDE_REQUIRE(g.x[s] && g.kx[s] > 0 && g.ldx[s] >= g.kx[s]);
         t.base[s] = kbig;
         kbig += (g.kx[s] + 63) / 64 * 64;
-        vec = vec && (g.kx[s] < 2 || (g.ldx[s] % 2 == 0 && al8(g.x[s])));
+        vec = vec && g.kx[s] >= 2 && g.ldx[s] % 2 == 0 && al8(g.x[s]);
     }
     t.kbig = kbig;
     t.cols = kbig + g.ns + 1;
@@ -663,13 +709,19 @@ extern "C" int mmpde_rgemm_tn(const mmpde_rgemm_tn_args *gp, void *workspace, in
     MMPDE_REQUIRE(chunks < 65536);
     hipStream_t st = as_stream(stream);
     const dim3 grid((unsigned)(kbig / 64), (unsigned)chunks, (unsigned)((g.gcols + 63) / 64));
+#define TN_LAUNCH(M, V, X) hipLaunchKernelGGL((rgemm_tn_partial_kernel<M, V, X>), grid, dim3(256), 0, st, t)
+#define TN_X(M, V)              \
+    if (g.ns > 0) TN_LAUNCH(M, V, true); \
+    else TN_LAUNCH(M, V, false);
     if (g.gmask) {
-        if (vec) hipLaunchKernelGGL((rgemm_tn_partial_kernel<true, true>), grid, dim3(256), 0, st, t);
-        else hipLaunchKernelGGL((rgemm_tn_partial_kernel<true, false>), grid, dim3(256), 0, st, t);
+        if (vec) { TN_X(true, true) }
+        else { TN_X(true, false) }
     } else {
-        if (vec) hipLaunchKernelGGL((rgemm_tn_partial_kernel<false, true>), grid, dim3(256), 0, st, t);
-        else hipLaunchKernelGGL((rgemm_tn_partial_kernel<false, false>), grid, dim3(256), 0, st, t);
+        if (vec) { TN_X(false, true) }
+        else { TN_X(false, false) }
     }
+#undef TN_X
+#undef TN_LAUNCH
     MMPDE_RET_LAUNCH();
     const int64_t outs = (int64_t)g.gcols * t.cols;
     hipLaunchKernelGGL(rgemm_tn_reduce_kernel, dim3((unsigned)ceil_div(outs, 256)), dim3(256), 0, st, t,

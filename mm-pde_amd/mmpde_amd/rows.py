@@ -91,10 +91,36 @@ def _halves(x: torch.Tensor, w: torch.Tensor, k: int):
     return kh, (_p(x), _p(x, kh)), (_p(w), _p(w, kh)), rest
 
 
+def _mfma_width(k: int) -> bool:
+    """K the MFMA row GEMM takes at full rate: two 16-byte-aligned halves of
+    32, 64 or 128 columns (the weight-stationary form), or wider multiples of 8."""
+    return k % 8 == 0 and (k // 2 in (32, 64, 128) or k > 256)
+
+
+def _skinny(k: int, nout: int) -> bool:
+    """Maps mmpde_rows_small takes instead (a 32 x 32 MFMA tile would run mostly
+    empty, or K splits into no aligned halves): the Conv1d head's windows, the
+    embedding's first Linear, ItpNet's 62- and 30-wide layers."""
+    return k <= 128 and nout <= 128 and (min(k, nout) <= 16 or not _mfma_width(k))
+
+
+def rows_small(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None, layout: int) -> torch.Tensor:
+    """mmpde_rows_small: NT y = x W^T + b; NN y = x W (W [N, K] either way)."""
+    n = x.shape[0]
+    nout, k = w.shape
+    width = nout if layout == L.RGEMM_NT else k
+    y = torch.empty((n, width), dtype=torch.float32, device=x.device)
+    L.check(L.lib().mmpde_rows_small(_p(x), x.stride(0), n, k, _p(w), w.stride(0), layout, _p(b), nout,
+                                     _p(y), width, L.stream(x.device)), "mmpde_rows_small")
+    return y
+
+
 def linear_fwd(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None) -> torch.Tensor:
     """y = x W^T + b (x [n, K] fp32 contiguous, W [N, K] contiguous)."""
     n, k = x.shape
     nout = w.shape[0]
+    if _skinny(k, nout):
+        return rows_small(x, w, b, L.RGEMM_NT)
     y = torch.empty((n, nout), dtype=torch.float32, device=x.device)
     st = L.stream(x.device)
     kh, a, wh, rest = _halves(x, w, k)
@@ -112,6 +138,8 @@ def linear_bwd_input(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     outputs, the last N - 2 kh of them in the small segment."""
     n, nout = dy.shape
     k = w.shape[1]
+    if k <= 128 and nout <= 128 and (min(k, nout) <= 16 or not _mfma_width(nout)):   # GEMM K = nout
+        return rows_small(dy, w, None, L.RGEMM_NN)
     gx = torch.empty((n, k), dtype=torch.float32, device=dy.device)
     st = L.stream(dy.device)
     kh, _, _, rest = _halves(dy, w, nout)
