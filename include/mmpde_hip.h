@@ -357,7 +357,8 @@ int mmpde_gnn_edge_backward_ex(const float *a, const float *b, const int32_t *nb
                                mmpde_stream_t stream);
 /* grad_b[j] = sum over q in [rev_off[j], rev_off[j+1]) of grad_edge[rev_edge[q]]
  * (rev_*: the reverse adjacency, slot ids i*k+e grouped by source j, in the
- * order given: deterministic). */
+ * order given; summation order fixed: the even list positions and the odd
+ * ones each added in list order, then the two sums: deterministic). */
 int mmpde_gnn_edge_source_sum(const float *grad_edge, const int64_t *rev_off, const int64_t *rev_edge,
                               int64_t n, float *grad_b, mmpde_stream_t stream);
 /* The backward with grad_edge in source-major order: the row of slot q is

@@ -14,7 +14,7 @@
 //              written out and summed per source over the reverse adjacency by
 //              edge_source_sum_kernel, in a fixed order)
 //   dL/dW2   = sum_e gz2 m1^T,  dL/db2 = sum_e gz2   (per-workgroup partials,
-//              reduced in workgroup order by partial_sum_kernel)
+//              reduced in a fixed order by partial_sum_kernel)
 //
 // Nothing is stored by the forward: z1, z2 are recomputed here.  Exact fp32
 // products on v_mfma_f32_16x16x4_f32 (the three 16 x 128 x 128 GEMMs of a
@@ -630,65 +630,63 @@ __global__ __launch_bounds__(256) void transpose128_kernel(const float *__restri
     wt[(i & 127) * BH + (i >> 7)] = w[i];
 }
 
-// out[j] = sum_{p in [off[j], off[j+1])} rows[edge[p]]: one wave per source
-// row j, two columns per lane, in list order.
+// out[j] = sum_{p in [off[j], off[j+1])} rows[edge[p]] (GATHER) or rows[p] (the
+// rows of source j stored contiguously by mmpde_gnn_edge_backward_sorted).  One
+// wave per source: lanes 0-31 take the even positions of the list and 32-63 the
+// odd ones, four columns per lane.  Rows go in batches of 32 (16 loads in
+// flight per lane, issued unconditionally: positions past the list re-read its
+// last row and are masked with an opaque all-ones / zero word, since a load
+// under a condition is waited for at once); each half adds its rows in list
+// order, then the odd half's sum is added to the even half's.  Both forms add
+// the same values in the same order: bitwise-equal sums.
+template <bool GATHER>
+__device__ __forceinline__ void source_sum(const float *__restrict__ rows, const int64_t *__restrict__ off,
+                                           const int64_t *__restrict__ edge, int64_t n,
+                                           float *__restrict__ out) {
+    const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int par = lane >> 5, c4 = lane & 31;
+    if (j >= n) return;
+    float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    const int64_t q0 = off[j], qe = off[j + 1];
+    for (int64_t qb = q0; qb < qe; qb += 32) {
+        int64_t src[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const int64_t q = min(qb + 2 * t + par, qe - 1);
+            src[t] = GATHER ? edge[q] : q;
+        }
+        float4 v[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) v[t] = ((const float4 *)(rows + src[t] * BH))[c4];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            int m = qb + 2 * t + par < qe ? -1 : 0;
+            asm volatile("" : "+v"(m));
+            acc.x += __int_as_float(__float_as_int(v[t].x) & m);
+            acc.y += __int_as_float(__float_as_int(v[t].y) & m);
+            acc.z += __int_as_float(__float_as_int(v[t].z) & m);
+            acc.w += __int_as_float(__float_as_int(v[t].w) & m);
+        }
+    }
+    acc.x += __shfl_down(acc.x, 32, 64);
+    acc.y += __shfl_down(acc.y, 32, 64);
+    acc.z += __shfl_down(acc.z, 32, 64);
+    acc.w += __shfl_down(acc.w, 32, 64);
+    if (par == 0) ((float4 *)(out + j * BH))[c4] = acc;
+}
+
 __global__ __launch_bounds__(256) void edge_source_sum_kernel(const float *__restrict__ rows,
                                                               const int64_t *__restrict__ off,
                                                               const int64_t *__restrict__ edge, int64_t n,
                                                               float *__restrict__ out) {
-    const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (j >= n) return;
-    float2 acc = make_float2(0.0f, 0.0f);
-    int64_t q = off[j];
-    const int64_t qe = off[j + 1];
-    // eight rows in flight per step, added in list order (the same sums)
-    for (; q + 8 <= qe; q += 8) {
-        float2 v[8];
-#pragma unroll
-        for (int t = 0; t < 8; ++t) v[t] = ((const float2 *)(rows + edge[q + t] * BH))[lane];
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            acc.x += v[t].x;
-            acc.y += v[t].y;
-        }
-    }
-    for (; q < qe; ++q) {
-        const float2 v = ((const float2 *)(rows + edge[q] * BH))[lane];
-        acc.x += v.x;
-        acc.y += v.y;
-    }
-    ((float2 *)(out + j * BH))[lane] = acc;
+    source_sum<true>(rows, off, edge, n, out);
 }
 
-// out[j] = sum_{p in [off[j], off[j+1])} rows[p]: the rows of source j stored
-// contiguously (mmpde_gnn_edge_backward_sorted); one wave per source, two
-// columns per lane, eight rows in flight, added in list order.
 __global__ __launch_bounds__(256) void edge_source_sum_sorted_kernel(const float *__restrict__ rows,
                                                                      const int64_t *__restrict__ off, int64_t n,
                                                                      float *__restrict__ out) {
-    const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (j >= n) return;
-    float2 acc = make_float2(0.0f, 0.0f);
-    int64_t q = off[j];
-    const int64_t qe = off[j + 1];
-    for (; q + 8 <= qe; q += 8) {
-        float2 v[8];
-#pragma unroll
-        for (int t = 0; t < 8; ++t) v[t] = ((const float2 *)(rows + (q + t) * BH))[lane];
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            acc.x += v[t].x;
-            acc.y += v[t].y;
-        }
-    }
-    for (; q < qe; ++q) {
-        const float2 v = ((const float2 *)(rows + q * BH))[lane];
-        acc.x += v.x;
-        acc.y += v.y;
-    }
-    ((float2 *)(out + j * BH))[lane] = acc;
+    source_sum<false>(rows, off, nullptr, n, out);
 }
 
 // out[j][c] = sum_{p in [off[j], off[j+1])} rows[edge[p]][c] for any row width:
@@ -705,21 +703,35 @@ __global__ __launch_bounds__(256) void segment_sum_kernel(const float *__restric
     out[t] = acc;
 }
 
-// out[i] = sum_{g < G} part[g * len + i], in g order.
+// out[i] = sum_{g < G} part[g * len + i] in a fixed order: thread (group gq =
+// tid / 32, i = 32 block + tid % 32) adds the partials of its eighth of g in
+// order (eight loads in flight, issued unconditionally: clamped and masked),
+// then the eight group sums are added in group order through LDS.
 __global__ __launch_bounds__(256) void partial_sum_kernel(const float *__restrict__ part, int G, int64_t len,
                                                           float *__restrict__ out) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= len) return;
+    __shared__ float red[8][32];
+    const int gq = threadIdx.x >> 5, l = threadIdx.x & 31;
+    const int64_t i = (int64_t)blockIdx.x * 32 + l;
+    const int64_t ic = min(i, len - 1);
+    const int per = (G + 7) / 8;
+    const int q0 = min(gq * per, G), q1 = min(q0 + per, G);
     float s = 0.0f;
-    int q = 0;
-    for (; q + 8 <= G; q += 8) {  // eight partials in flight, added in g order
+    for (int q = q0; q < q1; q += 8) {
         float v[8];
 #pragma unroll
-        for (int t = 0; t < 8; ++t) v[t] = part[(int64_t)(q + t) * len + i];
+        for (int t = 0; t < 8; ++t) v[t] = part[(int64_t)min(q + t, q1 - 1) * len + ic];
 #pragma unroll
-        for (int t = 0; t < 8; ++t) s += v[t];
+        for (int t = 0; t < 8; ++t) {
+            int m = q + t < q1 ? -1 : 0;
+            asm volatile("" : "+v"(m));
+            s += __int_as_float(__float_as_int(v[t]) & m);
+        }
     }
-    for (; q < G; ++q) s += part[(int64_t)q * len + i];
+    red[gq][l] = s;
+    __syncthreads();
+    if (gq != 0 || i >= len) return;
+#pragma unroll
+    for (int u = 1; u < 8; ++u) s += red[u][l];
     out[i] = s;
 }
 
@@ -758,9 +770,9 @@ static int edge_backward_f32(const float *a, const float *b, const int32_t *nbr,
     if (mask) hipLaunchKernelGGL(edge_bwd_kernel<true>, dim3(grid), dim3(256), 0, st, p);
     else hipLaunchKernelGGL(edge_bwd_kernel<false>, dim3(grid), dim3(256), 0, st, p);
     MMPDE_RET_LAUNCH();
-    hipLaunchKernelGGL(partial_sum_kernel, dim3(ceil_div(BH * BH, 256)), dim3(256), 0, st, pw2, grid,
+    hipLaunchKernelGGL(partial_sum_kernel, dim3(ceil_div(BH * BH, 32)), dim3(256), 0, st, pw2, grid,
                        (int64_t)BH * BH, grad_w2);
-    hipLaunchKernelGGL(partial_sum_kernel, dim3(1), dim3(256), 0, st, pb2, grid, (int64_t)BH, grad_b2);
+    hipLaunchKernelGGL(partial_sum_kernel, dim3(BH / 32), dim3(256), 0, st, pb2, grid, (int64_t)BH, grad_b2);
     MMPDE_RET_LAUNCH();
     return MMPDE_OK;
 }
@@ -810,9 +822,9 @@ static int edge_backward(const float *a, const float *b, const int32_t *nbr, con
     if (mask) hipLaunchKernelGGL(edge_bwd_f16_kernel<true>, dim3(grid), dim3(512), 0, st, p);
     else hipLaunchKernelGGL(edge_bwd_f16_kernel<false>, dim3(grid), dim3(512), 0, st, p);
     MMPDE_RET_LAUNCH();
-    hipLaunchKernelGGL(partial_sum_kernel, dim3(ceil_div(BH * BH, 256)), dim3(256), 0, st, pw2, grid,
+    hipLaunchKernelGGL(partial_sum_kernel, dim3(ceil_div(BH * BH, 32)), dim3(256), 0, st, pw2, grid,
                        (int64_t)BH * BH, grad_w2);
-    hipLaunchKernelGGL(partial_sum_kernel, dim3(1), dim3(256), 0, st, pb2, grid, (int64_t)BH, grad_b2);
+    hipLaunchKernelGGL(partial_sum_kernel, dim3(BH / 32), dim3(256), 0, st, pb2, grid, (int64_t)BH, grad_b2);
     MMPDE_RET_LAUNCH();
     return MMPDE_OK;
 }

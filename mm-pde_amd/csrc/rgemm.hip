@@ -559,32 +559,43 @@ __global__ __launch_bounds__(256, 2) void rgemm_tn_partial_kernel(TnArgs t) {
 
 // dw / db from the partials, chunks added in order.
 __global__ __launch_bounds__(256) void rgemm_tn_reduce_kernel(TnArgs t, int chunks) {
+    // thread (group gq = tid / 32, output idx = 32 block + tid % 32): the
+    // chunks of group gq (a contiguous eighth of them) added in order, their
+    // loads issued 8 at a time unconditionally (clamped, masked); then the 8
+    // groups' sums added in group order through LDS: a fixed order
+    __shared__ float red[8][32];
     const mmpde_rgemm_tn_args &g = t.g;
-    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (idx >= (int64_t)g.gcols * t.cols) return;
-    const int c = (int)(idx / t.cols), k = (int)(idx - (int64_t)c * t.cols);
-    int seg = -1, kk = 0;
-    if (k < t.kbig) {
-        seg = 0;
-        while (seg < g.nseg - 1 && k >= t.base[seg + 1]) ++seg;
-        kk = k - t.base[seg];
-        if (kk >= g.kx[seg]) return;  // padding column
-    }
-    // chunks added in order; the loads of 8 chunks are issued before their adds
-    float s = 0.0f;
+    const int gq = threadIdx.x >> 5;
+    const int64_t outs = (int64_t)g.gcols * t.cols;
+    const int64_t idx = (int64_t)blockIdx.x * 32 + (threadIdx.x & 31);
+    const int64_t ic = min(idx, outs - 1);
+    const int c = (int)(ic / t.cols), k = (int)(ic - (int64_t)c * t.cols);
+    const int per = (chunks + 7) / 8;
+    const int q0 = min(gq * per, chunks), q1 = min(q0 + per, chunks);
     const float *pp = t.part + (int64_t)c * t.cols + k;
     const int64_t cs = (int64_t)128 * t.cols;
-    int q = 0;
-    for (; q + 8 <= chunks; q += 8) {
+    float s = 0.0f;
+    for (int q = q0; q < q1; q += 8) {
         float v[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = pp[(q + u) * cs];
+        for (int u = 0; u < 8; ++u) v[u] = pp[(int64_t)min(q + u, q1 - 1) * cs];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) s += v[u];
+        for (int u = 0; u < 8; ++u) {
+            int m = q + u < q1 ? -1 : 0;
+            asm volatile("" : "+v"(m));
+            s += __int_as_float(__float_as_int(v[u]) & m);
+        }
     }
-    for (; q < chunks; ++q) s += pp[q * cs];
-    if (seg >= 0) {
-        g.dw[(int64_t)c * g.lddw + g.dwcol[seg] + kk] = s;
+    red[gq][threadIdx.x & 31] = s;
+    __syncthreads();
+    if (gq != 0 || idx >= outs) return;
+#pragma unroll
+    for (int u = 1; u < 8; ++u) s += red[u][threadIdx.x & 31];
+    if (k < t.kbig) {
+        int seg = 0;
+        while (seg < g.nseg - 1 && k >= t.base[seg + 1]) ++seg;
+        const int kk = k - t.base[seg];
+        if (kk < g.kx[seg]) g.dw[(int64_t)c * g.lddw + g.dwcol[seg] + kk] = s;  // else a padding column
     } else if (k < t.kbig + g.ns) {
         float *o = g.dw + (int64_t)c * g.lddw + g.dwcol_s + (k - t.kbig);
         const float v = g.sign_s * s;
@@ -724,7 +735,7 @@ extern "C" int mmpde_rgemm_tn(const mmpde_rgemm_tn_args *gp, void *workspace, in
 #undef TN_LAUNCH
     MMPDE_RET_LAUNCH();
     const int64_t outs = (int64_t)g.gcols * t.cols;
-    hipLaunchKernelGGL(rgemm_tn_reduce_kernel, dim3((unsigned)ceil_div(outs, 256)), dim3(256), 0, st, t,
+    hipLaunchKernelGGL(rgemm_tn_reduce_kernel, dim3((unsigned)ceil_div(outs, 32)), dim3(256), 0, st, t,
                        (int)chunks);
     MMPDE_RET_LAUNCH();
     return MMPDE_OK;
