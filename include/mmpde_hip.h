@@ -526,6 +526,19 @@ int mmpde_rgemm_tn(const mmpde_rgemm_tn_args *g, void *workspace, int64_t worksp
 int mmpde_rows_small(const float *x, int64_t ldx, int64_t n, int ki, const float *w, int64_t ldw, int layout,
                      const float *bias, int no, float *y, int64_t ldy, mmpde_stream_t stream);
 
+/* Training backward of the few-row linears (res_cut's MLP, interpolate.py:
+ * 54-60,95-97, M = B rows; reference loss.backward(), train_helper_2d.py:126):
+ *   mmpde_outer_rows: dw[i][j] = sum_{r<m} g[r][i] x[r][j], db[i] = sum_r
+ *     g[r][i] (db nullable; r ascending; m <= 32): the weight / bias gradient;
+ *   mmpde_transpose: y[c][r] = x[r][c] (rows x cols; W^T for dX = dY W through
+ *     mmpde_linear_skinny);
+ *   mmpde_tanh_bwd: dz[i] = dy[i] (1 - t[i]^2) (t = the forward's tanh output). */
+int mmpde_outer_rows(const float *g, int64_t ldg, const float *x, int64_t ldx, int m, int64_t n, int64_t k,
+                     float *dw, int64_t lddw, float *db, mmpde_stream_t stream);
+int mmpde_transpose(const float *x, int64_t rows, int64_t cols, int64_t ldx, float *y, int64_t ldy,
+                    mmpde_stream_t stream);
+int mmpde_tanh_bwd(const float *dy, const float *t, int64_t n, float *dz, mmpde_stream_t stream);
+
 /* out[n] = out_scale * output_mlp(h[:, None]) */
 int mmpde_gnn_head(const float *h, int64_t n, const mmpde_gnn_head_params *p, float *out,
                    mmpde_stream_t stream);

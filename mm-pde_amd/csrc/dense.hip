@@ -342,9 +342,107 @@ __global__ __launch_bounds__(256) void traj_mse_kernel(const float *__restrict__
     if (threadIdx.x == 0) out[blockIdx.x] = red[0] / (float)n_per;
 }
 
+// Training backward of the few-row linears (res_cut's MLP, interpolate.py:
+// 54-60,95-97, at M = B rows):
+//   outer_rows: dw[i][j] = sum_{r<m} g[r][i] x[r][j] and db[i] = sum_r g[r][i]
+//     (r ascending).  Workgroup = a 16 (i) x 64 (j) block of dw: the block's g
+//     and x columns staged in LDS (any row stride / alignment), each thread 4
+//     outputs of one i; HBM-bound on the dw write.
+//   transpose: y[c][r] = x[r][c] through 32 x 33 LDS tiles (dX = dY W as the
+//     skinny forward of W^T).
+//   tanh_bwd: dz = dy (1 - t^2) (torch's tanh_backward).
+constexpr int kOrMaxM = 32;
+__global__ __launch_bounds__(256) void outer_rows_kernel(const float *__restrict__ g, int64_t ldg,
+                                                         const float *__restrict__ x, int64_t ldx, int m,
+                                                         int64_t n, int64_t k, float *__restrict__ dw,
+                                                         int64_t lddw, float *__restrict__ db) {
+    __shared__ float sg[kOrMaxM][16], sx[kOrMaxM][64];
+    const int tid = threadIdx.x;
+    const int64_t i0 = (int64_t)blockIdx.y * 16, j0 = (int64_t)blockIdx.x * 64;
+    for (int e = tid; e < m * 64; e += 256) {
+        const int r = e >> 6, c = e & 63;
+        sx[r][c] = x[r * ldx + min(j0 + c, k - 1)];
+        if (c < 16) sg[r][c] = g[r * ldg + min(i0 + c, n - 1)];
+    }
+    __syncthreads();
+    const int il = tid >> 4, jl = 4 * (tid & 15);
+    float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    float sb = 0.0f;
+    for (int r = 0; r < m; ++r) {
+        const float gv = sg[r][il];
+        const float4 xv = *(const float4 *)&sx[r][jl];
+        acc.x = fmaf(gv, xv.x, acc.x);
+        acc.y = fmaf(gv, xv.y, acc.y);
+        acc.z = fmaf(gv, xv.z, acc.z);
+        acc.w = fmaf(gv, xv.w, acc.w);
+        sb += gv;
+    }
+    const int64_t i = i0 + il, j = j0 + jl;
+    if (i >= n) return;
+    float *o = dw + i * lddw + j;
+    if (j < k) o[0] = acc.x;
+    if (j + 1 < k) o[1] = acc.y;
+    if (j + 2 < k) o[2] = acc.z;
+    if (j + 3 < k) o[3] = acc.w;
+    if (db && blockIdx.x == 0 && jl == 0) db[i] = sb;
+}
+
+__global__ __launch_bounds__(256) void transpose_kernel(const float *__restrict__ x, int64_t rows, int64_t cols,
+                                                        int64_t ldx, float *__restrict__ y, int64_t ldy) {
+    __shared__ float t[32][33];
+    const int64_t r0 = (int64_t)blockIdx.y * 32, c0 = (int64_t)blockIdx.x * 32;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+    for (int q = ty; q < 32; q += 8) {
+        const int64_t r = r0 + q, c = c0 + tx;
+        t[q][tx] = (r < rows && c < cols) ? x[r * ldx + c] : 0.0f;
+    }
+    __syncthreads();
+    for (int q = ty; q < 32; q += 8) {
+        const int64_t c = c0 + q, r = r0 + tx;
+        if (c < cols && r < rows) y[c * ldy + r] = t[tx][q];
+    }
+}
+
+__global__ __launch_bounds__(256) void tanh_bwd_kernel(const float *__restrict__ dy, const float *__restrict__ t,
+                                                       int64_t n, float *__restrict__ dz) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float tv = t[i];
+    dz[i] = dy[i] * (1.0f - tv * tv);
+}
+
 }  // namespace
 
-extern "C" int mmpde_version(void) { return 11900; }
+extern "C" int mmpde_outer_rows(const float *g, int64_t ldg, const float *x, int64_t ldx, int m, int64_t n,
+                                int64_t k, float *dw, int64_t lddw, float *db, mmpde_stream_t stream) {
+    MMPDE_REQUIRE(g && x && dw && m >= 1 && m <= kOrMaxM && n >= 1 && k >= 1);
+    MMPDE_REQUIRE(ldg >= n && ldx >= k && lddw >= k && n < ((int64_t)1 << 31) && k < ((int64_t)1 << 31));
+    const dim3 grid((unsigned)((k + 63) / 64), (unsigned)((n + 15) / 16));
+    hipLaunchKernelGGL(outer_rows_kernel, grid, dim3(256), 0, as_stream(stream), g, ldg, x, ldx, m, n, k, dw,
+                       lddw, db);
+    MMPDE_RET_LAUNCH();
+    return MMPDE_OK;
+}
+
+extern "C" int mmpde_transpose(const float *x, int64_t rows, int64_t cols, int64_t ldx, float *y, int64_t ldy,
+                               mmpde_stream_t stream) {
+    MMPDE_REQUIRE(x && y && rows >= 1 && cols >= 1 && ldx >= cols && ldy >= rows);
+    MMPDE_REQUIRE(rows < ((int64_t)1 << 36) && cols < ((int64_t)1 << 36));
+    const dim3 grid((unsigned)((cols + 31) / 32), (unsigned)((rows + 31) / 32));
+    hipLaunchKernelGGL(transpose_kernel, grid, dim3(256), 0, as_stream(stream), x, rows, cols, ldx, y, ldy);
+    MMPDE_RET_LAUNCH();
+    return MMPDE_OK;
+}
+
+extern "C" int mmpde_tanh_bwd(const float *dy, const float *t, int64_t n, float *dz, mmpde_stream_t stream) {
+    MMPDE_REQUIRE(dy && t && dz && n >= 1);
+    hipLaunchKernelGGL(tanh_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), dy, t,
+                       n, dz);
+    MMPDE_RET_LAUNCH();
+    return MMPDE_OK;
+}
+
+extern "C" int mmpde_version(void) { return 12000; }
 
 extern "C" int mmpde_traj_mse(const float *pred, const float *labels, int64_t batches, int64_t n_per,
                               float *out, mmpde_stream_t stream) {

@@ -13,7 +13,7 @@ import os
 import torch
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libmmpde_hip.so")
-ABI_VERSION = 11900
+ABI_VERSION = 12000
 
 ACT_NONE, ACT_TANH, ACT_RELU, ACT_ELU = 0, 1, 2, 3
 PAD_ZEROS, PAD_CIRCULAR = 0, 1
@@ -150,6 +150,9 @@ _SIGS = {
     "mmpde_rgemm_tn_workspace_bytes": (_I64, [_I64, _I, _I]),
     "mmpde_rgemm_tn": (_I, [_P, _P, _I64, _P]),
     "mmpde_rows_small": (_I, [_P, _I64, _I64, _I, _P, _I64, _I, _P, _I, _P, _I64, _P]),
+    "mmpde_outer_rows": (_I, [_P, _I64, _P, _I64, _I, _I64, _I64, _P, _I64, _P, _P]),
+    "mmpde_transpose": (_I, [_P, _I64, _I64, _I64, _P, _I64, _P]),
+    "mmpde_tanh_bwd": (_I, [_P, _P, _I64, _P, _P]),
     "mmpde_gnn_workspace_bytes": (_I64, [_I64]),
     "mmpde_gnn_embed": (_I, [_P, _P, _I64, GnnScales, _P, _P, _P, _P]),
     "mmpde_gnn_layer": (_I, [_P, _P, _P, _I64, _I, _P, GnnScales, _P, _P, _P, _P]),

@@ -29,6 +29,57 @@ def _mlp(widths):
     return nn.ModuleList(nn.Linear(a, b) for a, b in zip(widths[:-1], widths[1:]))
 
 
+class ResCutMlp(torch.autograd.Function):
+    """The cylinder ``down`` MLP (interpolate.py:58-60: Linear, Tanh x 3, Linear)
+    in train mode at M = B rows: forward on mmpde_linear_skinny (tanh fused),
+    backward per layer dW = dZ^T X, db = sum dZ (mmpde_outer_rows), dX = dZ W as
+    the skinny forward of W^T (mmpde_transpose), times tanh' of the layer input
+    (mmpde_tanh_bwd).  Exact fp32 products in fixed orders: deterministic."""
+
+    @staticmethod
+    def forward(ctx, x, *params):
+        ws, bs = params[0::2], params[1::2]
+        acts = (L.ACT_TANH, L.ACT_TANH, L.ACT_TANH, L.ACT_NONE)
+        ins = [L.f32c(x)]
+        for w, b, act in zip(ws, bs, acts):
+            ins.append(ops.linear_skinny(ins[-1], w, b, act))
+        y = ins.pop()
+        ctx.save_for_backward(*ins, *[L.f32c(w) for w in ws])
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        saved = ctx.saved_tensors
+        ins, ws = saved[:4], saved[4:]
+        lib = L.lib()
+        dev = dy.device
+        st = L.stream(dev)
+        grads = [None] * 8
+        g = L.f32c(dy)
+        m = g.shape[0]
+        for layer in (3, 2, 1, 0):
+            w, xin = ws[layer], ins[layer]
+            n, k = w.shape
+            need_w, need_b = ctx.needs_input_grad[1 + 2 * layer], ctx.needs_input_grad[2 + 2 * layer]
+            if need_w or need_b:
+                dw = torch.empty((n, k), dtype=torch.float32, device=dev)
+                db = torch.empty((n,), dtype=torch.float32, device=dev) if need_b else None
+                L.check(lib.mmpde_outer_rows(L.ptr(g), n, L.ptr(xin), k, m, n, k, L.ptr(dw), k, L.ptr(db), st),
+                        "mmpde_outer_rows")
+                grads[2 * layer] = dw if need_w else None
+                grads[2 * layer + 1] = db
+            if layer == 0 and not ctx.needs_input_grad[0]:
+                g = None
+                break
+            wt = torch.empty((k, n), dtype=torch.float32, device=dev)
+            L.check(lib.mmpde_transpose(L.ptr(w), n, k, k, L.ptr(wt), n, st), "mmpde_transpose")
+            dx = ops.linear_skinny(g, wt)
+            if layer > 0:   # the layer's input is the previous layer's tanh output
+                L.check(lib.mmpde_tanh_bwd(L.ptr(dx), L.ptr(xin), dx.numel(), L.ptr(dx), st), "mmpde_tanh_bwd")
+            g = dx
+        return (g, *grads)
+
+
 class ItpNet(nn.Module):
     def __init__(self, ori_nx, ori_ny, layers1, layers2, layers3, normalize=False):
         super().__init__()
@@ -104,9 +155,16 @@ class ItpNet(nn.Module):
         """``down`` network (interpolate.py:95-97): data [B, N] (cylinder) or
         [B, 1, s, s] (Burgers)."""
         L.require_device(data)
-        if self.training:
-            return self.down(data)
         d = self.down
+        if self.training:
+            # differentiable, on the HIP kernels (no library GEMM / MIOpen)
+            if self.conv:
+                x = data
+                for i in (0, 2, 4, 6):
+                    x = torch.tanh(ops.Conv2dSame.apply(x, d[i].weight, d[i].bias, False))
+                return x
+            params = [t for i in (0, 2, 4, 6) for t in (d[i].weight, d[i].bias)]
+            return ResCutMlp.apply(data.reshape(data.shape[0], -1), *params)
         if self.conv:
             x = data
             for i in (0, 2, 4, 6):

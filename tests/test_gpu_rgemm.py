@@ -185,3 +185,33 @@ def test_gnn_layer_train_vs_fp64(dev, edge_gemm):
         print(f"{edge_gemm} {k}: rel max err {e:.2e} (fp32 oracle {f:.2e})")
         bar = 1e-5 if k.startswith("norm.module.running") else max(4 * f, 2e-6)
         assert e <= bar, (k, e, f)
+
+
+@pytest.mark.parametrize("conv", [False, True])
+def test_res_cut_train_vs_fp64(dev, conv):
+    """ItpNet.res_cut in train mode (interpolate.py:54-60,95-97) on the HIP
+    kernels (cy: ResCutMlp on mmpde_linear_skinny / _outer_rows / _transpose /
+    _tanh_bwd; Burgers: ops.Conv2dSame + tanh) against float64 autograd through
+    the module itself: output and every parameter gradient within 1e-5 of
+    max|ref| (exact fp32 products, K <= 2521)."""
+    from mmpde_amd.interpolate import ItpNet
+
+    torch.manual_seed(0)
+    itp = ItpNet(48, 48, [128, 64], [128, 64], [1, 4, 16, 4, 1]) if conv else \
+        ItpNet(2521, None, [128, 64], [128, 64], [1, 4, 16, 4, 1])
+    g = torch.Generator().manual_seed(5)
+    B = 16
+    data = torch.randn(B, 1, 48, 48, generator=g) if conv else torch.randn(B, 2521, generator=g)
+    dy = torch.randn(B, 1, 48, 48, generator=g) if conv else torch.randn(B, 2521, generator=g)
+    ref = ItpNet(48, 48, [128, 64], [128, 64], [1, 4, 16, 4, 1]) if conv else \
+        ItpNet(2521, None, [128, 64], [128, 64], [1, 4, 16, 4, 1])
+    ref.load_state_dict(itp.state_dict())
+    ref.double().train()
+    yr = ref.down(data.double())
+    (yr * dy.double()).sum().backward()
+    itp.to(dev).train()
+    y = itp.res_cut(data.to(dev))
+    (y * dy.to(dev)).sum().backward()
+    _close(y, yr, 1e-5, "res_cut train forward")
+    for (name, p), (_, pr) in zip(itp.down.named_parameters(), ref.down.named_parameters()):
+        _close(p.grad, pr.grad, 1e-5, f"d/d down.{name}")
