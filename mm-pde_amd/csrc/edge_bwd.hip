@@ -289,6 +289,16 @@ static_assert(kEdgeBwdF16Lds <= 160 * 1024, "edge_bwd_f16_kernel: LDS beyond gfx
 #define MMPDE_BWD_P1_FIRST 0
 #endif
 constexpr bool kBwdP1First = MMPDE_BWD_P1_FIRST != 0;
+// SIMD-partner stagger of the MASK kernel (below): 0 off; waves 4-7 run
+// 1: P1 P2 | P3, 2: P1 | P3 P2, 3: P2 | P3 P1 of each phase (0-3: P3 P1 P2).
+// Measured (tools/ubench bwd_ab_st*, cy B=16, k = 35, profiles/
+// r05_bwd_stagger_ab.log): 561-563 us off against 667-668 / 630 / 676-679:
+// the second loop body pushes the kernel from 254 VGPRs to 44-53 spilled, which
+// costs more than the overlap gains.  Off.
+#ifndef MMPDE_BWD_STAGGER
+#define MMPDE_BWD_STAGGER 0
+#endif
+constexpr int kBwdStagger = MMPDE_BWD_STAGGER;
 
 // MASK: message_net_2's ReLU pattern comes from the forward's bits instead of
 // recomputing z2 (P2 without its MFMAs; no row-major relu(z1) image).
@@ -537,14 +547,34 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
             // e + 1 while the others still multiply.  P1 / P2(e + 1) write the
             // (e + 1) & 1 buffers, last read by P3(e - 1), which every wave left
             // before the previous barrier.
+            // Stagger (MI355X_MICROARCH.md, "two waves that run the SAME program
+            // with one barrier per block"): waves w and w + 4 share a SIMD;
+            // waves 4-7 build slot e + 1 (VALU, LDS writes, loads) before their
+            // P3(e) MFMAs, waves 0-3 after theirs, so one wave of each SIMD
+            // pair multiplies while the other splits.  Both orders touch
+            // disjoint buffers within the phase (P3(e) reads parity e & 1, P1 /
+            // P2(e + 1) write parity (e + 1) & 1), and each wave's own sums run
+            // in the same order: the outputs are bitwise unchanged.
             p1(0);
             p2(0);
             __syncthreads();
-            for (int e = 0; e + 1 < k; ++e) {
-                p3(e, false);
-                p1(e + 1);
-                p2(e + 1);
-                __syncthreads();
+            if (kBwdStagger == 0 || wave < 4) {
+                for (int e = 0; e + 1 < k; ++e) {
+                    p3(e, false);
+                    p1(e + 1);
+                    p2(e + 1);
+                    __syncthreads();
+                }
+            } else {
+                for (int e = 0; e + 1 < k; ++e) {
+                    if (kBwdStagger != 3) p1(e + 1);
+                    if (kBwdStagger == 1 || kBwdStagger == 3) p2(e + 1);
+                    __builtin_amdgcn_sched_barrier(0);  // P3's fragment reads stay after the split
+                    p3(e, false);
+                    if (kBwdStagger == 2) p2(e + 1);
+                    if (kBwdStagger == 3) p1(e + 1);
+                    __syncthreads();
+                }
             }
             p3(k - 1, false);
         } else {
