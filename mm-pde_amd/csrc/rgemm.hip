@@ -19,6 +19,7 @@
 #include "common.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace {
 
@@ -638,12 +639,20 @@ extern "C" int mmpde_rgemm(const mmpde_rgemm_args *gp, mmpde_stream_t stream) {
     }
     const bool am = g.kh > 0 && g.amask[0] != nullptr;
     hipStream_t st = as_stream(stream);
-    if (vec && (g.kh == 32 || g.kh == 64 || g.kh == 128)) {
-        // weight-stationary persistent form: two workgroups per CU at most
-        // workgroups that fit a CU at once: the kh = 128 form holds ~240 registers per lane
+    // MMPDE_RGEMM_FORM=tile (A/B aid, tools/rgemm_bench.py): the 128 x 128 tile
+    // kernel for every shape
+    static const bool tile_only = [] {
+        const char *e = getenv("MMPDE_RGEMM_FORM");
+        return e && e[0] == 't';
+    }();
+    if (!tile_only && vec && (g.kh == 32 || g.kh == 64 || g.kh == 128)) {
+        // weight-stationary persistent form: the workgroups that fit the CUs at
+        // once (two per CU; the kh = 128 form holds ~240 registers per lane,
+        // one), shared by the parts
         const int64_t ntiles = (g.m + 31) / 32;
         const int per_cu = g.kh == 128 ? 1 : 2;
-        const dim3 wgrid((unsigned)std::min<int64_t>(ntiles, (int64_t)per_cu * rgemm_cus()), (unsigned)g.parts);
+        const int64_t slots = std::max<int64_t>(1, (int64_t)per_cu * rgemm_cus() / g.parts);
+        const dim3 wgrid((unsigned)std::min<int64_t>(ntiles, slots), (unsigned)g.parts);
 #define WS_LAUNCH(L, K, A, X) hipLaunchKernelGGL((rgemm_ws_kernel<L, K, A, X>), wgrid, dim3(256), 0, st, g)
 #define WS_K(L, A, X)                          \
     if (g.kh == 32) WS_LAUNCH(L, 32, A, X);    \

@@ -146,7 +146,17 @@ class ItpNet(nn.Module):
         for i, lin in enumerate(mods):
             # rows of every trajectory's queries: the row-chunked weight
             # gradient of ops.LinearRows (the library's K = rows GEMM is slow)
-            x = ops.linear_train(x, lin) if x.requires_grad or lin.weight.requires_grad else lin(x)
+            if not (x.requires_grad or lin.weight.requires_grad):
+                x = lin(x)
+            elif x.shape[-1] % 8:
+                # the 62-wide input zero-padded to a multiple of 8 (x and W alike:
+                # the extra products are exact zeros), so that the row GEMM's
+                # MFMA form takes it (interpolate.py:84's 2 * 30 + 2 features)
+                padk = -x.shape[-1] % 8
+                x = ops.LinearRows.apply(torch.nn.functional.pad(x, (0, padk)).contiguous(),
+                                         torch.nn.functional.pad(lin.weight, (0, padk)), lin.bias)
+            else:
+                x = ops.linear_train(x, lin)
             if i != len(mods) - 1:
                 x = torch.tanh(x)
         return x.reshape(*lead, x.shape[-1])
