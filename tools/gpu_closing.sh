@@ -35,7 +35,7 @@ for m in f16x3 f32; do
       || { tail $O/train_$m.json; exit 6; }
   tail -1 $O/train_$m.json
 done
-for cfg in cy-gnn burgers-mmpde; do
+for cfg in cy-gnn burgers-mmpde burgers-gnn; do
   timeout -k 10 300 python3 -u bench.py --config $cfg > $O/$cfg.bench.log 2>&1 || { tail -20 $O/$cfg.bench.log; exit 7; }
   grep '^{' $O/$cfg.bench.log | tail -1 > $O/$cfg.bench.json
   echo "$cfg bench ok"
