@@ -20,11 +20,23 @@ __host__ __device__ inline int64_t range_tiles(int64_t n) { return (n + kRangeRo
 __device__ __forceinline__ float segment_range(const float *rng, int64_t seg_n, int64_t s) {
     const int64_t r0 = s * seg_n, t0 = r0 / kRangeRows, t1 = (r0 + seg_n - 1) / kRangeRows;
     float ma = 0.0f, mb = 0.0f;
-    for (int64_t t = t0 + (threadIdx.x & 63); t <= t1; t += 64) {
-        const float4 v = *(const float4 *)(rng + 4 * t);
-        const bool own = t * kRangeRows >= r0;  // first row of the tile in s
-        ma = fmaxf(ma, own ? v.x : v.z);
-        mb = fmaxf(mb, own ? v.y : v.w);
+    // four records per lane per pass, loaded together (one memory round trip for
+    // segments of up to 256 records): indices past t1 re-read t1, which a max
+    // takes twice harmlessly
+    for (int64_t tb = t0; tb <= t1; tb += 256) {
+        float4 v[4];
+        int64_t tt[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            tt[q] = min(tb + (threadIdx.x & 63) + 64 * q, t1);
+            v[q] = *(const float4 *)(rng + 4 * tt[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const bool own = tt[q] * kRangeRows >= r0;  // first row of the tile in s
+            ma = fmaxf(ma, own ? v[q].x : v[q].z);
+            mb = fmaxf(mb, own ? v[q].y : v[q].w);
+        }
     }
     return wave_absmax(ma) + wave_absmax(mb);  // maxima of |x| >= 0; every lane active
 }
