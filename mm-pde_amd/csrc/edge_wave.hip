@@ -419,6 +419,11 @@ EdgePlan edge_wave_plan(int64_t nseg, int64_t S_seg, int cus, int64_t side_cap) 
     // segment alone
     int64_t U = 1;
     while (U * 2 * 22 <= S_seg) U *= 2;
+    // a segment that fills the chip alone (>= 16384 slots: the 96 x 96 Burgers
+    // grid, configs[0]) takes units of >= 11 slots, up to 1024 of them, so one
+    // trajectory still runs one wave per SIMD (still a function of the segment)
+    if (S_seg >= 16384)
+        while (U < 1024 && U * 2 * 11 <= S_seg) U *= 2;
     const int64_t cap = S_seg < side_cap / nseg ? S_seg : side_cap / nseg;
     if (U > cap) U = cap < 1 ? 1 : cap;
     // waves per segment: one wave per SIMD over the launch, at most one per unit

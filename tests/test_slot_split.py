@@ -25,6 +25,9 @@ def plan(nseg, S_seg, cus=256, side_cap=1 << 40):
     U = 1
     while U * 2 * 22 <= S_seg:
         U *= 2
+    if S_seg >= 16384:                    # one segment fills the chip alone
+        while U < 1024 and U * 2 * 11 <= S_seg:
+            U *= 2
     cap = min(S_seg, side_cap // nseg)
     if U > cap:
         U = max(cap, 1)
@@ -108,3 +111,8 @@ def test_plan_is_segment_only_and_fills_the_chip():
         assert waves <= 1024 and w <= U
     # the side-block cap (3 seg_n / 16 blocks per segment) is a function of the segment
     assert plan(16, 5530, side_cap=16 * (3 * 2521 // 16))[0] == 128
+    # a 96 x 96 Burgers trajectory (576 tiles x 35 slots) alone: 1024 units of
+    # 19-20 slots, one wave per SIMD (512 units with the 22-44 rule alone)
+    S_96 = 576 * 35
+    assert plan(1, S_96, side_cap=3 * 9216 // 16) == (1024, 1024, 1024)
+    assert len({plan(nseg, S_96)[0] for nseg in range(1, 9)}) == 1
