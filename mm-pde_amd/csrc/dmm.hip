@@ -64,20 +64,32 @@ __global__ __launch_bounds__(256) void dmm_embed_kernel(const float *__restrict_
 // results).
 struct DmmGnnSmem {
     float W1[44], B1[4], W2[16], B2[4], V1[32], C1[4], V2[16], C2[4];
+    float BW[4], BB[4], RM[4], RV[4];  // the layer's BatchNorm (eval), read at the end
     __device__ void load(const float *w1, const float *b1, const float *w2, const float *b2, const float *v1,
-                         const float *c1, const float *v2, const float *c2) {
+                         const float *c1, const float *v2, const float *c2, const float *bnw,
+                         const float *bnb, const float *bnrm, const float *bnrv) {
+        // every load unconditional (clamped index), the stores under the
+        // conditions: a load inside an `if` is waited for where the `if` ends
         const int t = threadIdx.x;
-        if (t < 44) W1[t] = w1[t];
+        const int t44 = min(t, 43), t32 = min(t, 31), t16 = min(t, 15), t4 = min(t, 3);
+        const float a0 = w1[t44], a1 = v1[t32], a2 = w2[t16], a3 = v2[t16];
+        const float a4 = b1[t4], a5 = b2[t4], a6 = c1[t4], a7 = c2[t4];
+        const float a8 = bnw[t4], a9 = bnb[t4], a10 = bnrm[t4], a11 = bnrv[t4];
+        if (t < 44) W1[t] = a0;
+        if (t < 32) V1[t] = a1;
         if (t < 16) {
-            W2[t] = w2[t];
-            V2[t] = v2[t];
+            W2[t] = a2;
+            V2[t] = a3;
         }
-        if (t < 32) V1[t] = v1[t];
         if (t < 4) {
-            B1[t] = b1[t];
-            B2[t] = b2[t];
-            C1[t] = c1[t];
-            C2[t] = c2[t];
+            B1[t] = a4;
+            B2[t] = a5;
+            C1[t] = a6;
+            C2[t] = a7;
+            BW[t] = a8;
+            BB[t] = a9;
+            RM[t] = a10;
+            RV[t] = a11;
         }
     }
 };
@@ -106,8 +118,7 @@ __device__ __forceinline__ void dmm_edge_acc(const DmmGnnSmem &w, const float (&
 
 // the quad's sums -> mean -> update -> BN (every lane of the quad returns it)
 __device__ __forceinline__ float4 dmm_node_update(const DmmGnnSmem &w, const float (&hi)[4], float (&sum)[4],
-                                                  int k, const float *bnw, const float *bnb,
-                                                  const float *bnrm, const float *bnrv, float eps) {
+                                                  int k, float eps) {
 #pragma unroll
     for (int o = 0; o < 4; ++o) {
         sum[o] += xor_lane_f<1>(sum[o]);
@@ -132,7 +143,7 @@ __device__ __forceinline__ float4 dmm_node_update(const DmmGnnSmem &w, const flo
         float v = w.C2[o];
 #pragma unroll
         for (int t = 0; t < 4; ++t) v += w.V2[o * 4 + t] * up1[t];
-        res[o] = bn_eval(hi[o] + tanhf(v), bnrm[o], bnrv[o], bnw[o], bnb[o], eps);
+        res[o] = bn_eval(hi[o] + tanhf(v), w.RM[o], w.RV[o], w.BW[o], w.BB[o], eps);
     }
     return make_float4(res[0], res[1], res[2], res[3]);
 }
@@ -157,7 +168,7 @@ __global__ __launch_bounds__(256) void dmm_gnn_kernel(const float4 *__restrict__
                                                       const float *__restrict__ bnrv, float eps,
                                                       float4 *__restrict__ h_out) {
     __shared__ DmmGnnSmem w;
-    w.load(w1, b1, w2, b2, v1, c1, v2, c2);
+    w.load(w1, b1, w2, b2, v1, c1, v2, c2, bnw, bnb, bnrm, bnrv);
     __syncthreads();
     const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 2;
     const int sub = threadIdx.x & 3;
@@ -170,12 +181,20 @@ __global__ __launch_bounds__(256) void dmm_gnn_kernel(const float4 *__restrict__
     const float2 gi = grid[p];
     float sum[4] = {0.f, 0.f, 0.f, 0.f};
     const int32_t *nr = nbr + p * k;
-    for (int e = sub; e < k; e += 4) {
-        const int64_t jl = min((uint32_t)nr[e], (uint32_t)(n_per - 1));
-        const int64_t j = b * n_per + jl;
-        dmm_edge_acc(w, hi, ui, gi, h[j], u[j], grid[jl], sum);
+    // neighbour indices eight edges at a time, loaded unconditionally (clamped):
+    // an index load inside the edge loop is one round trip per edge
+    for (int e0 = sub; e0 < k; e0 += 32) {
+        int64_t jl[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) jl[t] = min((uint32_t)nr[min(e0 + 4 * t, k - 1)], (uint32_t)(n_per - 1));
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            if (e0 + 4 * t >= k) break;
+            const int64_t j = b * n_per + jl[t];
+            dmm_edge_acc(w, hi, ui, gi, h[j], u[j], grid[jl[t]], sum);
+        }
     }
-    const float4 r = dmm_node_update(w, hi, sum, k, bnw, bnb, bnrm, bnrv, eps);
+    const float4 r = dmm_node_update(w, hi, sum, k, eps);
     if (sub == 0) h_out[i] = r;
 }
 
@@ -207,7 +226,7 @@ __global__ __launch_bounds__(512) void dmm_gnn_lds_kernel(const float4 *__restri
     float2 *sg = (float2 *)(sh + n_per);
     float *su = (float *)(sg + n_per);
     __shared__ DmmGnnSmem w;
-    w.load(w1, b1, w2, b2, v1, c1, v2, c2);
+    w.load(w1, b1, w2, b2, v1, c1, v2, c2, bnw, bnb, bnrm, bnrv);
     const int64_t base = (int64_t)blockIdx.y * n_per;
     for (int t = threadIdx.x; t < n_per; t += 512) {
         sh[t] = h[base + t];
@@ -224,11 +243,19 @@ __global__ __launch_bounds__(512) void dmm_gnn_lds_kernel(const float4 *__restri
     const float2 gi = sg[p];
     float sum[4] = {0.f, 0.f, 0.f, 0.f};
     const int32_t *nr = nbr + (int64_t)p * k;
-    for (int e = sub; e < k; e += 4) {
-        const int jl = (int)min((uint32_t)nr[e], (uint32_t)(n_per - 1));
-        dmm_edge_acc(w, hi, ui, gi, sh[jl], su[jl], sg[jl], sum);
+    // neighbour indices eight edges at a time, loaded unconditionally (clamped):
+    // an index load inside the edge loop is one round trip per edge
+    for (int e0 = sub; e0 < k; e0 += 32) {
+        int jl[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) jl[t] = (int)min((uint32_t)nr[min(e0 + 4 * t, k - 1)], (uint32_t)(n_per - 1));
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            if (e0 + 4 * t >= k) break;
+            dmm_edge_acc(w, hi, ui, gi, sh[jl[t]], su[jl[t]], sg[jl[t]], sum);
+        }
     }
-    const float4 r = dmm_node_update(w, hi, sum, k, bnw, bnb, bnrm, bnrv, eps);
+    const float4 r = dmm_node_update(w, hi, sum, k, eps);
     if (sub == 0) h_out[base + p] = r;
 }
 

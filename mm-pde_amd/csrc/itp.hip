@@ -130,6 +130,23 @@ __global__ __launch_bounds__(kItpThreads, 4) void itp_interp_kernel(
                 for (int r1 = 0; r1 < 4; ++r1)
                     a1[r1] = mfma16(img1[(r1 * 32 + rt * 4 + i) * 64 + lane], a0[i], a1[r1]);
         }
+        // the neighbour values of this lane's outputs o = 16 r2 + 4 g + i, all
+        // loaded before the L1 tanh and L2 (a load under the o < kNb test of the
+        // weighted sum is waited for at once: eight dependent round trips per
+        // tile; issuing them with the coordinates spills)
+        const float *vb = vals + b * n_src;
+        float nv[8];
+#pragma unroll
+        for (int r2 = 0; r2 < 2; ++r2)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int o = min(16 * r2 + 4 * g + i, kNb - 1);
+                nv[4 * r2 + i] = vb[min((uint32_t)ir[o], (uint32_t)(n_src - 1))];
+            }
+        // the epilogue's addends, unconditionally (a missing one reads the query
+        // array in its place and is dropped below)
+        const float ad1 = (addend ? addend : qry)[qrow];
+        const float ad2 = (addend2 ? addend2 : qry)[qrow];
 #pragma unroll
         for (int r1 = 0; r1 < 4; ++r1)
 #pragma unroll
@@ -149,20 +166,19 @@ __global__ __launch_bounds__(kItpThreads, 4) void itp_interp_kernel(
                     a2[r2] = mfma16(img2[(r2 * 16 + t * 4 + i) * 64 + lane], a1[t][i], a2[r2]);
         // weighted sum of the neighbour values (data_creator_2d.py:83): this lane's
         // outputs o = 16 r2 + 4 g + i, then the 4 lanes of the query
-        const float *vb = vals + b * n_src;
         float sum = 0.0f;
 #pragma unroll
         for (int r2 = 0; r2 < 2; ++r2)
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int o = 16 * r2 + 4 * g + i;
-                if (o < kNb) sum += a2[r2][i] * vb[min((uint32_t)ir[o], (uint32_t)(n_src - 1))];
+                if (o < kNb) sum += a2[r2][i] * nv[4 * r2 + i];
             }
         sum += __shfl_xor(sum, 16, 64);
         sum += __shfl_xor(sum, 32, 64);
         if (g == 0 && valid) {
-            float o = addend ? addend[qrow] + sum : sum;
-            if (addend2) o = o + addend2[qrow];  // (interp + res) + model(graph_uniform)
+            float o = addend ? ad1 + sum : sum;
+            if (addend2) o = o + ad2;  // (interp + res) + model(graph_uniform)
             out[qrow] = o;
         }
     }

@@ -803,19 +803,24 @@ __device__ __forceinline__ float cand_bound_cells(float rq, float2 q, const floa
     const float x0 = rec[kCells], y0 = rec[kCells + 1], hx = rec[kCells + 2], hy = rec[kCells + 3];
     const float eps = rec[kCells + 4];
     float L = 3.0e38f;
+    // every cell's record loaded first (a load whose value decides a branch
+    // is waited for at once: one memory round trip per cell group otherwise),
+    // then the bound of each occupied cell (dc >= 0) taken by a select
+    float dcs[kCells / 64];
+#pragma unroll
+    for (int t = 0; t < kCells / 64; ++t) dcs[t] = rec[lane + 64 * t];
 #pragma unroll
     for (int t = 0; t < kCells / 64; ++t) {
         const int c = lane + 64 * t;
-        const float dc = rec[c];
-        if (dc >= 0.0f) {
-            const int cx = c % kCellG, cy = c / kCellG;
-            const float lx = x0 + cx * hx - eps, ux = x0 + (cx + 1) * hx + eps;
-            const float ly = y0 + cy * hy - eps, uy = y0 + (cy + 1) * hy + eps;
-            const float ex = fmaxf(fmaxf(lx - q.x, q.x - ux), 0.0f);
-            const float ey = fmaxf(fmaxf(ly - q.y, q.y - uy), 0.0f);
-            const float dist = sqrtf(ex * ex + ey * ey) * kDown;
-            L = fminf(L, (fmaxf(dist, rq) - dc * kUp) * kDown);
-        }
+        const float dc = dcs[t];
+        const int cx = c % kCellG, cy = c / kCellG;
+        const float lx = x0 + cx * hx - eps, ux = x0 + (cx + 1) * hx + eps;
+        const float ly = y0 + cy * hy - eps, uy = y0 + (cy + 1) * hy + eps;
+        const float ex = fmaxf(fmaxf(lx - q.x, q.x - ux), 0.0f);
+        const float ey = fmaxf(fmaxf(ly - q.y, q.y - uy), 0.0f);
+        const float dist = sqrtf(ex * ex + ey * ey) * kDown;
+        const float bound = (fmaxf(dist, rq) - dc * kUp) * kDown;
+        L = dc >= 0.0f ? fminf(L, bound) : L;
     }
     return -wave_max(-L);
 }
