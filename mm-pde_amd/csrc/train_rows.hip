@@ -56,9 +56,8 @@ __global__ __launch_bounds__(256) void rows_grad_partial_kernel(RowsGradArgs p) 
     float acc[KB + 1];
 #pragma unroll
     for (int c = 0; c <= KB; ++c) acc[c] = 0.0f;
-    constexpr int RU = KB > 16 ? 1 : 2;  // rows per unrolled step (KB = 64: a row is 64 registers)
     if (rg < RG) {
-#pragma unroll RU
+#pragma unroll 2
         for (int64_t r = r0 + rg; r < r1; r += RG) {
             const float g = p.dy[r * p.ldy + n];
             const float *xr = p.x + r * p.ldx;
@@ -66,6 +65,26 @@ __global__ __launch_bounds__(256) void rows_grad_partial_kernel(RowsGradArgs p) 
             // row's last ones and are dropped): a load under the c < k test is
             // waited for where the test ends, one round trip per column group
             float xv[KB > 0 ? KB : 1];
+            if (KB > 16) {  // KB = 64: column groups as loaded (a whole row in
+                            // registers costs occupancy, profiles/r05_loads_ab.log)
+                if (VEC) {
+#pragma unroll
+                    for (int c = 0; c < KB; c += 4)
+                        if (c < k) {
+                            const float4 v = *(const float4 *)(xr + c);
+                            acc[c] = fmaf(g, v.x, acc[c]);
+                            acc[c + 1] = fmaf(g, v.y, acc[c + 1]);
+                            acc[c + 2] = fmaf(g, v.z, acc[c + 2]);
+                            acc[c + 3] = fmaf(g, v.w, acc[c + 3]);
+                        }
+                } else {
+#pragma unroll
+                    for (int c = 0; c < KB; ++c)
+                        if (c < k) acc[c] = fmaf(g, xr[c], acc[c]);
+                }
+                acc[KB] += g;
+                continue;
+            }
             if (VEC) {  // 16-byte row loads (k, ldx multiples of 4, x aligned)
 #pragma unroll
                 for (int c = 0; c < KB; c += 4) {
