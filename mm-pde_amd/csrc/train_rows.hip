@@ -135,6 +135,89 @@ __global__ __launch_bounds__(256) void rows_grad_partial_kernel(RowsGradArgs p) 
     }
 }
 
+// The same partials for narrow outputs (n_out <= 8) over 16-byte rows (k a
+// multiple of 4, k <= 64, ldx a multiple of 4, x aligned): lanes across the
+// row instead of across the outputs.  Lane (rr, cq) of a wave, cq < Q = k / 4,
+// rr < R = 64 / Q, takes columns 4 cq .. 4 cq + 3 of the rows r0 + 4 R s + R w +
+// rr (s = 0, 1, ...; w the wave): one float4 of x per row -- the wave's R rows
+// are one contiguous run when ldx = k -- and the row's NOUT dy values (a
+// broadcast within the row's lanes); it keeps 4 x NOUT weight sums (+ NOUT bias
+// sums, counted from the cq = 0 lanes).  Four rows per lane are loaded at once,
+// unconditionally (rows past the range re-read the last one and are masked).
+// The lanes' sums then meet in LDS and each output adds its (w, rr) lanes in
+// that order: fixed order, deterministic.  (rows_grad_partial_kernel puts one
+// output row per thread, so the threads of a row all read the whole row: 8 x
+// the L1 requests at n_out = 8, and at n_out = 1 a wave's lanes in 64 rows.)
+template <int NOUT>
+__global__ __launch_bounds__(256) void rows_grad_cols_kernel(RowsGradArgs p) {
+    constexpr int NV = 4 * NOUT + NOUT;  // sums per lane
+    __shared__ float red[256 * NV];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int k = p.k, Q = k >> 2, R = 64 / Q;
+    const int rr = lane / Q, cq = lane - rr * Q;
+    const int64_t r0 = (int64_t)blockIdx.x * p.rows_per;
+    const int64_t r1 = std::min(p.rows, r0 + p.rows_per);
+    float acc[4][NOUT], bacc[NOUT];
+#pragma unroll
+    for (int n = 0; n < NOUT; ++n) {
+        bacc[n] = 0.0f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[c][n] = 0.0f;
+    }
+    if (rr < R) {
+        const int64_t step = 4 * (int64_t)R;
+        for (int64_t rb = r0 + (int64_t)R * wave + rr; rb < r1; rb += 4 * step) {
+            float4 xv[4];
+            float gv[4][NOUT];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int64_t r = std::min(rb + u * step, r1 - 1);
+                xv[u] = *(const float4 *)(p.x + r * p.ldx + 4 * cq);
+                const float *dr = p.dy + r * p.ldy;
+#pragma unroll
+                for (int n = 0; n < NOUT; ++n) gv[u][n] = dr[n];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                int m = rb + u * step < r1 ? -1 : 0;
+                asm volatile("" : "+v"(m));
+                const float xs[4] = {xv[u].x, xv[u].y, xv[u].z, xv[u].w};
+#pragma unroll
+                for (int n = 0; n < NOUT; ++n) {
+                    const float g = __int_as_float(__float_as_int(gv[u][n]) & m);
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) acc[c][n] = fmaf(g, xs[c], acc[c][n]);
+                    bacc[n] += g;
+                }
+            }
+        }
+    }
+    float *rl = red + tid * NV;
+#pragma unroll
+    for (int n = 0; n < NOUT; ++n) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) rl[c * NOUT + n] = acc[c][n];
+        rl[4 * NOUT + n] = bacc[n];
+    }
+    __syncthreads();
+    float *pp = p.part + (int64_t)blockIdx.x * p.outs;
+    for (int o = tid; o < p.outs; o += 256) {
+        int l0, slot;  // lane (cq) and sum index of output o
+        if (o < k * NOUT) {
+            const int n = o / k, c = o - n * k;
+            l0 = c >> 2;
+            slot = (c & 3) * NOUT + n;
+        } else {
+            l0 = 0;
+            slot = 4 * NOUT + (o - k * NOUT);
+        }
+        float v = 0.0f;
+        for (int w = 0; w < 4; ++w)
+            for (int q = 0; q < R; ++q) v += red[(w * 64 + q * Q + l0) * NV + slot];
+        pp[o] = v;
+    }
+}
+
 // out[o] = sum_g part[g][o]: one wave per output, lane l summing g = l, l + 64,
 // ... in order, then a fixed butterfly.
 __global__ __launch_bounds__(256) void wave_partial_sum_kernel(const float *__restrict__ part, int G, int outs,
@@ -408,9 +491,22 @@ static int64_t rows_grad_blocks(int64_t rows, int n_out) {
     return std::max<int64_t>(1, std::min<int64_t>((int64_t)4 * device_cus(), (rows + per_block - 1) / per_block));
 }
 
+// rows_grad_cols_kernel's shapes (the 16-byte row alignment is checked at launch)
+static bool rows_grad_cols_shape(int k, int n_out) {
+    return k >= 16 && k <= KMAX && k % 4 == 0 && (n_out == 1 || n_out == 2 || n_out == 4 || n_out == 8);
+}
+
+// its workgroups: at least two unrolled passes (8 rows per lane) each
+static int64_t rows_grad_cols_blocks(int64_t rows, int k) {
+    const int64_t per_block = 32 * (int64_t)(64 / (k / 4));
+    return std::max<int64_t>(1, std::min<int64_t>((int64_t)4 * device_cus(), (rows + per_block - 1) / per_block));
+}
+
 extern "C" int64_t mmpde_rows_grad_weight_workspace_bytes(int64_t rows, int k, int n_out) {
     if (rows <= 0 || k < 0 || n_out <= 0 || n_out > 256) return 0;
-    return rows_grad_blocks(rows, n_out) * (int64_t)(k * n_out + n_out) * 4;
+    int64_t G = rows_grad_blocks(rows, n_out);
+    if (rows_grad_cols_shape(k, n_out)) G = std::max(G, rows_grad_cols_blocks(rows, k));
+    return G * (int64_t)(k * n_out + n_out) * 4;
 }
 
 extern "C" int mmpde_rows_grad_weight(const float *x, int64_t ldx, int64_t rows, int k, const float *dy, int64_t ldy,
@@ -422,13 +518,19 @@ extern "C" int mmpde_rows_grad_weight(const float *x, int64_t ldx, int64_t rows,
     const int outs = k * n_out + (db ? n_out : 0);
     MMPDE_REQUIRE(outs <= 1280);
     MMPDE_REQUIRE(workspace && workspace_bytes >= mmpde_rows_grad_weight_workspace_bytes(rows, k, n_out));
-    const int64_t G0 = rows_grad_blocks(rows, n_out);
+    const bool vec = k % 4 == 0 && ldx % 4 == 0 && ((uintptr_t)x & 15) == 0;
+    const bool cols = vec && rows_grad_cols_shape(k, n_out);
+    const int64_t G0 = cols ? rows_grad_cols_blocks(rows, k) : rows_grad_blocks(rows, n_out);
     const int64_t per = (rows + G0 - 1) / G0, G = (rows + per - 1) / per;
     RowsGradArgs p{x, ldx, rows, k, dy, ldy, n_out, outs, db != nullptr, per, workspace};
     hipStream_t st = as_stream(stream);
-    const bool vec = k % 4 == 0 && ldx % 4 == 0 && ((uintptr_t)x & 15) == 0;
     auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, dim3((unsigned)G), dim3(256), 0, st, p); };
-    if (k == 0)
+    if (cols) {
+        if (n_out == 1) launch(rows_grad_cols_kernel<1>);
+        else if (n_out == 2) launch(rows_grad_cols_kernel<2>);
+        else if (n_out == 4) launch(rows_grad_cols_kernel<4>);
+        else launch(rows_grad_cols_kernel<8>);
+    } else if (k == 0)
         launch(rows_grad_partial_kernel<0, false>);
     else if (k <= 4)
         vec ? launch(rows_grad_partial_kernel<4, true>) : launch(rows_grad_partial_kernel<4, false>);

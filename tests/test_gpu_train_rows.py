@@ -32,6 +32,9 @@ def _close(got, ref, rtol, what):
     (40336, 4, 128, True, 4),           # embedding Linear(4, 128)
     (9999, 5, 100, False, 7),           # strided rows, no bias, ragged last tile
     (50000, 0, 128, True, 0),           # bias only (the node GEMMs' db)
+    (7, 16, 8, True, 16),               # column-lane kernel: fewer rows than one pass
+    (100003, 32, 2, False, 36),         # column-lane kernel: strided 16-byte rows, ragged
+    (70001, 64, 4, True, 64),           # column-lane kernel: k = 64
 ])
 def test_rows_grad_weight_vs_fp64(dev, rows, k, nout, bias, ldx):
     from mmpde_amd import ops
