@@ -359,9 +359,9 @@ __device__ __forceinline__ float2 ld2(const float *p, bool vec) {
 }
 
 template <bool GMASK, bool VEC, bool XS>
-__global__ __launch_bounds__(256, 2) void rgemm_tn_partial_kernel(TnArgs t) {
+__global__ __launch_bounds__(256, GMASK && XS ? 2 : 3) void rgemm_tn_partial_kernel(TnArgs t) {
     constexpr int NRED = 64 + 2 + 8;  // per lane: the block (4 tiles x 16), db (2), small segment (2 x 4)
-    __shared__ float red[3][NRED][64];
+    __shared__ float red[NRED][64];
     const mmpde_rgemm_tn_args &g = t.g;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int par = lane >> 5, j = lane & 31;
@@ -499,42 +499,46 @@ __global__ __launch_bounds__(256, 2) void rgemm_tn_partial_kernel(TnArgs t) {
             for (int e = 0; e < 4; ++e) sx[ct][e] += __shfl_xor(sx[ct][e], 32, 64);
         }
     }
-    if (wave > 0) {
-        float(*rw)[64] = red[wave - 1];
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-            for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) rw[(2 * ct + kt) * 16 + r][lane] = acc[ct][kt][r];
-        if (first) {
-#pragma unroll
-            for (int ct = 0; ct < 2; ++ct) {
-                rw[64 + ct][lane] = sb[ct];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) rw[66 + 4 * ct + e][lane] = sx[ct][e];
-            }
-        }
-    }
-    __syncthreads();
-    if (wave != 0) return;
+    // one LDS block, filled by waves 1, 2, 3 in turn (19 KB instead of 57: LDS
+    // no longer caps the workgroups per CU), wave 0 adding each as it lands
 #pragma unroll 1
-    for (int w = 0; w < 3; ++w) {
+    for (int w = 1; w < 4; ++w) {
+        if (wave == w) {
 #pragma unroll
-        for (int ct = 0; ct < 2; ++ct)
+            for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
-            for (int kt = 0; kt < 2; ++kt)
+                for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) acc[ct][kt][r] += red[w][(2 * ct + kt) * 16 + r][lane];
-        if (first) {
+                    for (int r = 0; r < 16; ++r) red[(2 * ct + kt) * 16 + r][lane] = acc[ct][kt][r];
+            if (first) {
 #pragma unroll
-            for (int ct = 0; ct < 2; ++ct) {
-                sb[ct] += red[w][64 + ct][lane];
+                for (int ct = 0; ct < 2; ++ct) {
+                    red[64 + ct][lane] = sb[ct];
 #pragma unroll
-                for (int e = 0; e < 4; ++e) sx[ct][e] += red[w][66 + 4 * ct + e][lane];
+                    for (int e = 0; e < 4; ++e) red[66 + 4 * ct + e][lane] = sx[ct][e];
+                }
             }
         }
+        __syncthreads();
+        if (wave == 0) {
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+                for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) acc[ct][kt][r] += red[(2 * ct + kt) * 16 + r][lane];
+            if (first) {
+#pragma unroll
+                for (int ct = 0; ct < 2; ++ct) {
+                    sb[ct] += red[64 + ct][lane];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) sx[ct][e] += red[66 + 4 * ct + e][lane];
+                }
+            }
+        }
+        __syncthreads();
     }
+    if (wave != 0) return;
     if (cb >= gcols) return;
     float *pp = t.part + (int64_t)chunk * 128 * t.cols;
 #pragma unroll

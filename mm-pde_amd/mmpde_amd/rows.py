@@ -17,13 +17,16 @@ Exact fp32 products, fixed summation orders: deterministic.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
 from . import _lib as L
 
 _F4 = 4  # bytes per float
-CHUNK_ROWS = 256  # rows per weight-gradient partial (fixed: deterministic sums)
+# rows per weight-gradient partial (fixed: deterministic sums); MMPDE_TN_CHUNK
+# (an even row count) overrides it for A/B runs (tools/rgemm_bench.py)
+CHUNK_ROWS = int(os.environ.get("MMPDE_TN_CHUNK", "256"))
 
 
 def _p(t: torch.Tensor | None, col: int = 0) -> int | None:
