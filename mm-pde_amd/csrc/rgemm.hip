@@ -174,7 +174,7 @@ __global__ __launch_bounds__(256, 2) void rgemm_kernel(mmpde_rgemm_args g) {
 // next tile loaded into registers under the current tile's kh MFMAs and
 // stored to the other LDS buffer; one barrier per tile.
 template <int LAYOUT, int KH, bool AMASK, bool XS>
-__global__ __launch_bounds__(256, 1) void rgemm_ws_kernel(mmpde_rgemm_args g) {
+__global__ __launch_bounds__(256, KH == 128 ? 1 : 2) void rgemm_ws_kernel(mmpde_rgemm_args g) {
     constexpr int PITCH = 2 * KH + 4;        // floats per staged row (both halves)
     constexpr int NF4 = 32 * 2 * KH / 4;     // float4 pieces of a tile
     constexpr int PER = NF4 / 256;           // per thread
