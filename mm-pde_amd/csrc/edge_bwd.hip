@@ -666,7 +666,8 @@ __global__ __launch_bounds__(256) void transpose128_kernel(const float *__restri
 // odd ones, four columns per lane.  Rows go in batches of 32 (16 loads in
 // flight per lane, issued unconditionally: positions past the list re-read its
 // last row and are masked with an opaque all-ones / zero word, since a load
-// under a condition is waited for at once); each half adds its rows in list
+// under a condition is waited for at once; non-temporal loads, the rows are
+// read once); each half adds its rows in list
 // order, then the odd half's sum is added to the even half's.  Both forms add
 // the same values in the same order: bitwise-equal sums.
 template <bool GATHER>
@@ -688,7 +689,13 @@ __device__ __forceinline__ void source_sum(const float *__restrict__ rows, const
         }
         float4 v[16];
 #pragma unroll
-        for (int t = 0; t < 16; ++t) v[t] = ((const float4 *)(rows + src[t] * BH))[c4];
+        for (int t = 0; t < 16; ++t) {
+            // non-temporal: each row is read once (115 vs 162 us at cy B=16,
+            // profiles/r05_loads_ab.log)
+            typedef float nt4 __attribute__((ext_vector_type(4)));
+            const nt4 q = __builtin_nontemporal_load((const nt4 *)(rows + src[t] * BH) + c4);
+            v[t] = make_float4(q.x, q.y, q.z, q.w);
+        }
 #pragma unroll
         for (int t = 0; t < 16; ++t) {
             int m = qb + 2 * t + par < qe ? -1 : 0;
