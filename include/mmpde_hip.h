@@ -539,6 +539,30 @@ int mmpde_transpose(const float *x, int64_t rows, int64_t cols, int64_t ldx, flo
                     mmpde_stream_t stream);
 int mmpde_tanh_bwd(const float *dy, const float *t, int64_t n, float *dz, mmpde_stream_t stream);
 
+/* The Conv1d head in train mode (gnn_2d.py:108-114,136 at time_window 1:
+ * Conv1d(1, 4, 16, stride 3) -> ReLU -> Conv1d(4, 8, 12, stride 3) -> ReLU ->
+ * Conv1d(8, 1, 8, stride 2) over each row of h [n, 128]; replaces the
+ * output_mlp forward and its backward under loss.backward(),
+ * train_helper_2d.py:126).  Weights in torch's layouts: w1 [4][1][16], b1 [4],
+ * w2 [8][4][12], b2 [8], w3 [1][8][8], b3 [1].  h rows 16-B aligned (ldh % 4
+ * == 0).
+ *   mmpde_head_train_forward: y[i] = output_mlp(h[i]) (one value per row).
+ *   mmpde_head_train_backward: from dy[i] = dL/dy[i]: dh[i][:] = dL/dh[i]
+ *     (written; rows lddh apart, 16-B aligned) and grads[0 ..
+ *     MMPDE_HEAD_TRAIN_GRADS) = [dW1 | db1 | dW2 | db2 | dW3 | db3] (torch
+ *     layouts, concatenated); per-row terms summed over 64-row groups by a
+ *     fixed butterfly, the groups in order: deterministic.  workspace >=
+ *     mmpde_head_train_workspace_bytes(n). */
+#define MMPDE_HEAD_TRAIN_GRADS 525
+int64_t mmpde_head_train_workspace_bytes(int64_t n);
+int mmpde_head_train_forward(const float *h, int64_t ldh, int64_t n, const float *w1, const float *b1,
+                             const float *w2, const float *b2, const float *w3, const float *b3, float *y,
+                             mmpde_stream_t stream);
+int mmpde_head_train_backward(const float *h, int64_t ldh, int64_t n, const float *w1, const float *b1,
+                              const float *w2, const float *b2, const float *w3, const float *b3,
+                              const float *dy, float *dh, int64_t lddh, float *grads, float *workspace,
+                              int64_t workspace_bytes, mmpde_stream_t stream);
+
 /* out[n] = out_scale * output_mlp(h[:, None]) */
 int mmpde_gnn_head(const float *h, int64_t n, const mmpde_gnn_head_params *p, float *out,
                    mmpde_stream_t stream);

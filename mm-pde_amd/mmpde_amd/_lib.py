@@ -153,6 +153,10 @@ _SIGS = {
     "mmpde_outer_rows": (_I, [_P, _I64, _P, _I64, _I, _I64, _I64, _P, _I64, _P, _P]),
     "mmpde_transpose": (_I, [_P, _I64, _I64, _I64, _P, _I64, _P]),
     "mmpde_tanh_bwd": (_I, [_P, _P, _I64, _P, _P]),
+    "mmpde_head_train_workspace_bytes": (_I64, [_I64]),
+    "mmpde_head_train_forward": (_I, [_P, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "mmpde_head_train_backward": (_I, [_P, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _I64,
+                                       _P]),
     "mmpde_gnn_workspace_bytes": (_I64, [_I64]),
     "mmpde_gnn_embed": (_I, [_P, _P, _I64, GnnScales, _P, _P, _P, _P]),
     "mmpde_gnn_layer": (_I, [_P, _P, _P, _I64, _I, _P, GnnScales, _P, _P, _P, _P]),

@@ -29,7 +29,8 @@ import torch
 from torch import nn
 
 from . import _lib as L
-from .ops import LinearRows, batch_norm_rows, linear_train, nbr_table_from_edge_index, reverse_adjacency
+from .ops import (HeadTrain, LinearRows, batch_norm_rows, head_train_fits, linear_train, nbr_table_from_edge_index,
+                  reverse_adjacency)
 
 
 class BatchNorm(nn.Module):
@@ -593,6 +594,10 @@ class MP_PDE_Solver_2D(nn.Module):  # noqa: N801 - reference name
         cost ~1 ms per training iteration and a multi-second search on first
         use)."""
         o = self.output_mlp
+        if head_train_fits(o, h):
+            # the whole head, forward and backward, in two HIP launches
+            c0, c2, c4 = o[0], o[2], o[4]
+            return HeadTrain.apply(h, c0.weight, c0.bias, c2.weight, c2.bias, c4.weight, c4.bias)
         n = h.shape[0]
         x = h
         y = None

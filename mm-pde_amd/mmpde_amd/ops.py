@@ -7,6 +7,8 @@ from __future__ import annotations
 
 import ctypes
 
+import os
+
 import torch
 
 from . import _lib as L
@@ -525,6 +527,73 @@ class LinearRows(torch.autograd.Function):
 def rows_grad_fits(k: int, nout: int) -> bool:
     """Shapes mmpde_rows_grad_weight takes with the weight gradient."""
     return 0 < k <= 64 and nout <= 128 and k * nout + nout <= 1280
+
+
+class HeadTrain(torch.autograd.Function):
+    """output_mlp(h[:, None]) of MP_PDE_Solver_2D at time_window 1 (gnn_2d.py:
+    108-114: Conv1d(1, 4, 16, 3) -> ReLU -> Conv1d(4, 8, 12, 3) -> ReLU ->
+    Conv1d(8, 1, 8, 2)) in train mode: y [n, 1] from h [n, 128] on
+    mmpde_head_train_forward, dL/dh and the six weight / bias gradients on
+    mmpde_head_train_backward (one lane per node, fixed summation orders)."""
+
+    @staticmethod
+    def forward(ctx, h, w1, b1, w2, b2, w3, b3):
+        L.require_device(h, w1, b1, w2, b2, w3, b3)
+        h = L.f32c(h)
+        ws = [L.f32c(t) for t in (w1, b1, w2, b2, w3, b3)]
+        n = h.shape[0]
+        y = torch.empty((n, 1), dtype=torch.float32, device=h.device)
+        L.check(L.lib().mmpde_head_train_forward(L.ptr(h), h.stride(0), n, *[L.ptr(t) for t in ws], L.ptr(y),
+                                                 L.stream(h.device)), "mmpde_head_train_forward")
+        ctx.save_for_backward(h, *ws)
+        ctx.shapes = [tuple(t.shape) for t in (w1, b1, w2, b2, w3, b3)]
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        h, *ws = ctx.saved_tensors
+        dy = L.f32c(dy)
+        n = h.shape[0]
+        dev = h.device
+        dh = torch.empty_like(h)
+        grads = torch.empty((HEAD_TRAIN_GRADS,), dtype=torch.float32, device=dev)
+        nb = L.lib().mmpde_head_train_workspace_bytes(n)
+        wk = torch.empty((nb // 4,), dtype=torch.float32, device=dev)
+        L.check(L.lib().mmpde_head_train_backward(L.ptr(h), h.stride(0), n, *[L.ptr(t) for t in ws], L.ptr(dy),
+                                                  L.ptr(dh), dh.stride(0), L.ptr(grads), L.ptr(wk), nb,
+                                                  L.stream(dev)), "mmpde_head_train_backward")
+        out, o = [], 0
+        for shp in ctx.shapes:
+            k = 1
+            for d in shp:
+                k *= d
+            out.append(grads[o:o + k].view(shp))
+            o += k
+        gh = dh if ctx.needs_input_grad[0] else None
+        return (gh, *[g if ctx.needs_input_grad[1 + j] else None for j, g in enumerate(out)])
+
+
+HEAD_TRAIN_GRADS = 525  # include/mmpde_hip.h MMPDE_HEAD_TRAIN_GRADS
+
+
+def head_train_fits(output_mlp, h: torch.Tensor) -> bool:
+    """The Conv1d head HeadTrain implements (gnn_2d.py:108-114 at time_window 1).
+    MMPDE_HEAD_FUSED=0 keeps the unfold + LinearRows form (A/B runs)."""
+    if os.environ.get("MMPDE_HEAD_FUSED", "1") == "0":
+        return False
+    try:
+        convs = [output_mlp[i] for i in (0, 2, 4)]
+    except (IndexError, TypeError):
+        return False
+    if len(output_mlp) != 5 or not all(isinstance(c, torch.nn.Conv1d) for c in convs):
+        return False
+    want = [((4, 1, 16), 3), ((8, 4, 12), 3), ((1, 8, 8), 2)]
+    for c, (shape, st) in zip(convs, want):
+        if (tuple(c.weight.shape) != shape or c.stride[0] != st or c.padding[0] != 0 or c.dilation[0] != 1
+                or c.groups != 1 or c.bias is None or c.padding_mode != "zeros"):
+            return False
+    return (isinstance(output_mlp[1], torch.nn.ReLU) and isinstance(output_mlp[3], torch.nn.ReLU)
+            and h.dim() == 2 and h.shape[1] == 128 and h.is_cuda and h.dtype == torch.float32)
 
 
 def rows_grad_weight(x: torch.Tensor, dy: torch.Tensor, k: int, bias: bool):

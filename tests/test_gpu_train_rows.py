@@ -272,3 +272,43 @@ def test_edge_backward_sorted_equals_gather_path(dev, edge_gemm, ragged):
     torch.cuda.synchronize()
     for x, y in zip(*outs):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("n", [5, 1000, 40336])
+def test_head_train_vs_fp64(dev, n):
+    """ops.HeadTrain (the Conv1d head, gnn_2d.py:108-114, forward and backward
+    on mmpde_head_train_*) against float64 autograd of the same nn.Sequential:
+    y and dL/dh within 2e-5 of max|ref|, the six weight / bias gradients
+    (sums over n nodes) within 5e-5; a second backward gives the same bits."""
+    from mmpde_amd import ops
+
+    torch.manual_seed(n)
+    mlp = torch.nn.Sequential(torch.nn.Conv1d(1, 4, 16, stride=3), torch.nn.ReLU(),
+                              torch.nn.Conv1d(4, 8, 12, stride=3), torch.nn.ReLU(),
+                              torch.nn.Conv1d(8, 1, 8, stride=2))
+    h = torch.randn(n, 128)
+    gy = torch.randn(n, 1)
+    ref = mlp.double()
+    hr = h.double().requires_grad_(True)
+    yr = ref(hr[:, None]).squeeze(1)
+    yr.backward(gy.double())
+    mlp_d = mlp.float().to(dev)
+    assert ops.head_train_fits(mlp_d, h.to(dev))
+
+    def run():
+        hd = h.to(dev).requires_grad_(True)
+        for p in mlp_d.parameters():
+            p.grad = None
+        y = ops.HeadTrain.apply(hd, mlp_d[0].weight, mlp_d[0].bias, mlp_d[2].weight, mlp_d[2].bias,
+                                mlp_d[4].weight, mlp_d[4].bias)
+        y.backward(gy.to(dev))
+        torch.cuda.synchronize()
+        return y, hd.grad, [p.grad.clone() for p in mlp_d.parameters()]
+
+    y, gh, gp = run()
+    _close(y, yr, 2e-5, f"head y n={n}")
+    _close(gh, hr.grad, 2e-5, f"head dL/dh n={n}")
+    for name, g, r in zip(("w1", "b1", "w2", "b2", "w3", "b3"), gp, [p.grad for p in ref.parameters()]):
+        _close(g, r, 5e-5, f"head d{name} n={n}")
+    y2, gh2, gp2 = run()
+    assert torch.equal(y, y2) and torch.equal(gh, gh2) and all(torch.equal(a, b) for a, b in zip(gp, gp2))
