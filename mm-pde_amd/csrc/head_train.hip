@@ -132,22 +132,27 @@ __device__ __forceinline__ void put(float *__restrict__ pp, int o, float v) {
     if (__lane_id() == 0) pp[o] = v;
 }
 
-constexpr int RN = 32, RP = RN + 1;  // terms per transpose, its row pitch (conflict-free both ways)
+constexpr int RN = 32, RP = 64 + 4;  // terms per transpose; its column pitch (16-B aligned)
 
 // N <= RN per-node terms v[] of every lane summed over the wave's 64 lanes in
-// lane order (through LDS: lane l's terms in row l, lane t adding column t)
-// and stored as partials o0 .. o0 + N - 1.  The workgroup is this one wave.
+// lane order (through LDS: term t of lane l at red[t][l]; lane t reads its 64
+// values as 16-byte vectors and adds them in lane order) and stored as partials
+// o0 .. o0 + N - 1.  The workgroup is this one wave.
 template <int N>
 __device__ __forceinline__ void flush(float *red, float *__restrict__ pp, int o0, const float *v) {
     static_assert(N <= RN, "transpose width");
     const int lane = __lane_id();
 #pragma unroll
-    for (int t = 0; t < N; ++t) red[lane * RP + t] = v[t];
+    for (int t = 0; t < N; ++t) red[t * RP + lane] = v[t];
     __syncthreads();
     if (lane < N) {
+        const float4 *col = (const float4 *)(red + lane * RP);
+        float4 q[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) q[k] = col[k];
         float s = 0.0f;
-#pragma unroll 8
-        for (int l = 0; l < 64; ++l) s += red[l * RP + lane];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) s = (((s + q[k].x) + q[k].y) + q[k].z) + q[k].w;
         pp[o0 + lane] = s;
     }
     __syncthreads();  // the buffer is free again
@@ -162,7 +167,7 @@ __global__ __launch_bounds__(64) void head_train_bwd_kernel(
     // them, so their wave-uniform loads stay scalar after the partial stores
     const HeadW w{w1, b1, w2, b2, w3, b3};
     __shared__ float ys[L1 * C1 * 64];  // y1, then dL/dz1, lane-minor (conflict-free)
-    __shared__ float red[64 * RP];      // the gradient terms' transposes
+    __shared__ float red[RN * RP];      // the gradient terms' transposes
     const int lane = threadIdx.x;
     const int64_t i0 = (int64_t)blockIdx.x * 64 + lane;
     const bool live = i0 < n;
