@@ -314,13 +314,18 @@ int mmpde_gnn_edge_mean_deg(const float *a, const float *b, const int32_t *nbr, 
 /* mmpde_gnn_edge_mean_deg in a chosen arithmetic: edge_gemm
  * MMPDE_EDGE_GEMM_F32 is mmpde_gnn_edge_mean_deg; MMPDE_EDGE_GEMM_F16X3 runs
  * message_net_2 in the fp16x3 split (the eval path's arithmetic), packing
- * W2 and the split scale (max|a| + max|b| over all n rows) into workspace
- * (>= mmpde_gnn_edge_mean_workspace_bytes(n, edge_gemm) bytes, 16-B aligned)
- * on every call: the forward of the f16x3 training path, whose weights
- * change every iteration.  relu_mask (nullable, 16-B aligned; F32 or F16X3):
+ * W2 and the row maxima of a, b (each target row i is split with a scale of
+ * its own, from max|a_i| + max over its neighbours of max|b_j|) into
+ * workspace (>= mmpde_gnn_edge_mean_workspace_bytes(n, edge_gemm) bytes, 16-B
+ * aligned) on every call: the f16x3 per-layer path, whose weights change
+ * every iteration.  relu_mask (nullable, 16-B aligned; F32 or F16X3):
  * [n * k][4] uint32, bit c % 32 of word c / 32 of slot q = i*k + e set where
  * message_net_2's pre-activation z2[c] > 0 for that edge -- the ReLU pattern
- * mmpde_gnn_edge_backward_sorted then reuses instead of recomputing z2. */
+ * mmpde_gnn_edge_backward_sorted then reuses instead of recomputing z2 (the
+ * training forward: the persistent ring kernel).  F16X3 without relu_mask
+ * (no backward to feed: eval / no-grad) runs the inference forward's
+ * one-wave-per-SIMD kernel over one segment of n rows, then adds its side
+ * blocks and divides. */
 int64_t mmpde_gnn_edge_mean_workspace_bytes(int64_t n, int edge_gemm);
 int mmpde_gnn_edge_mean_ex(const float *a, const float *b, const int32_t *nbr, const int32_t *deg,
                            int64_t n, int k, const float *msg2_w, const float *msg2_b, float *mean_out,
@@ -529,7 +534,8 @@ int mmpde_rows_small(const float *x, int64_t ldx, int64_t n, int ki, const float
 /* Training backward of the few-row linears (res_cut's MLP, interpolate.py:
  * 54-60,95-97, M = B rows; reference loss.backward(), train_helper_2d.py:126):
  *   mmpde_outer_rows: dw[i][j] = sum_{r<m} g[r][i] x[r][j], db[i] = sum_r
- *     g[r][i] (db nullable; r ascending; m <= 32): the weight / bias gradient;
+ *     g[r][i] (db nullable; r ascending, any m: rows staged 32 at a time): the
+ *     weight / bias gradient;
  *   mmpde_transpose: y[c][r] = x[r][c] (rows x cols; W^T for dX = dY W through
  *     mmpde_linear_skinny);
  *   mmpde_tanh_bwd: dz[i] = dy[i] (1 - t[i]^2) (t = the forward's tanh output). */

@@ -351,31 +351,37 @@ __global__ __launch_bounds__(256) void traj_mse_kernel(const float *__restrict__
 //   transpose: y[c][r] = x[r][c] through 32 x 33 LDS tiles (dX = dY W as the
 //     skinny forward of W^T).
 //   tanh_bwd: dz = dy (1 - t^2) (torch's tanh_backward).
-constexpr int kOrMaxM = 32;
+constexpr int kOrRows = 32;  // rows staged per pass (any m: passes in row order)
 __global__ __launch_bounds__(256) void outer_rows_kernel(const float *__restrict__ g, int64_t ldg,
                                                          const float *__restrict__ x, int64_t ldx, int m,
                                                          int64_t n, int64_t k, float *__restrict__ dw,
                                                          int64_t lddw, float *__restrict__ db) {
-    __shared__ float sg[kOrMaxM][16], sx[kOrMaxM][64];
+    __shared__ float sg[kOrRows][16], sx[kOrRows][64];
     const int tid = threadIdx.x;
     const int64_t i0 = (int64_t)blockIdx.y * 16, j0 = (int64_t)blockIdx.x * 64;
-    for (int e = tid; e < m * 64; e += 256) {
-        const int r = e >> 6, c = e & 63;
-        sx[r][c] = x[r * ldx + min(j0 + c, k - 1)];
-        if (c < 16) sg[r][c] = g[r * ldg + min(i0 + c, n - 1)];
-    }
-    __syncthreads();
     const int il = tid >> 4, jl = 4 * (tid & 15);
     float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     float sb = 0.0f;
-    for (int r = 0; r < m; ++r) {
-        const float gv = sg[r][il];
-        const float4 xv = *(const float4 *)&sx[r][jl];
-        acc.x = fmaf(gv, xv.x, acc.x);
-        acc.y = fmaf(gv, xv.y, acc.y);
-        acc.z = fmaf(gv, xv.z, acc.z);
-        acc.w = fmaf(gv, xv.w, acc.w);
-        sb += gv;
+    // rows r0 .. r0 + 31 per pass, r ascending over the passes: one fixed order
+    for (int r0 = 0; r0 < m; r0 += kOrRows) {
+        const int mr = min(kOrRows, m - r0);
+        if (r0 > 0) __syncthreads();  // the previous pass has read the tiles
+        for (int e = tid; e < mr * 64; e += 256) {
+            const int r = e >> 6, c = e & 63;
+            const int64_t row = r0 + r;
+            sx[r][c] = x[row * ldx + min(j0 + c, k - 1)];
+            if (c < 16) sg[r][c] = g[row * ldg + min(i0 + c, n - 1)];
+        }
+        __syncthreads();
+        for (int r = 0; r < mr; ++r) {
+            const float gv = sg[r][il];
+            const float4 xv = *(const float4 *)&sx[r][jl];
+            acc.x = fmaf(gv, xv.x, acc.x);
+            acc.y = fmaf(gv, xv.y, acc.y);
+            acc.z = fmaf(gv, xv.z, acc.z);
+            acc.w = fmaf(gv, xv.w, acc.w);
+            sb += gv;
+        }
     }
     const int64_t i = i0 + il, j = j0 + jl;
     if (i >= n) return;
@@ -415,7 +421,7 @@ __global__ __launch_bounds__(256) void tanh_bwd_kernel(const float *__restrict__
 
 extern "C" int mmpde_outer_rows(const float *g, int64_t ldg, const float *x, int64_t ldx, int m, int64_t n,
                                 int64_t k, float *dw, int64_t lddw, float *db, mmpde_stream_t stream) {
-    MMPDE_REQUIRE(g && x && dw && m >= 1 && m <= kOrMaxM && n >= 1 && k >= 1);
+    MMPDE_REQUIRE(g && x && dw && m >= 1 && n >= 1 && k >= 1);
     MMPDE_REQUIRE(ldg >= n && ldx >= k && lddw >= k && n < ((int64_t)1 << 31) && k < ((int64_t)1 << 31));
     const dim3 grid((unsigned)((k + 63) / 64), (unsigned)((n + 15) / 16));
     hipLaunchKernelGGL(outer_rows_kernel, grid, dim3(256), 0, as_stream(stream), g, ldg, x, ldx, m, n, k, dw,
@@ -442,7 +448,7 @@ extern "C" int mmpde_tanh_bwd(const float *dy, const float *t, int64_t n, float 
     return MMPDE_OK;
 }
 
-extern "C" int mmpde_version(void) { return 12000; }
+extern "C" int mmpde_version(void) { return 12100; }
 
 extern "C" int mmpde_traj_mse(const float *pred, const float *labels, int64_t batches, int64_t n_per,
                               float *out, mmpde_stream_t stream) {

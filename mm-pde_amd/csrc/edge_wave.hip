@@ -28,10 +28,13 @@
 // Physical waves: the wpsp waves of segment s (XCD-contiguous ranks s * wpsp
 // + j) split its U units as evenly as whole units allow, wave j taking units
 // [j U / wpsp, (j + 1) U / wpsp).  A wave never leaves its segment, so its
-// split scale comes from its segment's range records alone, and U is a
-// function of the segment alone (layer.hpp edge_wave_plan): a trajectory's
-// result does not depend on how many trajectories are launched beside it
-// (any per-rank shard of a batch sums every row in the same order).
+// U is a function of the segment alone (layer.hpp edge_wave_plan): a
+// trajectory's result does not depend on how many trajectories are launched
+// beside it (any per-rank shard of a batch sums every row in the same order).
+// Split scales: one per target row (layer.hpp row maxima), computed in the
+// prologue for every row of the wave's tiles from the node stage's row maxima
+// and the row's neighbour list, and kept in LDS: a row's scale depends on the
+// row and its neighbours only.
 // Deterministic: fixed summation order, no atomics.
 #include "common.hpp"
 #include "f16x3.hpp"
@@ -68,7 +71,7 @@ struct WaveArgs {
     int wpsp;                 // waves per segment (<= U)
     const float *b2;          // message_net_2.0 bias
     const char *pk;           // this layer's packed images (W2 at kPkW2)
-    const float *rng;         // range records of a, b (layer.hpp)
+    const float *rmx;         // row maxima of a, b (layer.hpp)
     float *out;               // neighbour sums of the units that start a tile
     float *side;              // [G][16][128]: the unit a wave starts inside a tile
 };
@@ -145,11 +148,44 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
     // destination of the run being computed: -1 = out (it starts its tile),
     // else the side block of the unit it starts
     int run_side = s0 % k ? seg * p.U + u_begin : -1;
-    // |a + b| <= max|a| + max|b| over the segment, scaled below 2^11 (split8_relu_rtz)
-    const float sc = 0.125f * split_scale(segment_range(p.rng, p.seg_n, seg));
-    // message_net_2: B operands (AGPRs), accumulator start (bias, scaled), unscale
+    // Split scales of the rows of this wave's tiles (at most kWaveTiles,
+    // edge_wave_plan): lane (g, r) takes row r of tile tb + g, its neighbours'
+    // row maxima, |a_i + b_j| <= max|a_i| + max_e max|b_j| scaled below 2^11
+    // (split8_relu_rtz).  The first four tiles (every wave of the cylinder and
+    // Burgers plans): the index loads go out before the W2 image, the gathers
+    // all together right after it, so the two round trips overlap the image.
+    constexpr int KU = 36;  // neighbour slots loaded unrolled (more: one by one)
+    __shared__ float rs_lds[kWaveTiles * ET];
+    const int t_first = (int)(s0 / k), t_last = min((int)((s1 - 1) / k), p.tps - 1);
+    const uint32_t *rmxb = (const uint32_t *)p.rmx;
+    const uint32_t nmaxu = (uint32_t)nmax;
+    auto pass_row = [&](int tb) { return base + min(min(tb + g, t_last) * ET + r, last); };
+    auto pass_kk = [&](int64_t row) { return RAGGED ? max(min(p.deg[row], k), 1) : k; };
+    auto pass_idx = [&](int64_t row, int kk, uint32_t *id) {
+#pragma unroll
+        for (int e = 0; e < KU; ++e) id[e] = (uint32_t)p.nbr[row * k + min(e, kk - 1)];
+    };
+    auto pass_scale = [&](int tb, int64_t row, int kk, const uint32_t *id, float ma) {
+        uint32_t v[KU];
+#pragma unroll
+        for (int e = 0; e < KU; ++e) v[e] = rmxb[2 * (uint64_t)min(id[e], nmaxu) + 1];
+        uint32_t m = 0;
+#pragma unroll
+        for (int e = 0; e < KU; ++e) m = max(m, v[e]);
+        for (int e = KU; e < kk; ++e) m = max(m, rmxb[2 * (uint64_t)min((uint32_t)p.nbr[row * k + e], nmaxu) + 1]);
+        if (tb + g <= t_last) rs_lds[(tb + g - t_first) * ET + r] = row_split_scale(ma + __uint_as_float(m));
+    };
+    const int64_t row_p0 = pass_row(t_first);
+    const int kk_p0 = pass_kk(row_p0);
+    uint32_t id_p0[KU];
+    pass_idx(row_p0, kk_p0, id_p0);
+    const float ma_p0 = p.rmx[2 * row_p0];
+    __builtin_amdgcn_sched_barrier(0);  // these loads issue before the image's
+    // message_net_2: B operands (AGPRs), accumulator start (bias in the column
+    // scale, times the row scales of the MFMA slot's tile), column unscale
     half8 wh[8][4], wl[8][4];
-    float bias[8], inv[8];
+    float bb0[8], inv[8];
+    f32x4 bias[8];
     {
         const char *img = p.pk + kPkW2;
 #pragma unroll
@@ -160,10 +196,28 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
                 wl[c][s] = pin_agpr(bfrag(img, 4, c, s, 1, lane));
             }
             const float sw = ((const float *)(img + 65536))[16 * c + r];
-            bias[c] = p.b2[16 * c + r] * sw * sc;
-            inv[c] = pow2_inv(sw) * pow2_inv(sc);
+            bb0[c] = p.b2[16 * c + r] * sw;
+            inv[c] = pow2_inv(sw);
         }
     }
+    pass_scale(t_first, row_p0, kk_p0, id_p0, ma_p0);
+    for (int tb = t_first + 4; tb <= t_last; tb += 4) {  // waves spanning more than four tiles
+        const int64_t row = pass_row(tb);
+        const int kk = pass_kk(row);
+        uint32_t id[KU];
+        pass_idx(row, kk, id);
+        pass_scale(tb, row, kk, id, p.rmx[2 * row]);
+    }
+    __syncthreads();  // one wave: the LDS writes of every lane before any read
+    // LDS slot of a tile's row scales (tiles past the wave's last, which only a
+    // prefetch past the end touches, read the last one's)
+    auto rs_of = [&](int tile) { return &rs_lds[(min(tile, t_last) - t_first) * ET]; };
+    // the accumulator start of a tile's slots: rows 4 g + t of this lane
+    auto set_bias = [&](int tile) {
+        const float4 s4 = *(const float4 *)(rs_of(tile) + 4 * g);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) bias[c] = (f32x4){bb0[c] * s4.x, bb0[c] * s4.y, bb0[c] * s4.z, bb0[c] * s4.w};
+    };
     // F16X3 operand piece i of this lane: k = 32 (i >> 1) + 8 g + 4 (i & 1) .. + 3
     auto piece = [&](int i) { return 32 * (i >> 1) + 8 * g + 4 * (i & 1); };
     auto unit_tile = [&](const SlotCtr &c) { return min(c.tile, p.tps - 1); };
@@ -196,11 +250,13 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
     cI.next(k);
     cI.next(k);
     float4 av[8];  // a rows of the split slot's tile (scaled), this lane's pieces
+    float sc = 1.0f;  // split scale of this lane's row (r) of the split slot's tile
     auto load_a = [&](int tile) {
         const float *ar = p.a + grow(tile * ET + r) * LH;
         float4 v[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) v[i] = *(const float4 *)(ar + piece(i));
+        sc = rs_of(tile)[r];
 #pragma unroll
         for (int i = 0; i < 8; ++i) av[i] = make_float4(v[i].x * sc, v[i].y * sc, v[i].z * sc, v[i].w * sc);
     };
@@ -228,6 +284,7 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
     float4 bx[8];
     int atile = unit_tile(cC);
     load_a(atile);
+    set_bias(atile);
     if (RAGGED) load_deg(dg, cC);
     gather(bx, src_of(cC));
 #pragma unroll
@@ -252,11 +309,12 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
         if (RAGGED) v = e < d[t] ? v : 0.0f;
         Sc[t] += v;
     };
-    // the finished unit's sums, unscaled (a power-of-two multiply: exact), to out
-    // (rows of the tile) or to side[rank].  The node stage adds the side buffers
-    // and divides by the degree (PyG mean = sum / count).  Stores are
-    // unconditional unless the tile runs past the segment (wave-uniform test),
-    // at immediate offsets from one base per lane.  row0: local row.
+    // the finished unit's sums, unscaled (by the column and row scales: a
+    // power-of-two multiply, exact), to out (rows of the tile) or to
+    // side[rank].  The node stage adds the side buffers and divides by the
+    // degree (PyG mean = sum / count).  Stores are unconditional unless the
+    // tile runs past the segment (wave-uniform test), at immediate offsets from
+    // one base per lane.  row0: local row.
     auto write_unit = [&](int row0, int side_idx) {
         const bool to_side = side_idx >= 0;
         if (DIAG & 64) {  // no stores: keep the sums alive only
@@ -264,18 +322,20 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
             for (int c = 0; c < 8; ++c) asm volatile("" ::"v"(S[c]));
             return;
         }
+        const float4 s4 = *(const float4 *)(rs_of(row0 / ET) + 4 * g);
+        const float irs[4] = {pow2_inv(s4.x), pow2_inv(s4.y), pow2_inv(s4.z), pow2_inv(s4.w)};
         float *o = (to_side ? p.side + (int64_t)side_idx * ET * LH : p.out + (base + row0) * LH) + 4 * g * LH + r;
         if (to_side || row0 + ET <= last + 1) {
 #pragma unroll
             for (int c = 0; c < 8; ++c)
 #pragma unroll
-                for (int t = 0; t < 4; ++t) o[t * LH + 16 * c] = S[c][t] * inv[c];
+                for (int t = 0; t < 4; ++t) o[t * LH + 16 * c] = S[c][t] * (inv[c] * irs[t]);
         } else {
 #pragma unroll
             for (int c = 0; c < 8; ++c)
 #pragma unroll
                 for (int t = 0; t < 4; ++t)
-                    if (row0 + 4 * g + t <= last) o[t * LH + 16 * c] = S[c][t] * inv[c];
+                    if (row0 + 4 * g + t <= last) o[t * LH + 16 * c] = S[c][t] * (inv[c] * irs[t]);
         }
     };
     auto body = [&](float4 *X, uint32_t (*h)[4], uint32_t (*l)[4], uint32_t (*nh)[4], uint32_t (*nl)[4]) {
@@ -310,7 +370,7 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
         float xs0 = 0.0f, xs1 = 0.0f;
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
-            acc[c] = (f32x4){bias[c], bias[c], bias[c], bias[c]};
+            acc[c] = bias[c];
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
                 const half8 ah = __builtin_bit_cast(half8, h[s]), al = __builtin_bit_cast(half8, l[s]);
@@ -382,6 +442,7 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
         }
         cC.next(k);
         cS.next(k);
+        if (cC.e == 0) set_bias(unit_tile(cC));  // the next MFMA slot opens a tile
         if (close_prev) {  // the next run starts at cC
             run_side = new_unit && cC.e != 0 ? seg * p.U + u_next : -1;
             if (new_unit) {
@@ -411,7 +472,7 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
 }  // namespace
 
 // Summation units and waves of one launch (layer.hpp edge_wave_plan).
-EdgePlan edge_wave_plan(int64_t nseg, int64_t S_seg, int cus, int64_t side_cap) {
+EdgePlan edge_wave_plan(int64_t nseg, int64_t S_seg, int k, int cus, int64_t side_cap) {
     EdgePlan pl;
     // U: the power of two that makes units of 22..44 slots (cylinder: 128
     // units of 43 slots), capped by the segment's slots and its share of the
@@ -429,8 +490,14 @@ EdgePlan edge_wave_plan(int64_t nseg, int64_t S_seg, int cus, int64_t side_cap) 
     // waves per segment: one wave per SIMD over the launch, at most one per unit
     int64_t w = 4 * (int64_t)cus / nseg;
     w = w < 1 ? 1 : (w > U ? U : w);
+    // ... and more (queued behind the first wave of a SIMD) while a wave would
+    // span more than kWaveTiles tiles: its row scales live in LDS.  Which wave
+    // runs a unit does not change any sum.
+    const int64_t spu = (S_seg + U - 1) / U;  // slots per unit, at most
+    auto tiles_of = [&](int64_t ww) { return (((U + ww - 1) / ww) * spu + k - 1) / k + 1; };
+    while (w < U && tiles_of(w) > kWaveTiles) w = 2 * w < U ? 2 * w : U;
     pl.U = (int)U;
-    pl.wpsp = (int)w;
+    pl.wpsp = tiles_of(w) <= kWaveTiles ? (int)w : 0;  // 0: no valid plan (units too long)
     pl.waves = nseg * w;
     return pl;
 }
@@ -438,14 +505,14 @@ EdgePlan edge_wave_plan(int64_t nseg, int64_t S_seg, int cus, int64_t side_cap) 
 namespace {
 // Kernel arguments and grid of one launch (slot split of layer.hpp EdgeSplit).
 int edge_wave_setup(const float *a, const float *b, const int32_t *nbr, const int32_t *deg, int64_t n,
-                    int k, int64_t seg_n, const float *msg2_b, const char *pk, const float *rng,
+                    int k, int64_t seg_n, const float *msg2_b, const char *pk, const float *rmx,
                     float *out, float *side, int64_t side_cap, int cus, WaveArgs *w, EdgeSplit *split) {
     seg_n = effective_seg(n, seg_n);
     const int64_t nseg = n / seg_n, tps = (seg_n + ET - 1) / ET, S = tps * k;
     if (!(tps < (int64_t)INT32_MAX && S < ((int64_t)1 << 40) && side_cap >= nseg)) return 0;
-    const EdgePlan pl = edge_wave_plan(nseg, S, cus, side_cap);
-    if (pl.waves > (int64_t)INT32_MAX || nseg * pl.U > (int64_t)INT32_MAX) return 0;
-    *w = WaveArgs{a, b, nbr, deg, n, k, seg_n, (int)tps, S, pl.U, pl.wpsp, msg2_b, pk, rng, out, side};
+    const EdgePlan pl = edge_wave_plan(nseg, S, k, cus, side_cap);
+    if (pl.wpsp < 1 || pl.waves > (int64_t)INT32_MAX || nseg * pl.U > (int64_t)INT32_MAX) return 0;
+    *w = WaveArgs{a, b, nbr, deg, n, k, seg_n, (int)tps, S, pl.U, pl.wpsp, msg2_b, pk, rmx, out, side};
     *split = EdgeSplit{side, S, pl.U, k, seg_n};
     return (int)pl.waves;
 }
@@ -454,11 +521,11 @@ int edge_wave_setup(const float *a, const float *b, const int32_t *nbr, const in
 // Profiling aid (tools/ubench): the non-ragged kernel with DIAG bits, one wave
 // per SIMD, one segment of n rows; side = a [4 cus][16][128] buffer.
 int launch_edge_wave_diag(const float *a, const float *b, const int32_t *nbr, int64_t n, int k,
-                          const float *msg2_b, const char *pk, const float *rng, float *out,
+                          const float *msg2_b, const char *pk, const float *rmx, float *out,
                           float *side, int cus, int diag, hipStream_t st) {
     WaveArgs w;
     EdgeSplit split;
-    const int grid = edge_wave_setup(a, b, nbr, nullptr, n, k, n, msg2_b, pk, rng, out, side,
+    const int grid = edge_wave_setup(a, b, nbr, nullptr, n, k, n, msg2_b, pk, rmx, out, side,
                                      4 * (int64_t)cus, cus, &w, &split);
     MMPDE_REQUIRE(grid > 0);
 #define MMPDE_DIAG(D) \
@@ -483,11 +550,11 @@ int launch_edge_wave_diag(const float *a, const float *b, const int32_t *nbr, in
 }
 
 int launch_edge_wave(const float *a, const float *b, const int32_t *nbr, const int32_t *deg, int64_t n,
-                     int k, int64_t seg_n, const float *msg2_b, const char *pk, const float *rng,
+                     int k, int64_t seg_n, const float *msg2_b, const char *pk, const float *rmx,
                      float *out, float *side, int64_t side_cap, int cus, EdgeSplit *split, hipStream_t st) {
-    MMPDE_REQUIRE(a && b && nbr && msg2_b && pk && rng && out && side && split && n > 0 && k > 0);
+    MMPDE_REQUIRE(a && b && nbr && msg2_b && pk && rmx && out && side && split && n > 0 && k > 0);
     WaveArgs w;
-    const int grid = edge_wave_setup(a, b, nbr, deg, n, k, seg_n, msg2_b, pk, rng, out, side, side_cap,
+    const int grid = edge_wave_setup(a, b, nbr, deg, n, k, seg_n, msg2_b, pk, rmx, out, side, side_cap,
                                      cus, &w, split);
     MMPDE_REQUIRE(grid > 0);
     if (deg) hipLaunchKernelGGL((gnn_edge_wave_kernel<true>), dim3(grid), dim3(64), 0, st, w);

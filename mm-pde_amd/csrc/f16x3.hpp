@@ -18,6 +18,11 @@ __device__ __forceinline__ float split_scale(float mx) {
     return __uint_as_float((uint32_t)se << 23);
 }
 
+// Split scale of one target row of the edge stage (f16x3.hpp split8_relu_rtz
+// needs |relu(a + b)| s < 2^11): s = split_scale(M) / 8 for a bound M >= every
+// |a_ik + b_jk| of the row (layer.hpp row maxima).
+__device__ __forceinline__ float row_split_scale(float M) { return 0.125f * split_scale(M); }
+
 // 1 / s for a power of two s from split_scale (exact).
 __device__ __forceinline__ float pow2_inv(float s) {
     const uint32_t eb = (__float_as_uint(s) >> 23) & 0xff;

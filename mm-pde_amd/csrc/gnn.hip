@@ -361,9 +361,9 @@ inline bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
 extern "C" int64_t mmpde_gnn_workspace_bytes(int64_t n) {
     // h ping-pong, a, b, the edge stage's sums and 3 x [n,128] for the wave edge
     // kernel's side blocks = 8 x [n,128] fp32 (the unfused per-layer API uses 4
-    // of them as a, b, mean, v), then the F16X3 range records (layer.hpp) and
+    // of them as a, b, mean, v), then the F16X3 row maxima (layer.hpp) and
     // room for per-call weight images
-    return kGnnBufs * n * H * (int64_t)sizeof(float) + range_tiles(n) * 16 +
+    return kGnnBufs * n * H * (int64_t)sizeof(float) + row_max_floats(n) * 4 +
            (int64_t)MMPDE_GNN_MAX_LAYERS * kLayerPack;
 }
 
@@ -567,10 +567,10 @@ extern "C" int mmpde_gnn_forward_ex(const float *u, const float *pos, int64_t n,
     float *hb[2] = {ws, ws + n * H};
     float *wa = ws + 2 * n * H, *wb = ws + 3 * n * H, *wmean = ws + 4 * n * H;
     const char *pack = nullptr;
-    // range records of the current layer's message inputs (F16X3 split scale):
+    // row maxima of the current layer's message inputs (F16X3 split scales):
     // written by the embed / node stage, read by the next edge stage
-    float *rng = ws + kGnnBufs * n * H;
-    // rows per trajectory segment: the split scale is taken per segment
+    float *rmx = ws + kGnnBufs * n * H;
+    // rows per trajectory segment (the edge stage's summation units)
     const int64_t seg_n = exec ? exec->seg_n : 0;
     int rc;
     if (mode == MMPDE_EDGE_GEMM_F16X3 && n_layers > 0) {
@@ -578,7 +578,7 @@ extern "C" int mmpde_gnn_forward_ex(const float *u, const float *pos, int64_t n,
             MMPDE_REQUIRE(aligned16(exec->packed));
             pack = (const char *)exec->packed;
         } else {
-            char *wpk = (char *)(ws + kGnnBufs * n * H) + range_tiles(n) * 16;
+            char *wpk = (char *)(ws + kGnnBufs * n * H + row_max_floats(n));
             rc = mmpde_gnn_pack_f16x3(layers, n_layers, wpk, stream);
             if (rc) return rc;
             pack = wpk;
@@ -587,7 +587,7 @@ extern "C" int mmpde_gnn_forward_ex(const float *u, const float *pos, int64_t n,
     if (n_layers > 0) {
         // embedding + layer 0's message_net_1 halves (later layers get theirs
         // from the previous layer's node stage)
-        rc = launch_embed_stage(u, pos, n, seg_n, sc, emb, &layers[0], pack, pack ? rng : nullptr, hb[0],
+        rc = launch_embed_stage(u, pos, n, seg_n, sc, emb, &layers[0], pack, pack ? rmx : nullptr, hb[0],
                                 wa, wb, st);
     } else {
         rc = mmpde_gnn_embed(u, pos, n, sc, emb, wmean, hb[0], stream);  // wmean: scratch
@@ -601,14 +601,14 @@ extern "C" int mmpde_gnn_forward_ex(const float *u, const float *pos, int64_t n,
         const mmpde_gnn_layer_params *next = l + 1 < n_layers ? &layers[l + 1] : nullptr;
         const char *pk = pack ? pack + (int64_t)l * kLayerPack : nullptr;
         const char *pkn = pack && next ? pack + (int64_t)(l + 1) * kLayerPack : nullptr;
-        // one record buffer serves every layer: edge stage l reads it before
-        // node stage l (stream order) writes layer l + 1's
-        float *rout = pack && next ? rng : nullptr;
+        // one row-maxima buffer serves every layer: edge stage l reads it
+        // before node stage l (stream order) writes layer l + 1's
+        float *rout = pack && next ? rmx : nullptr;
         if (eb && hipEventRecord(eb, st) != hipSuccess) return MMPDE_ERR_INVALID_ARG;
         EdgeSplit split;
         const int32_t *deg = exec ? exec->degree : nullptr;
         // side blocks of the wave edge kernel: the workspace after the mean
-        rc = launch_edge_stage(wa, wb, nbr, deg, n, k, seg_n, &layers[l], pk, pack ? rng : nullptr, wmean,
+        rc = launch_edge_stage(wa, wb, nbr, deg, n, k, seg_n, &layers[l], pk, pack ? rmx : nullptr, wmean,
                                wmean + n * H, (kGnnBufs - 5) * n * H / (16 * H), &split, st);
         if (rc) return rc;
         if (ee && hipEventRecord(ee, st) != hipSuccess) return MMPDE_ERR_INVALID_ARG;

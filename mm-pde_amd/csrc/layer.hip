@@ -33,7 +33,7 @@
 // weight operand once per workgroup (wave w owns output column tile w for all
 // row blocks); activations are staged in LDS as MFMA operand images with
 // per-row power-of-two scales (F16X3), and (F16X3) each workgroup stores the
-// range record of its rows (layer.hpp).  No atomics: every output is
+// row maxima of its a', b' rows (layer.hpp).  No atomics: every output is
 // deterministic.
 #include "common.hpp"
 #include "f16x3.hpp"
@@ -72,7 +72,7 @@ struct EdgeArgs {
     int k, ntiles;
     const float *w2, *b2;      // message_net_2.0 weight [128,128], bias
     const char *pk;            // F16X3: this layer's packed images (column scales of W2)
-    const float *rng;          // F16X3: range records of a, b (layer.hpp; one segment)
+    const float *rsc;          // F16X3: split scale of every target row (layer.hpp row maxima)
     float *mean;               // [n, 128]
     uint64_t *stamps;          // profiling builds (PH bit 10): per-round s_memtime of block 0
     const int32_t *deg;        // RAGGED: in-degree of every target (nbr row entries past it are ignored)
@@ -110,6 +110,9 @@ constexpr int EDGE_NP = MMPDE_EDGE_NP;
 #define MMPDE_EDGE_PH 27
 #endif
 constexpr int EDGE_PH = MMPDE_EDGE_PH;
+// relu_mask words need the SPLIT consumer layout (two waves per SIMD sharing 32
+// columns, cg < 4): other profiling builds reject relu_mask at launch
+constexpr bool kEdgeMaskOk = EDGE_NC == 2 && (EDGE_PH & 16);
 
 // Slot operand layout (v_mfma_f32_16x16x32_f16; F32: v_mfma_f32_16x16x4_f32): a
 // slot is the 16 x 128 message tile m[row][k] of one neighbour slot e of the
@@ -136,6 +139,10 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
     constexpr int NCT = 256 * NC;  // consumer threads
     __shared__ float4 ring[ERING * ESL * SLOT4];  // [round % ERING][slot][plane][lane]
     __shared__ float a_lds[2][ET * NLDA];        // a rows of tile j in [j & 1]
+    // F16X3: the split scales of tile j's rows in [j & 7] (staged with the a rows;
+    // eight deep: the consumers read a tile's until one round after its last,
+    // staging runs one tile ahead of the producers)
+    __shared__ float rs_ring[8][ET];
     // SPLIT: the odd-slot consumer's relu-sums of tile j, in [j & 1]
     __shared__ float4 xS[SPLIT ? 2 * 4 * CT * 64 : 1];
     const int tid = threadIdx.x;
@@ -153,33 +160,37 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
     const int NIT = NR + EPF;
     const int NIT2 = (NIT + 1) & ~1;  // even: the producer's 2x-unrolled body has no tail test
     const int64_t nmax = p.n - 1;
-    // F16X3: |a + b| <= max|a| + max|b|, scaled below 2^11 (split8_relu_rtz)
-    float sc = 1.0f;
-    if (F16X3) sc = 0.125f * split_scale(segment_range(p.rng, p.n, 0));
     auto tile_row = [&](int j, int row) { return min((int64_t)(first + j * stride) * ET + row, nmax); };
 
-    // a tiles (scaled by sc for F16X3): the consumer waves stage tile j + 1 while
-    // the producers work on tile j, 2 / NC float4 per consumer thread.
-    auto a_fetch = [&](int j, float4 *v) {
+    // a tiles (F16X3: scaled by their rows' split scales, |relu(a + b)| s < 2^11,
+    // split8_relu_rtz): the consumer waves stage tile j + 1 while the producers
+    // work on tile j, 2 / NC float4 per consumer thread.
+    auto a_fetch = [&](int j, float4 *v, float *sv) {
 #pragma unroll
         for (int u = 0; u < 2 / NC; ++u) {
             const int e = tid + NCT * u, row = e >> 5, c4 = e & 31;
             v[u] = *(const float4 *)(p.a + tile_row(j, row) * LH + 4 * c4);
+            sv[u] = F16X3 ? p.rsc[tile_row(j, row)] : 1.0f;
         }
     };
-    auto a_store = [&](int j, const float4 *v) {
+    auto a_store = [&](int j, const float4 *v, const float *sv) {
 #pragma unroll
         for (int u = 0; u < 2 / NC; ++u) {
             const int e = tid + NCT * u, row = e >> 5, c4 = e & 31;
             float4 x = v[u];
-            if (F16X3) x = make_float4(x.x * sc, x.y * sc, x.z * sc, x.w * sc);
+            if (F16X3) {
+                const float sc = sv[u];
+                x = make_float4(x.x * sc, x.y * sc, x.z * sc, x.w * sc);
+                if (c4 == 0) rs_ring[j & 7][row] = sc;
+            }
             *(float4 *)(&a_lds[j & 1][row * NLDA + 4 * c4]) = x;
         }
     };
     if (!producer && nt > 0) {
         float4 v[2 / NC];
-        a_fetch(0, v);
-        a_store(0, v);
+        float sv[2 / NC];
+        a_fetch(0, v, sv);
+        a_store(0, v, sv);
     }
     __syncthreads();
 
@@ -196,6 +207,7 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
             return F16X3 ? 32 * (ii >> 1) + 8 * g + 4 * (ii & 1) : 16 * ii + 4 * g;
         };
         float4 acur[NPC], bv0[NPC], bv1[NPC];
+        float sc = 1.0f;  // F16X3: split scale of this lane's row (r) of the tile
         // every round issues the same loads (clamped addresses past the end or
         // past k): 1 index + 8 gathers
         auto src_of = [&](const RoundCtr &c) -> uint32_t {
@@ -239,6 +251,7 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
                     const float *ar = &a_lds[cP.j & 1][r * NLDA];
 #pragma unroll
                     for (int i = 0; i < NPC; ++i) acur[i] = *(const float4 *)(ar + piece(i));
+                    if (F16X3) sc = rs_ring[cP.j & 7][r];
                 }
                 float4 *dst = ring + (slot * ESL + pw) * SLOT4 + i0 * 64 + lane;
                 uint32_t fold = 0;
@@ -306,7 +319,8 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
         auto slotq = [&](int qq) { return SPLIT ? hs + 2 * qq : qq; };
         float4 wf[CT][8];
         half8 wh[CT][4], wl[CT][4];
-        f32x4 bias[CT];  // accumulator initial value (message_net_2 bias, scaled)
+        f32x4 bias[CT];  // accumulator initial value (message_net_2 bias, scaled; F16X3 per row)
+        float bb0[CT];   // F16X3: the bias in the column scale (times the row scales per tile)
         float inv[CT];
 #pragma unroll
         for (int cc = 0; cc < CT; ++cc) {
@@ -320,14 +334,15 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
                     wl[cc][s4] = bfrag(img, 4, CT * cg + cc, s4, 1, lane);
                 }
                 const float sw = ((const float *)(img + 65536))[col];
-                bb = bb * sw * sc;
-                inv[cc] = pow2_inv(sw) * pow2_inv(sc);
+                bb = bb * sw;
+                inv[cc] = pow2_inv(sw);
             } else {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) wf[cc][j] = *(const float4 *)(p.w2 + col * LH + 16 * j + 4 * g);
                 inv[cc] = 1.0f;
             }
             bias[cc] = (f32x4){bb, bb, bb, bb};
+            bb0[cc] = bb;
         }
         const float kdiv = (float)k;
         int dg[4] = {k, k, k, k};  // RAGGED: in-degree of this lane's rows 4 g + t of the tile
@@ -335,17 +350,23 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
 #pragma unroll
         for (int cc = 0; cc < CT; ++cc) S[cc] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
         int pend = -1;  // SPLIT, even-slot wave: tile whose mean waits for the partner's sums
-        // T: relu-sums in the scaled domain (F16X3: x sw[col] sc, powers of two);
-        // inv undoes the scale exactly before the division by the degree
+        // T: relu-sums in the scaled domain (F16X3: x sw[col] s[row], powers of
+        // two); inv and the row scale undo it exactly before the division by the
+        // degree
         auto write_mean = [&](int j, const f32x4 *T) {
             const int64_t row0 = (int64_t)(first + j * stride) * ET + 4 * g;
+            float irs[4] = {1.0f, 1.0f, 1.0f, 1.0f};
+            if (F16X3) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) irs[t] = pow2_inv(rs_ring[j & 7][4 * g + t]);
+            }
 #pragma unroll
             for (int cc = 0; cc < CT; ++cc) {
                 const int col = 16 * (CT * cg + cc) + r;
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
                     const float div = RAGGED ? (float)max(dg[t], 1) : kdiv;
-                    if (row0 + t < p.n) p.mean[(row0 + t) * LH + col] = T[cc][t] * inv[cc] / div;
+                    if (row0 + t < p.n) p.mean[(row0 + t) * LH + col] = T[cc][t] * inv[cc] * irs[t] / div;
                 }
             }
         };
@@ -416,12 +437,14 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
                     S[cc][t] += v;
                 }
             }
-            if (p.relu_mask) {
+            if constexpr (SPLIT) if (p.relu_mask) {
                 // the z2 > 0 bits the backward reuses (mmpde_gnn_edge_backward_sorted):
                 // ballots per (column tile cc, row t) cover rows 4 g + t, g < 4,
                 // 16 columns each; lane l < 16 stores row 4 (l >> 2) + (l & 3)'s
-                // word of this wave's 32 columns (CT = 2 tiles): one store per slot
-                static_assert(!F16X3 || CT == 2, "relu mask words take two column tiles per wave");
+                // word of this wave's 32 columns (CT = 2 tiles, cg < 4): one store
+                // per slot.  Builds without SPLIT reject relu_mask at launch
+                // (kEdgeMaskOk).
+                static_assert(CT == 2, "relu mask words take two column tiles per wave");
                 uint64_t bal[CT][4];
 #pragma unroll
                 for (int cc = 0; cc < CT; ++cc)
@@ -441,6 +464,7 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
             }
         };
         float4 xa[4], xb[4], an[2 / NC];
+        float asv[2 / NC];
         int js = 1;  // next a tile to stage: stored in iteration js * rpt - 1 (the
                      // producers read it from iteration js * rpt), fetched up to two
                      // iterations earlier but after the previous store
@@ -449,9 +473,9 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
             finish_pending();
             if (js < nt) {
                 const int ts = js * rpt - 1;
-                if (it == ts - lead) a_fetch(js, an);
+                if (it == ts - lead) a_fetch(js, an, asv);
                 if (it == ts) {
-                    a_store(js, an);
+                    a_store(js, an, asv);
                     ++js;
                 }
             }
@@ -462,6 +486,12 @@ __global__ __launch_bounds__(64 * (4 * NC + 4 * NP), 1) void gnn_edge_kernel(Edg
                 if (RAGGED && cC.rd == 0) {  // a new tile (after finish_pending used the last one's)
 #pragma unroll
                     for (int t = 0; t < 4; ++t) dg[t] = p.deg[tile_row(cC.j, 4 * g + t)];
+                }
+                if (F16X3 && cC.rd == 0) {  // the new tile's row scales (rows 4 g + t)
+#pragma unroll
+                    for (int cc = 0; cc < CT; ++cc)
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) bias[cc][t] = bb0[cc] * rs_ring[cC.j & 7][4 * g + t];
                 }
                 // Straight-line round: every slot is multiplied (a slot past k, in
                 // a tile's last round only, holds a duplicate of the last
@@ -531,8 +561,7 @@ struct NodeArgs {
     const float *u, *pos;
     mmpde_gnn_scales sc;
     const char *pk, *pkn;  // F16X3 images: this layer (U1, U2), next layer (W1)
-    float *rng_out;        // F16X3: range records of a', b' (layer.hpp)
-    int64_t seg_n;         // rows per trajectory segment (range records)
+    float *rmx_out;        // F16X3: row maxima of a', b' (layer.hpp)
     int parts;             // mean = sum of `parts` buffers part_stride floats apart
     int64_t part_stride;
     // div_k > 0: the buffers hold neighbour sums (F16X3 wave edge kernel); the
@@ -807,22 +836,22 @@ template <bool F16X3, int RB>
 __device__ __forceinline__ void proj_phase(const BOps<F16X3, F16X3 ? 4 : 8> &bA, const float4 *img,
                                            const float *rs, const float *rowv, const W1C &w,
                                            const char *pk, const float *w1r, int tw, int64_t row0,
-                                           int64_t n, int64_t seg_n, float *a_out, float *b_out,
-                                           float *rng_out, uint32_t *arrived, int wave, int lane,
+                                           int64_t n, float *a_out, float *b_out,
+                                           float *rmx_out, uint32_t *arrived, int wave, int lane,
                                            const BOps<F16X3, F16X3 ? 4 : 8> *bBpre = nullptr) {
     constexpr int ROWS = 16 * RB, S1 = F16X3 ? 4 : 8;
     const int col = 16 * wave + (lane & 15), g = lane >> 4;
     f32x4 aA[RB], aB[RB];
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) aA[rb] = aB[rb] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
-    // |a|, |b| maxima of each 16-row block's rows in the block's first segment
-    // (0) and in the next one (1), for the block's range record (layer.hpp:
-    // kRangeRows = 16; seg_n >= 16: a block touches at most two segments)
-    // (as bit patterns: for x, y >= 0 the integer max is the float max, with no
-    // NaN canonicalisation)
-    uint32_t amx[RB][2], bmx[RB][2];
+    // |a'|, |b'| of this lane's rows (16 rb + 4 g + q, column col) as bit
+    // patterns (for x, y >= 0 the integer max is the float max, with no NaN
+    // canonicalisation): the rows' maxima for the edge stage's split scales
+    uint32_t amx[RB][4], bmx[RB][4];
 #pragma unroll
-    for (int rb = 0; rb < RB; ++rb) amx[rb][0] = amx[rb][1] = bmx[rb][0] = bmx[rb][1] = 0u;
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) amx[rb][q] = bmx[rb][q] = 0u;
     // stores at immediate offsets from one base per lane; the row test only
     // for a tile that runs past n (wave-uniform)
     const bool full = row0 + ROWS <= n;
@@ -833,15 +862,6 @@ __device__ __forceinline__ void proj_phase(const BOps<F16X3, F16X3 ? 4 : 8> &bA,
         for (int c = 1; c < tw; ++c) node += w1r[256 + c] * rowv[(3 + c) * ROWS + lr];
         return node + w.dx * rowv[ROWS + lr] + w.dy * rowv[2 * ROWS + lr];
     };
-    // first row of the segment after block rb's first segment: two divisions
-    // per wave here, not a 64-bit division per stored value in the epilogue
-    int64_t seg_next[RB];
-#pragma unroll
-    for (int rb = 0; rb < RB; ++rb) seg_next[rb] = ((row0 + 16 * rb) / seg_n + 1) * seg_n;
-    auto seg_of = [&](int rb, int lr) { return (int)(row0 + lr >= seg_next[rb]); };
-    // the tile crosses a segment boundary (wave-uniform): only then are there
-    // second-segment maxima to keep
-    const bool cross = seg_next[0] < row0 + ROWS;
     gemm_tile<F16X3, RB, S1>(aA, img, 128, 0, bA, lane);
     {
         if (bBpre) {  // operands of b preloaded (the weight-stationary node kernel)
@@ -851,61 +871,56 @@ __device__ __forceinline__ void proj_phase(const BOps<F16X3, F16X3 ? 4 : 8> &bA,
             bB.load(pk + kPkW1, 4, 8 + wave, 0, w1r, 128, lane);
             gemm_tile<F16X3, RB, S1>(aB, img, 128, 0, bB, lane);
         }
-        auto epilogue = [&](auto CROSS) {
-#pragma unroll
-            for (int rb = 0; rb < RB; ++rb) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int lr = 16 * rb + 4 * g + q;
-                    if (full || row0 + lr < n) {
-                        float za = aA[rb][q], zb = aB[rb][q];
-                        if (F16X3) {
-                            const float ir = pow2_inv(rs[lr]);
-                            za = za * ir * w.isa;
-                            zb = zb * ir * w.isb;
-                        }
-                        const float node = node_term(lr);
-                        const float va = za + node + w.t * rowv[lr] + w.b;
-                        const float vb = zb - node;
-                        ap[(16 * rb + q) * LH] = va;
-                        bp[(16 * rb + q) * LH] = vb;
-                        // |v| with NaN -> 0 (fmaxf ignores a NaN, as the float max did)
-                        const uint32_t ua = __builtin_bit_cast(uint32_t, fmaxf(fabsf(va), 0.0f));
-                        const uint32_t ub = __builtin_bit_cast(uint32_t, fmaxf(fabsf(vb), 0.0f));
-                        if (decltype(CROSS)::value) {
-                            const int sx = seg_of(rb, lr);
-                            amx[rb][sx] = max(amx[rb][sx], ua);
-                            bmx[rb][sx] = max(bmx[rb][sx], ub);
-                        } else {
-                            amx[rb][0] = max(amx[rb][0], ua);
-                            bmx[rb][0] = max(bmx[rb][0], ub);
-                        }
-                    }
-                }
-            }
-        };
-        if (cross) epilogue(std::true_type{});
-        else epilogue(std::false_type{});
-    }
-    if (rng_out) {
-        // wave maxima, then the workgroup's, one float4 record per 16-row block,
-        // without a barrier: each wave posts its maxima to LDS and counts itself
-        // in (LDS atomic); the last of the 8 to arrive reduces and stores.  (A
-        // __syncthreads here also waits for every wave's a' / b' stores: 7-8 us
-        // of the 54 us node launch at cy B=16.)  The max is order-free, so the
-        // record does not depend on the arrival order.
-        __shared__ float red[8][RB][4];
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) {
-            const float m0 = wave_absmax(__builtin_bit_cast(float, amx[rb][0]));
-            const float m1 = wave_absmax(__builtin_bit_cast(float, bmx[rb][0]));
-            const float m2 = cross ? wave_absmax(__builtin_bit_cast(float, amx[rb][1])) : 0.0f;
-            const float m3 = cross ? wave_absmax(__builtin_bit_cast(float, bmx[rb][1])) : 0.0f;
-            if (lane == 0) {
-                red[wave][rb][0] = m0;
-                red[wave][rb][1] = m1;
-                red[wave][rb][2] = m2;
-                red[wave][rb][3] = m3;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int lr = 16 * rb + 4 * g + q;
+                if (full || row0 + lr < n) {
+                    float za = aA[rb][q], zb = aB[rb][q];
+                    if (F16X3) {
+                        const float ir = pow2_inv(rs[lr]);
+                        za = za * ir * w.isa;
+                        zb = zb * ir * w.isb;
+                    }
+                    const float node = node_term(lr);
+                    const float va = za + node + w.t * rowv[lr] + w.b;
+                    const float vb = zb - node;
+                    ap[(16 * rb + q) * LH] = va;
+                    bp[(16 * rb + q) * LH] = vb;
+                    // |v| with NaN -> 0 (fmaxf ignores a NaN, as the float max did)
+                    amx[rb][q] = __builtin_bit_cast(uint32_t, fmaxf(fabsf(va), 0.0f));
+                    bmx[rb][q] = __builtin_bit_cast(uint32_t, fmaxf(fabsf(vb), 0.0f));
+                }
+            }
+        }
+    }
+    if (rmx_out) {
+        // row maxima: over this wave's 16 columns (the 16 lanes r of one DPP
+        // row: quad [1,0,3,2], quad [2,3,0,1], row_half_mirror, row_mirror), then
+        // over the 8 waves without a barrier: each wave posts its maxima to LDS
+        // and counts itself in (LDS atomic); the last of the 8 to arrive reduces
+        // and stores the tile's rows.  (A __syncthreads here also waits for every
+        // wave's a' / b' stores: 7-8 us of the 54 us node launch at cy B=16.)  The
+        // max is order-free, so the record does not depend on the arrival order.
+        __shared__ uint32_t red[8][ROWS][2];
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                uint32_t ua = amx[rb][q], ub = bmx[rb][q];
+                ua = max(ua, dpp_u<0xB1>(ua));
+                ub = max(ub, dpp_u<0xB1>(ub));
+                ua = max(ua, dpp_u<0x4E>(ua));
+                ub = max(ub, dpp_u<0x4E>(ub));
+                ua = max(ua, dpp_u<0x141>(ua));
+                ub = max(ub, dpp_u<0x141>(ub));
+                ua = max(ua, dpp_u<0x140>(ua));
+                ub = max(ub, dpp_u<0x140>(ub));
+                if ((lane & 15) == 0) {
+                    red[wave][16 * rb + 4 * g + q][0] = ua;
+                    red[wave][16 * rb + 4 * g + q][1] = ub;
+                }
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // posted before counted
@@ -913,12 +928,17 @@ __device__ __forceinline__ void proj_phase(const BOps<F16X3, F16X3 ? 4 : 8> &bA,
         if (lane == 0) prev = __hip_atomic_fetch_add(arrived, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         prev = __builtin_amdgcn_readfirstlane(prev);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (prev == 7 && lane < 4 * RB) {
-            const int rb = lane >> 2, e = lane & 3;
-            float m = red[0][rb][e];
+        if (prev == 7) {
 #pragma unroll
-            for (int w = 1; w < 8; ++w) m = fmaxf(m, red[w][rb][e]);
-            if (row0 + 16 * rb < n) rng_out[4 * (row0 / 16 + rb) + e] = m;
+            for (int l0 = 0; l0 < 2 * ROWS; l0 += 64) {
+                const int l = l0 + lane, row = l >> 1, e = l & 1;
+                if (l < 2 * ROWS) {
+                    uint32_t m = red[0][row][e];
+#pragma unroll
+                    for (int w2 = 1; w2 < 8; ++w2) m = max(m, red[w2][row][e]);
+                    if (row0 + row < n) rmx_out[2 * (row0 + row) + e] = __builtin_bit_cast(float, m);
+                }
+            }
         }
     }
 }
@@ -948,7 +968,7 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs p) {
     __shared__ float hres[ROWS * NLD];          // fp32 h (residual)
     __shared__ float rs[4][ROWS];               // row scales: h, mean, v, h'
     __shared__ float rowv[3 + MAX_TW][ROWS];    // per row: t / tmax, x / Lx, y / Ly, u_0 .. u_{tw-1}
-    __shared__ uint32_t rng_arrived;            // waves done with their range maxima (proj_phase)
+    __shared__ uint32_t rng_arrived;            // waves done with their row maxima (proj_phase)
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int r = lane & 15, g = lane >> 4;
     const int col = 16 * wave + r;  // this lane's output column (tile = wave)
@@ -1061,8 +1081,8 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs p) {
         __syncthreads();
         NODE_STAMP(6);
         // ---- next layer's message_net_1 node halves
-        proj_phase<F16X3, RB>(bA, img, rs[3], &rowv[0][0], w1c, p.pkn, w1r, tw, row0, p.n, p.seg_n,
-                              p.a_out, p.b_out, p.rng_out, &rng_arrived, wave, lane, NODE_EARLY_B ? &bB : nullptr);
+        proj_phase<F16X3, RB>(bA, img, rs[3], &rowv[0][0], w1c, p.pkn, w1r, tw, row0, p.n,
+                              p.a_out, p.b_out, p.rmx_out, &rng_arrived, wave, lane, NODE_EARLY_B ? &bB : nullptr);
     }
     NODE_STAMP(7);
 }
@@ -1084,8 +1104,7 @@ struct EmbedArgs {
     int64_t ld_w1;
     float *a_out, *b_out;
     const char *pk;        // F16X3: layer 0's packed images
-    float *rng_out;        // F16X3: layer 0's range records
-    int64_t seg_n;         // rows per trajectory segment (range records)
+    float *rmx_out;        // F16X3: layer 0's row maxima
 };
 
 template <bool F16X3, int RB>
@@ -1095,7 +1114,7 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_embed_kernel(EmbedArgs p) {
     __shared__ float4 img[RB * 8 * 64];   // K = 128 operand image
     __shared__ float stage[ROWS * NLD];   // fp32 z, then h0
     __shared__ float rs[ROWS];            // h0 row scales
-    __shared__ uint32_t rng_arrived;      // waves done with their range maxima (proj_phase)
+    __shared__ uint32_t rng_arrived;      // waves done with their row maxima (proj_phase)
     __shared__ float rsz[ROWS];           // z row scales (F16X3 embedding GEMM)
     __shared__ float rowv[3 + MAX_TW][ROWS];  // per row: t / tmax, x / Lx, y / Ly, u_0 .. u_{tw-1}
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -1192,8 +1211,8 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_embed_kernel(EmbedArgs p) {
     __syncthreads();
     prep<F16X3, ROWS>(stage, NLD, 0, ROWS, false, img, 128, 0, rs);
     __syncthreads();
-    proj_phase<F16X3, RB>(bA, img, rs, &rowv[0][0], w1c, p.pk, w1r, tw, row0, p.n, p.seg_n,
-                          p.a_out, p.b_out, p.rng_out, &rng_arrived, wave, lane, NODE_EARLY_B ? &bB : nullptr);
+    proj_phase<F16X3, RB>(bA, img, rs, &rowv[0][0], w1c, p.pk, w1r, tw, row0, p.n,
+                          p.a_out, p.b_out, p.rmx_out, &rng_arrived, wave, lane, NODE_EARLY_B ? &bB : nullptr);
 }
 
 inline bool al16(const void *q) { return ((uintptr_t)q & 15u) == 0; }
@@ -1213,88 +1232,142 @@ int device_cus() {
 #define MMPDE_NODE_RB 2
 #endif
 
-static_assert(16 * MMPDE_NODE_RB % kRangeRows == 0, "range records are per 16-row block of a node tile");
 
 int launch_edge_stage(const float *a, const float *b, const int32_t *nbr, const int32_t *deg,
                       int64_t n, int k, int64_t seg_n, const mmpde_gnn_layer_params *p, const char *pk,
-                      const float *rng, float *mean, float *side, int64_t side_cap,
+                      const float *rmx, float *mean, float *side, int64_t side_cap,
                       EdgeSplit *split, hipStream_t st, uint32_t *relu_mask) {
     if (split) *split = EdgeSplit{};
-    MMPDE_REQUIRE(!relu_mask || (!pk && al16(relu_mask)));  // the ring kernel's F32 training forward
+    MMPDE_REQUIRE(!relu_mask || (!pk && kEdgeMaskOk && al16(relu_mask)));  // the ring kernel's F32 training forward
     MMPDE_REQUIRE(a && b && nbr && p && mean && n > 0 && k > 0 && n <= (int64_t)INT32_MAX);
     MMPDE_REQUIRE(al16(a) && al16(b) && al16(p->msg2_w) && al16(mean));
-    MMPDE_REQUIRE(!pk || (rng && al16(pk) && al16(rng)));
+    MMPDE_REQUIRE(!pk || (rmx && al16(pk) && al16(rmx)));
     const int64_t ntiles = (n + ET - 1) / ET;
     MMPDE_REQUIRE(ntiles * ((k + ESL - 1) / ESL) < (int64_t)INT32_MAX);
-    EdgeArgs e{a, b, nbr, n, k, (int)ntiles, p->msg2_w, p->msg2_b, pk, rng, mean, nullptr, deg, relu_mask};
     const int cus = device_cus();
-#ifndef MMPDE_EDGE_RING
-    // F16X3: one wave per SIMD with the operands in registers (edge_wave.hip)
-    if (pk) {
-        // the wave kernel leaves the side blocks and the division to the node stage
-        return launch_edge_wave(a, b, nbr, deg, n, k, seg_n, p->msg2_b, pk, rng, mean, side, side_cap,
-                                cus, split, st);
-    }
-#endif
+    // F16X3: one wave per SIMD with the operands in registers (edge_wave.hip);
+    // the wave kernel leaves the side blocks and the division to the node stage
+    if (pk)
+        return launch_edge_wave(a, b, nbr, deg, n, k, seg_n, p->msg2_b, pk, rmx, mean, side, side_cap, cus,
+                                split, st);
+    // F32: the exact fp32 ring kernel
+    EdgeArgs e{a, b, nbr, n, k, (int)ntiles, p->msg2_w, p->msg2_b, nullptr, nullptr, mean, nullptr, deg, relu_mask};
     const int grid = ntiles < cus ? (int)ntiles : cus;
     const dim3 block(64 * (4 * EDGE_NC + 4 * EDGE_NP));
-    if (deg) {
-        if (pk) hipLaunchKernelGGL((gnn_edge_kernel<true, EDGE_PH, EDGE_NC, EDGE_NP, true>), dim3(grid), block, 0, st, e);
-        else hipLaunchKernelGGL((gnn_edge_kernel<false, EDGE_PH, EDGE_NC, EDGE_NP, true>), dim3(grid), block, 0, st, e);
-    } else {
-        if (pk) hipLaunchKernelGGL(gnn_edge_kernel<true>, dim3(grid), block, 0, st, e);
-        else hipLaunchKernelGGL(gnn_edge_kernel<false>, dim3(grid), block, 0, st, e);
-    }
+    if (deg) hipLaunchKernelGGL((gnn_edge_kernel<false, EDGE_PH, EDGE_NC, EDGE_NP, true>), dim3(grid), block, 0, st, e);
+    else hipLaunchKernelGGL(gnn_edge_kernel<false>, dim3(grid), block, 0, st, e);
     MMPDE_RET_LAUNCH();
     return MMPDE_OK;
 }
 
-// Range records (layer.hpp) of a, b over ONE segment of all n rows: per
-// 16-row block {max|a|, max|b|, 0, 0}.  One wave per block.
-__global__ __launch_bounds__(256) void range_records_kernel(const float *__restrict__ a, const float *__restrict__ b,
-                                                            int64_t n, float *__restrict__ rng) {
-    const int64_t blk = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (blk >= range_tiles(n)) return;  // wave-uniform
-    float ma = 0.0f, mb = 0.0f;
-    const int64_t r0 = blk * kRangeRows;
-    for (int i = lane; i < kRangeRows * (LH / 4); i += 64) {
-        const int64_t row = min(r0 + i / (LH / 4), n - 1);
-        const int c4 = i % (LH / 4);
-        ma = absmax4(ma, *(const float4 *)(a + row * LH + 4 * c4));
-        mb = absmax4(mb, *(const float4 *)(b + row * LH + 4 * c4));
+// Row maxima (layer.hpp) of a, b for the training forward: rmx[2 i] = max|a_i|,
+// rmx[2 i + 1] = max|b_i| (a NaN counts as 0).  Half a wave per row (32 lanes x
+// one float4 of each).
+__global__ __launch_bounds__(256) void row_max_kernel(const float *__restrict__ a, const float *__restrict__ b,
+                                                      int64_t n, float *__restrict__ rmx) {
+    const int64_t row = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
+    const int c4 = threadIdx.x & 31;
+    const int64_t rr = min(row, n - 1);
+    float ma = absmax4(0.0f, *(const float4 *)(a + rr * LH + 4 * c4));
+    float mb = absmax4(0.0f, *(const float4 *)(b + rr * LH + 4 * c4));
+#pragma unroll
+    for (int o = 16; o >= 1; o >>= 1) {
+        ma = fmaxf(ma, __shfl_xor(ma, o, 32));
+        mb = fmaxf(mb, __shfl_xor(mb, o, 32));
     }
-    ma = wave_max(ma);
-    mb = wave_max(mb);
-    if (lane == 0) *(float4 *)(rng + 4 * blk) = make_float4(ma, mb, 0.0f, 0.0f);
+    if (c4 == 0 && row < n) *(float2 *)(rmx + 2 * row) = make_float2(ma, mb);
 }
 
-int64_t edge_mean_f16x3_ws_bytes(int64_t n) { return kLayerPack + range_tiles(n) * 16; }
+// Split scale of every target row (f16x3.hpp row_split_scale): rsc[i] from
+// max|a_i| + max over the row's neighbours e < deg[i] (ragged tables) or k of
+// max|b_nbr(i,e)|.  One thread per row.
+__global__ __launch_bounds__(256) void row_scale_kernel(const float *__restrict__ rmx, const int32_t *__restrict__ nbr,
+                                                        const int32_t *__restrict__ deg, int64_t n, int k,
+                                                        float *__restrict__ rsc) {
+    const int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (row >= n) return;
+    const int kk = deg ? max(min(deg[row], k), 1) : k;
+    const float mb = nbr_bmax<36>(rmx, nbr + row * k, kk, (uint32_t)(n - 1));
+    rsc[row] = row_split_scale(rmx[2 * row] + mb);
+}
 
-// The edge stage writing the mean itself (the persistent ring kernel), F16X3
-// with this call's own W2 image and range records (one segment of n rows):
-// the training forward (mmpde_gnn_edge_mean_ex), where the weights change every
-// iteration; relu_mask (nullable) receives every slot's z2 > 0 bits for the
-// backward.
+// The edge stage's mean from the wave kernel's neighbour sums (in mean) and
+// side blocks (the node stage's prep_finish, for callers that want the mean
+// itself): sums + the side blocks of the units that start strictly inside
+// the row's tile, in unit order, / max(deg, 1) or / k.  8 threads per row.
+__global__ __launch_bounds__(256) void edge_finish_kernel(float *__restrict__ mean, EdgeSplit sp,
+                                                          const int32_t *__restrict__ deg, int64_t n) {
+    const int64_t row = (int64_t)blockIdx.x * 32 + (threadIdx.x >> 3);
+    const int part = threadIdx.x & 7;
+    if (row >= n) return;
+    float *mp = mean + row * LH + 16 * part;
+    float4 x[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) x[q] = *(const float4 *)(mp + 4 * q);
+    const int64_t S = sp.S, G = sp.units, kk = sp.k;
+    const int64_t sg = row / sp.seg_n, ql = row - sg * sp.seg_n, t = ql / 16;
+    const int64_t lo = max(((t * kk + 1) * G + S - 1) / S, (int64_t)1);
+    const int64_t hi = min(((t + 1) * kk * G + S - 1) / S - 1, G - 1);
+    for (int64_t w = lo; w <= hi; ++w) {
+        const float *q4 = sp.side + ((sg * G + w) * 16 + (ql & 15)) * LH + 16 * part;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float4 y = *(const float4 *)(q4 + 4 * q);
+            x[q] = make_float4(x[q].x + y.x, x[q].y + y.y, x[q].z + y.z, x[q].w + y.w);
+        }
+    }
+    div_rows_rn(x, deg ? (float)max(deg[row], 1) : (float)kk);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) *(float4 *)(mp + 4 * q) = x[q];
+}
+
+// workspace of the F16X3 edge mean: W2's image, the row maxima, then the ring
+// kernel's row scales or the wave kernel's side blocks (one per 16-row tile)
+int64_t edge_mean_f16x3_ws_bytes(int64_t n) {
+    const int64_t tail = ((n + 15) / 16) * 16 * LH;  // >= the n row scales
+    return kLayerPack + (row_max_floats(n) + tail) * 4;
+}
+
+// The edge stage writing the mean itself, F16X3 with this call's own W2 image
+// and row maxima: mmpde_gnn_edge_mean_ex, where the weights change every call.
+// With relu_mask (the training forward: every slot's z2 > 0 bits for the
+// backward) the persistent ring kernel on the rows' split scales; without it
+// the one-wave-per-SIMD kernel of the inference forward (one segment of n rows,
+// one side block per 16-row tile) and edge_finish_kernel.
 int launch_edge_mean_f16x3(const float *a, const float *b, const int32_t *nbr, const int32_t *deg, int64_t n,
                            int k, const float *w2, const float *b2, float *mean, uint32_t *relu_mask, void *ws,
                            hipStream_t st) {
     MMPDE_REQUIRE(a && b && nbr && w2 && b2 && mean && ws && n > 0 && k > 0 && n <= (int64_t)INT32_MAX);
     MMPDE_REQUIRE(al16(a) && al16(b) && al16(w2) && al16(mean) && al16(ws));
+    MMPDE_REQUIRE(!relu_mask || (kEdgeMaskOk && al16(relu_mask)));
     const int64_t ntiles = (n + ET - 1) / ET;
     MMPDE_REQUIRE(ntiles * ((k + ESL - 1) / ESL) < (int64_t)INT32_MAX);
     char *pk = (char *)ws;
-    float *rng = (float *)(pk + kLayerPack);
+    float *rmx = (float *)(pk + kLayerPack);
+    float *rsc = rmx + row_max_floats(n);
     PackSrc src{};
     src.w[0] = w2;
     src.ld[0] = LH;
     hipLaunchKernelGGL(pack_f16x3_kernel<128>, dim3(128, 1), dim3(128), 0, st, src, 0, kPkW2, (int64_t)128, pk);
     MMPDE_RET_LAUNCH();
-    hipLaunchKernelGGL(range_records_kernel, dim3((unsigned)ceil_div(range_tiles(n), 4)), dim3(256), 0, st, a, b, n,
-                       rng);
+    hipLaunchKernelGGL(row_max_kernel, dim3((unsigned)ceil_div(n, 8)), dim3(256), 0, st, a, b, n, rmx);
     MMPDE_RET_LAUNCH();
-    EdgeArgs e{a, b, nbr, n, k, (int)ntiles, w2, b2, pk, rng, mean, nullptr, deg, relu_mask};
     const int cus = device_cus();
+    if (!relu_mask) {
+        float *side = rsc;
+        EdgeSplit split;
+        const int rc = launch_edge_wave(a, b, nbr, deg, n, k, n, b2, pk, rmx, mean, side, ntiles, cus, &split, st);
+        if (rc) return rc;
+        MMPDE_REQUIRE(split.units > 0);
+        hipLaunchKernelGGL(edge_finish_kernel, dim3((unsigned)ceil_div(n, 32)), dim3(256), 0, st, mean, split,
+                           deg, n);
+        MMPDE_RET_LAUNCH();
+        return MMPDE_OK;
+    }
+    hipLaunchKernelGGL(row_scale_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, rmx, nbr, deg, n, k,
+                       rsc);
+    MMPDE_RET_LAUNCH();
+    EdgeArgs e{a, b, nbr, n, k, (int)ntiles, w2, b2, pk, rsc, mean, nullptr, deg, relu_mask};
     const int grid = ntiles < cus ? (int)ntiles : cus;
     const dim3 block(64 * (4 * EDGE_NC + 4 * EDGE_NP));
     if (deg) hipLaunchKernelGGL((gnn_edge_kernel<true, EDGE_PH, EDGE_NC, EDGE_NP, true>), dim3(grid), block, 0, st, e);
@@ -1308,7 +1381,7 @@ static int node_args(const NodeStageCall &c, NodeArgs *out) {
     const bool sums = c.split && c.split->units > 0;
     MMPDE_REQUIRE(!sums || (c.split->side && c.split->S > 0 && c.split->k > 0 && c.split->seg_n > 0 &&
                             c.n % c.split->seg_n == 0));
-    MMPDE_REQUIRE(!c.rng_out || al16(c.rng_out));
+    MMPDE_REQUIRE(!c.rmx_out || al16(c.rmx_out));
     MMPDE_REQUIRE(c.h && c.mean && c.u && c.pos && c.p && c.h_out && c.n > 0);
     MMPDE_REQUIRE(al16(c.h) && al16(c.mean) && al16(c.h_out));
     MMPDE_REQUIRE(c.p->upd1_ld >= 257 && (c.p->upd1_ld & 3) == 0 && al16(c.p->upd1_w) && al16(c.p->upd2_w));
@@ -1316,7 +1389,7 @@ static int node_args(const NodeStageCall &c, NodeArgs *out) {
     const mmpde_gnn_layer_params *p = c.p;
     NodeArgs a{c.h, c.mean, c.n, p->upd1_w, p->upd1_b, p->upd1_ld, p->upd2_w, p->upd2_b, p->bn_w, p->bn_b,
                p->bn_rm, p->bn_rv, p->eps, c.h_out, nullptr, nullptr, 0, c.a_out, c.b_out, c.u, c.pos, c.sc,
-               c.pk, c.pkn, c.rng_out, effective_seg(c.n, c.seg_n), 1, 0, sums ? c.deg : nullptr,
+               c.pk, c.pkn, c.rmx_out, 1, 0, sums ? c.deg : nullptr,
                sums ? c.split->k : 0};
     if (sums) a.split = *c.split;
     if (c.next) {
@@ -1353,9 +1426,9 @@ static int launch_node_stage(const NodeStageCall &c, hipStream_t st) {
 int launch_node_stage(const float *h, const float *mean, const EdgeSplit *split, const int32_t *deg,
                       const float *u, const float *pos, int64_t n, int64_t seg_n, mmpde_gnn_scales sc,
                       const mmpde_gnn_layer_params *p, const mmpde_gnn_layer_params *next,
-                      const char *pk, const char *pkn, float *rng_out, float *h_out, float *a_out,
+                      const char *pk, const char *pkn, float *rmx_out, float *h_out, float *a_out,
                       float *b_out, hipStream_t st) {
-    const NodeStageCall c{h, mean, split, deg, u, pos, n, seg_n, sc, p, next, pk, pkn, rng_out, h_out, a_out,
+    const NodeStageCall c{h, mean, split, deg, u, pos, n, seg_n, sc, p, next, pk, pkn, rmx_out, h_out, a_out,
                           b_out};
     return launch_node_stage(c, st);
 }
@@ -1364,9 +1437,9 @@ static int embed_args(const EmbedStageCall &c, EmbedArgs *out) {
     MMPDE_REQUIRE(c.u && c.pos && c.e && c.l0 && c.h_out && c.a_out && c.b_out && c.n > 0);
     MMPDE_REQUIRE(al16(c.e->w3) && al16(c.h_out) && al16(c.a_out) && al16(c.b_out));
     MMPDE_REQUIRE(c.l0->msg1_ld >= 260 && (c.l0->msg1_ld & 3) == 0 && al16(c.l0->msg1_w));
-    MMPDE_REQUIRE(!c.pk0 || (al16(c.pk0) && c.rng_out && al16(c.rng_out)));
+    MMPDE_REQUIRE(!c.pk0 || (al16(c.pk0) && c.rmx_out && al16(c.rmx_out)));
     *out = EmbedArgs{c.u, c.pos, c.n, c.sc, *c.e, c.h_out, c.l0->msg1_w, c.l0->msg1_b, c.l0->msg1_ld, c.a_out,
-                     c.b_out, c.pk0, c.rng_out, effective_seg(c.n, c.seg_n)};
+                     c.b_out, c.pk0, c.rmx_out};
     return MMPDE_OK;
 }
 
@@ -1386,8 +1459,8 @@ static int launch_embed_stage(const EmbedStageCall &c, hipStream_t st) {
 
 int launch_embed_stage(const float *u, const float *pos, int64_t n, int64_t seg_n, mmpde_gnn_scales sc,
                        const mmpde_gnn_embed_params *e, const mmpde_gnn_layer_params *l0,
-                       const char *pk0, float *rng_out, float *h_out, float *a_out,
+                       const char *pk0, float *rmx_out, float *h_out, float *a_out,
                        float *b_out, hipStream_t st) {
-    const EmbedStageCall c{u, pos, n, seg_n, sc, e, l0, pk0, rng_out, h_out, a_out, b_out};
+    const EmbedStageCall c{u, pos, n, seg_n, sc, e, l0, pk0, rmx_out, h_out, a_out, b_out};
     return launch_embed_stage(c, st);
 }

@@ -3,42 +3,34 @@
 #pragma once
 #include "common.hpp"
 
-// F16X3 range records: the node / embed stage writes, per 16-row block
-// (kRangeRows rows; block index = row / kRangeRows), the max |a| and max |b| of
-// its rows in each of the (at most two) trajectory segments the tile touches:
-// rng[tile] = {max|a| seg0, max|b| seg0, max|a| seg1, max|b| seg1}, seg0 =
-// first row / seg_n (the seg1 entries are 0 when the tile lies in one
-// segment).  The wave edge kernel takes its split scale from the records of
-// its own segment only, so a trajectory's f16x3 result does not depend on the
-// trajectories launched beside it.  Plain stores, no atomics, no zeroing.
-constexpr int kRangeRows = 16;
-__host__ __device__ inline int64_t range_tiles(int64_t n) { return (n + kRangeRows - 1) / kRangeRows; }
+// F16X3 row maxima: the node / embed stage writes, for every row i of the next
+// layer's message_net_1 node halves, rmx[2 i] = max_k |a_i[k]| and rmx[2 i + 1]
+// = max_k |b_i[k]| (a NaN counts as 0; plain stores, no atomics, no zeroing).
+// The edge stage splits target row i's messages relu(a_i + b_j) with a scale of
+// the row's own (f16x3.hpp row_split_scale), from
+//     M_i = max|a_i| + max_e max|b_nbr(i,e)|  >=  max_{e,k} |a_ik + b_jk|,
+// so each row keeps 22 significant bits relative to its own range however far
+// other rows of the trajectory lie above it (round 5's scale was one per
+// trajectory segment: rows 2^14 below the segment maximum fell to an absolute
+// error floor), and a row's result depends on the row and its neighbours only
+// -- not on its segment or on the trajectories launched beside it.
+inline int64_t row_max_floats(int64_t n) { return ((2 * n + 3) / 4) * 4; }  // 16-B multiple
 
-// max |a| + max |b| over segment s from the range records of the node tiles
-// that hold its rows (layer.hpp kRangeRows): a block whose first row lies in s
-// gives its seg0 entries, the block straddling into s from s - 1 its seg1 ones.
-__device__ __forceinline__ float segment_range(const float *rng, int64_t seg_n, int64_t s) {
-    const int64_t r0 = s * seg_n, t0 = r0 / kRangeRows, t1 = (r0 + seg_n - 1) / kRangeRows;
-    float ma = 0.0f, mb = 0.0f;
-    // four records per lane per pass, loaded together (one memory round trip for
-    // segments of up to 256 records): indices past t1 re-read t1, which a max
-    // takes twice harmlessly
-    for (int64_t tb = t0; tb <= t1; tb += 256) {
-        float4 v[4];
-        int64_t tt[4];
+// M_i's neighbour term for row `row`: max over e < kk of rmx[2 nbr[row k + e] + 1]
+// (as bit patterns, indices clamped to nmax), every index load issued before
+// the gathers (two memory round trips).  KU loads are unrolled (clamped to
+// e < kk), the rest (kk > KU) run one by one.
+template <int KU>
+__device__ __forceinline__ float nbr_bmax(const float *rmx, const int32_t *nr, int kk, uint32_t nmax) {
+    const uint32_t *rb = (const uint32_t *)rmx;
+    uint32_t id[KU];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            tt[q] = min(tb + (threadIdx.x & 63) + 64 * q, t1);
-            v[q] = *(const float4 *)(rng + 4 * tt[q]);
-        }
+    for (int e = 0; e < KU; ++e) id[e] = (uint32_t)nr[min(e, kk - 1)];
+    uint32_t m = 0;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const bool own = tt[q] * kRangeRows >= r0;  // first row of the tile in s
-            ma = fmaxf(ma, own ? v[q].x : v[q].z);
-            mb = fmaxf(mb, own ? v[q].y : v[q].w);
-        }
-    }
-    return wave_absmax(ma) + wave_absmax(mb);  // maxima of |x| >= 0; every lane active
+    for (int e = 0; e < KU; ++e) m = max(m, rb[2 * (uint64_t)min(id[e], nmax) + 1]);
+    for (int e = KU; e < kk; ++e) m = max(m, rb[2 * (uint64_t)min((uint32_t)nr[e], nmax) + 1]);
+    return __uint_as_float(m);
 }
 
 // How the wave edge kernel split a layer's neighbour slots (edge_wave.hip
@@ -60,29 +52,31 @@ struct EdgeSplit {
 // Edge stage: mean[i] = (1/k) sum_e relu(W2 relu(a_i + b_nbr(i,e)) + b2)
 // (message_net_2 + PyG mean aggregation); with deg != nullptr the sum runs
 // over e < deg[i] and divides by max(deg[i], 1).  F16X3: pk = this layer's
-// packed images, rng = range records of a, b (both required); it runs the
+// packed images, rmx = row maxima of a, b (both required); it runs the
 // one-wave-per-SIMD kernel, which stores neighbour SUMS to mean plus side
 // blocks (side: room for side_cap 16 x 128 blocks) and fills *split: the node
 // stage then adds the side blocks and divides (pass split to launch_node_stage).
+// rmx: the row maxima of a, b (F16X3).
 // F32 writes the mean itself and leaves split->units = 0.  seg_n: rows per
 // trajectory segment (n: one segment; must divide n and be >= kRangeRows,
 // else n is used).
 int launch_edge_stage(const float *a, const float *b, const int32_t *nbr, const int32_t *deg,
                       int64_t n, int k, int64_t seg_n, const mmpde_gnn_layer_params *p, const char *pk,
-                      const float *rng, float *mean, float *side, int64_t side_cap,
+                      const float *rmx, float *mean, float *side, int64_t side_cap,
                       EdgeSplit *split, hipStream_t st, uint32_t *relu_mask = nullptr);
 
 // The training forward's F16X3 edge stage (writes the mean; packs W2 and
-// computes the range records of a, b itself in ws, edge_mean_f16x3_ws_bytes).
+// computes the row maxima of a, b and every row's split scale itself in ws,
+// edge_mean_f16x3_ws_bytes).
 int64_t edge_mean_f16x3_ws_bytes(int64_t n);
 int launch_edge_mean_f16x3(const float *a, const float *b, const int32_t *nbr, const int32_t *deg, int64_t n,
                            int k, const float *w2, const float *b2, float *mean, uint32_t *relu_mask, void *ws,
                            hipStream_t st);
 
 // Segment size the kernels use for a requested seg_n (n when seg_n is 0, does
-// not divide n or is below kRangeRows).
+// not divide n or is below one 16-row tile).
 inline int64_t effective_seg(int64_t n, int64_t seg_n) {
-    return (seg_n >= kRangeRows && seg_n <= n && n % seg_n == 0) ? seg_n : n;
+    return (seg_n >= 16 && seg_n <= n && n % seg_n == 0) ? seg_n : n;
 }
 
 // Summation units per segment U and waves per segment wpsp of the wave kernel
@@ -90,30 +84,33 @@ inline int64_t effective_seg(int64_t n, int64_t seg_n) {
 // units of 22..44 slots, a function of the segment alone (capped by S_seg and
 // side_cap / nseg), so every launch sums a row in the same order whatever the
 // segment count; wpsp = floor(4 CUs / nseg) clamped to [1, U], each wave
-// taking a contiguous run of whole units.  nseg * U <= side_cap.
+// taking a contiguous run of whole units, raised (more waves than SIMDs) until
+// no wave spans more than kWaveTiles tiles (its row scales live in LDS).
+// nseg * U <= side_cap.
+constexpr int kWaveTiles = 64;
 struct EdgePlan {
     int U = 1, wpsp = 1;
     int64_t waves = 1;
 };
-EdgePlan edge_wave_plan(int64_t nseg, int64_t S_seg, int cus, int64_t side_cap);
+EdgePlan edge_wave_plan(int64_t nseg, int64_t S_seg, int k, int cus, int64_t side_cap);
 
 // Edge stage, F16X3, one wave per SIMD with the message_net_2 operands in
 // registers (edge_wave.hip): neighbour sums to out / side (see EdgeSplit).
 // cus = compute units.
 int launch_edge_wave(const float *a, const float *b, const int32_t *nbr, const int32_t *deg, int64_t n,
-                     int k, int64_t seg_n, const float *msg2_b, const char *pk, const float *rng,
+                     int k, int64_t seg_n, const float *msg2_b, const char *pk, const float *rmx,
                      float *out, float *side, int64_t side_cap, int cus, EdgeSplit *split, hipStream_t st);
 
 // Node stage (mean: the edge stage's buffer, or with split->units > 0 the wave
 // kernel's sums plus side blocks divided by max(deg[row], 1) or split->k):
 // h' = BN(h + relu(U2 relu(U1 [h | mean | t] + c1) + c2)) and, when
 // next != nullptr, the next layer's message_net_1 node halves a', b' (and,
-// F16X3, their range records rng_out over segments of seg_n rows).  F16X3 when
-// pk != nullptr (pkn: the next layer's images).
+// F16X3, their row maxima rmx_out).  F16X3 when pk != nullptr (pkn: the next
+// layer's images).
 int launch_node_stage(const float *h, const float *mean, const EdgeSplit *split, const int32_t *deg,
                       const float *u, const float *pos, int64_t n, int64_t seg_n, mmpde_gnn_scales sc,
                       const mmpde_gnn_layer_params *p, const mmpde_gnn_layer_params *next,
-                      const char *pk, const char *pkn, float *rng_out, float *h_out, float *a_out,
+                      const char *pk, const char *pkn, float *rmx_out, float *h_out, float *a_out,
                       float *b_out, hipStream_t st);
 
 // The arguments of one launch_node_stage call.
@@ -126,7 +123,7 @@ struct NodeStageCall {
     mmpde_gnn_scales sc;
     const mmpde_gnn_layer_params *p, *next;
     const char *pk, *pkn;
-    float *rng_out, *h_out, *a_out, *b_out;
+    float *rmx_out, *h_out, *a_out, *b_out;
 };
 
 // Embedding (gnn_2d.py:99-106) + layer 0's message_net_1 node halves in one
@@ -134,7 +131,7 @@ struct NodeStageCall {
 // launch_node_stage's.  F16X3 projection when pk0 (layer 0's images) != nullptr.
 int launch_embed_stage(const float *u, const float *pos, int64_t n, int64_t seg_n, mmpde_gnn_scales sc,
                        const mmpde_gnn_embed_params *e, const mmpde_gnn_layer_params *l0,
-                       const char *pk0, float *rng_out, float *h_out, float *a_out,
+                       const char *pk0, float *rmx_out, float *h_out, float *a_out,
                        float *b_out, hipStream_t st);
 
 // launch_embed_stage's arguments.
@@ -145,5 +142,5 @@ struct EmbedStageCall {
     const mmpde_gnn_embed_params *e;
     const mmpde_gnn_layer_params *l0;
     const char *pk0;
-    float *rng_out, *h_out, *a_out, *b_out;
+    float *rmx_out, *h_out, *a_out, *b_out;
 };

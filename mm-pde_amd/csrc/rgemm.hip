@@ -371,7 +371,9 @@ __global__ __launch_bounds__(256, GMASK && XS ? 2 : 3) void rgemm_tn_partial_ker
     const int kb = 64 * blockIdx.x;       // first partial column of this block
     const int64_t c0r = (int64_t)chunk * g.chunk_rows;
     const int64_t c1r = min(c0r + (int64_t)g.chunk_rows, g.m);
-    const int64_t qrows = (g.chunk_rows / 4 + 1) & ~(int64_t)1;  // even rows per wave
+    // even rows per wave, 4 * qrows >= chunk_rows (the same split as chunk_rows / 4
+    // rounded up to even for every multiple of 4)
+    const int64_t qrows = ((g.chunk_rows + 3) / 4 + 1) & ~(int64_t)1;
     const int64_t r0 = min(c0r + wave * qrows, c1r), r1 = min(r0 + qrows, c1r);
     // G columns c0, c0 + 1 of this lane (tiles ct = 0, 1); clamped loads, masked values
     const int c0 = cb + 2 * j;

@@ -29,6 +29,17 @@ import torch
 from torch import nn
 
 from . import _lib as L
+
+# Diagnostic record (tests only; None in normal use): while it is a list, every
+# train-mode forward appends the activation pattern the HIP kernels evaluated
+# -- ("emb", z > 0) for the embedding's ReLU of each solver, then per fused GNN
+# layer ("layer", a, b, v > 0, upd > 0, relu_mask): message_net_1's halves (the
+# z1 = a_i + b_j > 0 pattern), message_net_2's z2 > 0 bits (relu_mask words,
+# mmpde_gnn_edge_mean_ex) and update_net_1 / _2's patterns.  The training tests
+# feed it to the float64 oracle (oracle/refcpu.py RELU_PATTERN), so gradients
+# are compared on one activation pattern.
+RELU_RECORD = None
+
 from .ops import (HeadTrain, LinearRows, batch_norm_rows, head_train_fits, linear_train, nbr_table_from_edge_index,
                   reverse_adjacency)
 
@@ -84,9 +95,11 @@ class EdgeGraph:
         return self._rev
 
 
-def _edge_mean_fwd(a, b, w2, b2, graph: EdgeGraph, edge_gemm: str):
+def _edge_mean_fwd(a, b, w2, b2, graph: EdgeGraph, edge_gemm: str, keep_mask: bool = True):
     """mean_i over the in-edges of relu(W2 relu(a_i + b_j) + b2) (EdgeMean's
-    forward): (mean [n, 128], the f16x3 ReLU pattern of message_net_2 or None)."""
+    forward): (mean [n, 128], the f16x3 ReLU pattern of message_net_2 or None).
+    keep_mask False (no backward will run): no ReLU pattern, and the f16x3
+    mode runs the inference forward's wave kernel instead of the ring kernel."""
     n, k = graph.nbr.shape
     mean = torch.empty((n, 128), dtype=torch.float32, device=a.device)
     mode = L.EDGE_GEMM[edge_gemm]
@@ -96,7 +109,7 @@ def _edge_mean_fwd(a, b, w2, b2, graph: EdgeGraph, edge_gemm: str):
     # the forward keeps message_net_2's ReLU pattern (16 B per edge) for the
     # backward, which then skips recomputing z2 (and differentiates exactly the
     # function the forward evaluated: its own z2 summation order differs)
-    mask = torch.empty((n * k, 4), dtype=torch.int32, device=a.device) if k <= 64 else None
+    mask = torch.empty((n * k, 4), dtype=torch.int32, device=a.device) if k <= 64 and keep_mask else None
     L.check(lib.mmpde_gnn_edge_mean_ex(L.ptr(a), L.ptr(b), L.ptr(graph.nbr), L.ptr(graph.deg), n, k,
                                        L.ptr(w2), L.ptr(b2), L.ptr(mean), L.ptr(mask), mode, L.ptr(ws), wsb,
                                        L.stream(a.device)),
@@ -146,7 +159,7 @@ class EdgeMean(torch.autograd.Function):
             raise ValueError("EdgeMean takes a, b [n, 128] and W2 [128, 128]")
         L.require_device(a, b, w2, b2, graph.nbr, graph.deg)
         a, b, w2, b2 = L.f32c(a), L.f32c(b), L.f32c(w2), L.f32c(b2)
-        mean, mask = _edge_mean_fwd(a, b, w2, b2, graph, edge_gemm)
+        mean, mask = _edge_mean_fwd(a, b, w2, b2, graph, edge_gemm, keep_mask=any(ctx.needs_input_grad[:4]))
         ctx.save_for_backward(a, b, w2, b2)
         ctx.graph = graph
         ctx.mask = mask
@@ -221,6 +234,8 @@ class GnnLayerTrain(torch.autograd.Function):
             L.ptr(h), L.ptr(upd), n, 128, L.ptr(BW), L.ptr(L.f32c(bnb) if bnb is not None else None),
             float(bn.eps), float(factor), L.ptr(rm), L.ptr(rv), L.ptr(hn), L.ptr(stats), L.ptr(ws), nb, st),
             "mmpde_batch_norm_rows_train")
+        if RELU_RECORD is not None:
+            RELU_RECORD.append(("layer", a, b, v > 0, upd > 0, mask))
         ctx.save_for_backward(h, extras, a, b, mean, v, upd, stats, W1, B1, W2, B2, U1, U2, BW)
         ctx.graph, ctx.mask, ctx.edge_gemm, ctx.bn_ws = graph, mask, edge_gemm, nb
         ctx.has_bn = (bnw is not None, bnb is not None)
@@ -341,9 +356,12 @@ class GNN_Layer_FS_2D(nn.Module):  # noqa: N801 - reference name
 
     def fused_train_ok(self):
         """GnnLayerTrain covers the reference defaults (width 128, time_window 1,
-        one variable)."""
+        one variable) with its BatchNorm in training mode (batch statistics,
+        running-stat update); a BatchNorm held in eval mode inside a training
+        model (e.g. a frozen norm) takes the unfused path, whose BatchNormRows
+        applies the running statistics."""
         return (self.in_features == self.out_features == self.hidden_features == 128
-                and self.time_window == 1 and self.n_variables == 1)
+                and self.time_window == 1 and self.n_variables == 1 and self.norm.module.training)
 
     def train_forward_fused(self, h, extras, graph: EdgeGraph, edge_gemm: str = "f32"):
         """gnn_2d.py:53-69 in train mode as one GnnLayerTrain (extras = (u, x/Lx,
@@ -575,6 +593,8 @@ class MP_PDE_Solver_2D(nn.Module):  # noqa: N801 - reference name
         e = self.embedding_mlp
         node_input = torch.cat((u, pos_x, pos_y, variables), -1)
         z = torch.relu(batch_norm_rows(e[1], linear_train(node_input, e[0])))
+        if RELU_RECORD is not None:
+            RELU_RECORD.append(("emb", (z > 0).detach()))
         h = batch_norm_rows(e[4], linear_train(z, e[3]))
         for layer in self.gnn_layers:
             if layer.fused_train_ok() and self.time_window == 1 and h.shape[0] >= 2:

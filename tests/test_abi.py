@@ -41,7 +41,7 @@ def test_version_and_status_strings_without_gpu():
     assert lib.mmpde_status_string(-1) == b"invalid argument"
     # sizing helpers are pure host arithmetic
     # 8 [n, 128] buffers, one 16-B range record per 32-row node tile, 16 layers' images
-    assert lib.mmpde_gnn_workspace_bytes(1000) == 8 * 1000 * 128 * 4 + 63 * 16 + 16 * 395776  # 16-row range records
+    assert lib.mmpde_gnn_workspace_bytes(1000) == 8 * 1000 * 128 * 4 + 2000 * 4 + 16 * 395776  # row maxima
     assert lib.mmpde_gnn_pack_bytes(6) == 6 * 395776
     assert lib.mmpde_itp_pack_bytes() > 0
 

@@ -79,10 +79,11 @@ def _row_err(out, ref64, mag):
 # the node and the embed kernels): u is scaled by 2^p on a compact region of
 # 1.5 % of each trajectory's nodes, which carries hidden states far above the
 # rest (eval BatchNorm is affine; with layers = 1 the hot rows reach one hop).
-# The edge kernel's split scale is one per trajectory segment, so the cold
-# rows sit far below it; the node / embed kernels scale per row.  Each row's
-# error vs float64, relative to that row's own magnitude (max |h_L| of the row
-# in float64), stays within 4x of the fp32 errors on the cold and the hot rows.
+# The edge kernels split each target row with a scale of its own (from the
+# row's max|a| and its neighbours' max|b|, layer.hpp row maxima), the node /
+# embed kernels scale per row.  Each row's error vs float64, relative to that
+# row's own magnitude (max |h_L| of the row in float64), stays within 4x of the
+# fp32 errors on the cold and the hot rows.
 @pytest.mark.parametrize("layers", [1, 6])
 @pytest.mark.parametrize("p", [8, 12, 16, 20])
 def test_f16x3_wide_range_solver(dev, p, layers):
@@ -123,19 +124,21 @@ def test_f16x3_wide_range_solver(dev, p, layers):
 
 
 # The split's range (f16x3.hpp split2_relu_rtz): relu(a_i + b_j) is scaled by
-# sc with sc * M in [2^10, 2^11), M = max|a| + max|b| over the trajectory
-# segment; hi is fp16 (RTZ), lo = RN_f16(x - hi).  lo stays a normal fp16 number
-# -- 22 significant bits in all, fp32-class -- while |x| >= 2^-14 M; below it
-# lo's spacing is the fp16 subnormal 2^-24, an absolute error <= 2^-25 / sc
-# <= 2^-35 M per element.  Per output row i (|z1| <= m_i):
-#     |err_i| <= fp32-class + 2^-35 M L1(W2)   (relative: + 2^-35 M / m_i).
-# Rows within 2^14 of M meet the 4x-of-fp32 bar; p = 16, 20 check the floor.
+# s_i with s_i M_i in [2^10, 2^11), M_i = max|a_i| + max_e max|b_nbr(i,e)| -- a
+# scale per TARGET ROW (layer.hpp row maxima); hi is fp16 (RTZ), lo = RN_f16(x -
+# hi).  lo stays a normal fp16 number -- 22 significant bits in all, fp32-class
+# -- while |x| >= 2^-14 M_i; below it lo's spacing is the fp16 subnormal 2^-24,
+# an absolute error <= 2^-35 M_i per element, i.e. relative to the row's own
+# range.  Round 5's scale was one per trajectory segment (M = max|a| + max|b|
+# over the segment), and rows 2^16-2^20 below it missed the 4x bar on the
+# cold rows (9x at p = 16, 119x at p = 20); with the row scale every p
+# asserts the same bar.
 @pytest.mark.parametrize("p", [8, 12, 16, 20])
 def test_f16x3_wide_range_edge_mean(dev, p):
     """EdgeMean (the training forward's f16x3 edge stage, gnn_2d.py:59-63 +
     mean) on a, b whose hot rows (1.5 %) are 2^p above the rest, against
     float64 per row, relative to the row's own magnitude m_i L1(W2),
-    m_i = max_e |a_i + b_j|."""
+    m_i = max_e |a_i + b_j|: within 4x of the fp32 errors on cold and hot rows."""
     from mmpde_amd.gnn_2d import EdgeGraph, EdgeMean
     from mmpde_amd.synth import cy_synth_mesh
 
@@ -158,27 +161,25 @@ def test_f16x3_wide_range_edge_mean(dev, p):
     m_row = s64.abs().amax((1, 2))
     l1 = w2.abs().sum(1).max().double()
     mag = m_row * l1
-    # the kernel's M: one segment (the whole call)
     M = (a.abs().max() + b.abs().max()).double()
     graph = EdgeGraph(nbr.int().to(dev))
     outs = {"cpu-f32": cpu32}
-    for mode in ("f32", "f16x3"):
-        outs[mode] = EdgeMean.apply(a.to(dev), b.to(dev), w2.to(dev), b2.to(dev), graph,
-                                    mode).double().cpu()
+    # f16x3-ring: the training forward (inputs that need a gradient: the
+    # persistent ring kernel, which also keeps the ReLU pattern); f16x3-wave:
+    # no gradient, the inference forward's one-wave-per-SIMD kernel
+    for name, mode, grad in (("f32", "f32", False), ("f16x3-ring", "f16x3", True),
+                             ("f16x3-wave", "f16x3", False)):
+        ad = a.to(dev).requires_grad_(grad)
+        outs[name] = EdgeMean.apply(ad, b.to(dev), w2.to(dev), b2.to(dev), graph, mode).detach().double().cpu()
     rows_hot = m_row > 2 ** (p - 2)
     msg = [f"p={p}: M / min m_i = {(M / m_row.min()).item():.3g}"]
     for name, rows in (("cold", ~rows_hot), ("hot", rows_hot)):
         e = {m: _row_err(o[rows], ref64[rows], mag[rows][:, None]) for m, o in outs.items()}
         msg.append(f"{name} rows ({int(rows.sum())}) rel err max / rms: "
                    + ", ".join(f"{m} {e[m][0]:.3e} / {e[m][1]:.3e}" for m in e))
-        f32_max = max(e["f32"][0], e["cpu-f32"][0])
-        if p <= 12:
+        for m in ("f16x3-ring", "f16x3-wave"):
             for i in (0, 1):
-                assert e["f16x3"][i] <= 4.0 * max(e["f32"][i], e["cpu-f32"][i]) + 1e-12, "\n".join(msg)
-        else:
-            rel = ((outs["f16x3"][rows] - ref64[rows]).abs() / mag[rows][:, None]).amax(1)
-            bound = 4.0 * f32_max + 2.0 ** -35 * M / m_row[rows]
-            assert bool((rel <= bound).all()), "\n".join(msg)
+                assert e[m][i] <= 4.0 * max(e["f32"][i], e["cpu-f32"][i]) + 1e-12, "\n".join(msg)
     print("\n".join(msg))
 
 

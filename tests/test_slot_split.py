@@ -20,7 +20,10 @@ def closed_form(t, k, U, S):
     return lo, hi
 
 
-def plan(nseg, S_seg, cus=256, side_cap=1 << 40):
+K_WAVE_TILES = 64   # layer.hpp kWaveTiles: a wave's row split scales live in LDS
+
+
+def plan(nseg, S_seg, cus=256, side_cap=1 << 40, k=35):
     """edge_wave_plan (edge_wave.hip): (U, waves per segment, waves)."""
     U = 1
     while U * 2 * 22 <= S_seg:
@@ -32,7 +35,26 @@ def plan(nseg, S_seg, cus=256, side_cap=1 << 40):
     if U > cap:
         U = max(cap, 1)
     w = min(max(4 * cus // nseg, 1), U)
+    spu = -(-S_seg // U)
+
+    def tiles_of(ww):
+        return (-(-U // ww) * spu + k - 1) // k + 1
+
+    while w < U and tiles_of(w) > K_WAVE_TILES:
+        w = min(2 * w, U)
+    assert tiles_of(w) <= K_WAVE_TILES
     return U, w, nseg * w
+
+
+def tiles_spanned(ntiles, k, U, w):
+    """Largest number of tiles one wave's slot range touches."""
+    S = ntiles * k
+    most = 0
+    for j in range(w):
+        s0, s1 = (j * U // w) * S // U, ((j + 1) * U // w) * S // U
+        if s0 < s1:
+            most = max(most, (s1 - 1) // k - s0 // k + 1)
+    return most
 
 
 def runs(ntiles, k, U, w):
@@ -116,3 +138,17 @@ def test_plan_is_segment_only_and_fills_the_chip():
     S_96 = 576 * 35
     assert plan(1, S_96, side_cap=3 * 9216 // 16) == (1024, 1024, 1024)
     assert len({plan(nseg, S_96)[0] for nseg in range(1, 9)}) == 1
+
+
+@pytest.mark.parametrize("nseg,ntiles,k", [(16, 158, 35), (2048, 158, 35), (4096, 144, 35), (1, 65536, 35),
+                                           (3000, 300, 8), (1, 1 << 20, 35)])
+def test_plan_keeps_a_wave_within_its_lds_tiles(nseg, ntiles, k):
+    """Many segments (one wave per segment by the SIMD count) or one huge
+    segment: the plan adds waves until none spans more than kWaveTiles tiles
+    (its row split scales are computed once into LDS); U, hence every sum,
+    is unchanged."""
+    S = ntiles * k
+    U, w, waves = plan(nseg, S, side_cap=nseg * 3 * ntiles, k=k)
+    U0 = plan(1, S, side_cap=3 * ntiles, k=k)[0]
+    assert U == U0
+    assert tiles_spanned(ntiles, k, U, w) <= K_WAVE_TILES
