@@ -183,10 +183,11 @@ def main():
                     help="message_net_2 arithmetic (include/mmpde_hip.h MMPDE_EDGE_GEMM_*)")
     ap.add_argument("--no-f32-exact", action="store_true",
                     help="skip the second, exact-fp32-MFMA timed run reported as f32_exact")
-    ap.add_argument("--graph", action="store_true",
-                    help="replay one hipGraph capture of the step instead of launching it "
-                         "eagerly (measured 2.50 vs 2.44 ms/step eager at cy B=16: the "
-                         "eager three-stream step is not launch-bound)")
+    ap.add_argument("--graph", nargs="?", const="streams", default=None, choices=["streams", "serial"],
+                    help="replay hipGraph captures of the step instead of launching it eagerly: "
+                         "'streams' (default) one graph per stage replayed on the stage's own "
+                         "stream (MMPDERollout.enable_graph); 'serial' every stage on one stream "
+                         "(the diagnostic baseline of the stream overlap)")
     ap.add_argument("--dist-backend", default=None, choices=["nccl", "gloo"],
                     help="process-group backend under torchrun (default nccl = RCCL; gloo "
                          "lets several ranks share one GPU, for rehearsing the multi-rank path)")
@@ -262,7 +263,7 @@ def main():
                 u = eng.step(u, 1 + i % n_t)
             if graph:  # capture after the eager warmup (weights packed, caches built)
                 hook, eng.trace_hook = eng.trace_hook, None
-                eng.enable_graph(u)
+                eng.enable_graph(u, serial=args.graph == "serial")
                 eng.trace_hook = hook
                 u = u.clone()
             run = eng.graph_step if graph else eng.step
@@ -345,7 +346,10 @@ def main():
                    "shard": "contiguous trajectory blocks, dist.shard_range; rank 0 holds "
                             f"{hi - lo}",
                    "rollout": "autoregressive (pred -> next input)",
-                   "launch": "hipGraph replay of the step" if args.graph else "eager, three HIP streams"},
+                   "launch": ("hipGraph replay of the step, one graph per stage on its own stream"
+                              if args.graph == "streams" else
+                              "hipGraph replay of the step, every stage on one stream" if args.graph else
+                              "eager, three HIP streams")},
         "roofline": {"kernel": ("gnn_edge_wave_kernel" if args.edge_gemm == "f16x3" else "gnn_edge_kernel")
                                + " (message_net_2 over every edge + mean aggregation, one launch "
                                "per GNN layer, 12 per step)",

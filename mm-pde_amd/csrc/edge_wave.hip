@@ -72,6 +72,7 @@ struct WaveArgs {
     const float *b2;          // message_net_2.0 bias
     const char *pk;           // this layer's packed images (W2 at kPkW2)
     const float *rmx;         // row maxima of a, b (layer.hpp)
+    const float *rec;         // their range records (nullable: every segment per-row)
     float *out;               // neighbour sums of the units that start a tile
     float *side;              // [G][16][128]: the unit a wave starts inside a tile
 };
@@ -148,76 +149,6 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
     // destination of the run being computed: -1 = out (it starts its tile),
     // else the side block of the unit it starts
     int run_side = s0 % k ? seg * p.U + u_begin : -1;
-    // Split scales of the rows of this wave's tiles (at most kWaveTiles,
-    // edge_wave_plan): lane (g, r) takes row r of tile tb + g, its neighbours'
-    // row maxima, |a_i + b_j| <= max|a_i| + max_e max|b_j| scaled below 2^11
-    // (split8_relu_rtz).  The first four tiles (every wave of the cylinder and
-    // Burgers plans): the index loads go out before the W2 image, the gathers
-    // all together right after it, so the two round trips overlap the image.
-    constexpr int KU = 36;  // neighbour slots loaded unrolled (more: one by one)
-    __shared__ float rs_lds[kWaveTiles * ET];
-    const int t_first = (int)(s0 / k), t_last = min((int)((s1 - 1) / k), p.tps - 1);
-    const uint32_t *rmxb = (const uint32_t *)p.rmx;
-    const uint32_t nmaxu = (uint32_t)nmax;
-    auto pass_row = [&](int tb) { return base + min(min(tb + g, t_last) * ET + r, last); };
-    auto pass_kk = [&](int64_t row) { return RAGGED ? max(min(p.deg[row], k), 1) : k; };
-    auto pass_idx = [&](int64_t row, int kk, uint32_t *id) {
-#pragma unroll
-        for (int e = 0; e < KU; ++e) id[e] = (uint32_t)p.nbr[row * k + min(e, kk - 1)];
-    };
-    auto pass_scale = [&](int tb, int64_t row, int kk, const uint32_t *id, float ma) {
-        uint32_t v[KU];
-#pragma unroll
-        for (int e = 0; e < KU; ++e) v[e] = rmxb[2 * (uint64_t)min(id[e], nmaxu) + 1];
-        uint32_t m = 0;
-#pragma unroll
-        for (int e = 0; e < KU; ++e) m = max(m, v[e]);
-        for (int e = KU; e < kk; ++e) m = max(m, rmxb[2 * (uint64_t)min((uint32_t)p.nbr[row * k + e], nmaxu) + 1]);
-        if (tb + g <= t_last) rs_lds[(tb + g - t_first) * ET + r] = row_split_scale(ma + __uint_as_float(m));
-    };
-    const int64_t row_p0 = pass_row(t_first);
-    const int kk_p0 = pass_kk(row_p0);
-    uint32_t id_p0[KU];
-    pass_idx(row_p0, kk_p0, id_p0);
-    const float ma_p0 = p.rmx[2 * row_p0];
-    __builtin_amdgcn_sched_barrier(0);  // these loads issue before the image's
-    // message_net_2: B operands (AGPRs), accumulator start (bias in the column
-    // scale, times the row scales of the MFMA slot's tile), column unscale
-    half8 wh[8][4], wl[8][4];
-    float bb0[8], inv[8];
-    f32x4 bias[8];
-    {
-        const char *img = p.pk + kPkW2;
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                wh[c][s] = pin_agpr(bfrag(img, 4, c, s, 0, lane));
-                wl[c][s] = pin_agpr(bfrag(img, 4, c, s, 1, lane));
-            }
-            const float sw = ((const float *)(img + 65536))[16 * c + r];
-            bb0[c] = p.b2[16 * c + r] * sw;
-            inv[c] = pow2_inv(sw);
-        }
-    }
-    pass_scale(t_first, row_p0, kk_p0, id_p0, ma_p0);
-    for (int tb = t_first + 4; tb <= t_last; tb += 4) {  // waves spanning more than four tiles
-        const int64_t row = pass_row(tb);
-        const int kk = pass_kk(row);
-        uint32_t id[KU];
-        pass_idx(row, kk, id);
-        pass_scale(tb, row, kk, id, p.rmx[2 * row]);
-    }
-    __syncthreads();  // one wave: the LDS writes of every lane before any read
-    // LDS slot of a tile's row scales (tiles past the wave's last, which only a
-    // prefetch past the end touches, read the last one's)
-    auto rs_of = [&](int tile) { return &rs_lds[(min(tile, t_last) - t_first) * ET]; };
-    // the accumulator start of a tile's slots: rows 4 g + t of this lane
-    auto set_bias = [&](int tile) {
-        const float4 s4 = *(const float4 *)(rs_of(tile) + 4 * g);
-#pragma unroll
-        for (int c = 0; c < 8; ++c) bias[c] = (f32x4){bb0[c] * s4.x, bb0[c] * s4.y, bb0[c] * s4.z, bb0[c] * s4.w};
-    };
     // F16X3 operand piece i of this lane: k = 32 (i >> 1) + 8 g + 4 (i & 1) .. + 3
     auto piece = [&](int i) { return 32 * (i >> 1) + 8 * g + 4 * (i & 1); };
     auto unit_tile = [&](const SlotCtr &c) { return min(c.tile, p.tps - 1); };
@@ -249,6 +180,88 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
     cI = cS;
     cI.next(k);
     cI.next(k);
+    // Split scales of the rows of this wave's tiles (at most kWaveTiles,
+    // edge_wave_plan), |relu(a_i + b_j)| s_i < 2^11 (split8_relu_rtz), into LDS.
+    // A segment whose range records (layer.hpp) show a narrow range -- every
+    // row's bound within 2^12 of the segment's -- gives every row the
+    // segment's scale (no neighbour gathers; the records go out before the W2
+    // image).  Otherwise each lane takes one row of four tiles (a pass):
+    // M_i = max|a_i| + max_e max|b_nbr(i,e)| from the row maxima, the index
+    // loads and then the gathers all in flight together.
+    constexpr int KU = 36;  // neighbour slots loaded unrolled (more: one by one)
+    __shared__ float rs_lds[kWaveTiles * ET];
+    const int t_first = (int)(s0 / k), t_last = min((int)((s1 - 1) / k), p.tps - 1);
+    const uint32_t *rmxb = (const uint32_t *)p.rmx;
+    const uint32_t nmaxu = (uint32_t)nmax;
+    auto pass_row = [&](int tb) { return base + min(min(tb + g, t_last) * ET + r, last); };
+    auto pass_scale = [&](int tb) {
+        const int64_t row = pass_row(tb);
+        const int kk = RAGGED ? max(min(p.deg[row], k), 1) : k;
+        uint32_t id[KU], v[KU];
+#pragma unroll
+        for (int e = 0; e < KU; ++e) id[e] = (uint32_t)p.nbr[row * k + min(e, kk - 1)];
+        const float ma = p.rmx[2 * row];
+#pragma unroll
+        for (int e = 0; e < KU; ++e) v[e] = rmxb[2 * (uint64_t)min(id[e], nmaxu) + 1];
+        uint32_t m = 0;
+#pragma unroll
+        for (int e = 0; e < KU; ++e) m = max(m, v[e]);
+        for (int e = KU; e < kk; ++e) m = max(m, rmxb[2 * (uint64_t)min((uint32_t)p.nbr[row * k + e], nmaxu) + 1]);
+        if (tb + g <= t_last) rs_lds[(tb + g - t_first) * ET + r] = row_split_scale(ma + __uint_as_float(m));
+    };
+    // slot 0's neighbour index and a rows, then the segment's range records,
+    // all before the W2 image; slot 0's b rows go out after it
+    const int atile0 = unit_tile(cC);
+    const uint32_t src0 = src_of(cC);
+    float4 araw[8];
+    {
+        const float *ar = p.a + grow(atile0 * ET + r) * LH;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) araw[i] = *(const float4 *)(ar + piece(i));
+    }
+    float2 seg_ml = make_float2(0.0f, 0.0f);
+    if (p.rec) seg_ml = segment_stats(p.rec, p.seg_n, seg);
+    __builtin_amdgcn_sched_barrier(0);  // these loads issue before the image's
+    // message_net_2: B operands (AGPRs), accumulator start (bias in the column
+    // scale, times the row scales of the MFMA slot's tile), column unscale
+    half8 wh[8][4], wl[8][4];
+    float bb0[8], inv[8];
+    f32x4 bias[8];
+    {
+        const char *img = p.pk + kPkW2;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                wh[c][s] = pin_agpr(bfrag(img, 4, c, s, 0, lane));
+                wl[c][s] = pin_agpr(bfrag(img, 4, c, s, 1, lane));
+            }
+            const float sw = ((const float *)(img + 65536))[16 * c + r];
+            bb0[c] = p.b2[16 * c + r] * sw;
+            inv[c] = pow2_inv(sw);
+        }
+    }
+    float4 bx[8];
+    gather(bx, src0);
+    // narrow: L_seg >= 2^-12 M_seg (layer.hpp range records; an infinite or NaN
+    // M_seg never is, and takes the per-row path)
+    const bool narrow = p.rec && seg_ml.y >= 0x1p-12f * seg_ml.x;
+    if (narrow) {
+        const float ss = row_split_scale(seg_ml.x);
+        for (int i = lane; i < (t_last - t_first + 1) * ET; i += 64) rs_lds[i] = ss;
+    } else {
+        for (int tb = t_first; tb <= t_last; tb += 4) pass_scale(tb);
+    }
+    __syncthreads();  // one wave: the LDS writes of every lane before any read
+    // LDS slot of a tile's row scales (tiles past the wave's last, which only a
+    // prefetch past the end touches, read the last one's)
+    auto rs_of = [&](int tile) { return &rs_lds[(min(tile, t_last) - t_first) * ET]; };
+    // the accumulator start of a tile's slots: rows 4 g + t of this lane
+    auto set_bias = [&](int tile) {
+        const float4 s4 = *(const float4 *)(rs_of(tile) + 4 * g);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) bias[c] = (f32x4){bb0[c] * s4.x, bb0[c] * s4.y, bb0[c] * s4.z, bb0[c] * s4.w};
+    };
     float4 av[8];  // a rows of the split slot's tile (scaled), this lane's pieces
     float sc = 1.0f;  // split scale of this lane's row (r) of the split slot's tile
     auto load_a = [&](int tile) {
@@ -281,12 +294,12 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
     f32x4 S[8];
     int dg[4] = {k, k, k, k}, dg_prev[4] = {k, k, k, k};
     uint32_t hA[4][4], lA[4][4], hB[4][4], lB[4][4];
-    float4 bx[8];
-    int atile = unit_tile(cC);
-    load_a(atile);
+    int atile = atile0;
+    sc = rs_of(atile)[r];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) av[i] = make_float4(araw[i].x * sc, araw[i].y * sc, araw[i].z * sc, araw[i].w * sc);
     set_bias(atile);
     if (RAGGED) load_deg(dg, cC);
-    gather(bx, src_of(cC));
 #pragma unroll
     for (int j = 0; j < 16; ++j) split_pair(j, bx, hA, lA);
     gather(bx, src_of(cS));
@@ -505,14 +518,15 @@ EdgePlan edge_wave_plan(int64_t nseg, int64_t S_seg, int k, int cus, int64_t sid
 namespace {
 // Kernel arguments and grid of one launch (slot split of layer.hpp EdgeSplit).
 int edge_wave_setup(const float *a, const float *b, const int32_t *nbr, const int32_t *deg, int64_t n,
-                    int k, int64_t seg_n, const float *msg2_b, const char *pk, const float *rmx,
+                    int k, int64_t seg_n, const float *msg2_b, const char *pk, const float *rmx, bool rng,
                     float *out, float *side, int64_t side_cap, int cus, WaveArgs *w, EdgeSplit *split) {
     seg_n = effective_seg(n, seg_n);
     const int64_t nseg = n / seg_n, tps = (seg_n + ET - 1) / ET, S = tps * k;
     if (!(tps < (int64_t)INT32_MAX && S < ((int64_t)1 << 40) && side_cap >= nseg)) return 0;
     const EdgePlan pl = edge_wave_plan(nseg, S, k, cus, side_cap);
     if (pl.wpsp < 1 || pl.waves > (int64_t)INT32_MAX || nseg * pl.U > (int64_t)INT32_MAX) return 0;
-    *w = WaveArgs{a, b, nbr, deg, n, k, seg_n, (int)tps, S, pl.U, pl.wpsp, msg2_b, pk, rmx, out, side};
+    *w = WaveArgs{a, b, nbr, deg, n, k, seg_n, (int)tps, S, pl.U, pl.wpsp, msg2_b, pk, rmx,
+                  rng ? rmx + row_max_floats(n) : nullptr, out, side};
     *split = EdgeSplit{side, S, pl.U, k, seg_n};
     return (int)pl.waves;
 }
@@ -525,7 +539,7 @@ int launch_edge_wave_diag(const float *a, const float *b, const int32_t *nbr, in
                           float *side, int cus, int diag, hipStream_t st) {
     WaveArgs w;
     EdgeSplit split;
-    const int grid = edge_wave_setup(a, b, nbr, nullptr, n, k, n, msg2_b, pk, rmx, out, side,
+    const int grid = edge_wave_setup(a, b, nbr, nullptr, n, k, n, msg2_b, pk, rmx, false, out, side,
                                      4 * (int64_t)cus, cus, &w, &split);
     MMPDE_REQUIRE(grid > 0);
 #define MMPDE_DIAG(D) \
@@ -550,11 +564,11 @@ int launch_edge_wave_diag(const float *a, const float *b, const int32_t *nbr, in
 }
 
 int launch_edge_wave(const float *a, const float *b, const int32_t *nbr, const int32_t *deg, int64_t n,
-                     int k, int64_t seg_n, const float *msg2_b, const char *pk, const float *rmx,
+                     int k, int64_t seg_n, const float *msg2_b, const char *pk, const float *rmx, bool rng,
                      float *out, float *side, int64_t side_cap, int cus, EdgeSplit *split, hipStream_t st) {
     MMPDE_REQUIRE(a && b && nbr && msg2_b && pk && rmx && out && side && split && n > 0 && k > 0);
     WaveArgs w;
-    const int grid = edge_wave_setup(a, b, nbr, deg, n, k, seg_n, msg2_b, pk, rmx, out, side, side_cap,
+    const int grid = edge_wave_setup(a, b, nbr, deg, n, k, seg_n, msg2_b, pk, rmx, rng, out, side, side_cap,
                                      cus, &w, split);
     MMPDE_REQUIRE(grid > 0);
     if (deg) hipLaunchKernelGGL((gnn_edge_wave_kernel<true>), dim3(grid), dim3(64), 0, st, w);

@@ -363,7 +363,7 @@ extern "C" int64_t mmpde_gnn_workspace_bytes(int64_t n) {
     // kernel's side blocks = 8 x [n,128] fp32 (the unfused per-layer API uses 4
     // of them as a, b, mean, v), then the F16X3 row maxima (layer.hpp) and
     // room for per-call weight images
-    return kGnnBufs * n * H * (int64_t)sizeof(float) + row_max_floats(n) * 4 +
+    return kGnnBufs * n * H * (int64_t)sizeof(float) + row_records_floats(n) * 4 +
            (int64_t)MMPDE_GNN_MAX_LAYERS * kLayerPack;
 }
 
@@ -567,7 +567,8 @@ extern "C" int mmpde_gnn_forward_ex(const float *u, const float *pos, int64_t n,
     float *hb[2] = {ws, ws + n * H};
     float *wa = ws + 2 * n * H, *wb = ws + 3 * n * H, *wmean = ws + 4 * n * H;
     const char *pack = nullptr;
-    // row maxima of the current layer's message inputs (F16X3 split scales):
+    // row maxima and range records of the current layer's message inputs
+    // (F16X3 split scales):
     // written by the embed / node stage, read by the next edge stage
     float *rmx = ws + kGnnBufs * n * H;
     // rows per trajectory segment (the edge stage's summation units)
@@ -578,7 +579,7 @@ extern "C" int mmpde_gnn_forward_ex(const float *u, const float *pos, int64_t n,
             MMPDE_REQUIRE(aligned16(exec->packed));
             pack = (const char *)exec->packed;
         } else {
-            char *wpk = (char *)(ws + kGnnBufs * n * H + row_max_floats(n));
+            char *wpk = (char *)(ws + kGnnBufs * n * H + row_records_floats(n));
             rc = mmpde_gnn_pack_f16x3(layers, n_layers, wpk, stream);
             if (rc) return rc;
             pack = wpk;

@@ -36,6 +36,7 @@
 // row maxima of its a', b' rows (layer.hpp).  No atomics: every output is
 // deterministic.
 #include "common.hpp"
+#include <type_traits>
 #include "f16x3.hpp"
 #include "layer.hpp"
 
@@ -561,7 +562,8 @@ struct NodeArgs {
     const float *u, *pos;
     mmpde_gnn_scales sc;
     const char *pk, *pkn;  // F16X3 images: this layer (U1, U2), next layer (W1)
-    float *rmx_out;        // F16X3: row maxima of a', b' (layer.hpp)
+    float *rmx_out;        // F16X3: row maxima of a', b' and their range records (layer.hpp)
+    int64_t seg_n;         // rows per trajectory segment (range records)
     int parts;             // mean = sum of `parts` buffers part_stride floats apart
     int64_t part_stride;
     // div_k > 0: the buffers hold neighbour sums (F16X3 wave edge kernel); the
@@ -836,7 +838,7 @@ template <bool F16X3, int RB>
 __device__ __forceinline__ void proj_phase(const BOps<F16X3, F16X3 ? 4 : 8> &bA, const float4 *img,
                                            const float *rs, const float *rowv, const W1C &w,
                                            const char *pk, const float *w1r, int tw, int64_t row0,
-                                           int64_t n, float *a_out, float *b_out,
+                                           int64_t n, int64_t seg_n, float *a_out, float *b_out,
                                            float *rmx_out, uint32_t *arrived, int wave, int lane,
                                            const BOps<F16X3, F16X3 ? 4 : 8> *bBpre = nullptr) {
     constexpr int ROWS = 16 * RB, S1 = F16X3 ? 4 : 8;
@@ -929,14 +931,45 @@ __device__ __forceinline__ void proj_phase(const BOps<F16X3, F16X3 ? 4 : 8> &bA,
         prev = __builtin_amdgcn_readfirstlane(prev);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (prev == 7) {
+            // per lane: row l >> 1, value e = l & 1 (max|a'| / max|b'|); then the
+            // tile's 16-row blocks' range records (layer.hpp) by butterflies over
+            // the row bits (l ^ 2 .. l ^ 16: the 16 rows of one block), each row
+            // in part 0 (its block's first segment) or part 1 (the next)
+            static_assert(2 * ROWS % 64 == 0, "row maxima: whole waves");
 #pragma unroll
             for (int l0 = 0; l0 < 2 * ROWS; l0 += 64) {
                 const int l = l0 + lane, row = l >> 1, e = l & 1;
-                if (l < 2 * ROWS) {
-                    uint32_t m = red[0][row][e];
+                uint32_t m = red[0][row][e];
 #pragma unroll
-                    for (int w2 = 1; w2 < 8; ++w2) m = max(m, red[w2][row][e]);
-                    if (row0 + row < n) rmx_out[2 * (row0 + row) + e] = __builtin_bit_cast(float, m);
+                for (int w2 = 1; w2 < 8; ++w2) m = max(m, red[w2][row][e]);
+                const int64_t grow = row0 + row, b0 = row0 + 16 * (row >> 4);
+                const bool live = grow < n;
+                if (live) rmx_out[2 * grow + e] = __builtin_bit_cast(float, m);
+                const bool part1 = grow >= (b0 / seg_n + 1) * seg_n;
+                uint32_t mx0 = live && !part1 ? m : 0u, mx1 = live && part1 ? m : 0u;
+                uint32_t mn0 = live && !part1 ? m : 0x7f800000u, mn1 = live && part1 ? m : 0x7f800000u;
+                auto xmax = [&](uint32_t &v, auto O) {
+                    v = max(v, __builtin_bit_cast(uint32_t, xor_lane_f<decltype(O)::value>(__builtin_bit_cast(float, v))));
+                };
+                auto xmin = [&](uint32_t &v, auto O) {
+                    v = min(v, __builtin_bit_cast(uint32_t, xor_lane_f<decltype(O)::value>(__builtin_bit_cast(float, v))));
+                };
+                using X2 = std::integral_constant<int, 2>;
+                using X4 = std::integral_constant<int, 4>;
+                using X8 = std::integral_constant<int, 8>;
+                using X16 = std::integral_constant<int, 16>;
+                xmax(mx0, X2{}); xmax(mx1, X2{}); xmin(mn0, X2{}); xmin(mn1, X2{});
+                xmax(mx0, X4{}); xmax(mx1, X4{}); xmin(mn0, X4{}); xmin(mn1, X4{});
+                xmax(mx0, X8{}); xmax(mx1, X8{}); xmin(mn0, X8{}); xmin(mn1, X8{});
+                xmax(mx0, X16{}); xmax(mx1, X16{}); xmin(mn0, X16{}); xmin(mn1, X16{});
+                // lanes 0, 1 (and 32, 33) of each block hold its e = 0 / 1 results:
+                // record fields {max a, max b, min a, min b} of part 0, then part 1
+                if ((l & 31) < 2 && b0 < n) {
+                    float *rec = rmx_out + row_max_floats(n) + 8 * (b0 / 16);
+                    rec[e] = __builtin_bit_cast(float, mx0);
+                    rec[2 + e] = __builtin_bit_cast(float, mn0);
+                    rec[4 + e] = __builtin_bit_cast(float, mx1);
+                    rec[6 + e] = __builtin_bit_cast(float, mn1);
                 }
             }
         }
@@ -1081,7 +1114,7 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_node_kernel(NodeArgs p) {
         __syncthreads();
         NODE_STAMP(6);
         // ---- next layer's message_net_1 node halves
-        proj_phase<F16X3, RB>(bA, img, rs[3], &rowv[0][0], w1c, p.pkn, w1r, tw, row0, p.n,
+        proj_phase<F16X3, RB>(bA, img, rs[3], &rowv[0][0], w1c, p.pkn, w1r, tw, row0, p.n, p.seg_n,
                               p.a_out, p.b_out, p.rmx_out, &rng_arrived, wave, lane, NODE_EARLY_B ? &bB : nullptr);
     }
     NODE_STAMP(7);
@@ -1104,7 +1137,8 @@ struct EmbedArgs {
     int64_t ld_w1;
     float *a_out, *b_out;
     const char *pk;        // F16X3: layer 0's packed images
-    float *rmx_out;        // F16X3: layer 0's row maxima
+    float *rmx_out;        // F16X3: layer 0's row maxima and range records
+    int64_t seg_n;         // rows per trajectory segment (range records)
 };
 
 template <bool F16X3, int RB>
@@ -1211,7 +1245,7 @@ __global__ __launch_bounds__(512, NODE_WPE) void gnn_embed_kernel(EmbedArgs p) {
     __syncthreads();
     prep<F16X3, ROWS>(stage, NLD, 0, ROWS, false, img, 128, 0, rs);
     __syncthreads();
-    proj_phase<F16X3, RB>(bA, img, rs, &rowv[0][0], w1c, p.pk, w1r, tw, row0, p.n,
+    proj_phase<F16X3, RB>(bA, img, rs, &rowv[0][0], w1c, p.pk, w1r, tw, row0, p.n, p.seg_n,
                           p.a_out, p.b_out, p.rmx_out, &rng_arrived, wave, lane, NODE_EARLY_B ? &bB : nullptr);
 }
 
@@ -1236,7 +1270,7 @@ int device_cus() {
 int launch_edge_stage(const float *a, const float *b, const int32_t *nbr, const int32_t *deg,
                       int64_t n, int k, int64_t seg_n, const mmpde_gnn_layer_params *p, const char *pk,
                       const float *rmx, float *mean, float *side, int64_t side_cap,
-                      EdgeSplit *split, hipStream_t st, uint32_t *relu_mask) {
+                      EdgeSplit *split, hipStream_t st, uint32_t *relu_mask, bool rng) {
     if (split) *split = EdgeSplit{};
     MMPDE_REQUIRE(!relu_mask || (!pk && kEdgeMaskOk && al16(relu_mask)));  // the ring kernel's F32 training forward
     MMPDE_REQUIRE(a && b && nbr && p && mean && n > 0 && k > 0 && n <= (int64_t)INT32_MAX);
@@ -1248,7 +1282,7 @@ int launch_edge_stage(const float *a, const float *b, const int32_t *nbr, const 
     // F16X3: one wave per SIMD with the operands in registers (edge_wave.hip);
     // the wave kernel leaves the side blocks and the division to the node stage
     if (pk)
-        return launch_edge_wave(a, b, nbr, deg, n, k, seg_n, p->msg2_b, pk, rmx, mean, side, side_cap, cus,
+        return launch_edge_wave(a, b, nbr, deg, n, k, seg_n, p->msg2_b, pk, rmx, rng, mean, side, side_cap, cus,
                                 split, st);
     // F32: the exact fp32 ring kernel
     EdgeArgs e{a, b, nbr, n, k, (int)ntiles, p->msg2_w, p->msg2_b, nullptr, nullptr, mean, nullptr, deg, relu_mask};
@@ -1356,7 +1390,8 @@ int launch_edge_mean_f16x3(const float *a, const float *b, const int32_t *nbr, c
     if (!relu_mask) {
         float *side = rsc;
         EdgeSplit split;
-        const int rc = launch_edge_wave(a, b, nbr, deg, n, k, n, b2, pk, rmx, mean, side, ntiles, cus, &split, st);
+        const int rc = launch_edge_wave(a, b, nbr, deg, n, k, n, b2, pk, rmx, false, mean, side, ntiles, cus,
+                                        &split, st);
         if (rc) return rc;
         MMPDE_REQUIRE(split.units > 0);
         hipLaunchKernelGGL(edge_finish_kernel, dim3((unsigned)ceil_div(n, 32)), dim3(256), 0, st, mean, split,
@@ -1389,7 +1424,7 @@ static int node_args(const NodeStageCall &c, NodeArgs *out) {
     const mmpde_gnn_layer_params *p = c.p;
     NodeArgs a{c.h, c.mean, c.n, p->upd1_w, p->upd1_b, p->upd1_ld, p->upd2_w, p->upd2_b, p->bn_w, p->bn_b,
                p->bn_rm, p->bn_rv, p->eps, c.h_out, nullptr, nullptr, 0, c.a_out, c.b_out, c.u, c.pos, c.sc,
-               c.pk, c.pkn, c.rmx_out, 1, 0, sums ? c.deg : nullptr,
+               c.pk, c.pkn, c.rmx_out, effective_seg(c.n, c.seg_n), 1, 0, sums ? c.deg : nullptr,
                sums ? c.split->k : 0};
     if (sums) a.split = *c.split;
     if (c.next) {
@@ -1439,7 +1474,7 @@ static int embed_args(const EmbedStageCall &c, EmbedArgs *out) {
     MMPDE_REQUIRE(c.l0->msg1_ld >= 260 && (c.l0->msg1_ld & 3) == 0 && al16(c.l0->msg1_w));
     MMPDE_REQUIRE(!c.pk0 || (al16(c.pk0) && c.rmx_out && al16(c.rmx_out)));
     *out = EmbedArgs{c.u, c.pos, c.n, c.sc, *c.e, c.h_out, c.l0->msg1_w, c.l0->msg1_b, c.l0->msg1_ld, c.a_out,
-                     c.b_out, c.pk0, c.rmx_out};
+                     c.b_out, c.pk0, c.rmx_out, effective_seg(c.n, c.seg_n)};
     return MMPDE_OK;
 }
 

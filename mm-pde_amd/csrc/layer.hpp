@@ -14,7 +14,53 @@
 // trajectory segment: rows 2^14 below the segment maximum fell to an absolute
 // error floor), and a row's result depends on the row and its neighbours only
 // -- not on its segment or on the trajectories launched beside it.
-inline int64_t row_max_floats(int64_t n) { return ((2 * n + 3) / 4) * 4; }  // 16-B multiple
+__host__ __device__ inline int64_t row_max_floats(int64_t n) { return ((2 * n + 3) / 4) * 4; }  // 16-B multiple
+
+// Range records beside the row maxima (the edge kernel's fast path): per
+// 16-row block blk, 8 floats at rmx + row_max_floats(n) + 8 blk: {max, max, min,
+// min} of the block rows' max|a|, max|b| over the rows in the block's first
+// trajectory segment (part 0), then the same over its rows in the next segment
+// (part 1: a block straddles at most one boundary; empty parts hold max 0, min
+// +inf).  A segment whose rows all have M_i >= min max|a| + min max|b| >= 2^-12
+// of M_seg = max max|a| + max max|b| loses at most 12 bits of headroom under
+// ONE scale from M_seg: its error floor 2^-35 M_seg stays below 2^-23 M_i, the
+// split's own 22-bit representation error -- so such a segment skips the
+// per-row neighbour gathers (every row gets the segment scale); wider ranges
+// take the per-row scales.
+__host__ __device__ inline int64_t range_tiles(int64_t n) { return (n + 15) / 16; }
+__host__ __device__ inline int64_t row_records_floats(int64_t n) { return row_max_floats(n) + 8 * range_tiles(n); }
+
+// {M_seg, L_seg} of segment s (seg_n rows) from the range records rec (every
+// lane active; four blocks per lane per pass, loaded together).
+__device__ __forceinline__ float2 segment_stats(const float *rec, int64_t seg_n, int64_t s) {
+    const int64_t r0 = s * seg_n, t0 = r0 / 16, t1 = (r0 + seg_n - 1) / 16;
+    uint32_t ma = 0, mb = 0, na = 0x7f800000u, nb = 0x7f800000u;
+    for (int64_t tb = t0; tb <= t1; tb += 256) {
+        float4 v[4];
+        int64_t tt[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            tt[q] = min(tb + (threadIdx.x & 63) + 64 * q, t1);
+            const bool own = tt[q] * 16 >= r0;  // the block's first row lies in s: part 0
+            v[q] = *(const float4 *)(rec + 8 * tt[q] + (own ? 0 : 4));
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {  // indices past t1 re-read t1: harmless for max / min
+            ma = max(ma, __float_as_uint(v[q].x));
+            mb = max(mb, __float_as_uint(v[q].y));
+            na = min(na, __float_as_uint(v[q].z));
+            nb = min(nb, __float_as_uint(v[q].w));
+        }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        ma = max(ma, (uint32_t)__shfl_xor((int)ma, o, 64));
+        mb = max(mb, (uint32_t)__shfl_xor((int)mb, o, 64));
+        na = min(na, (uint32_t)__shfl_xor((int)na, o, 64));
+        nb = min(nb, (uint32_t)__shfl_xor((int)nb, o, 64));
+    }
+    return make_float2(__uint_as_float(ma) + __uint_as_float(mb), __uint_as_float(na) + __uint_as_float(nb));
+}
 
 // M_i's neighbour term for row `row`: max over e < kk of rmx[2 nbr[row k + e] + 1]
 // (as bit patterns, indices clamped to nmax), every index load issued before
@@ -56,14 +102,15 @@ struct EdgeSplit {
 // one-wave-per-SIMD kernel, which stores neighbour SUMS to mean plus side
 // blocks (side: room for side_cap 16 x 128 blocks) and fills *split: the node
 // stage then adds the side blocks and divides (pass split to launch_node_stage).
-// rmx: the row maxima of a, b (F16X3).
+// rmx: the row maxima of a, b and their range records (F16X3, layer.hpp; rng
+// false: the row maxima alone, every segment takes the per-row scales).
 // F32 writes the mean itself and leaves split->units = 0.  seg_n: rows per
 // trajectory segment (n: one segment; must divide n and be >= kRangeRows,
 // else n is used).
 int launch_edge_stage(const float *a, const float *b, const int32_t *nbr, const int32_t *deg,
                       int64_t n, int k, int64_t seg_n, const mmpde_gnn_layer_params *p, const char *pk,
                       const float *rmx, float *mean, float *side, int64_t side_cap,
-                      EdgeSplit *split, hipStream_t st, uint32_t *relu_mask = nullptr);
+                      EdgeSplit *split, hipStream_t st, uint32_t *relu_mask = nullptr, bool rng = true);
 
 // The training forward's F16X3 edge stage (writes the mean; packs W2 and
 // computes the row maxima of a, b and every row's split scale itself in ws,
@@ -98,15 +145,15 @@ EdgePlan edge_wave_plan(int64_t nseg, int64_t S_seg, int k, int cus, int64_t sid
 // registers (edge_wave.hip): neighbour sums to out / side (see EdgeSplit).
 // cus = compute units.
 int launch_edge_wave(const float *a, const float *b, const int32_t *nbr, const int32_t *deg, int64_t n,
-                     int k, int64_t seg_n, const float *msg2_b, const char *pk, const float *rmx,
+                     int k, int64_t seg_n, const float *msg2_b, const char *pk, const float *rmx, bool rng,
                      float *out, float *side, int64_t side_cap, int cus, EdgeSplit *split, hipStream_t st);
 
 // Node stage (mean: the edge stage's buffer, or with split->units > 0 the wave
 // kernel's sums plus side blocks divided by max(deg[row], 1) or split->k):
 // h' = BN(h + relu(U2 relu(U1 [h | mean | t] + c1) + c2)) and, when
 // next != nullptr, the next layer's message_net_1 node halves a', b' (and,
-// F16X3, their row maxima rmx_out).  F16X3 when pk != nullptr (pkn: the next
-// layer's images).
+// F16X3, their row maxima and range records rmx_out, row_records_floats(n)).
+// F16X3 when pk != nullptr (pkn: the next layer's images).
 int launch_node_stage(const float *h, const float *mean, const EdgeSplit *split, const int32_t *deg,
                       const float *u, const float *pos, int64_t n, int64_t seg_n, mmpde_gnn_scales sc,
                       const mmpde_gnn_layer_params *p, const mmpde_gnn_layer_params *next,

@@ -119,9 +119,9 @@ class MMPDERollout:
             # and model_b
             self.side2 = torch.cuda.Stream(self.device)
 
-        # hipGraph replay of the whole step (enable_graph): static input / time /
-        # output buffers, captured once, replayed every step
-        self._graph = None
+        # hipGraph replay of the step (enable_graph): static input / time /
+        # output buffers, one graph per stage, replayed on the stage's stream
+        self._graphs = None
         self._g_u = self._g_t = self._g_out = None
 
     def _trace(self):
@@ -135,79 +135,48 @@ class MMPDERollout:
             return _Nodes(u, xy, nbr, self.N, t_slot=step_idx)
         return _Nodes(u, xy, nbr, self.N, t=float(self.t[step_idx]))
 
-    # ------------------------------------------------------------ hipGraph
-    def enable_graph(self, u_like: torch.Tensor) -> None:
-        """Capture one step (every kernel of all three streams, fork/join on the
-        capture stream) into a hipGraph; `graph_step` then replays it.  The step
-        must have run eagerly once before (weight images packed, DMM head cache
-        built).  Inputs are copied into static buffers; the time value is read
-        from a one-element device slot, so one graph serves every step index."""
-        if self.trace_hook is not None:
-            raise ValueError("graph replay records no per-kernel events; clear trace_hook")
-        self._g_u = torch.empty_like(u_like).contiguous()
-        self._g_u.copy_(u_like)
-        self._g_t = torch.zeros((1,), dtype=torch.float32, device=self.device)
-        g = torch.cuda.CUDAGraph()
-        torch.cuda.synchronize(self.device)
-        with torch.cuda.graph(g):
-            self._g_out = self.step(self._g_u, self._g_t)
-        torch.cuda.synchronize(self.device)
-        self._graph = g
-
-    def graph_step(self, u: torch.Tensor, step_idx: int) -> torch.Tensor:
-        """`step` by replaying the captured graph.  Returns the graph's static
-        output buffer (overwritten by the next replay; clone to keep it)."""
-        if self._graph is None:
-            raise RuntimeError("enable_graph() first")
-        if u.data_ptr() != self._g_u.data_ptr():
-            self._g_u.copy_(u.reshape(self._g_u.shape))
-        self._g_t.fill_(float(self.t[step_idx]))
-        self._graph.replay()
-        return self._g_out
-
-    def step(self, u: torch.Tensor, step_idx) -> torch.Tensor:
-        """u: [B, N] (cylinder) or [B, s, s] (Burgers) on the device -> pred, same shape.
-        step_idx: time index (int), or during graph capture the device slot holding t."""
-        B, N = self.B, self.N
-        u = u.contiguous()
-        u_flat = u.reshape(-1)
-        if not self.moving_mesh:
-            return self.model(self._nodes(u_flat, self.grid_rep, self.nbr_u, step_idx), out=self.out_u,
-                              workspace=self.ws_gnn, trace=self._trace()).reshape(u.shape)
-        cur = torch.cuda.current_stream(self.device)
-        side = self.side if self.overlap else cur
+    # ------------------------------------------------------------ the stages
+    # The moving-mesh step is five stages on three streams (every kernel is one
+    # of the C-ABI's; each stage runs on the caller's current stream):
+    #   side   model(u) on the fixed grid                       needs u
+    #   main1  DMM mesh, per-trajectory displacement record     needs u
+    #   side2  kNN-30 query onto the fixed grid, res_cut(u)     needs main1
+    #   main2  moved-mesh kNN-35 graph (Burgers: u onto the moved mesh), model_b
+    #   final  interpolation + res_cut + model(u) in one kernel  needs all
+    def _st_side(self, u_flat, step_idx):
         nodes_u = self._nodes(u_flat, self.grid_rep, self.nbr_u, step_idx)
-        side.wait_stream(cur)
-        with torch.cuda.stream(side):
-            u.record_stream(side)
-            out_u = self.model(nodes_u, out=self.out_u, workspace=self.ws_gnn_u, trace=self._trace())
-        mesh = self.dmm.mesh(u, self.xi, out=self.mesh, workspace=self.ws_dmm,
-                             head_cache=self.dmm_cache)
+        self.model(nodes_u, out=self.out_u, workspace=self.ws_gnn_u, trace=self._trace())
+
+    def _st_main1(self, u):
+        B = self.B
+        self.dmm.mesh(u, self.xi, out=self.mesh, workspace=self.ws_dmm, head_cache=self.dmm_cache)
         pol = self.knn_policy
-        use_g, use_q = pol.use_table("graph"), pol.use_table("query")
-        self._knn_used = {"graph": use_g, "query": use_q}
-        cells = ops.knn_moved_cells(mesh, self.xi, B, out=self.knn_cells) \
-            if self.knn_cand is not None and (use_g or use_q) else None
-        side2 = self.side2 if self.overlap else cur
-        side2.wait_stream(cur)
-        with torch.cuda.stream(side2):
-            u.record_stream(side2)
-            if use_q:
-                idx2 = ops.knn_query_moved(mesh, self.grid_rep, self.xi, self.knn_cand_q, B, 30,
-                                           self.knn_scratch_q, ref=self.grid, cells=cells,
-                                           skip_above=self.knn_skip_q, ties=self.knn_ties)
-                if cells is not None:
-                    pol.after_table("query", cells, 1)
-            else:
-                idx2 = ops.knn_query(mesh, self.grid_rep, B, 30, ties=self.knn_ties)
-            self.idx2 = idx2
-            if self.kind == "burgers":
-                res = self.itp.res_cut(u.reshape(B, 1, self.s, self.s)).reshape(-1)
-            else:
-                res = self.itp.res_cut(u.reshape(B, N)).reshape(-1)
-            idx2.record_stream(cur)
-            res.record_stream(cur)
-        if use_g:
+        self._use_g, self._use_q = pol.use_table("graph"), pol.use_table("query")
+        self._knn_used = {"graph": self._use_g, "query": self._use_q}
+        self._cells = ops.knn_moved_cells(self.mesh, self.xi, B, out=self.knn_cells) \
+            if self.knn_cand is not None and (self._use_g or self._use_q) else None
+
+    def _st_side2(self, u):
+        B, N = self.B, self.N
+        pol, cells, mesh = self.knn_policy, self._cells, self.mesh
+        if self._use_q:
+            idx2 = ops.knn_query_moved(mesh, self.grid_rep, self.xi, self.knn_cand_q, B, 30,
+                                       self.knn_scratch_q, ref=self.grid, cells=cells,
+                                       skip_above=self.knn_skip_q, ties=self.knn_ties)
+            if cells is not None:
+                pol.after_table("query", cells, 1)
+        else:
+            idx2 = ops.knn_query(mesh, self.grid_rep, B, 30, ties=self.knn_ties)
+        self.idx2 = idx2
+        if self.kind == "burgers":
+            self._res = self.itp.res_cut(u.reshape(B, 1, self.s, self.s)).reshape(-1)
+        else:
+            self._res = self.itp.res_cut(u.reshape(B, N)).reshape(-1)
+
+    def _st_main2(self, u_flat, step_idx):
+        B = self.B
+        pol, cells, mesh = self.knn_policy, self._cells, self.mesh
+        if self._use_g:
             nbr_m = ops.knn_graph_moved(mesh, self.xi, self.knn_cand, B, self.gc.n, self.knn_scratch,
                                         cells=cells, skip_above=self.knn_skip)
             if cells is not None:
@@ -231,14 +200,115 @@ class MMPDERollout:
         else:
             u_m = u_flat
         nodes_m = self._nodes(u_m, mesh, nbr_m, step_idx)
-        out_b = self.model_b(nodes_m, out=self.out_b, workspace=self.ws_gnn, trace=self._trace())
-        cur.wait_stream(side)
-        cur.wait_stream(side2)
+        self.model_b(nodes_m, out=self.out_b, workspace=self.ws_gnn, trace=self._trace())
+
+    def _st_final(self):
         # interpolate_pred(...) + model(graph_uniform) (train_helper_2d.py:178-185):
         # (interp + res_cut) + out_u in the interpolation kernel's epilogue
-        pred = ops.itp_interp(mesh, out_b, self.grid_rep, idx2, B, self.itp.packed("2"),
-                              addend=res, addend2=out_u.reshape(-1))
-        return pred.reshape(u.shape)
+        return ops.itp_interp(self.mesh, self.out_b, self.grid_rep, self.idx2, self.B, self.itp.packed("2"),
+                              addend=self._res, addend2=self.out_u.reshape(-1))
+
+    # ------------------------------------------------------------ hipGraph
+    def enable_graph(self, u_like: torch.Tensor, serial: bool = False) -> None:
+        """Capture the step for replay: one hipGraph per stage (see the stage
+        list above), each captured on the stream it replays on, with its own
+        memory pool (two stages that replay concurrently never share scratch).
+        `graph_step` replays them with the eager step's cross-stream waits, so
+        the side streams' stages still run beside the main chain (a single
+        graph of the whole step replays its branches one after the other).
+        The step must have run eagerly once before (weight images packed, DMM
+        head cache built).  Inputs are copied into static buffers; the time
+        value is read from a one-element device slot, so the graphs serve every
+        step index.  serial: every stage captured and replayed on one stream (the
+        measurement baseline of the side streams' overlap)."""
+        if self.trace_hook is not None:
+            raise ValueError("graph replay records no per-kernel events; clear trace_hook")
+        self._g_u = torch.empty_like(u_like).contiguous()
+        self._g_u.copy_(u_like)
+        self._g_t = torch.zeros((1,), dtype=torch.float32, device=self.device)
+        u, t = self._g_u, self._g_t
+        u_flat = u.reshape(-1)
+        torch.cuda.synchronize(self.device)
+        cap = torch.cuda.Stream(self.device)
+        graphs = {}
+
+        def capture(name, stream, fn):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=stream):
+                out = fn()
+            torch.cuda.synchronize(self.device)
+            graphs[name] = g
+            return out
+
+        if not self.moving_mesh:
+            self._g_out = capture("main", cap, lambda: self.model(
+                self._nodes(u_flat, self.grid_rep, self.nbr_u, t), out=self.out_u,
+                workspace=self.ws_gnn).reshape(u.shape))
+        else:
+            capture("side", cap if serial else self.side, lambda: self._st_side(u_flat, t))
+            capture("main1", cap, lambda: self._st_main1(u))
+            capture("side2", cap if serial else self.side2, lambda: self._st_side2(u))
+            capture("main2", cap, lambda: self._st_main2(u_flat, t))
+            self._g_out = capture("final", cap, self._st_final).reshape(u.shape)
+        self._graphs = graphs
+        self._graph_serial = serial
+
+    def graph_step(self, u: torch.Tensor, step_idx: int) -> torch.Tensor:
+        """`step` by replaying the captured graphs.  Returns the static output
+        buffer (overwritten by the next replay; clone to keep it)."""
+        if self._graphs is None:
+            raise RuntimeError("enable_graph() first")
+        if u.data_ptr() != self._g_u.data_ptr():
+            self._g_u.copy_(u.reshape(self._g_u.shape))
+        self._g_t.fill_(float(self.t[step_idx]))
+        g = self._graphs
+        if not self.moving_mesh:
+            g["main"].replay()
+            return self._g_out
+        if self._graph_serial:
+            for name in ("side", "main1", "side2", "main2", "final"):
+                g[name].replay()
+            return self._g_out
+        cur = torch.cuda.current_stream(self.device)
+        self.side.wait_stream(cur)
+        with torch.cuda.stream(self.side):
+            g["side"].replay()
+        g["main1"].replay()
+        self.side2.wait_stream(cur)
+        with torch.cuda.stream(self.side2):
+            g["side2"].replay()
+        g["main2"].replay()
+        cur.wait_stream(self.side)
+        cur.wait_stream(self.side2)
+        g["final"].replay()
+        return self._g_out
+
+    def step(self, u: torch.Tensor, step_idx) -> torch.Tensor:
+        """u: [B, N] (cylinder) or [B, s, s] (Burgers) on the device -> pred, same shape.
+        step_idx: time index (int), or during graph capture the device slot holding t."""
+        u = u.contiguous()
+        u_flat = u.reshape(-1)
+        if not self.moving_mesh:
+            return self.model(self._nodes(u_flat, self.grid_rep, self.nbr_u, step_idx), out=self.out_u,
+                              workspace=self.ws_gnn, trace=self._trace()).reshape(u.shape)
+        cur = torch.cuda.current_stream(self.device)
+        side = self.side if self.overlap else cur
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            u.record_stream(side)
+            self._st_side(u_flat, step_idx)
+        self._st_main1(u)
+        side2 = self.side2 if self.overlap else cur
+        side2.wait_stream(cur)
+        with torch.cuda.stream(side2):
+            u.record_stream(side2)
+            self._st_side2(u)
+            self.idx2.record_stream(cur)
+            self._res.record_stream(cur)
+        self._st_main2(u_flat, step_idx)
+        cur.wait_stream(side)
+        cur.wait_stream(side2)
+        return self._st_final().reshape(u.shape)
 
     def knn_table_share(self):
         """(graph, query[, burgers mode-'1' query]): the share of the last step's

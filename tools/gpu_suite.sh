@@ -7,7 +7,7 @@ T=${1:-suite}; K=${2:-}
 O=gpurun_out/$T
 mkdir -p $O
 if [ -n "$K" ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -v --timeout 240 --timeout-method thread -k "$K" > $O/gpu_tests.log 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -v -rP --timeout 240 --timeout-method thread -k "$K" > $O/gpu_tests.log 2>&1
 else
   timeout -k 10 900 python -u -m pytest tests -m gpu -q -v --timeout 240 --timeout-method thread > $O/gpu_tests.log 2>&1
 fi
