@@ -40,8 +40,9 @@ def test_version_and_status_strings_without_gpu():
     assert lib.mmpde_status_string(0) == b"ok"
     assert lib.mmpde_status_string(-1) == b"invalid argument"
     # sizing helpers are pure host arithmetic
-    # 8 [n, 128] buffers, one 16-B range record per 32-row node tile, 16 layers' images
-    assert lib.mmpde_gnn_workspace_bytes(1000) == 8 * 1000 * 128 * 4 + 2000 * 4 + 16 * 395776  # row maxima
+    # 8 [n, 128] buffers, per-row maxima (row_max_floats = 2000) plus one
+    # 32-B range record per 16-row tile (63 tiles), 16 layers' images
+    assert lib.mmpde_gnn_workspace_bytes(1000) == 8 * 1000 * 128 * 4 + (2000 + 8 * 63) * 4 + 16 * 395776
     assert lib.mmpde_gnn_pack_bytes(6) == 6 * 395776
     assert lib.mmpde_itp_pack_bytes() > 0
 

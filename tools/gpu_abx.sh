@@ -5,6 +5,7 @@
 set -u
 export TMPDIR=/tmp
 L=mm-pde_amd/mmpde_amd/lib
+mkdir -p gpurun_out/${AB_OUT:-ab}
 cp $L/libmmpde_hip.so /tmp/libmmpde_hip.orig.so
 for so in $L/${AB_DIR:-ab}/*.so; do
   v=$(basename $so .so)
