@@ -6,6 +6,7 @@
 #                 with the cy-gnn whole-step HBM record (tools/gpu_configs.sh)
 #   node          node / embed kernel counter passes (SQ wait breakdown, L2 / L1 requests)
 #   train         training tests, the training-iteration bench and its kernel profile
+#   bwd           edge backward kernel counter passes (SQ wait breakdown, LDS, VALU / MFMA issue)
 set -u
 export TMPDIR=/tmp
 
@@ -25,6 +26,17 @@ node() {
     "TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE" \
     "TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum TCC_REQ_sum" \
     > $O/counters.log 2>&1; local rc=$?; tail -12 $O/counters.log; return $rc
+}
+
+bwd() {
+  local O=gpurun_out/bwd_ctr
+  mkdir -p $O
+  export PMC_OUT=$O PMC_REGEX="edge_bwd_f16_kernel" PMC_TIMEOUT=240 PMC_SCRIPT=tools/train_bench.py \
+         PMC_BENCH_ARGS="--edge-gemm f16x3 --iters 1 --warmup 1"
+  bash tools/gpu_counters.sh \
+    "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES" \
+    "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES" \
+    > $O/counters.log 2>&1; local rc=$?; tail -14 $O/counters.log; return $rc
 }
 
 train() {
@@ -59,6 +71,7 @@ for what in "$@"; do
     pmc:*) pmc "${what#pmc:}" "${STEP_HBM:-}" || exit $? ;;
     node) node || exit $? ;;
     train) train || exit $? ;;
+    bwd) bwd || exit $? ;;
     *) echo "unknown record $what"; exit 2 ;;
   esac
 done

@@ -94,7 +94,10 @@ def main():
     torch.cuda.synchronize()
     bwd_us = e0.elapsed_time(e1) * 1e3 / reps
     edges = n * 35
-    flops = 3 * 2 * edges * 128 * 128          # z2, gm1 and the dW2 outer products
+    # algorithmic: the two GEMMs of a linear layer's backward (gm1 = gz2 W2 and
+    # the dW2 outer products); message_net_2's ReLU pattern comes from the
+    # forward's bits (relu_mask), so z2 is not recomputed and not counted
+    flops = 2 * 2 * edges * 128 * 128
     print(json.dumps({
         "what": "MM-PDE training iteration (train_helper_2d.py:95-131), cy synthetic",
         "batch": B, "nodes": n, "edge_gemm": args.edge_gemm, "ms_per_iter": round(ms, 3),
