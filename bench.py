@@ -43,9 +43,9 @@ F32_MFMA_PEAK_TFLOPS = 157.3          # MI355X_MICROARCH.md: dense fp32 matrix p
 F16_MFMA_PEAK_TFLOPS = 2516.6         # 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz (~2.5 PF dense)
 HBM_PEAK_GBS = 8000.0
 # counter records regenerated on the current kernels (tools/gpu_pmc.sh with
-# PMC_NAME=edge_pmc_r04; tools/gpu_configs.sh with STEP_HBM=...: tools/gpu_records.sh pmc:NAME)
-EDGE_PMC_RECORD = "edge_pmc_r04.json"
-STEP_HBM_RECORD = "r04_cy_gnn_step_hbm.json"
+# PMC_NAME=edge_pmc_r06; tools/gpu_configs.sh with STEP_HBM=...: tools/gpu_records.sh pmc:NAME)
+EDGE_PMC_RECORD = "edge_pmc_r06.json"
+STEP_HBM_RECORD = "r06_cy_gnn_step_hbm.json"
 CONFIGS = {
     # name: (kind, moving_mesh, default trajectories per GPU, BASELINE.json config,
     #        Burgers grid side: 48 = the MM-PDE --base_resolution, 96 = PDEs.py's default)
