@@ -191,6 +191,9 @@ def main():
     ap.add_argument("--dist-backend", default=None, choices=["nccl", "gloo"],
                     help="process-group backend under torchrun (default nccl = RCCL; gloo "
                          "lets several ranks share one GPU, for rehearsing the multi-rank path)")
+    ap.add_argument("--priorities", choices=["on", "off"], default=None,
+                    help="stream priorities of the step (MMPDERollout.set_priorities): the "
+                         "moving-mesh chain high, the fixed-grid model low (default: the engine's)")
     ap.add_argument("--serial", action="store_true",
                     help="one stream in every pass (per-kernel profiles without concurrent "
                          "kernels sharing the GPU)")
@@ -239,6 +242,8 @@ def main():
         u_all = fields(pts, total, t_len).reshape(total, t_len, side, side)[lo:hi]
     n_nodes = pts.shape[0]
     eng = MMPDERollout(kind, model, model_b, itp, dmm, gc, hi - lo, device, moving_mesh=moving)
+    if args.priorities is not None:
+        eng.set_priorities(args.priorities == "on")
     n_gnn = 2 if moving else 1
     tracer = EdgeTracer(n_forwards=n_gnn * args.steps)
     eng.trace_hook = tracer
@@ -349,7 +354,8 @@ def main():
                    "launch": ("hipGraph replay of the step, one graph per stage on its own stream"
                               if args.graph == "streams" else
                               "hipGraph replay of the step, every stage on one stream" if args.graph else
-                              "eager, three HIP streams")},
+                              "eager, three HIP streams"),
+                   "stream_priorities": bool(getattr(eng, "priorities", False))},
         "roofline": {"kernel": ("gnn_edge_wave_kernel" if args.edge_gemm == "f16x3" else "gnn_edge_kernel")
                                + " (message_net_2 over every edge + mean aggregation, one launch "
                                "per GNN layer, 12 per step)",

@@ -33,6 +33,10 @@ from . import _lib as L
 from . import ops
 
 
+# default of MMPDERollout.priorities (set_priorities)
+PRIORITIES = False
+
+
 class MMPDERollout:
     def __init__(self, kind, model, model_b, itp, dmm, graph_creator, batches: int, device,
                  moving_mesh: bool = True):
@@ -47,6 +51,9 @@ class MMPDERollout:
         # run the fixed-grid model beside the moving-mesh chain (False: one stream,
         # e.g. to time single kernels without a concurrent neighbour)
         self.overlap = True
+        # stream priorities (set_priorities): the moving-mesh chain and the
+        # kNN-30 query at high priority, the fixed-grid model at low priority
+        self.priorities = PRIORITIES
         gc = graph_creator
         self.grid = gc.uniform_grid(self.device).contiguous()           # [N, 2]
         self.N = N = self.grid.shape[0]
@@ -112,17 +119,33 @@ class MMPDERollout:
                 self.device, batches, N, ("graph", "query") + (("query1",) if kind == "burgers" else ()))
             # the fixed-grid model depends on u only: it runs on a side stream,
             # with its own workspace, beside the moving-mesh chain
-            self.side = torch.cuda.Stream(self.device)
             self.ws_gnn_u = torch.empty_like(self.ws_gnn)
             # the kNN-30 query onto the fixed grid and res_cut need only the mesh
             # and u: a second side stream runs them beside the moved-mesh graph
             # and model_b
-            self.side2 = torch.cuda.Stream(self.device)
+            self.set_priorities(self.priorities)
 
         # hipGraph replay of the step (enable_graph): static input / time /
         # output buffers, one graph per stage, replayed on the stage's stream
         self._graphs = None
         self._g_u = self._g_t = self._g_out = None
+
+    def set_priorities(self, on: bool) -> None:
+        """on: the moving-mesh chain (DMM, kNN graph, model_b) runs on a
+        high-priority stream and the kNN-30 query / res_cut on another, the
+        fixed-grid model(u) on a low-priority one, so that the chain's small
+        kernels take the SIMDs the fixed-grid GNN's kernels free before that
+        GNN's next launch does (the chain gates model_b).  off: default
+        priorities, the chain on the caller's stream.  Which stream runs a
+        kernel does not change its result."""
+        if not self.moving_mesh:
+            return
+        self.priorities = bool(on)
+        hi, lo = (-8, 8) if on else (0, 0)   # torch clamps to the device's range
+        self.side = torch.cuda.Stream(self.device, priority=lo)
+        self.side2 = torch.cuda.Stream(self.device, priority=hi)
+        self.main_hi = torch.cuda.Stream(self.device, priority=hi) if on else None
+        self._graphs = None
 
     def _trace(self):
         return self.trace_hook() if self.trace_hook is not None else None
@@ -293,19 +316,30 @@ class MMPDERollout:
                               workspace=self.ws_gnn, trace=self._trace()).reshape(u.shape)
         cur = torch.cuda.current_stream(self.device)
         side = self.side if self.overlap else cur
+        main = self.main_hi if self.overlap and self.main_hi is not None else cur
+        if main is not cur:   # the chain first: its first kernel is queued before model(u)'s
+            main.wait_stream(cur)
+            u.record_stream(main)
         side.wait_stream(cur)
+        if main is not cur:
+            with torch.cuda.stream(main):
+                self._st_main1(u)
         with torch.cuda.stream(side):
             u.record_stream(side)
             self._st_side(u_flat, step_idx)
-        self._st_main1(u)
+        if main is cur:
+            self._st_main1(u)
         side2 = self.side2 if self.overlap else cur
-        side2.wait_stream(cur)
+        side2.wait_stream(main)
         with torch.cuda.stream(side2):
             u.record_stream(side2)
             self._st_side2(u)
             self.idx2.record_stream(cur)
             self._res.record_stream(cur)
-        self._st_main2(u_flat, step_idx)
+        with torch.cuda.stream(main):
+            self._st_main2(u_flat, step_idx)
+        if main is not cur:
+            cur.wait_stream(main)
         cur.wait_stream(side)
         cur.wait_stream(side2)
         return self._st_final().reshape(u.shape)

@@ -695,6 +695,39 @@ def test_graph_replay_matches_eager(dev, kind):
         assert torch.equal(u, ref[i]), f"{kind} graph step {s}: max|diff| {(u - ref[i]).abs().max()}"
 
 
+@pytest.mark.parametrize("kind", ["cy", "burgers"])
+def test_stream_priorities_match_default(dev, kind):
+    """The step with stream priorities on (the moving-mesh chain on its own
+    high-priority stream, model(u) low: MMPDERollout.set_priorities) equals the
+    default streams bit for bit over an autoregressive rollout: which stream a
+    kernel runs on changes no sum."""
+    from mmpde_amd.rollout import MMPDERollout
+    from mmpde_amd.synth import build_models, burgers_grid_points, fields
+
+    pde, model, model_b, itp, dmm, gc = build_models(kind)
+    B = 2
+    if kind == "cy":
+        u0 = fields(pde.ori_grid, B, 30)[:, 3]
+    else:
+        u0 = fields(burgers_grid_points(), B, 31).reshape(B, 31, 48, 48)[:, 3]
+    for m in (model, model_b, itp, dmm):
+        m.to(dev)
+    for m in (model, model_b):
+        m.edge_gemm = "f16x3"
+    eng = MMPDERollout(kind, model, model_b, itp, dmm, gc, B, dev)
+    u0 = u0.to(dev).contiguous()
+    outs = {}
+    for on in (False, True):
+        eng.set_priorities(on)
+        u, outs[on] = u0, []
+        for s in range(4, 8):
+            u = eng.step(u, s)
+            outs[on].append(u.clone())
+    torch.cuda.synchronize(dev)
+    for i, (a, b) in enumerate(zip(outs[False], outs[True])):
+        assert torch.equal(a, b), f"{kind} step {4 + i}: max|diff| {(a - b).abs().max()}"
+
+
 # ============================================================================ full size vs oracle
 @pytest.mark.parametrize("edge_gemm", ["f16x3", "f32"])
 def test_full_size_step_matches_oracle_sampled(dev, edge_gemm):
