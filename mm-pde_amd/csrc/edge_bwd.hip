@@ -249,9 +249,37 @@ __global__ __launch_bounds__(256, 1) void edge_bwd_kernel(EdgeBwdArgs p) {
 // ---------------------------------------------------------------------------
 constexpr int FT = 32;          // targets per tile
 constexpr int FAW = BH + 4;     // fp32 row stride of the a / g tiles
-constexpr int FAS = BH + 8;     // half row stride, row-major images (272 B: 16-B row skew)
+constexpr int FAS = BH + 16;    // half row stride, row-major images (288 B = 72 dwords: the
+                                // A-operand reads' 16 rows x 4 chunks land on 64 distinct
+                                // chunk banks, 8 ≡ 72 mod 64; 272 B left one 2-way pair per
+                                // lane group; the ds_write_b16 stores are then 2-way, free)
 constexpr int FCS = FT;         // half row stride, column-major images [128][32 edges]
 constexpr int FKMAX = 64;       // neighbour slots per target this kernel takes
+
+// The column-major images zb [kk][edge] and gt [c][edge] (rows of FCS = 32
+// halves = four 16-B chunks) store chunk q of row x at chunk q ^ csw(x).  With
+// a plain 64-B row stride the dW2 operand reads (lanes r = 16 rows, g = chunk)
+// hit 4 rows per bank group -- 4-way conflicts on every ds_read_b128 -- the P1
+// zb writes (64 consecutive rows, one chunk) 4-way and the P2 gt writes 8-way
+// (SQ_LDS_BANK_CONFLICT was 57 % of the kernel's LDS cycles).  csw = bits 1-2
+// of the row makes every ds_read_b128 lane group and every 8-lane ds_write_b128
+// group conflict-free and the 8-B gt writes 2-way (the least a 16-dword row
+// stride allows).  Only the layout changes: the same values, the same sums.
+__device__ __forceinline__ int csw(int row) { return (row >> 1) & 3; }
+// gt [c][edge] (the gz2 image) takes bits 1 and 3 of its row instead: the same
+// conflict-free dW2 reads and 2-way writes, and with MASK it is also gm1's A
+// operand, read transposed (ds_read_b64_tr_b16: a 32-lane half reads rows
+// c0 .. c0 + 3 and c0 + 8 .. c0 + 11, which bit 3 sends to the other two
+// chunks of each row) without conflicts.
+__device__ __forceinline__ int gsw(int row) { return ((row >> 1) & 1) | ((row >> 2) & 2); }
+
+typedef __fp16 fp16x4_t __attribute__((__vector_size__(4 * sizeof(__fp16))));
+// ds_read_b64_tr_b16 (MI355X: per 16-lane group, lane 4q + p addresses row q's
+// columns 4p .. 4p + 3 of a 4 x 16 block; lane i receives column i, row q in
+// element q).  EXEC must be all ones.
+__device__ __forceinline__ fp16x4_t lds_read_tr16(const _Float16 *p) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) fp16x4_t *)p);
+}
 
 struct EdgeBwdF16Args {
     const float *a, *b;
@@ -313,7 +341,9 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
     constexpr int NZA = MASK ? 1 : 2, NGB = MASK ? 2 : 1;
     __shared__ _Float16 za[NZA][2][MASK ? 8 : FT * FAS];  // [slot & 1] relu(z1) sz: hi, lo, [edge][kk]
     __shared__ _Float16 zb[2][2][BH * FCS];    // the same, [kk][edge]
-    __shared__ _Float16 grb[NGB][2][FT * FAS];  // gz2 sg, [edge][c] ([slot & 1] with MASK)
+    // gz2 sg, [edge][c]: without MASK only (MASK reads gm1's A operand from gt
+    // transposed: one image, no row-major stores)
+    __shared__ _Float16 grb[MASK ? 1 : NGB][2][MASK ? 8 : FT * FAS];
     __shared__ _Float16 gtb[NGB][2][BH * FCS];  // the same, [c][edge]
     __shared__ __attribute__((aligned(16))) uint8_t zm[2][BH * (FT / 8)];  // z1 > 0, [kk][edge / 8] bits
     __shared__ int nb[FT * FKMAX];             // the tile's neighbour rows (clamped)
@@ -412,8 +442,8 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
                     za[MASK ? 0 : sb][1][ed * FAS + kk1] = l;
                 }
             }
-            *(half8 *)&zb[sb][0][kk1 * FCS + 8 * eg] = hi;
-            *(half8 *)&zb[sb][1][kk1 * FCS + 8 * eg] = lo;
+            *(half8 *)&zb[sb][0][kk1 * FCS + 8 * (eg ^ csw(kk1))] = hi;
+            *(half8 *)&zb[sb][1][kk1 * FCS + 8 * (eg ^ csw(kk1))] = lo;
             zm[sb][kk1 * 4 + eg] = (uint8_t)bits;
             const int en = min(e + 1, k - 1);
 #pragma unroll
@@ -422,7 +452,7 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
         // ---- P2: z2 and gz2 (column c = col) of slot e
         auto p2 = [&](int e) {
             const int sb = e & 1;
-            _Float16(*gr)[FT * FAS] = grb[MASK ? sb : 0];
+            _Float16(*gr)[MASK ? 8 : FT * FAS] = grb[0];
             _Float16(*gt)[BH * FCS] = gtb[MASK ? sb : 0];
             f32x4 acc[2] = {(f32x4){0.0f, 0.0f, 0.0f, 0.0f}, (f32x4){0.0f, 0.0f, 0.0f, 0.0f}};
             if (!MASK) {
@@ -463,12 +493,16 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
                     const float v = on ? (MASK ? gmv[MASK ? 4 * rb + q : 0] : gms[rr * FAW + col]) : 0.0f;
                     db += v;
                     split1(v * sg, hv[q], lv[q]);
-                    gr[0][rr * FAS + col] = hv[q];
-                    gr[1][rr * FAS + col] = lv[q];
+                    if (!MASK) {
+                        gr[0][rr * FAS + col] = hv[q];
+                        gr[1][rr * FAS + col] = lv[q];
+                    }
                 }
                 typedef _Float16 half4 __attribute__((ext_vector_type(4)));
-                *(half4 *)&gt[0][col * FCS + 16 * rb + 4 * g] = (half4){hv[0], hv[1], hv[2], hv[3]};
-                *(half4 *)&gt[1][col * FCS + 16 * rb + 4 * g] = (half4){lv[0], lv[1], lv[2], lv[3]};
+                // edges 16 rb + 4 g .. + 3: chunk 2 rb + (g >> 1), half 4 (g & 1)
+                const int go = col * FCS + 8 * ((2 * rb + (g >> 1)) ^ gsw(col)) + 4 * (g & 1);
+                *(half4 *)&gt[0][go] = (half4){hv[0], hv[1], hv[2], hv[3]};
+                *(half4 *)&gt[1][go] = (half4){lv[0], lv[1], lv[2], lv[3]};
             }
         };
         // ---- P3 of slot e: gm1 -> gz1 (column kk = col); this wave's dW2 tiles
@@ -478,16 +512,31 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
         // writes and VALU work in the MFMAs' shadow.
         auto p3 = [&](int e, bool next) {
             const int sb = e & 1;
-            const _Float16(*gr)[FT * FAS] = grb[MASK ? sb : 0];
+            const _Float16(*gr)[MASK ? 8 : FT * FAS] = grb[0];
             const _Float16(*gt)[BH * FCS] = gtb[MASK ? sb : 0];
             if (next) p1(e + 1);
             f32x4 acc[2] = {(f32x4){0.0f, 0.0f, 0.0f, 0.0f}, (f32x4){0.0f, 0.0f, 0.0f, 0.0f}};
+            // MASK: the A operand (gz2 [edge 16 rb + r][c = 32 s + 8 g + j]) by
+            // two transposed reads of gt per (s, rb): lane 4q + p (q, p < 4) of
+            // group g addresses row c = 32 s + 8 g + 4 h + q, edges 16 rb + 4 p
+            // .. + 3 (chunk 2 rb + (p >> 1) ^ gsw(c), half 4 (p & 1)); gsw(c)
+            // = bit 1 of q | bit 0 of g << 1 for every s, h
+            const int tq = (lane & 15) >> 2, tp = lane & 3;
+            const int tsw = ((tq >> 1) & 1) | ((g & 1) << 1);
+            auto a_tr = [&](int plane, int s, int rb) {
+                const _Float16 *b0 = &gt[plane][(32 * s + 8 * g + tq) * FCS + 8 * ((2 * rb + (tp >> 1)) ^ tsw) +
+                                                 4 * (tp & 1)];
+                const fp16x4_t lo4 = lds_read_tr16(b0), hi4 = lds_read_tr16(b0 + 4 * FCS);
+                return __builtin_bit_cast(half8, __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7));
+            };
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
 #pragma unroll
                 for (int rb = 0; rb < 2; ++rb) {
-                    const half8 ah = *(const half8 *)&gr[0][(16 * rb + r) * FAS + 32 * s + 8 * g];
-                    const half8 al = *(const half8 *)&gr[1][(16 * rb + r) * FAS + 32 * s + 8 * g];
+                    const half8 ah = MASK ? a_tr(0, s, rb)
+                                          : *(const half8 *)&gr[0][(16 * rb + r) * FAS + 32 * s + 8 * g];
+                    const half8 al = MASK ? a_tr(1, s, rb)
+                                          : *(const half8 *)&gr[1][(16 * rb + r) * FAS + 32 * s + 8 * g];
                     acc[rb] = mfma_f16(ah, w2h[s], acc[rb]);
                     acc[rb] = mfma_f16(ah, w2l[s], acc[rb]);
                     acc[rb] = mfma_f16(al, w2h[s], acc[rb]);
@@ -497,10 +546,11 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
             // 4 (wave >> 2) + jj (jj < 4): 4 A and 8 B fragment reads per slot
             // (a c-row of tiles would read 2 A and all 16 B fragments)
             const int cw = 32 * (wave & 3) + r;
-            const half8 gh0 = *(const half8 *)&gt[0][cw * FCS + 8 * g];
-            const half8 gl0 = *(const half8 *)&gt[1][cw * FCS + 8 * g];
-            const half8 gh1 = *(const half8 *)&gt[0][(cw + 16) * FCS + 8 * g];
-            const half8 gl1 = *(const half8 *)&gt[1][(cw + 16) * FCS + 8 * g];
+            const int gq = 8 * (g ^ gsw(cw));  // gsw(cw + 16) = gsw(cw)
+            const half8 gh0 = *(const half8 *)&gt[0][cw * FCS + gq];
+            const half8 gl0 = *(const half8 *)&gt[1][cw * FCS + gq];
+            const half8 gh1 = *(const half8 *)&gt[0][(cw + 16) * FCS + gq];
+            const half8 gl1 = *(const half8 *)&gt[1][(cw + 16) * FCS + gq];
             // the epilogue's LDS values, read ahead of the dW2 MFMAs: the z1 > 0
             // bits of column col (bit rr of the 4 bytes), and (MASK, registers
             // to spare) the gz1 rows of the lane's 8 slots
@@ -513,8 +563,9 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
 #pragma unroll
             for (int jj = 0; jj < 4; ++jj) {
                 const int j = 4 * (wave >> 2) + jj;
-                const half8 bh = *(const half8 *)&zb[sb][0][(16 * j + r) * FCS + 8 * g];
-                const half8 bl = *(const half8 *)&zb[sb][1][(16 * j + r) * FCS + 8 * g];
+                const int zq = (16 * j + r) * FCS + 8 * (g ^ csw(r));  // csw(16 j + r) = csw(r)
+                const half8 bh = *(const half8 *)&zb[sb][0][zq];
+                const half8 bl = *(const half8 *)&zb[sb][1][zq];
                 dw[2 * jj] = mfma_f16(gh0, bh, dw[2 * jj]);
                 dw[2 * jj] = mfma_f16(gh0, bl, dw[2 * jj]);
                 dw[2 * jj] = mfma_f16(gl0, bh, dw[2 * jj]);

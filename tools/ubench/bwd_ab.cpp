@@ -5,7 +5,11 @@
 // mmpde_reverse_adjacency), plus the two source sums.  Built per variant of
 // the kernel's compile-time placement flags (Makefile bwd_ab_%).
 //   make -C tools/ubench bwd_ab_base && tools/ubench/bwd_ab_base
-#include "../../mm-pde_amd/csrc/edge_bwd.hip"
+// BWD_SRC: another edge_bwd.hip for a same-box A/B (built with -I mm-pde_amd/csrc)
+#ifndef BWD_SRC
+#define BWD_SRC "../../mm-pde_amd/csrc/edge_bwd.hip"
+#endif
+#include BWD_SRC
 #include "../../mm-pde_amd/csrc/train_rows.hip"
 #include <cstdio>
 #include <random>
@@ -92,6 +96,22 @@ int main() {
         mmpde_gnn_edge_backward_sorted(da, db, dnb, nullptr, n, K, dw2, db2, dg, pos, mask, ga, ge, part, gw2, gb2,
                                        1, nullptr);
     });
+    {   // output hash of the masked sorted backward (variants must match bit for bit)
+        CK(mmpde_gnn_edge_backward_sorted(da, db, dnb, nullptr, n, K, dw2, db2, dg, pos, mask, ga, ge, part, gw2,
+                                          gb2, 1, nullptr));
+        CK(hipDeviceSynchronize());
+        uint64_t h = 1469598103934665603ull;
+        auto mix = [&](const float *d, size_t cnt) {
+            std::vector<uint32_t> v(cnt);
+            hipMemcpy(v.data(), d, cnt * 4, hipMemcpyDeviceToHost);
+            for (uint32_t x : v) h = (h ^ x) * 1099511628211ull;
+        };
+        mix(ga, n * 128);
+        mix(ge, n * K * 128);
+        mix(gw2, 128 * 128);
+        mix(gb2, 128);
+        printf("  output hash (ga, gz1, dW2, db2 of the masked sorted backward): %016llx\n", (unsigned long long)h);
+    }
     timed("source_sum_sorted (contiguous)", [&] { mmpde_gnn_edge_source_sum_sorted(ge, off, n, gb, nullptr); });
     timed("reverse_adjacency (+ slot positions)", [&] {
         mmpde_reverse_adjacency(dnb, n, K, nullptr, n, off, edge, pos, scratch, sb, bad, nullptr);
