@@ -349,6 +349,14 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
     __shared__ int nb[FT * FKMAX];             // the tile's neighbour rows (clamped)
     __shared__ int gzr[FT * FKMAX];            // the gz1 rows of the tile's slots
     __shared__ int dg[FT];                     // degrees (0 past n)
+    // MASK: the tile's z2 > 0 words, [row][slot][4] at a row stride of 4 FKMAX + 1
+    // words (the 4 rows a ds_read_b32 takes sit on different banks), staged with
+    // the neighbour table: P2 reads them from LDS.  (Round 5 prefetched each
+    // slot's words into registers one slot ahead; the loop-carried registers made
+    // the compiler copy them at the loop's back edge, waiting there -- after the
+    // barrier -- for the loads just issued, every slot.)
+    constexpr int MLS = 4 * FKMAX + 1;
+    __shared__ uint32_t mlds[MASK ? FT * MLS : 1];
     const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int r = lane & 15, g = lane >> 4;
     const int64_t nmax = p.n - 1;
@@ -396,18 +404,16 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
             gzr[rr * FKMAX + e] = p.pos ? p.pos[q] : (int)q;
         }
         if (tid < FT) dg[tid] = row0 + tid < p.n ? (p.deg ? p.deg[row0 + tid] : k) : 0;
+        if (MASK) {  // rows row0 .. row0 + 31 of the mask are contiguous: coalesced
+            for (int i = tid; i < FT * 4 * k; i += 512) {
+                const int rr = i / (4 * k), w = i - rr * 4 * k;
+                mlds[rr * MLS + w] = p.mask[(min(row0 + rr, nmax) * k) * 4 + w];
+            }
+        }
         __syncthreads();
         float bv[8];
 #pragma unroll
         for (int t = 0; t < 8; ++t) bv[t] = p.b[(int64_t)nb[(8 * eg + t) * FKMAX] * BH + kk1];
-        uint32_t mnext[8];  // MASK: the z2 > 0 bits of the slot P2 runs next
-        if (MASK) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const int rr = 16 * (i >> 2) + 4 * g + (i & 3);
-                mnext[i] = p.mask[(min(row0 + rr, nmax) * k) * 4 + (wave >> 1)];
-            }
-        }
         // MASK (registers to spare without the z2 operands): the tile's a values
         // of P1, and g / deg and the degrees of P2, in registers for the tile
         float atv[MASK ? 8 : 1], gmv[MASK ? 8 : 1];
@@ -470,16 +476,10 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
             }
             uint32_t mk[8];
             if (MASK) {
-                // this slot's bits (column tile = wave, bit r) of the 8 rows of
-                // this lane, then the next slot's issued (in flight over P3)
+                // this slot's words (column tile = wave, bit r) of the lane's 8 rows
 #pragma unroll
-                for (int i = 0; i < 8; ++i) mk[i] = mnext[i];
-                const int en = min(e + 1, k - 1);
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    const int rr = 16 * (i >> 2) + 4 * g + (i & 3);
-                    mnext[i] = p.mask[(min(row0 + rr, nmax) * k + en) * 4 + (wave >> 1)];
-                }
+                for (int i = 0; i < 8; ++i)
+                    mk[i] = mlds[(16 * (i >> 2) + 4 * g + (i & 3)) * MLS + 4 * e + (wave >> 1)];
             }
 #pragma unroll
             for (int rb = 0; rb < 2; ++rb) {
