@@ -330,7 +330,10 @@ constexpr int kBwdStagger = MMPDE_BWD_STAGGER;
 
 // MASK: message_net_2's ReLU pattern comes from the forward's bits instead of
 // recomputing z2 (P2 without its MFMAs; no row-major relu(z1) image).
-template <bool MASK>
+// O32: every byte offset into b (n x 512 B) and gz1 (n k x 512 B) fits in 32
+// bits, so the per-slot gathers and the per-edge stores take one 32-bit
+// multiply-add over a scalar base instead of 64-bit address arithmetic.
+template <bool MASK, bool O32>
 __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) {
     __shared__ float at[FT * FAW];             // a rows of the tile
     __shared__ float gms[FT * FAW];            // g / deg rows (0 for rows past n)
@@ -382,8 +385,18 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
     float db = 0.0f;
     // P1 role: column kk1 of edges 8 eg .. 8 eg + 7
     const int kk1 = tid & (BH - 1), eg = tid >> 7;
+    // b[src][kk1] and the gz1 element (row, col): 32-bit byte offsets with O32
+    auto b_at = [&](int src) -> float {
+        if (O32) return *(const float *)((const char *)p.b + ((uint32_t)src * (BH * 4u) + (uint32_t)kk1 * 4u));
+        return p.b[(int64_t)src * BH + kk1];
+    };
+    auto gz1_store = [&](int grow, float v) {
+        if (O32) *(float *)((char *)p.gz1 + ((uint32_t)grow * (BH * 4u) + (uint32_t)col * 4u)) = v;
+        else p.gz1[(int64_t)grow * BH + col] = v;
+    };
     for (int tile = blockIdx.x; tile < p.ntiles; tile += gridDim.x) {
         const int64_t row0 = (int64_t)tile * FT;
+        const bool tile_full = row0 + FT <= p.n;
         __syncthreads();  // the previous tile's readers are done
         for (int i = tid; i < FT * BH / 4; i += 512) {
             const int rr = i >> 5, c4 = i & 31;
@@ -413,7 +426,7 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
         __syncthreads();
         float bv[8];
 #pragma unroll
-        for (int t = 0; t < 8; ++t) bv[t] = p.b[(int64_t)nb[(8 * eg + t) * FKMAX] * BH + kk1];
+        for (int t = 0; t < 8; ++t) bv[t] = b_at(nb[(8 * eg + t) * FKMAX]);
         // MASK (registers to spare without the z2 operands): the tile's a values
         // of P1, and g / deg and the degrees of P2, in registers for the tile
         float atv[MASK ? 8 : 1], gmv[MASK ? 8 : 1];
@@ -453,7 +466,7 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
             zm[sb][kk1 * 4 + eg] = (uint8_t)bits;
             const int en = min(e + 1, k - 1);
 #pragma unroll
-            for (int t = 0; t < 8; ++t) bv[t] = p.b[(int64_t)nb[(8 * eg + t) * FKMAX + en] * BH + kk1];
+            for (int t = 0; t < 8; ++t) bv[t] = b_at(nb[(8 * eg + t) * FKMAX + en]);
         };
         // ---- P2: z2 and gz2 (column c = col) of slot e
         auto p2 = [&](int e) {
@@ -573,6 +586,7 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
                 dw[2 * jj + 1] = mfma_f16(gh1, bl, dw[2 * jj + 1]);
                 dw[2 * jj + 1] = mfma_f16(gl1, bh, dw[2 * jj + 1]);
             }
+            float gv[8];
 #pragma unroll
             for (int rb = 0; rb < 2; ++rb) {
 #pragma unroll
@@ -581,8 +595,21 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
                     const bool pos = (zbits >> rr) & 1u;
                     const float v = pos ? acc[rb][q] * un2 : 0.0f;
                     gacc[rb][q] += v;
-                    const int grow = MASK ? gzrow[MASK ? 4 * rb + q : 0] : gzr[rr * FKMAX + e];
-                    if (row0 + rr < p.n) p.gz1[(int64_t)grow * BH + col] = v;
+                    gv[4 * rb + q] = v;
+                }
+            }
+            // the rows past n (the last tile only) keep no gz1: one uniform test
+            // per tile instead of a lane branch per store
+            if (tile_full) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    gz1_store(MASK ? gzrow[MASK ? i : 0] : gzr[(16 * (i >> 2) + 4 * g + (i & 3)) * FKMAX + e], gv[i]);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const int rr = 16 * (i >> 2) + 4 * g + (i & 3);
+                    if (row0 + rr < p.n)
+                        gz1_store(MASK ? gzrow[MASK ? i : 0] : gzr[rr * FKMAX + e], gv[i]);
                 }
             }
         };
@@ -907,8 +934,11 @@ static int edge_backward(const float *a, const float *b, const int32_t *nbr, con
     MMPDE_RET_LAUNCH();
     EdgeBwdF16Args p{a, b, nbr, deg, n, k, (int)ntiles, img1, img2, msg2_b, grad_mean, mx, grad_a, grad_edge,
                      pw2, pb2, pos, mask};
-    if (mask) hipLaunchKernelGGL(edge_bwd_f16_kernel<true>, dim3(grid), dim3(512), 0, st, p);
-    else hipLaunchKernelGGL(edge_bwd_f16_kernel<false>, dim3(grid), dim3(512), 0, st, p);
+    const bool o32 = n * BH * 4 < ((int64_t)1 << 32) && n * k * BH * 4 < ((int64_t)1 << 32);
+    if (mask && o32) hipLaunchKernelGGL((edge_bwd_f16_kernel<true, true>), dim3(grid), dim3(512), 0, st, p);
+    else if (mask) hipLaunchKernelGGL((edge_bwd_f16_kernel<true, false>), dim3(grid), dim3(512), 0, st, p);
+    else if (o32) hipLaunchKernelGGL((edge_bwd_f16_kernel<false, true>), dim3(grid), dim3(512), 0, st, p);
+    else hipLaunchKernelGGL((edge_bwd_f16_kernel<false, false>), dim3(grid), dim3(512), 0, st, p);
     MMPDE_RET_LAUNCH();
     hipLaunchKernelGGL(partial_sum_kernel, dim3(ceil_div(BH * BH, 32)), dim3(256), 0, st, pw2, grid,
                        (int64_t)BH * BH, grad_w2);
