@@ -330,6 +330,16 @@ constexpr int kBwdStagger = MMPDE_BWD_STAGGER;
 
 // MASK: message_net_2's ReLU pattern comes from the forward's bits instead of
 // recomputing z2 (P2 without its MFMAs; no row-major relu(z1) image).
+// MASK kernel: s_setprio 1 around P3's MFMA cluster (the guide's T5; the wave
+// in its MFMA phase wins issue over its SIMD partner's P1 / P2 VALU), same-box
+// A/B (profiles/r06_bwd_lds_ab.log): 443-446 against 457-459 us with the same
+// hash; the unmasked kernel was 1-3 % slower with it, so MASK only.  Waves 4-7
+// at priority 1 for the whole launch (the guide's static form) measured no
+// change and is not kept.  0 turns it off.
+#ifndef MMPDE_BWD_PRIO
+#define MMPDE_BWD_PRIO 1
+#endif
+
 // O32: every byte offset into b (n x 512 B) and gz1 (n k x 512 B) fits in 32
 // bits, so the per-slot gathers and the per-edge stores take one 32-bit
 // multiply-add over a scalar base instead of 64-bit address arithmetic.
@@ -542,6 +552,7 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
                 const fp16x4_t lo4 = lds_read_tr16(b0), hi4 = lds_read_tr16(b0 + 4 * FCS);
                 return __builtin_bit_cast(half8, __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7));
             };
+            if (MASK && MMPDE_BWD_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
 #pragma unroll
@@ -586,6 +597,7 @@ __global__ __launch_bounds__(512, 1) void edge_bwd_f16_kernel(EdgeBwdF16Args p) 
                 dw[2 * jj + 1] = mfma_f16(gh1, bl, dw[2 * jj + 1]);
                 dw[2 * jj + 1] = mfma_f16(gl1, bh, dw[2 * jj + 1]);
             }
+            if (MASK && MMPDE_BWD_PRIO) __builtin_amdgcn_s_setprio(0);
             float gv[8];
 #pragma unroll
             for (int rb = 0; rb < 2; ++rb) {
