@@ -75,6 +75,7 @@ struct WaveArgs {
     const float *rec;         // their range records (nullable: every segment per-row)
     float *out;               // neighbour sums of the units that start a tile
     float *side;              // [G][16][128]: the unit a wave starts inside a tile
+    uint64_t *stamps;         // DIAG & 256 only: [G] exit times (100 MHz clock)
 };
 
 
@@ -480,6 +481,10 @@ __global__ __launch_bounds__(64, 1) void gnn_edge_wave_kernel(WaveArgs p) {
 #pragma unroll
     for (int t = 0; t < 4; ++t) relu_add(S[7], acc7[t], t, e_prev, dg_prev);
     write_unit(row0_prev, side_prev);
+    if (DIAG & 256) {  // profiling builds: the wave's exit time (vector store)
+        const uint64_t t = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0) p.stamps[blockIdx.x] = t;
+    }
 }
 
 }  // namespace
@@ -526,7 +531,7 @@ int edge_wave_setup(const float *a, const float *b, const int32_t *nbr, const in
     const EdgePlan pl = edge_wave_plan(nseg, S, k, cus, side_cap);
     if (pl.wpsp < 1 || pl.waves > (int64_t)INT32_MAX || nseg * pl.U > (int64_t)INT32_MAX) return 0;
     *w = WaveArgs{a, b, nbr, deg, n, k, seg_n, (int)tps, S, pl.U, pl.wpsp, msg2_b, pk, rmx,
-                  rng ? rmx + row_max_floats(n) : nullptr, out, side};
+                  rng ? rmx + row_max_floats(n) : nullptr, out, side, nullptr};
     *split = EdgeSplit{side, S, pl.U, k, seg_n};
     return (int)pl.waves;
 }
@@ -561,6 +566,26 @@ int launch_edge_wave_diag(const float *a, const float *b, const int32_t *nbr, in
 #undef MMPDE_DIAG
     MMPDE_RET_LAUNCH();
     return MMPDE_OK;
+}
+
+// Profiling aid (tools/ubench/edge_exit): the production launch (segments of
+// seg_n rows, range records) of the kernel built with DIAG bit 8 (256), which
+// stores each wave's exit time (100 MHz clock) to stamps[block] (an entry stamp
+// as well made that build spill 48 VGPRs); returns the launch's wave count or a
+// negative status.
+int launch_edge_wave_exit_stamps(const float *a, const float *b, const int32_t *nbr, int64_t n, int k,
+                                 int64_t seg_n, const float *msg2_b, const char *pk, const float *rmx,
+                                 float *out, float *side, int64_t side_cap, int cus, uint64_t *stamps,
+                                 hipStream_t st) {
+    WaveArgs w;
+    EdgeSplit split;
+    const int grid = edge_wave_setup(a, b, nbr, nullptr, n, k, seg_n, msg2_b, pk, rmx, true, out, side, side_cap,
+                                     cus, &w, &split);
+    if (grid <= 0) return -1;
+    w.stamps = stamps;
+    if (stamps) hipLaunchKernelGGL((gnn_edge_wave_kernel<false, 256>), dim3(grid), dim3(64), 0, st, w);
+    else hipLaunchKernelGGL((gnn_edge_wave_kernel<false, 0>), dim3(grid), dim3(64), 0, st, w);
+    return hipGetLastError() == hipSuccess ? grid : -2;
 }
 
 int launch_edge_wave(const float *a, const float *b, const int32_t *nbr, const int32_t *deg, int64_t n,
