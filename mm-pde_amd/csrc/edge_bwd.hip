@@ -51,18 +51,24 @@ struct EdgeBwdArgs {
 // the forward evaluated, whose z2 summation order differs from this kernel's.
 template <bool MASK>
 __global__ __launch_bounds__(256, 1) void edge_bwd_kernel(EdgeBwdArgs p) {
-    __shared__ float w2s[BH * BWS];    // W2 [c][kk], row stride BWS
-    __shared__ float at[BT * BWS];     // a rows of the tile
-    __shared__ float z1s[BT * BWS];    // z1 of the current slot
-    __shared__ float gz2s[BT * BWS];   // gz2 of the current slot
-    __shared__ float gms[BT * BWS];    // g / deg of the tile
+    // Row strides (round 6, SQ_LDS_BANK_CONFLICT was 61 % of this kernel's LDS
+    // cycles at one common 136-float stride): W2 and the z1 / a / g rows at
+    // 144 floats (≡ 16 mod 32: the rows 4 s + g, g = 0, 1 of a 32-lane half, read
+    // at 16 consecutive columns, fill all 32 banks), gz2 at 130 (≡ 2: its
+    // A-operand reads, 16 rows r at column 4 s + g, fill all 32 banks)
+    constexpr int WS = BWS + 8, GS = BWS - 6;
+    __shared__ float w2s[BH * WS];     // W2 [c][kk], row stride WS
+    __shared__ float at[BT * WS];      // a rows of the tile
+    __shared__ float z1s[BT * WS];     // z1 of the current slot
+    __shared__ float gz2s[BT * GS];    // gz2 of the current slot
+    __shared__ float gms[BT * WS];     // g / deg of the tile
     __shared__ int srcs[BT];
     const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int r = lane & 15, g = lane >> 4;
     const int64_t nmax = p.n - 1;
     const int k = p.k;
     for (int i = tid; i < BH * BH / 4; i += 256)
-        *(float4 *)&w2s[(i >> 5) * BWS + 4 * (i & 31)] = ((const float4 *)p.w2)[i];
+        *(float4 *)&w2s[(i >> 5) * WS + 4 * (i & 31)] = ((const float4 *)p.w2)[i];
     // persistent accumulators: dW2 tiles (c tile 2 wave + ci, kk tile kj), db2
     f32x4 dw[2][8];
 #pragma unroll
@@ -81,8 +87,8 @@ __global__ __launch_bounds__(256, 1) void edge_bwd_kernel(EdgeBwdArgs p) {
             const float inv_deg = live ? 1.0f / (float)max(dgv, 1) : 0.0f;
             const float4 av = ((const float4 *)(p.a + row * BH))[c4];
             const float4 gv = ((const float4 *)(p.gmean + row * BH))[c4];
-            *(float4 *)&at[rr * BWS + 4 * c4] = av;
-            *(float4 *)&gms[rr * BWS + 4 * c4] =
+            *(float4 *)&at[rr * WS + 4 * c4] = av;
+            *(float4 *)&gms[rr * WS + 4 * c4] =
                 make_float4(gv.x * inv_deg, gv.y * inv_deg, gv.z * inv_deg, gv.w * inv_deg);
         }
         // dL/da accumulators: rows 4 g + t, columns 16 (2 wave + ci) + r
@@ -104,12 +110,8 @@ __global__ __launch_bounds__(256, 1) void edge_bwd_kernel(EdgeBwdArgs p) {
             for (int i = tid; i < BT * BH / 4; i += 256) {
                 const int rr = i >> 5, c4 = i & 31;
                 const float4 bv = ((const float4 *)(p.b + (int64_t)srcs[rr] * BH))[c4];
-                float *zp = &z1s[rr * BWS + 4 * c4];
-                const float *ap = &at[rr * BWS + 4 * c4];
-                zp[0] = ap[0] + bv.x;
-                zp[1] = ap[1] + bv.y;
-                zp[2] = ap[2] + bv.z;
-                zp[3] = ap[3] + bv.w;
+                const float4 av = *(const float4 *)&at[rr * WS + 4 * c4];
+                *(float4 *)&z1s[rr * WS + 4 * c4] = make_float4(av.x + bv.x, av.y + bv.y, av.z + bv.z, av.w + bv.w);
             }
             __syncthreads();
             // z2 = W2 relu(z1) + b2 and gz2 = g / deg [z2 > 0]: wave owns columns
@@ -128,9 +130,9 @@ __global__ __launch_bounds__(256, 1) void edge_bwd_kernel(EdgeBwdArgs p) {
                     for (int t = 0; t < 4; ++t) {
                         const int rr = 4 * g + t;
                         const bool on = e < dgr[t] && ((mw[t] >> (16 * ci + r)) & 1u);
-                        const float v = on ? gms[rr * BWS + c] : 0.0f;
+                        const float v = on ? gms[rr * WS + c] : 0.0f;
                         gz2v[ci][t] = v;
-                        gz2s[rr * BWS + c] = v;
+                        gz2s[rr * GS + c] = v;
                     }
                 }
             }
@@ -140,8 +142,8 @@ __global__ __launch_bounds__(256, 1) void edge_bwd_kernel(EdgeBwdArgs p) {
                 f32x4 acc = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll 8
                 for (int s = 0; s < BH / 4; ++s) {
-                    const float av = fmaxf(z1s[r * BWS + 4 * s + g], 0.0f);
-                    const float bv = w2s[c * BWS + 4 * s + g];
+                    const float av = fmaxf(z1s[r * WS + 4 * s + g], 0.0f);
+                    const float bv = w2s[c * WS + 4 * s + g];
                     acc = mfma16(av, bv, acc);
                 }
                 const float bb = p.b2[c];
@@ -149,9 +151,9 @@ __global__ __launch_bounds__(256, 1) void edge_bwd_kernel(EdgeBwdArgs p) {
                 for (int t = 0; t < 4; ++t) {
                     const int rr = 4 * g + t;
                     const bool on = e < dgr[t] && acc[t] + bb > 0.0f;
-                    const float v = on ? gms[rr * BWS + c] : 0.0f;
+                    const float v = on ? gms[rr * WS + c] : 0.0f;
                     gz2v[ci][t] = v;
-                    gz2s[rr * BWS + c] = v;
+                    gz2s[rr * GS + c] = v;
                 }
             }
 #pragma unroll
@@ -166,14 +168,14 @@ __global__ __launch_bounds__(256, 1) void edge_bwd_kernel(EdgeBwdArgs p) {
                 f32x4 acc = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll 8
                 for (int s = 0; s < BH / 4; ++s) {
-                    const float av = gz2s[r * BWS + 4 * s + g];
-                    const float bv = w2s[(4 * s + g) * BWS + kk];
+                    const float av = gz2s[r * GS + 4 * s + g];
+                    const float bv = w2s[(4 * s + g) * WS + kk];
                     acc = mfma16(av, bv, acc);
                 }
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
                     const int rr = 4 * g + t;
-                    const float v = z1s[rr * BWS + kk] > 0.0f ? acc[t] : 0.0f;
+                    const float v = z1s[rr * WS + kk] > 0.0f ? acc[t] : 0.0f;
                     gacc[ci][t] += v;
                     if (row0 + rr < p.n) {
                         const int64_t q = (row0 + rr) * k + e;
@@ -191,8 +193,8 @@ __global__ __launch_bounds__(256, 1) void edge_bwd_kernel(EdgeBwdArgs p) {
 #pragma unroll
                     for (int s = 0; s < 4; ++s) {
                         // A[c][row] = gz2[row][c] (lane: c = r, row = 4 s + g); B[row][kk]
-                        const float av = gz2s[(4 * s + g) * BWS + 16 * (2 * wave + ci) + r];
-                        const float bv = fmaxf(z1s[(4 * s + g) * BWS + kk], 0.0f);
+                        const float av = gz2s[(4 * s + g) * GS + 16 * (2 * wave + ci) + r];
+                        const float bv = fmaxf(z1s[(4 * s + g) * WS + kk], 0.0f);
                         dw[ci][kj] = mfma16(av, bv, dw[ci][kj]);
                     }
                 }

@@ -112,6 +112,26 @@ int main() {
         mix(gb2, 128);
         printf("  output hash (ga, gz1, dW2, db2 of the masked sorted backward): %016llx\n", (unsigned long long)h);
     }
+    timed("backward_sorted exact fp32 + relu mask", [&] {
+        mmpde_gnn_edge_backward_sorted(da, db, dnb, nullptr, n, K, dw2, db2, dg, pos, mask, ga, ge, part, gw2, gb2,
+                                       MMPDE_EDGE_GEMM_F32, nullptr);
+    });
+    {   // the same hash for the exact-fp32 masked sorted backward
+        CK(mmpde_gnn_edge_backward_sorted(da, db, dnb, nullptr, n, K, dw2, db2, dg, pos, mask, ga, ge, part, gw2,
+                                          gb2, MMPDE_EDGE_GEMM_F32, nullptr));
+        CK(hipDeviceSynchronize());
+        uint64_t h = 1469598103934665603ull;
+        auto mix = [&](const float *d, size_t cnt) {
+            std::vector<uint32_t> v(cnt);
+            hipMemcpy(v.data(), d, cnt * 4, hipMemcpyDeviceToHost);
+            for (uint32_t x : v) h = (h ^ x) * 1099511628211ull;
+        };
+        mix(ga, n * 128);
+        mix(ge, n * K * 128);
+        mix(gw2, 128 * 128);
+        mix(gb2, 128);
+        printf("  output hash (exact fp32 masked sorted backward): %016llx\n", (unsigned long long)h);
+    }
     timed("source_sum_sorted (contiguous)", [&] { mmpde_gnn_edge_source_sum_sorted(ge, off, n, gb, nullptr); });
     timed("reverse_adjacency (+ slot positions)", [&] {
         mmpde_reverse_adjacency(dnb, n, K, nullptr, n, off, edge, pos, scratch, sb, bad, nullptr);
