@@ -223,7 +223,12 @@ class GraphCreator_FS_2D(nn.Module):  # noqa: N801 - reference name
         # steps[b] for the B trajectories only: training_itp passes 128 x batch_size
         # steps for a batch of batch_size (train_helper_2d.py:44,47; the reference
         # loops b over the data, data_creator_2d.py:243-254)
-        t_nodes = t[list(steps)[:B]].to(device).repeat_interleave(n)
+        # a pageable host->device copy waits for the stream to drain: stage the B
+        # times in pinned memory and copy asynchronously (no sync per graph)
+        t_b = t[list(steps)[:B]]
+        if torch.device(device).type == "cuda":
+            t_b = t_b.pin_memory().to(device, non_blocking=True)
+        t_nodes = t_b.to(device).repeat_interleave(n)
         deg = None
         if self.e == "radius":   # torch_cluster default max_num_neighbors = 32
             nbr, deg = ops.radius_graph_nbr(mesh.contiguous(), B, self.radius(), 32)

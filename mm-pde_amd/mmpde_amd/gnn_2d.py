@@ -603,7 +603,19 @@ class MP_PDE_Solver_2D(nn.Module):  # noqa: N801 - reference name
             else:
                 h = layer.train_forward(h, u, pos_x, pos_y, variables, graph, self.edge_gemm)
         diff = self._head_train(h)
-        return self.out_scales()[None].to(h.device) * diff
+        return self.out_scales_on(h.device)[None] * diff
+
+    def out_scales_on(self, device) -> torch.Tensor:
+        """out_scales() on `device`, cached per (device, dt, tw): a pageable
+        host->device copy per forward would wait for the stream to drain."""
+        key = (str(device), float(self.pde.dt), self.time_window)
+        cache = self.__dict__.setdefault("_out_scales_cache", {})
+        hit = cache.get(key)
+        if hit is None:
+            hit = self.out_scales().to(device)
+            cache.clear()
+            cache[key] = hit
+        return hit
 
     def _head_train(self, h: torch.Tensor) -> torch.Tensor:
         """output_mlp(h[:, None]).squeeze(1) (gnn_2d.py:108-114,136), as the

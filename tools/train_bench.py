@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--edge-gemm", default="f32", choices=["f32", "f16x3"])
+    ap.add_argument("--host-profile", default=None,
+                    help="write a cProfile summary (tottime order) of the timed iterations here")
     args = ap.parse_args()
     from mmpde_amd.gnn_2d import EdgeGraph, EdgeMean
     from mmpde_amd.synth import build_models, fields
@@ -66,11 +68,25 @@ def main():
     for _ in range(args.warmup):
         it()
     torch.cuda.synchronize()
+    prof = None
+    if args.host_profile:
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
+    issue = 0.0
     for _ in range(args.iters):
+        t1 = time.perf_counter()
         loss = it()
+        issue += time.perf_counter() - t1
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3 / args.iters
+    if prof is not None:
+        import pstats
+        prof.disable()
+        with open(args.host_profile, "w") as f:
+            pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(45)
+        prof.dump_stats(args.host_profile + ".prof")
 
     # one layer's edge backward alone (HIP events on the current stream)
     n = B * 2521
@@ -101,6 +117,7 @@ def main():
     print(json.dumps({
         "what": "MM-PDE training iteration (train_helper_2d.py:95-131), cy synthetic",
         "batch": B, "nodes": n, "edge_gemm": args.edge_gemm, "ms_per_iter": round(ms, 3),
+        "host_issue_ms_per_iter": round(issue * 1e3 / args.iters, 3),
         "train_node_updates_per_s": round(2 * 6 * n / (ms * 1e-3)),
         "loss": float(loss),
         "edge_backward_layer_us": round(bwd_us, 1),
