@@ -352,23 +352,50 @@ struct TnArgs {
     int cols, kbig;  // partial columns; rounded big-segment columns
     int base[3];     // first partial column of each segment
     float *part;
+    int nkb, ncb, chunks;  // k blocks, c blocks, row chunks
 };
+
+// Workgroup -> (k block, chunk, c block).  The k and c blocks of one chunk read
+// the same G and X rows; workgroups are dealt to the 8 XCDs round-robin by id
+// (b and b + 8 share an XCD and its L2), so the nkb * ncb blocks of chunk c take
+// ids 8 (nb (c / 8) + b) + c % 8: one XCD, consecutive slots (dispatched
+// together), and each row is fetched from HBM once instead of once per block.
+// Ids past the last chunk exit at once.  Speed only: every block computes the
+// same partial as before.
+struct TnBlock {
+    int kb, chunk, cb;
+};
+__device__ __forceinline__ TnBlock tn_block(const TnArgs &t) {
+    const int id = blockIdx.x, nb = t.nkb * t.ncb;
+    const int slot = id >> 3, b = slot % nb;
+    return {64 * (b % t.nkb), (slot / nb) * 8 + (id & 7), 64 * (b / t.nkb)};
+}
 
 __device__ __forceinline__ float2 ld2(const float *p, bool vec) {
     return vec ? *(const float2 *)p : make_float2(p[0], p[1]);
 }
 
+// row-step batches per wave of the straight-line main loop (32 steps = the
+// 64 rows of a 256-row chunk's quarter)
+constexpr int kTnBatches = 8;
+
+#ifndef MMPDE_TN_XS_OCC
+#define MMPDE_TN_XS_OCC 3
+#endif
+
 template <bool GMASK, bool VEC, bool XS>
-__global__ __launch_bounds__(256, GMASK && XS ? 2 : 3) void rgemm_tn_partial_kernel(TnArgs t) {
+__global__ __launch_bounds__(256, GMASK && XS ? 2 : (XS ? MMPDE_TN_XS_OCC : 3)) void rgemm_tn_partial_kernel(TnArgs t) {
     constexpr int NRED = 64 + 2 + 8;  // per lane: the block (4 tiles x 16), db (2), small segment (2 x 4)
     __shared__ float red[NRED][64];
     const mmpde_rgemm_tn_args &g = t.g;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int par = lane >> 5, j = lane & 31;
-    const int chunk = blockIdx.y;
+    const TnBlock blk = tn_block(t);
+    if (blk.chunk >= t.chunks) return;    // the whole workgroup: no barrier reached
+    const int chunk = blk.chunk;
     const int gcols = g.gcols;
-    const int cb = 64 * blockIdx.z;       // first G column of this block
-    const int kb = 64 * blockIdx.x;       // first partial column of this block
+    const int cb = blk.cb;                // first G column of this block
+    const int kb = blk.kb;                // first partial column of this block
     const int64_t c0r = (int64_t)chunk * g.chunk_rows;
     const int64_t c1r = min(c0r + (int64_t)g.chunk_rows, g.m);
     // even rows per wave, 4 * qrows >= chunk_rows (the same split as chunk_rows / 4
@@ -390,7 +417,7 @@ __global__ __launch_bounds__(256, GMASK && XS ? 2 : 3) void rgemm_tn_partial_ker
     const int64_t ldx = g.ldx[seg];
     const float *gp = g.g + cc;
     const float *gm = GMASK ? g.gmask + cc : nullptr;
-    const bool first = blockIdx.x == 0;
+    const bool first = kb == 0;
     const int ns = first ? g.ns : 0;
     // [c tile][k tile]: four independent accumulators cover the MFMA latency
     f32x16 acc[2][2];
@@ -407,7 +434,10 @@ __global__ __launch_bounds__(256, GMASK && XS ? 2 : 3) void rgemm_tn_partial_ker
     // issued before this batch's 16 MFMAs.  The loads are unconditional and
     // keep raw values; compute() masks them (a select on a freshly loaded value
     // lets the compiler sink the load under a branch, where it is waited for
-    // at once).  Single-column operands read their one column twice.
+    // at once).  Single-column operands read their one column twice.  The small
+    // segment's loads are issued by every block of an XS launch (its sums only
+    // by k block 0): loads behind a branch on `first` left the waits at the
+    // join conservative.
     struct Buf {
         float2 a[4], b[4], q[4];
         float x[4][4];
@@ -426,9 +456,9 @@ __global__ __launch_bounds__(256, GMASK && XS ? 2 : 3) void rgemm_tn_partial_ker
                 const float *pm = gm + i * g.ldg;
                 o.q[q] = VEC ? *(const float2 *)pm : make_float2(pm[0], pm[g1 ? 1 : 0]);
             }
-            if (xsum) {
+            if (XS) {
 #pragma unroll
-                for (int e = 0; e < 4; ++e) o.x[q][e] = g.xs[i * g.ldxs + min(e, ns - 1)];
+                for (int e = 0; e < 4; ++e) o.x[q][e] = g.xs[i * g.ldxs + min(e, g.ns - 1)];
             }
         }
     };
@@ -476,7 +506,27 @@ __global__ __launch_bounds__(256, GMASK && XS ? 2 : 3) void rgemm_tn_partial_ker
             }
         }
     };
-    if (steps > 0) {
+    if (steps > 0 && steps <= 4 * kTnBatches) {
+        // the production chunk (256 rows: 32 steps per wave) as straight-line
+        // code: the rolled loop below carries b0 / b1 across its back edge,
+        // where the compiler waited for every outstanding load (vmcnt(0)) before
+        // issuing the next batch -- each batch then paid a full memory latency
+        Buf b0, b1;
+        load(0, b0);
+        // (sched_barrier: the scheduler hoisted the next compute's masking
+        // above the loads, waiting for the batch in flight before issuing them)
+#pragma unroll
+        for (int s0 = 0; s0 < 4 * kTnBatches; s0 += 8) {
+            load(s0 + 4, b1);
+            __builtin_amdgcn_sched_barrier(0);
+            compute(s0, b0);
+            if (s0 + 4 >= steps) break;
+            load(s0 + 8, b0);
+            __builtin_amdgcn_sched_barrier(0);
+            compute(s0 + 4, b1);
+            if (s0 + 8 >= steps) break;
+        }
+    } else if (steps > 0) {
         Buf b0, b1;
         load(0, b0);
         // the next batch is loaded unconditionally (rows clamped, masked as
@@ -734,7 +784,10 @@ extern "C" int mmpde_rgemm_tn(const mmpde_rgemm_tn_args *gp, void *workspace, in
     MMPDE_REQUIRE(workspace_bytes >= mmpde_rgemm_tn_workspace_bytes(g.m, g.chunk_rows, t.cols));
     MMPDE_REQUIRE(chunks < 65536);
     hipStream_t st = as_stream(stream);
-    const dim3 grid((unsigned)(kbig / 64), (unsigned)chunks, (unsigned)((g.gcols + 63) / 64));
+    t.nkb = kbig / 64;
+    t.ncb = (g.gcols + 63) / 64;
+    t.chunks = (int)chunks;
+    const dim3 grid((unsigned)(8 * t.nkb * t.ncb * ceil_div(chunks, 8)));
 #define TN_LAUNCH(M, V, X) hipLaunchKernelGGL((rgemm_tn_partial_kernel<M, V, X>), grid, dim3(256), 0, st, t)
 #define TN_X(M, V)              \
     if (g.ns > 0) TN_LAUNCH(M, V, true); \
