@@ -133,6 +133,15 @@ int main() {
         printf("  output hash (exact fp32 masked sorted backward): %016llx\n", (unsigned long long)h);
     }
     timed("source_sum_sorted (contiguous)", [&] { mmpde_gnn_edge_source_sum_sorted(ge, off, n, gb, nullptr); });
+    {   // hash of the source sums (of the exact-fp32 gz1 rows above)
+        CK(mmpde_gnn_edge_source_sum_sorted(ge, off, n, gb, nullptr));
+        CK(hipDeviceSynchronize());
+        std::vector<uint32_t> v(n * 128);
+        hipMemcpy(v.data(), gb, v.size() * 4, hipMemcpyDeviceToHost);
+        uint64_t h = 1469598103934665603ull;
+        for (uint32_t x : v) h = (h ^ x) * 1099511628211ull;
+        printf("  output hash (source_sum_sorted): %016llx\n", (unsigned long long)h);
+    }
     timed("reverse_adjacency (+ slot positions)", [&] {
         mmpde_reverse_adjacency(dnb, n, K, nullptr, n, off, edge, pos, scratch, sb, bad, nullptr);
     });
