@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--edge-gemm", default="f32", choices=["f32", "f16x3"])
+    ap.add_argument("--op-profile", default=None,
+                    help="write torch.profiler's per-op counts of 3 iterations here, then exit")
     ap.add_argument("--host-profile", default=None,
                     help="write a cProfile summary (tottime order) of the timed iterations here")
     args = ap.parse_args()
@@ -68,6 +70,15 @@ def main():
     for _ in range(args.warmup):
         it()
     torch.cuda.synchronize()
+    if args.op_profile:
+        from torch.profiler import ProfilerActivity, profile
+        with profile(activities=[ProfilerActivity.CPU]) as prof:
+            for _ in range(3):
+                it()
+            torch.cuda.synchronize()
+        with open(args.op_profile, "w") as f:
+            f.write(prof.key_averages().table(sort_by="count", row_limit=60))
+        return
     prof = None
     if args.host_profile:
         import cProfile
